@@ -1,0 +1,131 @@
+"""ctypes binding of libdecagon_hip.so (include/decagon_hip.h).
+
+This is the one place the Python layer touches native code.  There is no fallback: if the
+library is missing or fails to load, importing the compute path raises, and every op of the
+package fails loudly instead of silently running on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, c_float, c_int32, c_int64, c_uint64, c_void_p
+
+from . import _build
+
+DG_OK = 0
+DG_EINVAL = -1
+DG_EALIGN = -2
+DG_ETOOMANY = -3
+DG_MAX_GROUPS = 8
+DG_EPI_L2NORM = 1
+DG_EPI_RELU = 2
+DG_EPI_CHUNK_RELU = 4
+ABI_VERSION = 2
+
+_ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
+
+
+class DgRelGroup(ctypes.Structure):
+    _fields_ = [
+        ("rowptr", c_void_p),
+        ("col", c_void_p),
+        ("val", c_void_p),
+        ("x", c_void_p),
+        ("out", c_void_p),
+        ("rel_map", c_void_p),
+        ("x_rel_stride", c_int64),
+        ("x_ld", c_int64),
+        ("rowptr_rel_stride", c_int32),
+        ("n_rows", c_int32),
+        ("n_rels", c_int32),
+        ("chunk", c_int32),
+        ("reserved", c_int32 * 4),
+    ]
+
+
+class DgEpiGroup(ctypes.Structure):
+    _fields_ = [("partial", c_void_p), ("n_chunks", c_int32), ("reserved", c_int32)]
+
+
+class DgGemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("a", c_void_p),
+        ("b", c_void_p),
+        ("c", c_void_p),
+        ("sa", c_void_p),
+        ("sc", c_void_p),
+        ("b_map", c_void_p),
+        ("a_bs", c_int64),
+        ("a_sm", c_int64),
+        ("a_sk", c_int64),
+        ("b_bs", c_int64),
+        ("b_sk", c_int64),
+        ("b_sn", c_int64),
+        ("c_bs", c_int64),
+        ("c_sm", c_int64),
+        ("c_sn", c_int64),
+        ("m", c_int32),
+        ("n", c_int32),
+        ("k", c_int32),
+        ("batch", c_int32),
+    ]
+
+
+# name -> (restype, argtypes); must match include/decagon_hip.h exactly.
+SIGNATURES = {
+    "dg_abi_version": (c_int32, []),
+    "dg_spmm_groups_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
+    "dg_spmm_csr_f32": (
+        c_int32,
+        [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p],
+    ),
+    "dg_gcn_epilogue_f32": (
+        c_int32,
+        [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    ),
+    "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_void_p]),
+    "dg_decoder_score_f32": (
+        c_int32,
+        [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+         c_int32, c_void_p, c_void_p],
+    ),
+    "dg_hinge_loss_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p]),
+    "dg_xent_loss_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p]),
+    "dg_unigram_sample": (
+        c_int32,
+        [c_void_p, c_int32, c_int32, c_uint64, c_uint64, c_void_p, c_void_p],
+    ),
+}
+
+_LIB = None
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def load(build_if_missing: bool = True) -> ctypes.CDLL:
+    """Load (building first if needed and allowed) and type the native library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = _build.lib_path()
+    if not path.exists() or (build_if_missing and _build.needs_build()):
+        if not build_if_missing:
+            raise ImportError(f"{path} missing: run __graft_entry__.build() or python -m decagon_amd._build")
+        _build.build()
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    got = lib.dg_abi_version()
+    if got != ABI_VERSION:
+        raise ImportError(f"libdecagon_hip ABI {got} != expected {ABI_VERSION}; rebuild")
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != DG_OK:
+        name = _ERRS.get(rc, f"hipError_t {rc}")
+        raise KernelError(f"{what} failed: {name}")

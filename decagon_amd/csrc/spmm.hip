@@ -1,0 +1,324 @@
+// Relation-group CSR SpMM and the fused GCN epilogue for gfx950 (MI355X).
+//
+// Reference ops replaced (paths relative to the reference root):
+//   tf.sparse_tensor_dense_matmul(adj_mats[edge_type][k], x)  decagon/deep/layers.py:90, :114
+//   tf.sparse_tensor_dense_matmul(x_sparse_feat, weights_k)   decagon/deep/layers.py:89
+//   tf.add_n(outputs) / tf.nn.l2_normalize(outputs, dim=1)     decagon/deep/layers.py:92-93, :116-117
+//   tf.nn.relu(tf.add_n(hid1)) / tf.add_n(embeds)              decagon/deep/model.py:75, :88
+//
+// Work decomposition:
+//   one launch covers every (i,j) group of a layer; a wave owns one output row r of one
+//   relation chunk c and walks the nonzeros of row r in every relation of the chunk.
+//   A dense row of width d is covered by LP = d/4 lanes holding one float4 each, so a wave
+//   consumes G = 64/LP nonzeros per step (d=64: 16 lanes x 4 nonzeros; d=32: 8 x 8).
+//   The (col,val) pairs of up to 64 nonzeros are loaded by one coalesced load and handed to
+//   the lane groups with ds_bpermute; row pointers of up to 64 relations likewise with one
+//   load, read back with v_readlane (wave-uniform).  The G partial sums are folded with a
+//   shuffle butterfly and written once per (chunk, row): no atomics, fixed order.
+//   Blocks are dealt to XCDs round-robin; the block->work-item map gives each XCD a
+//   contiguous run of items (chunk-major), so the dense operands X_k of one chunk stay in
+//   one XCD's L2 while all its rows are processed.
+#include "common.h"
+
+namespace {
+
+struct SpmmGroupK {
+    const int32_t* rowptr;
+    const int32_t* col;
+    const float* val;
+    const float* x;
+    float* out;
+    const int32_t* rel_map;
+    int64_t x_rel_stride;
+    int64_t x_ld;
+    int32_t rowptr_rel_stride;
+    int32_t n_rows;
+    int32_t n_rels;
+    int32_t chunk;
+    int32_t n_chunks;
+    int32_t row_blocks;
+    int32_t block_begin;
+    int32_t n_blocks;
+};
+
+struct SpmmArgs {
+    SpmmGroupK g[DG_MAX_GROUPS];
+    int32_t n_groups;
+    int32_t d;
+};
+
+constexpr int kRowsPerBlock = 4;  // 4 waves x 1 row
+
+template <int LP>
+__global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
+    constexpr int G = dg::kWave / LP;  // nonzeros consumed per wave step
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane / LP;
+    const int q = lane % LP;
+    const int b = blockIdx.x;
+
+    int gi = 0;
+#pragma unroll 1
+    while (gi + 1 < args.n_groups && b >= args.g[gi + 1].block_begin) ++gi;
+    const SpmmGroupK& g = args.g[gi];
+
+    // XCD-contiguous item map: local block lb runs on XCD label lb % 8.
+    const int lb = b - g.block_begin;
+    const int per = g.n_blocks >> 3;
+    const int item = (lb & 7) * per + (lb >> 3);
+    if (item >= g.n_chunks * g.row_blocks) return;
+    const int c = item / g.row_blocks;
+    const int r = (item - c * g.row_blocks) * kRowsPerBlock + wave;
+    if (r >= g.n_rows) return;  // wave-uniform; no barriers in this kernel
+
+    const int d = args.d;
+    const bool qact = q * 4 < d;
+    const int k0 = c * g.chunk;
+    const int k1 = min(k0 + g.chunk, g.n_rels);
+    const float* __restrict__ xq = g.x + q * 4;
+    const int32_t* __restrict__ colp = g.col;
+    const float* __restrict__ valp = g.val;
+
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int kb = k0; kb < k1; kb += 64) {
+        const int nk = min(64, k1 - kb);
+        int beg_l = 0, end_l = 0, rel_l = kb + lane;
+        if (lane < nk) {
+            const int32_t* rp = g.rowptr + (int64_t)(kb + lane) * g.rowptr_rel_stride + r;
+            beg_l = rp[0];
+            end_l = rp[1];
+            if (g.rel_map) rel_l = g.rel_map[kb + lane];
+        }
+#pragma unroll 1
+        for (int t = 0; t < nk; ++t) {
+            const int beg = __builtin_amdgcn_readlane(beg_l, t);
+            const int end = __builtin_amdgcn_readlane(end_l, t);
+            const int rel = __builtin_amdgcn_readlane(rel_l, t);
+            const float* __restrict__ X = xq + (int64_t)rel * g.x_rel_stride;
+#pragma unroll 1
+            for (int base = beg; base < end; base += 64) {
+                const int n = min(64, end - base);
+                int cl = 0;
+                float vl = 0.f;
+                if (lane < n) {
+                    cl = colp[base + lane];
+                    vl = valp[base + lane];
+                }
+                // Four steps per trip: all bpermutes, then all gathers, then the FMAs,
+                // so four 16-byte gathers per lane are in flight at once.
+                for (int s0 = 0; s0 < n; s0 += 4 * G) {
+                    int cc[4];
+                    float vv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int src = (s0 + u * G + sub) & 63;
+                        cc[u] = __shfl(cl, src);
+                        vv[u] = __shfl(vl, src);
+                    }
+                    float4 xv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool ok = qact && (s0 + u * G + sub) < n;
+                        xv[u] = ok ? *reinterpret_cast<const float4*>(X + (int64_t)cc[u] * g.x_ld)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (!ok) vv[u] = 0.f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) dg::fma4(acc, vv[u], xv[u]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+    if (sub == 0 && qact) {
+        float* o = g.out + ((int64_t)c * g.n_rows + r) * d + q * 4;
+        *reinterpret_cast<float4*>(o) = acc;
+    }
+}
+
+struct EpiGroupK {
+    const float* partial;
+    int32_t n_chunks;
+    int32_t pad;
+};
+
+struct EpiArgs {
+    EpiGroupK g[DG_MAX_GROUPS];
+    float* out;
+    int32_t n_groups;
+    int32_t n_rows;
+    int32_t d;
+    int32_t flags;
+};
+
+template <int LP>
+__global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
+    constexpr int G = dg::kWave / LP;  // rows per wave
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane / LP;
+    const int q = lane % LP;
+    const int r = (blockIdx.x * 4 + wave) * G + sub;
+    const int d = a.d;
+    const bool active = r < a.n_rows && q * 4 < d;
+    const int64_t plane = (int64_t)a.n_rows * d;
+    const int64_t off = (int64_t)r * d + q * 4;
+
+    float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int gi = 0; gi < a.n_groups; ++gi) {
+        const float* __restrict__ p = a.g[gi].partial + off;
+        const int nc = a.g[gi].n_chunks;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (active) {
+#pragma unroll 1
+            for (int c = 0; c < nc; ++c) {
+                float4 v = *reinterpret_cast<const float4*>(p + c * plane);
+                if (a.flags & DG_EPI_CHUNK_RELU) {
+                    v.x = fmaxf(v.x, 0.f);
+                    v.y = fmaxf(v.y, 0.f);
+                    v.z = fmaxf(v.z, 0.f);
+                    v.w = fmaxf(v.w, 0.f);
+                }
+                dg::add4(s, v);
+            }
+        }
+        if (a.flags & DG_EPI_L2NORM) {
+            // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); all-zero rows stay zero.
+            float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
+#pragma unroll
+            for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
+            const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+            s.x *= inv;
+            s.y *= inv;
+            s.z *= inv;
+            s.w *= inv;
+        }
+        dg::add4(tot, s);
+    }
+    if (a.flags & DG_EPI_RELU) {
+        tot.x = fmaxf(tot.x, 0.f);
+        tot.y = fmaxf(tot.y, 0.f);
+        tot.z = fmaxf(tot.z, 0.f);
+        tot.w = fmaxf(tot.w, 0.f);
+    }
+    if (active) *reinterpret_cast<float4*>(a.out + off) = tot;
+}
+
+#define DG_LP_SWITCH(LPV, CALL)                     \
+    switch (LPV) {                                  \
+        case 1: CALL(1); break;                     \
+        case 2: CALL(2); break;                     \
+        case 4: CALL(4); break;                     \
+        case 8: CALL(8); break;                     \
+        case 16: CALL(16); break;                   \
+        case 32: CALL(32); break;                   \
+        case 64: CALL(64); break;                   \
+        default: return DG_EINVAL;                  \
+    }
+
+}  // namespace
+
+extern "C" int32_t dg_abi_version(void) { return 2; }
+
+extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, int32_t d,
+                                  void* stream) {
+    if (n_groups < 0 || (n_groups > 0 && groups == nullptr)) return DG_EINVAL;
+    if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
+    if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
+    SpmmArgs args{};
+    args.d = d;
+    int64_t blocks = 0;
+    int ng = 0;
+    for (int i = 0; i < n_groups; ++i) {
+        const dg_rel_group& s = groups[i];
+        if (s.n_rows < 0 || s.n_rels < 0 || s.chunk < 1 || s.rowptr_rel_stride < 0)
+            return DG_EINVAL;
+        if (s.n_rows == 0 || s.n_rels == 0) continue;
+        if (!s.rowptr || !s.col || !s.val || !s.x || !s.out) return DG_EINVAL;
+        if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || (s.x_ld & 3) || (s.x_rel_stride & 3))
+            return DG_EALIGN;
+        if (s.x_ld < d) return DG_EINVAL;
+        SpmmGroupK& k = args.g[ng++];
+        k.rowptr = s.rowptr;
+        k.col = s.col;
+        k.val = s.val;
+        k.x = s.x;
+        k.out = s.out;
+        k.rel_map = s.rel_map;
+        k.x_rel_stride = s.x_rel_stride;
+        k.x_ld = s.x_ld;
+        k.rowptr_rel_stride = s.rowptr_rel_stride;
+        k.n_rows = s.n_rows;
+        k.n_rels = s.n_rels;
+        k.chunk = s.chunk;
+        k.n_chunks = dg::ceil_div(s.n_rels, s.chunk);
+        k.row_blocks = dg::ceil_div(s.n_rows, kRowsPerBlock);
+        const int64_t items = (int64_t)k.n_chunks * k.row_blocks;
+        k.n_blocks = static_cast<int32_t>(8 * ((items + 7) / 8));
+        k.block_begin = static_cast<int32_t>(blocks);
+        blocks += k.n_blocks;
+        if (blocks > 0x7fffffff) return DG_EINVAL;
+    }
+    args.n_groups = ng;
+    if (blocks == 0) return DG_OK;
+    const int lp = dg::lanes_per_row(d);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(blocks)), block(256);
+#define DG_LAUNCH_SPMM(L) hipLaunchKernelGGL(spmm_groups_kernel<L>, grid, block, 0, st, args)
+    DG_LP_SWITCH(lp, DG_LAUNCH_SPMM)
+#undef DG_LAUNCH_SPMM
+    return dg::launch_status();
+}
+
+extern "C" int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                               int32_t n_rows, const float* x, int64_t ldx, float* y,
+                               int64_t ldy, int32_t d, void* stream) {
+    if (ldy != d) return DG_EINVAL;
+    dg_rel_group g{};
+    g.rowptr = rowptr;
+    g.col = col;
+    g.val = val;
+    g.x = x;
+    g.out = y;
+    g.x_rel_stride = 0;
+    g.x_ld = ldx;
+    g.rowptr_rel_stride = 0;
+    g.n_rows = n_rows;
+    g.n_rels = 1;
+    g.chunk = 1;
+    return dg_spmm_groups_f32(&g, 1, d, stream);
+}
+
+extern "C" int dg_gcn_epilogue_f32(const dg_epi_group* groups, int32_t n_groups, float* out,
+                                   int32_t n_rows, int32_t d, int32_t flags, void* stream) {
+    if (n_groups < 1 || groups == nullptr) return DG_EINVAL;
+    if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
+    if (d < 4 || d > 256 || (d & 3) || n_rows < 0) return DG_EINVAL;
+    if (flags & ~(DG_EPI_L2NORM | DG_EPI_RELU | DG_EPI_CHUNK_RELU)) return DG_EINVAL;
+    if (n_rows == 0) return DG_OK;
+    if (!out || !dg::aligned16(out)) return out ? DG_EALIGN : DG_EINVAL;
+    EpiArgs a{};
+    for (int i = 0; i < n_groups; ++i) {
+        if (!groups[i].partial || groups[i].n_chunks < 1) return DG_EINVAL;
+        if (!dg::aligned16(groups[i].partial)) return DG_EALIGN;
+        a.g[i].partial = groups[i].partial;
+        a.g[i].n_chunks = groups[i].n_chunks;
+    }
+    a.out = out;
+    a.n_groups = n_groups;
+    a.n_rows = n_rows;
+    a.d = d;
+    a.flags = flags;
+    const int lp = dg::lanes_per_row(d);
+    const int rows_per_block = 4 * (dg::kWave / lp);
+    dim3 grid(dg::ceil_div(n_rows, rows_per_block)), block(256);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define DG_LAUNCH_EPI(L) hipLaunchKernelGGL(epilogue_kernel<L>, grid, block, 0, st, a)
+    DG_LP_SWITCH(lp, DG_LAUNCH_EPI)
+#undef DG_LAUNCH_EPI
+    return dg::launch_status();
+}

@@ -1,0 +1,322 @@
+"""Typed Python entry points over the C ABI (include/decagon_hip.h).
+
+Every wrapper checks on the host, before launching, that the device buffers are large
+enough for the indices the kernel will form (a bad shape must fail here, never fault on the
+GPU), then launches on the current torch stream.  Launches are asynchronous and
+graph-capturable; no wrapper synchronises.
+
+The `Prepared*` classes hold the ctypes argument blocks of a fixed launch so that the hot
+loop (engine.py) pays one ctypes call per kernel and nothing else.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import DgEpiGroup, DgGemmDesc, DgRelGroup, check
+
+
+def _stream_ptr(stream: Optional[torch.cuda.Stream] = None) -> int:
+    s = torch.cuda.current_stream() if stream is None else stream
+    return s.cuda_stream
+
+
+def _dev(t: torch.Tensor, dtype: torch.dtype, what: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{what}: expected a torch.Tensor, got {type(t).__name__}")
+    if not t.is_cuda:
+        raise ValueError(f"{what}: must be a device (HIP) tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{what}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: must be contiguous")
+    return t
+
+
+# --------------------------------------------------------------------------------------
+# SpMM over relation groups
+# --------------------------------------------------------------------------------------
+@dataclass
+class RelGroupSpec:
+    """One (i,j) group (or any set of relations sharing n_rows) for dg_spmm_groups_f32."""
+
+    rowptr: torch.Tensor          # int32
+    col: torch.Tensor             # int32
+    val: torch.Tensor             # float32
+    x: torch.Tensor               # float32, dense operand storage
+    out: torch.Tensor             # float32, [n_chunks, n_rows, d]
+    n_rows: int
+    n_cols: int
+    n_rels: int
+    chunk: int
+    x_rel_stride: int
+    x_ld: int
+    rowptr_rel_stride: int
+    x_offset: int = 0             # element offset of X_0 inside x
+    rel_map: Optional[torch.Tensor] = None   # int32 [n_rels]: X_k = X_{rel_map[k]}
+    x_rels: Optional[int] = None  # relation slabs addressable in x (default n_rels)
+    rel_map_max: Optional[int] = None  # host-known max(rel_map), checked against x_rels
+
+    @property
+    def n_chunks(self) -> int:
+        return -(-self.n_rels // self.chunk)
+
+    def validate(self, d: int) -> None:
+        _dev(self.rowptr, torch.int32, "rowptr")
+        _dev(self.col, torch.int32, "col")
+        _dev(self.val, torch.float32, "val")
+        _dev(self.x, torch.float32, "x")
+        _dev(self.out, torch.float32, "out")
+        if self.n_rows == 0 or self.n_rels == 0:
+            return
+        if self.chunk < 1:
+            raise ValueError("chunk must be >= 1")
+        need_rp = (self.n_rels - 1) * self.rowptr_rel_stride + self.n_rows + 1
+        if self.rowptr.numel() < need_rp:
+            raise ValueError(f"rowptr has {self.rowptr.numel()} entries, kernel reads {need_rp}")
+        if self.col.numel() != self.val.numel():
+            raise ValueError("col/val length mismatch")
+        x_rels = self.n_rels if self.x_rels is None else self.x_rels
+        if self.rel_map is not None:
+            _dev(self.rel_map, torch.int32, "rel_map")
+            if self.rel_map.numel() < self.n_rels:
+                raise ValueError("rel_map shorter than n_rels")
+            if self.rel_map_max is None or not (0 <= self.rel_map_max < x_rels):
+                raise ValueError("rel_map_max must be given and index inside x")
+        elif x_rels < self.n_rels:
+            raise ValueError("x holds fewer relation slabs than n_rels")
+        need_x = self.x_offset + (x_rels - 1) * self.x_rel_stride + (self.n_cols - 1) * self.x_ld + d
+        if self.n_cols > 0 and self.x.numel() < need_x:
+            raise ValueError(f"x has {self.x.numel()} elements, kernel may read {need_x}")
+        if self.x_ld < d:
+            raise ValueError("x_ld < d")
+        if self.out.numel() < self.n_chunks * self.n_rows * d:
+            raise ValueError("out too small for [n_chunks, n_rows, d]")
+
+
+class PreparedSpmm:
+    """A fixed dg_spmm_groups_f32 launch (descriptor block built once)."""
+
+    def __init__(self, specs: Sequence[RelGroupSpec], d: int):
+        if len(specs) > _lib.DG_MAX_GROUPS:
+            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups per launch")
+        for s in specs:
+            s.validate(d)
+        self.specs = list(specs)  # keep tensors alive
+        self.d = d
+        arr = (DgRelGroup * max(1, len(specs)))()
+        for i, s in enumerate(specs):
+            g = arr[i]
+            g.rowptr = s.rowptr.data_ptr()
+            g.col = s.col.data_ptr()
+            g.val = s.val.data_ptr()
+            g.x = s.x.data_ptr() + 4 * s.x_offset
+            g.out = s.out.data_ptr()
+            g.rel_map = s.rel_map.data_ptr() if s.rel_map is not None else None
+            g.x_rel_stride = s.x_rel_stride
+            g.x_ld = s.x_ld
+            g.rowptr_rel_stride = s.rowptr_rel_stride
+            g.n_rows = s.n_rows
+            g.n_rels = s.n_rels
+            g.chunk = s.chunk
+        self._arr = arr
+        self._n = len(specs)
+        self._fn = _lib.load().dg_spmm_groups_f32
+
+    def __call__(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_groups_f32")
+
+
+def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:
+    PreparedSpmm(specs, d)(stream)
+
+
+def spmm_csr(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x: torch.Tensor,
+             n_rows: int, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """Y = A·X for one CSR relation (tf.sparse_tensor_dense_matmul, layers.py:90)."""
+    if x.dim() != 2:
+        raise ValueError("x must be 2-D")
+    n_cols, d = x.shape
+    if out is None:
+        out = torch.empty((n_rows, d), device=x.device, dtype=torch.float32)
+    spec = RelGroupSpec(rowptr, col, val, x.contiguous(), out, n_rows, n_cols, 1, 1, 0, d, 0)
+    PreparedSpmm([spec], d)(stream)
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# Epilogue
+# --------------------------------------------------------------------------------------
+class PreparedEpilogue:
+    def __init__(self, partials: Sequence[Tuple[torch.Tensor, int]], out: torch.Tensor, n_rows: int,
+                 d: int, flags: int):
+        if not partials:
+            raise ValueError("at least one group")
+        if len(partials) > _lib.DG_MAX_GROUPS:
+            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups")
+        _dev(out, torch.float32, "out")
+        if out.numel() < n_rows * d:
+            raise ValueError("out too small")
+        arr = (DgEpiGroup * len(partials))()
+        for i, (p, nc) in enumerate(partials):
+            _dev(p, torch.float32, "partial")
+            if p.numel() < nc * n_rows * d:
+                raise ValueError("partial too small for [n_chunks, n_rows, d]")
+            arr[i].partial = p.data_ptr()
+            arr[i].n_chunks = nc
+        self._keep = [p for p, _ in partials] + [out]
+        self._arr = arr
+        self._args = (len(partials), out.data_ptr(), n_rows, d, flags)
+        self._fn = _lib.load().dg_gcn_epilogue_f32
+
+    def __call__(self, stream=None) -> None:
+        n, o, r, d, f = self._args
+        check(self._fn(self._arr, n, o, r, d, f, _stream_ptr(stream)), "dg_gcn_epilogue_f32")
+
+
+def gcn_epilogue(partials, out, n_rows, d, flags, stream=None) -> None:
+    PreparedEpilogue(partials, out, n_rows, d, flags)(stream)
+
+
+# --------------------------------------------------------------------------------------
+# GEMM
+# --------------------------------------------------------------------------------------
+class PreparedGemm:
+    """C_b = diag(sc)·((A_b·diag(sa))·B_b) on the fp32 MFMA, batched and strided.
+
+    a, b, c are given as (tensor, (bs, s0, s1)) with element strides; sizes m, n, k, batch.
+    """
+
+    def __init__(self, a: torch.Tensor, a_strides, b: torch.Tensor, b_strides, c: torch.Tensor,
+                 c_strides, m: int, n: int, k: int, batch: int = 1,
+                 sa: Optional[torch.Tensor] = None, sc: Optional[torch.Tensor] = None,
+                 b_map: Optional[torch.Tensor] = None, b_batches: Optional[int] = None,
+                 b_map_max: Optional[int] = None):
+        for t, nm in ((a, "a"), (b, "b"), (c, "c")):
+            if not (t.is_cuda and t.dtype == torch.float32):
+                raise ValueError(f"{nm}: float32 device tensor required")
+
+        def span(strides, d0, d1, nb=batch):
+            bs, s0, s1 = strides
+            return (nb - 1) * bs + (d0 - 1) * s0 + (d1 - 1) * s1 + 1
+
+        nb_b = batch
+        if b_map is not None:
+            _dev(b_map, torch.int32, "b_map")
+            nb_b = batch if b_batches is None else b_batches
+            if b_map.numel() < batch or b_map_max is None or not (0 <= b_map_max < nb_b):
+                raise ValueError("b_map must cover the batch and index inside b")
+        if m and n and k and batch:
+            if a.numel() < span(a_strides, m, k) or b.numel() < span(b_strides, k, n, nb_b):
+                raise ValueError("gemm operand too small for its strides")
+        if m and n and batch and c.numel() < span(c_strides, m, n):
+            raise ValueError("gemm output too small for its strides")
+        if sa is not None and (sa.numel() < k or sa.dtype != torch.float32 or not sa.is_cuda):
+            raise ValueError("sa must be a float32 device vector of length k")
+        if sc is not None and (sc.numel() < n or sc.dtype != torch.float32 or not sc.is_cuda):
+            raise ValueError("sc must be a float32 device vector of length n")
+        desc = DgGemmDesc()
+        desc.a, desc.b, desc.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
+        desc.sa = sa.data_ptr() if sa is not None else None
+        desc.sc = sc.data_ptr() if sc is not None else None
+        desc.b_map = b_map.data_ptr() if b_map is not None else None
+        desc.a_bs, desc.a_sm, desc.a_sk = a_strides
+        desc.b_bs, desc.b_sk, desc.b_sn = b_strides
+        desc.c_bs, desc.c_sm, desc.c_sn = c_strides
+        desc.m, desc.n, desc.k, desc.batch = m, n, k, batch
+        self._desc = desc
+        self._keep = (a, b, c, sa, sc, b_map)
+        self._fn = _lib.load().dg_gemm_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(ctypes.byref(self._desc), _stream_ptr(stream)), "dg_gemm_f32")
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+           sa: Optional[torch.Tensor] = None, sc: Optional[torch.Tensor] = None, stream=None):
+    """out = diag-scaled a @ b for 2-D fp32 device tensors (any strides)."""
+    m, k = a.shape
+    k2, n = b.shape
+    if k != k2:
+        raise ValueError("inner dimensions differ")
+    if out is None:
+        out = torch.empty((m, n), device=a.device, dtype=torch.float32)
+    PreparedGemm(a, (0, a.stride(0), a.stride(1)), b, (0, b.stride(0), b.stride(1)), out,
+                 (0, out.stride(0), out.stride(1)), m, n, k, 1, sa, sc)(stream)
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# Decoder, losses, sampler
+# --------------------------------------------------------------------------------------
+def decoder_score(row_table: torch.Tensor, col_table: torch.Tensor, row_idx: torch.Tensor,
+                  col_idx: torch.Tensor, G: torch.Tensor, l: Optional[torch.Tensor],
+                  out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """out[p] = row_table[row_idx[p]]ᵀ · L · G · L · col_table[col_idx[p]]."""
+    _dev(row_table, torch.float32, "row_table")
+    _dev(col_table, torch.float32, "col_table")
+    _dev(row_idx, torch.int32, "row_idx")
+    _dev(col_idx, torch.int32, "col_idx")
+    _dev(G, torch.float32, "G")
+    d = G.shape[0]
+    if G.shape != (d, d) or row_table.shape[1] != d or col_table.shape[1] != d:
+        raise ValueError("decoder: d mismatch")
+    n = row_idx.numel()
+    if col_idx.numel() != n:
+        raise ValueError("row_idx / col_idx length mismatch")
+    if l is not None:
+        _dev(l, torch.float32, "l")
+        if l.numel() != d:
+            raise ValueError("l must have d entries")
+    if out is None:
+        out = torch.empty(n, device=G.device, dtype=torch.float32)
+    fn = _lib.load().dg_decoder_score_f32
+    check(fn(row_table.data_ptr(), row_table.shape[1], col_table.data_ptr(), col_table.shape[1],
+             row_idx.data_ptr(), col_idx.data_ptr(), n, G.data_ptr(),
+             l.data_ptr() if l is not None else None, d, out.data_ptr(), _stream_ptr(stream)),
+          "dg_decoder_score_f32")
+    return out
+
+
+def hinge_loss(pos: torch.Tensor, neg: torch.Tensor, margin: float,
+               out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    _dev(pos, torch.float32, "pos")
+    _dev(neg, torch.float32, "neg")
+    if pos.numel() != neg.numel():
+        raise ValueError("pos/neg length mismatch")
+    if out is None:
+        out = torch.empty(1, device=pos.device, dtype=torch.float32)
+    check(_lib.load().dg_hinge_loss_f32(pos.data_ptr(), neg.data_ptr(), pos.numel(), float(margin),
+                                         out.data_ptr(), _stream_ptr(stream)), "dg_hinge_loss_f32")
+    return out
+
+
+def xent_loss(pos: torch.Tensor, neg: torch.Tensor, neg_weight: float,
+              out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    _dev(pos, torch.float32, "pos")
+    _dev(neg, torch.float32, "neg")
+    if pos.numel() != neg.numel():
+        raise ValueError("pos/neg length mismatch")
+    if out is None:
+        out = torch.empty(1, device=pos.device, dtype=torch.float32)
+    check(_lib.load().dg_xent_loss_f32(pos.data_ptr(), neg.data_ptr(), pos.numel(), float(neg_weight),
+                                        out.data_ptr(), _stream_ptr(stream)), "dg_xent_loss_f32")
+    return out
+
+
+def unigram_sample(cdf: torch.Tensor, n: int, seed: int, offset: int,
+                   out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    _dev(cdf, torch.float32, "cdf")
+    if out is None:
+        out = torch.empty(n, device=cdf.device, dtype=torch.int32)
+    _dev(out, torch.int32, "out")
+    if out.numel() < n:
+        raise ValueError("out too small")
+    check(_lib.load().dg_unigram_sample(cdf.data_ptr(), cdf.numel(), n, seed & (2**64 - 1),
+                                         offset & (2**64 - 1), out.data_ptr(), _stream_ptr(stream)),
+          "dg_unigram_sample")
+    return out

@@ -1,0 +1,266 @@
+"""Layer classes with the reference's constructor signatures and variable layout
+(decagon/deep/layers.py:12-213).
+
+In the reference each layer's `_call` emits one TF op per relation.  Here a layer owns its
+weights as one device stack [K, d_in, d_out] (the per-relation `vars['weights_%d']` are
+views of it), and `DecagonModel` runs all layers of a model through the fused plan in
+engine.py.  Calling a layer on its own (`layer(inputs)`) still works and returns a lazily
+evaluated node that runs the same HIP kernels for that one edge type.
+
+Activations are classified by probing (`act_kind`): identity (`lambda x: x`, what
+DecagonModel passes, model.py:71/83/99/...) and relu are supported on the device path.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import inits, kernels, runtime
+from ._lib import DG_EPI_CHUNK_RELU, DG_EPI_L2NORM
+from .graph import InvalidArgumentError, Node, Variable
+
+# global unique layer ID dictionary for layer name assignment (layers.py:9-20)
+_LAYER_UIDS: Dict[str, int] = {}
+
+
+def get_layer_uid(layer_name: str = "") -> int:
+    _LAYER_UIDS[layer_name] = _LAYER_UIDS.get(layer_name, 0) + 1
+    return _LAYER_UIDS[layer_name]
+
+
+def relu(x):
+    """tf.nn.relu on torch / numpy values (an activation marker the kernels recognise)."""
+    if isinstance(x, torch.Tensor):
+        return torch.clamp_min(x, 0)
+    return np.maximum(x, 0)
+
+
+def sigmoid(x):
+    if isinstance(x, torch.Tensor):
+        return torch.sigmoid(x)
+    return 1.0 / (1.0 + np.exp(-np.asarray(x)))
+
+
+def act_kind(act) -> str:
+    """'identity' | 'relu' | 'sigmoid' for a callable activation, by probing it."""
+    probe = torch.tensor([-1.5, 0.0, 2.0])
+    try:
+        out = act(probe)
+    except Exception as e:  # pragma: no cover - exotic activations
+        raise ValueError(f"unsupported activation {act!r}: {e}") from e
+    if out is probe:
+        return "identity"
+    out = torch.as_tensor(out, dtype=torch.float32)
+    if torch.equal(out, probe):
+        return "identity"
+    if torch.equal(out, torch.tensor([0.0, 0.0, 2.0])):
+        return "relu"
+    if torch.allclose(out, torch.sigmoid(probe)):
+        return "sigmoid"
+    raise ValueError(f"unsupported activation {act!r} (identity, relu or sigmoid)")
+
+
+def dropout_sparse(x, keep_prob, num_nonzero_elems):
+    """layers.py:23-31.  keep_prob == 1 (dropout 0, the only forward with defined parity)
+    is the identity; stochastic dropout belongs to the training path."""
+    if float(keep_prob) != 1.0:
+        raise NotImplementedError("sparse dropout with keep_prob < 1 is not on the HIP path yet")
+    return x
+
+
+class MultiLayer:
+    """Base layer (layers.py:34-67): name assignment, kwargs check, `vars` dict."""
+
+    def __init__(self, edge_type=(), num_types=-1, **kwargs):
+        self.edge_type = edge_type
+        self.num_types = num_types
+        allowed_kwargs = {"name", "logging"}
+        for kwarg in kwargs.keys():
+            assert kwarg in allowed_kwargs, "Invalid keyword argument: " + kwarg
+        name = kwargs.get("name")
+        if not name:
+            layer = self.__class__.__name__.lower()
+            name = layer + "_" + str(get_layer_uid(layer))
+        self.name = name
+        self.vars: Dict[str, Variable] = {}
+        self.logging = kwargs.get("logging", False)
+        self.issparse = False
+
+    def _scope(self) -> str:
+        return runtime.scoped(f"{self.name}_vars")
+
+    def _call(self, inputs):
+        return inputs
+
+    def __call__(self, inputs):
+        return self._call(inputs)
+
+
+def _glorot_stack(k: int, d_in: int, d_out: int) -> torch.Tensor:
+    arr = np.stack([inits.glorot_array(d_in, d_out) for _ in range(k)]) if k else \
+        np.zeros((0, d_in, d_out), np.float32)
+    return torch.from_numpy(arr).to(runtime.param_device())
+
+
+def _check_dropout(ctx, dropout) -> None:
+    v = ctx.value(dropout) if isinstance(dropout, Node) else dropout
+    if float(v) != 0.0:
+        raise NotImplementedError(
+            "dropout > 0 is the training path (SURVEY §8f); the forward parity path runs at 0")
+
+
+class _GraphConvBase(MultiLayer):
+    def _make_weights(self, d_in: int, d_out: int) -> None:
+        self.weights_stack = _glorot_stack(self.num_types, d_in, d_out)
+        scope = self._scope()
+        for k in range(self.num_types):
+            self.vars["weights_%d" % k] = Variable(self.weights_stack[k], f"{scope}/weights_{k}:0")
+
+    def _adj_group(self, ctx):
+        """Upload (cached) this layer's adjacency feeds as one device group."""
+        nodes = self.adj_mats[self.edge_type]
+        return runtime.device_group(ctx, nodes)
+
+
+class GraphConvolutionSparseMulti(_GraphConvBase):
+    """Graph convolution on sparse features (layers.py:70-94):
+    l2norm_rows( Σ_k act(Â_k · (X_j · W_k)) )."""
+
+    def __init__(self, input_dim, output_dim, adj_mats, nonzero_feat, dropout=0., act=relu, **kwargs):
+        super().__init__(**kwargs)
+        self.dropout = dropout
+        self.adj_mats = adj_mats
+        self.act = act
+        self.issparse = True
+        self.nonzero_feat = nonzero_feat
+        self.input_dim = input_dim
+        self.output_dim = output_dim
+        self._make_weights(input_dim[self.edge_type[1]], output_dim)
+
+    def _call(self, inputs):
+        kind = act_kind(self.act)
+        if kind == "sigmoid":
+            raise NotImplementedError("sigmoid activation inside a GCN layer is not on the HIP path")
+
+        def fn(ctx):
+            _check_dropout(ctx, self.dropout)
+            grp = self._adj_group(ctx)
+            feat = runtime.feature_csr(ctx, inputs)
+            return runtime.gcn_layer(grp, self.weights_stack, feat, self.output_dim, kind == "relu")
+
+        return Node(f"{self.name}/out", fn)
+
+
+class GraphConvolutionMulti(_GraphConvBase):
+    """Graph convolution on dense inputs (layers.py:97-118):
+    l2norm_rows( Σ_k act(Â_k · (H_j · W_k)) )."""
+
+    def __init__(self, input_dim, output_dim, adj_mats, dropout=0., act=relu, **kwargs):
+        super().__init__(**kwargs)
+        self.adj_mats = adj_mats
+        self.dropout = dropout
+        self.act = act
+        self.input_dim = input_dim
+        self.output_dim = output_dim
+        self._make_weights(input_dim, output_dim)
+
+    def _call(self, inputs):
+        kind = act_kind(self.act)
+        if kind == "sigmoid":
+            raise NotImplementedError("sigmoid activation inside a GCN layer is not on the HIP path")
+
+        def fn(ctx):
+            _check_dropout(ctx, self.dropout)
+            grp = self._adj_group(ctx)
+            h = ctx.value(inputs)
+            h = runtime.as_device_f32(h)
+            return runtime.gcn_layer_dense(grp, self.weights_stack, h, self.output_dim, kind == "relu")
+
+        return Node(f"{self.name}/out", fn)
+
+
+class _DecoderBase(MultiLayer):
+    """Decoders own parameters; DecagonModel reads them into latent_inters/latent_varies
+    (model.py:116-137).  `_call` (dead code in the reference, §0.4 of SURVEY) is provided:
+    it returns per-relation full score matrices act(row·L·G·L·colᵀ)."""
+
+    def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
+        super().__init__(**kwargs)
+        self.dropout = dropout
+        self.act = act
+        self.input_dim = input_dim
+
+    def _var(self, name: str, arr: np.ndarray) -> Variable:
+        t = torch.from_numpy(np.ascontiguousarray(arr, np.float32)).to(runtime.param_device())
+        v = Variable(t, f"{self._scope()}/{name}:0")
+        self.vars[name] = v
+        return v
+
+    def latent(self, k: int):
+        """(G kind, G variable or None, L kind, L variable or None) for relation k."""
+        raise NotImplementedError
+
+    def _call(self, inputs):
+        i, j = self.edge_type
+        kind = act_kind(self.act)
+        outs = []
+        for k in range(self.num_types):
+            def fn(ctx, k=k):
+                _check_dropout(ctx, self.dropout)
+                rows = runtime.as_device_f32(ctx.value(inputs[i]))
+                cols = runtime.as_device_f32(ctx.value(inputs[j]))
+                G, l = runtime.latent_operands(ctx, *self.latent(k), d=self.input_dim)
+                rec = runtime.full_scores(rows, cols, G, l)
+                if kind == "sigmoid":
+                    rec = runtime.sigmoid_(rec)
+                elif kind == "relu":
+                    rec.clamp_min_(0)
+                return rec
+            outs.append(Node(f"{self.name}/rec_{k}", fn))
+        return outs
+
+
+class DEDICOMDecoder(_DecoderBase):
+    """layers.py:121-147: global R (d×d) + per-relation diagonal D_k."""
+
+    def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
+        super().__init__(input_dim, dropout, act, **kwargs)
+        self._var("global_interaction", inits.glorot_array(input_dim, input_dim))
+        for k in range(self.num_types):
+            self._var("local_variation_%d" % k, inits.glorot_array(input_dim, 1).reshape(-1))
+
+    def latent(self, k):
+        return "dense", self.vars["global_interaction"], "diag", self.vars["local_variation_%d" % k]
+
+
+class DistMultDecoder(_DecoderBase):
+    """layers.py:150-172: G = diag(r_k), L = I."""
+
+    def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
+        super().__init__(input_dim, dropout, act, **kwargs)
+        for k in range(self.num_types):
+            self._var("relation_%d" % k, inits.glorot_array(input_dim, 1).reshape(-1))
+
+    def latent(self, k):
+        return "diag", self.vars["relation_%d" % k], "eye", None
+
+
+class BilinearDecoder(_DecoderBase):
+    """layers.py:175-195: G = M_k (d×d), L = I."""
+
+    def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
+        super().__init__(input_dim, dropout, act, **kwargs)
+        for k in range(self.num_types):
+            self._var("relation_%d" % k, inits.glorot_array(input_dim, input_dim))
+
+    def latent(self, k):
+        return "dense", self.vars["relation_%d" % k], "eye", None
+
+
+class InnerProductDecoder(_DecoderBase):
+    """layers.py:198-213: G = I, L = I (no parameters)."""
+
+    def latent(self, k):
+        return "eye", None, "eye", None

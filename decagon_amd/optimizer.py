@@ -1,0 +1,206 @@
+"""DecagonOptimizer with the reference's constructor and attributes
+(decagon/deep/optimizer.py:8-160).
+
+Scores: the reference forms the B×B product row·L·G·L·colᵀ and keeps its diagonal
+(optimizer.py:51-57, :63-85); here `outputs` / `neg_outputs` come from
+dg_decoder_score_f32, which computes exactly the diagonal.  `preds` / `neg_preds` (the
+full B×B matrices) and `predictions` (E_i·L·G·L·E_jᵀ, :87-106) are fp32-MFMA GEMMs.
+Negatives are drawn on the device from the same distortion-0.75 unigram distribution as
+tf.nn.fixed_unigram_candidate_sampler (:37-49); feeding `opt.neg_samples` injects them
+(TF semantics: any tensor may be fed), which is how parity tests pin them.
+
+`opt_op` (backward + Adam, :108-114) is the next row of SURVEY §8f: fetching it raises.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import kernels, runtime
+from .flags import FLAGS
+from .graph import InvalidArgumentError, Node, Operation, RunContext
+
+
+class _Sampler:
+    """Per-relation device CDFs of degree^0.75 (built once per session)."""
+
+    def __init__(self, degrees_list, device):
+        self.cdfs = []
+        for deg in degrees_list:
+            w = np.power(np.asarray(deg, np.float64), 0.75)
+            cdf = np.cumsum(w).astype(np.float32)
+            if cdf.size == 0 or cdf[-1] <= 0:
+                raise ValueError("unigram sampler needs a positive total degree")
+            self.cdfs.append(torch.from_numpy(cdf).to(device))
+        self.counter = 0
+
+
+class DecagonOptimizer:
+    def __init__(self, embeddings, latent_inters, latent_varies, degrees, edge_types,
+                 edge_type2dim, placeholders, margin=0.1, neg_sample_weights=1., batch_size=100):
+        self.embeddings = embeddings
+        self.latent_inters = latent_inters
+        self.latent_varies = latent_varies
+        self.edge_types = edge_types
+        self.degrees = degrees
+        self.edge_type2dim = edge_type2dim
+        self.obj_type2n = {i: self.edge_type2dim[i, j][0][0] for i, j in self.edge_types}
+        self.margin = margin
+        self.neg_sample_weights = neg_sample_weights
+        self.batch_size = batch_size
+        self.seed = 0
+
+        self.placeholders = placeholders
+        self.inputs = placeholders["batch"]
+        self.batch_edge_type_idx = placeholders["batch_edge_type_idx"]
+        self.batch_row_edge_type = placeholders["batch_row_edge_type"]
+        self.batch_col_edge_type = placeholders["batch_col_edge_type"]
+
+        # flat relation index r -> (i, j, k), in edge-type order (minibatch.py:45-54)
+        self._rel_degrees = []
+        self._rel_of = []
+        for i, j in self.edge_types:
+            for k in range(self.edge_types[i, j]):
+                self._rel_of.append((i, j, k))
+                self._rel_degrees.append(self.degrees[i][k])
+
+        self.row_inputs = Node("optimizer/row_inputs", lambda ctx: self._batch(ctx)[:, 0])
+        self.col_inputs = Node("optimizer/col_inputs", lambda ctx: self._batch(ctx)[:, 1])
+        obj_type_n = [self.obj_type2n[i] for i in range(len(self.embeddings))]
+        self.obj_type_lookup_start = np.cumsum([0] + obj_type_n[:-1])
+        self.obj_type_lookup_end = np.cumsum(obj_type_n)
+
+        self.neg_samples = Node("optimizer/neg_samples", self._sample_negatives)
+        self.outputs = Node("optimizer/outputs", lambda ctx: self._scores(ctx, self.row_inputs))
+        self.neg_outputs = Node("optimizer/neg_outputs", lambda ctx: self._scores(ctx, self.neg_samples))
+        self.preds = Node("optimizer/preds", lambda ctx: self._full(ctx, self.row_inputs))
+        self.neg_preds = Node("optimizer/neg_preds", lambda ctx: self._full(ctx, self.neg_samples))
+        self.predict()
+        self._build()
+
+    # ------------------------------------------------------------------ graph pieces
+    def _batch(self, ctx: RunContext) -> np.ndarray:
+        b = np.asarray(ctx.value(self.inputs))
+        if b.ndim != 2 or b.shape[1] != 2:
+            raise InvalidArgumentError(f"batch must be [B, 2], got {b.shape}")
+        return b.astype(np.int32, copy=False)
+
+    def _edge(self, ctx):
+        e = int(np.asarray(ctx.value(self.batch_edge_type_idx)))
+        rt = int(np.asarray(ctx.value(self.batch_row_edge_type)))
+        ct = int(np.asarray(ctx.value(self.batch_col_edge_type)))
+        if not 0 <= e < len(self._rel_of):
+            raise InvalidArgumentError(f"batch_edge_type_idx {e} out of range")
+        return e, rt, ct
+
+    def _idx_dev(self, ctx, node: Node, n_max: int) -> torch.Tensor:
+        v = ctx.value(node)
+        if isinstance(v, torch.Tensor):
+            t = v.to(device=ctx.session.device, dtype=torch.int32)
+            if t.numel():
+                lo, hi = int(t.min()), int(t.max())
+                if lo < 0 or hi >= n_max:
+                    raise InvalidArgumentError(f"{node.name}: index out of range [0, {n_max})")
+            return t.contiguous()
+        a = np.asarray(v).astype(np.int64).reshape(-1)
+        if a.size and (a.min() < 0 or a.max() >= n_max):
+            raise InvalidArgumentError(f"{node.name}: index out of range [0, {n_max})")
+        return torch.from_numpy(a.astype(np.int32)).to(ctx.session.device)
+
+    def _tables(self, ctx, rt, ct):
+        row = runtime.as_device_f32(ctx.value(self.embeddings[rt]))
+        col = runtime.as_device_f32(ctx.value(self.embeddings[ct]))
+        return row, col
+
+    def _latent(self, ctx, e):
+        gi, gv = self.latent_inters[e], self.latent_varies[e]
+        if hasattr(gi, "kind") and hasattr(gv, "kind"):  # DecagonModel's latent nodes
+            return runtime.latent_operands(ctx, gi.kind, gi.var, gv.kind, gv.var, gi.d, gi, gv)
+        # arbitrary user nodes: fold a dense L into G (uᵀ·L·G·L·v = uᵀ·(LGL)·v)
+        G = runtime.as_device_f32(ctx.value(gi))
+        L = runtime.as_device_f32(ctx.value(gv))
+        return kernels.matmul(kernels.matmul(L, G), L), None
+
+    def _sample_negatives(self, ctx: RunContext) -> torch.Tensor:
+        e, _, _ = self._edge(ctx)
+        cache = ctx.session.caches
+        key = ("sampler", id(self))
+        if key not in cache:
+            cache[key] = _Sampler(self._rel_degrees, ctx.session.device)
+        s = cache[key]
+        n = self._batch(ctx).shape[0]
+        out = kernels.unigram_sample(s.cdfs[e], n, self.seed, s.counter)
+        s.counter += n
+        return out
+
+    def _scores(self, ctx: RunContext, rows_node: Node) -> torch.Tensor:
+        e, rt, ct = self._edge(ctx)
+        row_t, col_t = self._tables(ctx, rt, ct)
+        rows = self._idx_dev(ctx, rows_node, row_t.shape[0])
+        cols = self._idx_dev(ctx, self.col_inputs, col_t.shape[0])
+        if rows.numel() != cols.numel():
+            raise InvalidArgumentError("row / column index counts differ")
+        G, l = self._latent(ctx, e)
+        return kernels.decoder_score(row_t, col_t, rows, cols, G, l)
+
+    def _full(self, ctx: RunContext, rows_node: Node) -> torch.Tensor:
+        e, rt, ct = self._edge(ctx)
+        row_t, col_t = self._tables(ctx, rt, ct)
+        rows = self._idx_dev(ctx, rows_node, row_t.shape[0]).long()
+        cols = self._idx_dev(ctx, self.col_inputs, col_t.shape[0]).long()
+        G, l = self._latent(ctx, e)
+        return runtime.full_scores(row_t.index_select(0, rows).contiguous(),
+                                   col_t.index_select(0, cols).contiguous(), G, l)
+
+    def batch_predict(self, row_inputs, col_inputs):
+        """optimizer.py:63-85 as a node: the full B×B score matrix."""
+        return Node("optimizer/batch_predict", lambda ctx: self._full(ctx, row_inputs))
+
+    def predict(self):
+        """optimizer.py:87-106: predictions = E_i·L·G·L·E_jᵀ for the fed edge type."""
+        def fn(ctx):
+            e, rt, ct = self._edge(ctx)
+            row_t, col_t = self._tables(ctx, rt, ct)
+            G, l = self._latent(ctx, e)
+            return runtime.full_scores(row_t, col_t, G, l)
+        self.predictions = Node("optimizer/predictions", fn)
+
+    def _build(self):
+        self.cost = self._hinge_loss(self.outputs, self.neg_outputs)
+        self.optimizer = None
+
+        def _not_yet(ctx):
+            raise NotImplementedError(
+                "opt_op (backward + Adam, optimizer.py:108-114) is the next row of SURVEY §8f; "
+                "the HIP forward path serves cost / outputs / predictions")
+        self.opt_op = Operation("optimizer/opt_op", _not_yet)
+        self.grads_vars = Operation("optimizer/grads_vars", _not_yet)
+
+    def _hinge_loss(self, aff, neg_aff):
+        """optimizer.py:116-120: sum(relu(neg - (pos - margin)))."""
+        def fn(ctx):
+            pos = runtime.as_device_f32(ctx.value(aff))
+            neg = runtime.as_device_f32(ctx.value(neg_aff))
+            return kernels.hinge_loss(pos, neg, self.margin)[0]
+        return Node("optimizer/cost", fn)
+
+    def _xent_loss(self, aff, neg_aff):
+        """optimizer.py:122-127."""
+        def fn(ctx):
+            pos = runtime.as_device_f32(ctx.value(aff))
+            neg = runtime.as_device_f32(ctx.value(neg_aff))
+            return kernels.xent_loss(pos, neg, self.neg_sample_weights)[0]
+        return Node("optimizer/xent_cost", fn)
+
+
+def gather_cols(params, indices, name=None):
+    """optimizer.py:130-160: gather columns of a 2-D array (host-side index plumbing)."""
+    p = np.asarray(params)
+    if p.ndim != 2:
+        raise ValueError("'params' must be 2D.")
+    idx = np.asarray(indices)
+    if idx.ndim != 1:
+        raise ValueError("'params' must be 1D.")
+    return p[:, idx]

@@ -1,0 +1,167 @@
+"""Host-side sparse formats at the drop-in boundary.
+
+The reference feeds every adjacency matrix as a COO tuple `(coords[nnz,2], values[nnz],
+shape)` (decagon/utility/preprocessing.py:20-26, decagon/deep/minibatch.py:259-267) into a
+`tf.sparse_placeholder(tf.float32)` (main.py:103-104).  Here those tuples are converted
+once to CSR (rows ascending, the order of the nonzeros inside a row preserved — TF's
+SparseTensorDenseMatMul visits nonzeros in feed order) and uploaded; the values are cast
+float64 -> float32 exactly as the placeholder's dtype does.
+"""
+from __future__ import annotations
+
+from collections import namedtuple
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import scipy.sparse as sp
+
+SparseTensorValue = namedtuple("SparseTensorValue", ["indices", "values", "dense_shape"])
+
+
+def sparse_to_tuple(sparse_mx) -> Tuple[np.ndarray, np.ndarray, Tuple[int, int]]:
+    """COO wire format of the reference (decagon/utility/preprocessing.py:20-26)."""
+    m = sparse_mx.tocoo() if not sp.isspmatrix_coo(sparse_mx) else sparse_mx
+    coords = np.stack([m.row, m.col], axis=1)
+    return coords, m.data, tuple(int(s) for s in m.shape)
+
+
+def preprocess_graph(adj) -> Tuple[np.ndarray, np.ndarray, Tuple[int, int]]:
+    """Normalized adjacency, restating EdgeMinibatchIterator.preprocess_graph
+    (decagon/deep/minibatch.py:80-93) in float64:
+
+      square   (N×N):  Â = D^-½ (A+I)ᵀ D^-½,  D = diag(rowsum(A+I))
+      rectangular:     Â = Dr^-½ A Dc^-½ (nan_to_num on the degrees, as the reference;
+                       a zero-degree row/column holds no entry, so its factor is never used)
+
+    For the square case each stored value is (v·d[c])·d[r] for entry (r,c) of A+I, stored
+    at (c,r) — the same product order as the reference's `adj_.dot(D).transpose().dot(D)`.
+    Returns the COO tuple; entry order is row-major (the CSR build does not depend on it).
+    """
+    a = sp.coo_matrix(adj, dtype=np.float64)
+    n_r, n_c = a.shape
+    if n_r == n_c:
+        a = (a + sp.eye(n_r, dtype=np.float64)).tocsr()
+        a.sum_duplicates()
+        rowsum = np.asarray(a.sum(axis=1)).ravel()
+        with np.errstate(divide="ignore"):
+            dinv = np.power(rowsum, -0.5)
+        a = a.tocoo()
+        vals = (a.data * dinv[a.col]) * dinv[a.row]
+        out = sp.coo_matrix((vals, (a.col, a.row)), shape=(n_c, n_r)).tocsr()
+    else:
+        rowsum = np.asarray(a.sum(axis=1)).ravel()
+        colsum = np.asarray(a.sum(axis=0)).ravel()
+        with np.errstate(divide="ignore"):
+            rinv = np.nan_to_num(np.power(rowsum, -0.5))
+            cinv = np.nan_to_num(np.power(colsum, -0.5))
+        a = a.tocsr()
+        a.sum_duplicates()
+        a = a.tocoo()
+        vals = (rinv[a.row] * a.data) * cinv[a.col]
+        out = sp.coo_matrix((vals, (a.row, a.col)), shape=(n_r, n_c)).tocsr()
+    out.sort_indices()
+    return sparse_to_tuple(out)
+
+
+def as_coo_tuple(value) -> Tuple[np.ndarray, np.ndarray, Tuple[int, int]]:
+    """Accept what a tf.sparse_placeholder accepts: (coords, values, shape), a
+    SparseTensorValue, or a scipy sparse matrix."""
+    if sp.issparse(value):
+        return sparse_to_tuple(value)
+    if isinstance(value, SparseTensorValue):
+        return np.asarray(value.indices), np.asarray(value.values), tuple(value.dense_shape)
+    if isinstance(value, (tuple, list)) and len(value) == 3:
+        c, v, s = value
+        return np.asarray(c), np.asarray(v), tuple(int(x) for x in s)
+    raise TypeError(f"cannot feed {type(value).__name__} to a sparse placeholder")
+
+
+@dataclass
+class HostCSR:
+    """One relation in CSR, int32 indices, float32 values."""
+
+    rowptr: np.ndarray
+    col: np.ndarray
+    val: np.ndarray
+    shape: Tuple[int, int]
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.shape[0])
+
+
+def coo_to_csr(coords, values, shape) -> HostCSR:
+    coords = np.asarray(coords)
+    values = np.asarray(values)
+    n_r, n_c = int(shape[0]), int(shape[1])
+    if coords.size == 0:
+        return HostCSR(np.zeros(n_r + 1, np.int32), np.zeros(0, np.int32), np.zeros(0, np.float32), (n_r, n_c))
+    if coords.ndim != 2 or coords.shape[1] != 2 or coords.shape[0] != values.shape[0]:
+        raise ValueError("coords must be [nnz, 2] and match values")
+    rows = coords[:, 0].astype(np.int64)
+    cols = coords[:, 1].astype(np.int64)
+    if rows.min() < 0 or rows.max() >= n_r or cols.min() < 0 or cols.max() >= n_c:
+        raise ValueError(f"sparse index out of range for shape {shape}")
+    if n_r >= 2**31 or n_c >= 2**31 or rows.shape[0] >= 2**31:
+        raise ValueError("sparse operand exceeds int32 indexing")
+    order = np.argsort(rows, kind="stable")
+    counts = np.bincount(rows, minlength=n_r)
+    rowptr = np.zeros(n_r + 1, np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    return HostCSR(rowptr.astype(np.int32), cols[order].astype(np.int32),
+                   values[order].astype(np.float32), (n_r, n_c))
+
+
+def is_identity(coords, values, shape) -> bool:
+    """True when a feature feed is the identity (featureless nodes, main.py:186-193): then
+    X·W ≡ W exactly and the T2 SpMM is skipped."""
+    n_r, n_c = int(shape[0]), int(shape[1])
+    coords = np.asarray(coords)
+    values = np.asarray(values)
+    if n_r != n_c or coords.shape[0] != n_r:
+        return False
+    idx = np.arange(n_r)
+    return bool(np.array_equal(coords[:, 0], idx) and np.array_equal(coords[:, 1], idx)
+                and np.all(values == 1))
+
+
+@dataclass
+class StackedCSR:
+    """K relations of one (i,j) group with a common shape, stacked: relation k's row r is
+    rowptr[k*n_rows + r] .. rowptr[k*n_rows + r + 1] into col/val (global offsets)."""
+
+    rowptr: np.ndarray
+    col: np.ndarray
+    val: np.ndarray
+    n_rows: int
+    n_cols: int
+    n_rels: int
+    rel_nnz: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.shape[0])
+
+
+def stack_relations(csrs: Sequence[HostCSR]) -> StackedCSR:
+    if not csrs:
+        raise ValueError("empty relation group")
+    n_r, n_c = csrs[0].shape
+    for c in csrs:
+        if c.shape != (n_r, n_c):
+            raise ValueError("all relations of a group must share one shape")
+    nnz = [c.nnz for c in csrs]
+    total = int(np.sum(nnz))
+    if total >= 2**31:
+        raise ValueError("group exceeds int32 nonzero offsets")
+    rowptr = np.empty(len(csrs) * n_r + 1, np.int64)
+    off = 0
+    for k, c in enumerate(csrs):
+        rowptr[k * n_r:(k + 1) * n_r] = c.rowptr[:-1].astype(np.int64) + off
+        off += c.nnz
+    rowptr[-1] = off
+    col = np.concatenate([c.col for c in csrs]) if total else np.zeros(0, np.int32)
+    val = np.concatenate([c.val for c in csrs]) if total else np.zeros(0, np.float32)
+    return StackedCSR(rowptr.astype(np.int32), col.astype(np.int32), val.astype(np.float32),
+                      n_r, n_c, len(csrs), np.asarray(nnz, np.int64))

@@ -1,0 +1,177 @@
+/*
+ * decagon_hip.h — C ABI of libdecagon_hip.so, the MI355X (gfx950) kernels behind the
+ * Decagon multi-relational GCN forward and its edge decoders.
+ *
+ * The reference (jrectorb/decagon, TF 1.8) has no FFI: its "boundary" is a set of TF ops
+ * called from the decagon/deep modules.  Every entry point below replaces one or a fused run of
+ * those ops; the replaced call sites are cited per function (paths relative to the
+ * reference root).  The Python layer in decagon_amd/ binds these with ctypes
+ * (decagon_amd/_lib.py); INTEGRATION.md shows the binding.
+ *
+ * Conventions (all entry points):
+ *   - every pointer argument is a caller-owned DEVICE pointer unless documented as host;
+ *     the library never allocates or frees caller memory and keeps no state between calls;
+ *   - launches are asynchronous on `stream` (a hipStream_t passed as void*; NULL = the
+ *     null stream) and are safe to capture into a hipGraph;
+ *   - the return value is DG_OK (0), a negative DG_E* code for an argument error detected
+ *     on the host before any launch, or a positive hipError_t from the launch.
+ *   - float arithmetic is IEEE fp32 (no fast-math); sums are in a fixed order, so results
+ *     are bitwise reproducible run to run (no float atomics anywhere).
+ */
+#ifndef DECAGON_HIP_H
+#define DECAGON_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DG_OK 0
+#define DG_EINVAL (-1)     /* bad size / null pointer / unsupported shape            */
+#define DG_EALIGN (-2)     /* a dense operand is not 16-byte aligned row by row      */
+#define DG_ETOOMANY (-3)   /* more groups than DG_MAX_GROUPS in one launch           */
+
+#define DG_MAX_GROUPS 8
+
+/* ABI version (2); bumped whenever a struct layout or a signature changes. */
+int32_t dg_abi_version(void);
+
+/* --------------------------------------------------------------------------------------
+ * Relation group SpMM (T3 + T4 of SURVEY §2.2):  for every group g and chunk c,
+ *
+ *     out_g[c][r][:] = sum_{k in chunk c} sum_{p in row r of A_g,k} val[p] * X_g,k[col[p]][:]
+ *
+ * A_g,k is relation k of the group, stored as stacked CSR: relation k's row pointer for row
+ * r is rowptr[k*rowptr_rel_stride + r] (rowptr_rel_stride = n_rows for K stacked CSRs whose
+ * offsets are global into col/val, or 0 when all K relations share one CSR, the T2 case
+ * X_j * W_k of layers.py:89).  X_g,k = x + k*x_rel_stride, row stride x_ld (elements).
+ * If rel_map is non-NULL, X_g,k = x + rel_map[k]*x_rel_stride instead (a rank's shard of
+ * the relations, picked out of the full weight stack without a copy).
+ * Chunks hold `chunk` consecutive relations; n_chunks = ceil(n_rels/chunk).  out_g is dense
+ * [n_chunks][n_rows][d].  With chunk == n_rels the output is the add_n of layers.py:92/116.
+ *
+ * Replaces: tf.sparse_tensor_dense_matmul(adj_mats[edge_type][k], x)  layers.py:90, :114
+ *           tf.sparse_tensor_dense_matmul(x, weights_k) (sparse features) layers.py:89
+ *           tf.add_n(outputs)                                         layers.py:92, :116
+ * Requirements: d % 4 == 0, 4 <= d <= 256, x and x_ld 16-byte aligned (x_ld % 4 == 0).
+ * -------------------------------------------------------------------------------------- */
+typedef struct dg_rel_group {
+    const int32_t* rowptr;      /* device */
+    const int32_t* col;         /* device, [nnz] column indices, 0 <= col < n_cols     */
+    const float* val;           /* device, [nnz] normalized adjacency values           */
+    const float* x;             /* device, dense operand of relation 0                 */
+    float* out;                 /* device, [n_chunks][n_rows][d]                       */
+    const int32_t* rel_map;     /* device, [n_rels] or NULL (identity)                 */
+    int64_t x_rel_stride;       /* elements between X_k and X_{k+1}                    */
+    int64_t x_ld;               /* elements between consecutive rows of X_k            */
+    int32_t rowptr_rel_stride;  /* n_rows (stacked) or 0 (shared CSR)                  */
+    int32_t n_rows;
+    int32_t n_rels;
+    int32_t chunk;              /* relations per output chunk, >= 1                    */
+    int32_t reserved[4];        /* zero; filled in by the library                      */
+} dg_rel_group;
+
+int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
+                       int32_t d, void* stream);
+
+/* Single relation, no chunking: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
+ * Replaces one tf.sparse_tensor_dense_matmul (layers.py:90).  ldy must equal d. */
+int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                    int32_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
+                    int32_t d, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * GCN epilogue (T4 tail + T5 + T6):  for one node type i with groups g = (i, j_1..j_m),
+ *
+ *     s_g[r]   = sum_{c < n_chunks_g} partial_g[c][r][:]              (chunk order)
+ *     y_g[r]   = s_g[r] * rsqrt(max(sum(s_g[r]^2), 1e-12))            if DG_EPI_L2NORM
+ *     out[r]   = act( sum_g y_g[r] )                                  (group order)
+ *
+ * act = relu if DG_EPI_RELU.  With DG_EPI_CHUNK_RELU each chunk partial is passed through
+ * relu before the chunk sum (a layer built with act=relu and chunk = 1 applies the
+ * activation per relation before add_n, layers.py:91).  With one group and no flags this is
+ * the plain chunk reduce used before the cross-GPU all-reduce.
+ * Replaces: tf.nn.l2_normalize(outputs, dim=1)   layers.py:93, :117
+ *           tf.nn.relu(tf.add_n(hid1))           model.py:75
+ *           tf.add_n(embeds)                     model.py:88
+ * -------------------------------------------------------------------------------------- */
+#define DG_EPI_L2NORM 1
+#define DG_EPI_RELU 2
+#define DG_EPI_CHUNK_RELU 4
+
+typedef struct dg_epi_group {
+    const float* partial;       /* device, [n_chunks][n_rows][d] */
+    int32_t n_chunks;
+    int32_t reserved;
+} dg_epi_group;
+
+int dg_gcn_epilogue_f32(const dg_epi_group* groups /* HOST array */, int32_t n_groups,
+                        float* out, int32_t n_rows, int32_t d, int32_t flags, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Batched strided fp32 GEMM on the f32-input MFMA (v_mfma_f32_32x32x2_f32, exact fp32):
+ *
+ *   C_b[m][n] = sc[n] * sum_k (sa[k] * A_b[m][k]) * B_b[k][n]        b < batch
+ *
+ * Element (m,k) of A_b is A[b*a_bs + m*a_sm + k*a_sk]; likewise B (k,n) and C (m,n).
+ * sa / sc are optional (NULL = ones).  If b_map is non-NULL, B_b starts at
+ * b + b_map[b]*b_bs (relation shard of a weight stack).  No alignment requirement.
+ * Replaces: tf.matmul(x, weights_k)                          layers.py:113 (batched over k)
+ *           tf.matmul chain row·L·G·L·colᵀ (predict)         optimizer.py:87-106
+ * -------------------------------------------------------------------------------------- */
+typedef struct dg_gemm_desc {
+    const float* a;
+    const float* b;
+    float* c;
+    const float* sa;            /* [K] or NULL */
+    const float* sc;            /* [N] or NULL */
+    const int32_t* b_map;       /* [batch] or NULL */
+    int64_t a_bs, a_sm, a_sk;
+    int64_t b_bs, b_sk, b_sn;
+    int64_t c_bs, c_sm, c_sn;
+    int32_t m, n, k, batch;
+} dg_gemm_desc;
+
+int dg_gemm_f32(const dg_gemm_desc* desc /* HOST */, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Edge decoder scores (T8 + T9):  for pair p,
+ *     u = row_table[row_idx[p]],  v = col_table[col_idx[p]]       (rows of length d)
+ *     out[p] = sum_j ( sum_k u[k] l[k] G[k][j] ) l[j] v[j]         (= uᵀ·L·G·L·v)
+ * G is dense d×d row-major; l is the diagonal of L (NULL = identity).  This is the diagonal
+ * of the reference's B×B product, computed without forming it.
+ * Replaces: batch_predict + tf.diag_part   optimizer.py:51-57, :63-85
+ * Requirements: d % 32 == 0, d <= 256.
+ * -------------------------------------------------------------------------------------- */
+int dg_decoder_score_f32(const float* row_table, int64_t ld_row, const float* col_table,
+                         int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
+                         int32_t n_pairs, const float* G, const float* l, int32_t d,
+                         float* out, void* stream);
+
+/* Hinge loss (T12):  loss[0] = sum_p relu(neg[p] - pos[p] + margin).
+ * Replaces DecagonOptimizer._hinge_loss  optimizer.py:116-120.  Single workgroup,
+ * fixed summation order. */
+int dg_hinge_loss_f32(const float* pos, const float* neg, int32_t n, float margin,
+                      float* loss, void* stream);
+
+/* Cross-entropy loss:  loss[0] = sum_p softplus(-pos[p]) + w * sum_p softplus(neg[p])
+ * (sigmoid_cross_entropy_with_logits with labels 1 / 0).  optimizer.py:122-127. */
+int dg_xent_loss_f32(const float* pos, const float* neg, int32_t n, float neg_weight,
+                     float* loss, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, drawn by
+ * inverse CDF from a counter-based hash (seed, offset + i).  cdf is the inclusive prefix
+ * sum of the (distorted) weights, cdf[range-1] > 0.
+ * Replaces tf.nn.fixed_unigram_candidate_sampler(distortion=0.75, unique=False)
+ * optimizer.py:40-47 (distribution only — TF's RNG stream is not reproducible).
+ * -------------------------------------------------------------------------------------- */
+int dg_unigram_sample(const float* cdf, int32_t range, int32_t n, uint64_t seed,
+                      uint64_t offset, int32_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DECAGON_HIP_H */

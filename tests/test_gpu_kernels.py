@@ -1,0 +1,227 @@
+"""Kernel-level parity: every C-ABI entry point against the float64 oracle on seeded inputs,
+including the edge cases the reference's data produce (empty rows — genes without drug
+targets in (0,1); empty relations; single-relation groups; rectangular Â; d in
+{4..256}).  Tolerance: max|y − y_ref| / max|y_ref| ≤ 1e-4 for fp32 outputs;
+integer outputs bit-exact.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import rel_err
+from oracle import decagon_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def K():
+    from decagon_amd import kernels
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return kernels
+
+
+def _rand_csr(rng, n_r, n_c, density, empty_rows=0.0):
+    m = sp.random(n_r, n_c, density=density, random_state=rng, format="csr", dtype=np.float64)
+    if empty_rows:
+        drop = rng.random(n_r) < empty_rows
+        m = sp.diags((~drop).astype(np.float64)) @ m
+        m = m.tocsr()
+    m.eliminate_zeros()
+    m.sort_indices()
+    return m
+
+
+def _dev_csr(m):
+    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple
+
+    h = coo_to_csr(*sparse_to_tuple(m))
+    return (torch.from_numpy(h.rowptr).cuda(), torch.from_numpy(h.col).cuda(),
+            torch.from_numpy(h.val).cuda(), h)
+
+
+@pytest.mark.parametrize("d", [4, 8, 16, 32, 48, 64, 128, 256])
+def test_spmm_csr_matches_oracle(K, d):
+    rng = np.random.default_rng(d)
+    m = _rand_csr(rng, 301, 257, 0.05, empty_rows=0.2)
+    x = rng.standard_normal((257, d)).astype(np.float32)
+    rp, cl, vl, h = _dev_csr(m)
+    y = K.spmm_csr(rp, cl, vl, torch.from_numpy(x).cuda(), 301)
+    want = orc.sparse_dense_matmul((np.stack(m.nonzero(), 1), m.data, m.shape), x.astype(np.float64))
+    # (nonzero order differs from CSR order only by summation order)
+    assert rel_err(y.cpu().numpy(), want) <= 1e-5
+    zero_rows = np.diff(m.indptr) == 0
+    assert np.all(y.cpu().numpy()[zero_rows] == 0)
+
+
+def test_spmm_long_rows(K):
+    """Rows longer than one 64-nonzero batch, and a dense row."""
+    rng = np.random.default_rng(3)
+    m = _rand_csr(rng, 40, 3000, 0.2).tolil()
+    m[5, :] = rng.random(3000)
+    m = m.tocsr()
+    m.sort_indices()
+    x = rng.standard_normal((3000, 64)).astype(np.float32)
+    rp, cl, vl, _ = _dev_csr(m)
+    y = K.spmm_csr(rp, cl, vl, torch.from_numpy(x).cuda(), 40).cpu().numpy()
+    want = m @ x.astype(np.float64)
+    assert rel_err(y, want) <= 1e-5
+
+
+def test_spmm_empty_matrix(K):
+    m = sp.csr_matrix((17, 9))
+    rp, cl, vl, _ = _dev_csr(m)
+    x = torch.ones((9, 32), device="cuda")
+    y = K.spmm_csr(rp, cl, vl, x, 17)
+    assert torch.count_nonzero(y) == 0
+
+
+@pytest.mark.parametrize("chunk", [1, 2, 3, 7])
+@pytest.mark.parametrize("d", [32, 64])
+def test_spmm_groups_chunks_and_relmap(K, chunk, d):
+    """Stacked relations, chunked partial sums, a relation map into a bigger weight stack,
+    and two groups in one launch."""
+    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, stack_relations
+
+    rng = np.random.default_rng(chunk * 100 + d)
+    groups, wants, specs = [], [], []
+    for (n_r, n_c, nrel) in ((120, 90, 7), (90, 120, 3)):
+        mats = [_rand_csr(rng, n_r, n_c, 0.04, empty_rows=0.1) for _ in range(nrel)]
+        st = stack_relations([coo_to_csr(*sparse_to_tuple(m)) for m in mats])
+        total = nrel + 4
+        X = rng.standard_normal((total, n_c, d)).astype(np.float32)
+        rel_ids = rng.choice(total, size=nrel, replace=False).astype(np.int32)
+        nch = -(-nrel // chunk)
+        out = torch.zeros((nch, n_r, d), device="cuda")
+        spec = K.RelGroupSpec(torch.from_numpy(st.rowptr).cuda(), torch.from_numpy(st.col).cuda(),
+                              torch.from_numpy(st.val).cuda(), torch.from_numpy(X).cuda(), out, n_r, n_c,
+                              nrel, chunk, n_c * d, d, n_r, rel_map=torch.from_numpy(rel_ids).cuda(),
+                              x_rels=total, rel_map_max=int(rel_ids.max()))
+        specs.append(spec)
+        want = np.zeros((nch, n_r, d))
+        for k, m in enumerate(mats):
+            want[k // chunk] += m @ X[rel_ids[k]].astype(np.float64)
+        wants.append(want)
+    K.spmm_groups(specs, d)
+    for s, w in zip(specs, wants):
+        assert rel_err(s.out.cpu().numpy(), w) <= 1e-5
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2, 3, 5])
+def test_epilogue(K, flags):
+    from decagon_amd._lib import DG_EPI_CHUNK_RELU, DG_EPI_L2NORM, DG_EPI_RELU
+
+    rng = np.random.default_rng(flags)
+    n, d = 333, 64
+    parts = []
+    for nch in (3, 1, 2):
+        p = rng.standard_normal((nch, n, d)).astype(np.float32)
+        p[:, ::7] = 0.0  # all-zero rows: l2_normalize keeps them 0
+        parts.append(p)
+    out = torch.empty((n, d), device="cuda")
+    K.gcn_epilogue([(torch.from_numpy(p).cuda(), p.shape[0]) for p in parts], out, n, d, flags)
+    tot = np.zeros((n, d))
+    for p in parts:
+        p = p.astype(np.float64)
+        if flags & DG_EPI_CHUNK_RELU:
+            p = np.maximum(p, 0)
+        s = p.sum(0)
+        if flags & DG_EPI_L2NORM:
+            s = orc.l2_normalize_rows(s)
+        tot += s
+    if flags & DG_EPI_RELU:
+        tot = np.maximum(tot, 0)
+    assert rel_err(out.cpu().numpy(), tot) <= 1e-5
+    assert np.all(out.cpu().numpy()[::7] == 0)
+
+
+@pytest.mark.parametrize("m,n,k,batch", [(645, 32, 64, 5), (37, 70, 19, 3), (1, 1, 1, 1), (500, 32, 32, 2),
+                                         (64, 96, 0, 1)])
+def test_gemm(K, m, n, k, batch):
+    rng = np.random.default_rng(m * n + k)
+    A = rng.standard_normal((m, k)).astype(np.float32)
+    B = rng.standard_normal((batch + 2, k, n)).astype(np.float32)
+    bmap = rng.permutation(batch + 2)[:batch].astype(np.int32)
+    sa = rng.standard_normal(k).astype(np.float32)
+    sc = rng.standard_normal(n).astype(np.float32)
+    C = torch.empty((batch, m, n), device="cuda")
+    K.PreparedGemm(torch.from_numpy(A).cuda(), (0, k, 1), torch.from_numpy(B).cuda(), (k * n, n, 1), C,
+                   (m * n, n, 1), m, n, k, batch, torch.from_numpy(sa).cuda(), torch.from_numpy(sc).cuda(),
+                   b_map=torch.from_numpy(bmap).cuda(), b_batches=batch + 2, b_map_max=int(bmap.max()))()
+    for b in range(batch):
+        want = ((A.astype(np.float64) * sa) @ B[bmap[b]].astype(np.float64)) * sc
+        got = C[b].cpu().numpy()
+        if k == 0:
+            assert np.all(got == 0)
+        else:
+            assert rel_err(got, want) <= 1e-5
+
+
+def test_gemm_transposed_strides(K):
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((50, 32)).astype(np.float32)
+    E = rng.standard_normal((70, 32)).astype(np.float32)
+    Ad, Ed = torch.from_numpy(A).cuda(), torch.from_numpy(E).cuda()
+    out = K.matmul(Ad, Ed.t())
+    assert rel_err(out.cpu().numpy(), A.astype(np.float64) @ E.T.astype(np.float64)) <= 1e-5
+
+
+@pytest.mark.parametrize("d", [32, 64, 256])
+@pytest.mark.parametrize("diag", [False, True])
+def test_decoder_score(K, d, diag):
+    rng = np.random.default_rng(d + diag)
+    n_r, n_c, npairs = 300, 200, 1000 + 17
+    U = rng.standard_normal((n_r, d)).astype(np.float32)
+    V = rng.standard_normal((n_c, d)).astype(np.float32)
+    G = rng.standard_normal((d, d)).astype(np.float32) / np.sqrt(d)
+    l = rng.standard_normal(d).astype(np.float32) if diag else None
+    ri = rng.integers(0, n_r, npairs).astype(np.int32)
+    ci = rng.integers(0, n_c, npairs).astype(np.int32)
+    got = K.decoder_score(torch.from_numpy(U).cuda(), torch.from_numpy(V).cuda(), torch.from_numpy(ri).cuda(),
+                          torch.from_numpy(ci).cuda(), torch.from_numpy(G).cuda(),
+                          None if l is None else torch.from_numpy(l).cuda()).cpu().numpy()
+    L = np.eye(d) if l is None else np.diag(l.astype(np.float64))
+    want = orc.batch_predict([U.astype(np.float64), V.astype(np.float64)], 0, 1, G.astype(np.float64), L, ri, ci)
+    assert rel_err(got, want) <= 1e-5
+
+
+def test_losses(K):
+    rng = np.random.default_rng(5)
+    pos = rng.standard_normal(1000).astype(np.float32)
+    neg = rng.standard_normal(1000).astype(np.float32)
+    P, N = torch.from_numpy(pos).cuda(), torch.from_numpy(neg).cuda()
+    h = float(K.hinge_loss(P, N, 0.1)[0])
+    x = float(K.xent_loss(P, N, 1.0)[0])
+    assert abs(h - orc.hinge_loss(pos, neg, 0.1)) <= 1e-4 * abs(orc.hinge_loss(pos, neg, 0.1))
+    assert abs(x - orc.xent_loss(pos, neg, 1.0)) <= 1e-4 * abs(orc.xent_loss(pos, neg, 1.0))
+    # deterministic: same bits twice
+    assert float(K.hinge_loss(P, N, 0.1)[0]) == h
+
+
+def test_unigram_sampler_distribution(K):
+    rng = np.random.default_rng(9)
+    deg = rng.integers(0, 50, 400).astype(np.float64)
+    deg[:10] = 0
+    p = orc.unigram_distribution(deg)
+    cdf = torch.from_numpy(np.cumsum(np.power(deg, 0.75)).astype(np.float32)).cuda()
+    n = 400000
+    s = K.unigram_sample(cdf, n, seed=1, offset=0).cpu().numpy()
+    assert s.min() >= 0 and s.max() < 400
+    assert np.all(np.bincount(s, minlength=400)[:10] == 0)  # zero degree never drawn
+    freq = np.bincount(s, minlength=400) / n
+    assert np.max(np.abs(freq - p)) < 5e-3
+    s2 = K.unigram_sample(cdf, n, seed=1, offset=0).cpu().numpy()
+    assert np.array_equal(s, s2)  # counter-based: reproducible
+
+
+def test_shape_checks_fail_before_launch(K):
+    """Host checks reject buffers too small for the indices the kernel would form."""
+    m = sp.random(10, 10, density=0.3, random_state=0, format="csr")
+    rp, cl, vl, _ = _dev_csr(m)
+    x = torch.zeros((5, 32), device="cuda")  # fewer rows than n_cols
+    with pytest.raises(ValueError):
+        K.RelGroupSpec(rp, cl, vl, x, torch.zeros((1, 10, 32), device="cuda"), 10, 10, 1, 1, 0, 32, 0).validate(32)
