@@ -1,0 +1,297 @@
+"""Benchmark: GCN-layer edges/s + achieved HBM GB/s of the Decagon forward on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config S|P]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+A step is one full forward of the hot path over one batch: GCN layer 1 + layer 2 over every
+relation (SpMM, projection, add_n, L2-norm, ReLU) + the DEDICOM decoder on B=512 positive
+and 512 device-sampled negative pairs + the hinge loss.  Edges per step = 2 × Σ nnz (each
+layer visits every stored nonzero of every normalised Â_r, self-loops and transposed copies
+included — SURVEY §8d).  Inputs are resident in HBM before timing (uploaded once).
+
+Workloads (BASELINE.json configs):
+  S (default, configs[1]): main.py's 5-relation / 10-matrix synthetic, the exact
+     reference-normalised adjacencies (tests/golden/synthetic_S.npz), d = 64/32, fp32.
+     At N GPUs the graph holds N relation sets, one per GPU (weak scaling); each layer
+     all-reduces the per-(i,j) pre-normalisation sums over RCCL.
+  P (configs[2]/[3]): polypharmacy-shaped 19,085 + 645 nodes, 964 side effects ⇒ 1,932
+     drug-drug matrices, ≈23 M nnz; at N GPUs the relations are LPT-sharded (strong scaling).
+
+Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "GCN-layer edges/sec + achieved HBM GB/s, 5-relation synthetic, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md §Chip-level parameters)
+H1, H2, BATCH, MARGIN = 64, 32, 512, 0.1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", choices=["S", "P"], default="S")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=200)
+    ap.add_argument("--target-waves", type=int, default=32768)
+    ap.add_argument("--chunk", type=int, default=None)
+    return ap.parse_args()
+
+
+def glorot_stack(rng, k, d_in, d_out):
+    r = np.sqrt(6.0 / (d_in + d_out))
+    return rng.uniform(-r, r, size=(k, d_in, d_out)).astype(np.float32)
+
+
+def build_workload(args, rank, world):
+    import torch
+
+    from decagon_amd import synthetic
+    from decagon_amd.sharding import RelationShard, torch_allreduce
+
+    allreduce = torch_allreduce() if world > 1 else None
+    if args.config == "S":
+        base = synthetic.load_S()
+        graph = synthetic.replicate_sets(base, world) if world > 1 else base
+        shard = RelationShard.blocks(base.edge_types, rank, world, allreduce) if world > 1 else None
+        scaling = "weak"
+        workload = ("S: main.py 5-relation / 10-matrix synthetic (reference-normalised, 105,974 nnz "
+                    "per relation set), 2 GCN layers d=64/32 + DEDICOM decoder B=512+512")
+    else:
+        graph = synthetic.make_P(seed=0)
+        shard = None
+        if world > 1:
+            nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
+            shard = RelationShard.lpt(graph.edge_types, nnz, rank, world, allreduce)
+        scaling = "strong"
+        workload = ("P: polypharmacy-shaped 19,085 proteins + 645 drugs, 964 side effects "
+                    "(1,932 drug-drug matrices), 2 GCN layers d=64/32 + DEDICOM decoder B=512+512")
+    return graph, shard, scaling, workload
+
+
+def make_plan(args, graph, shard, device):
+    import torch
+
+    from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
+
+    csr = graph.csr()
+    if shard is not None:  # only local relations need host CSR / upload
+        csr = {et: [c if k in set(shard.local[et]) else None for k, c in enumerate(v)] for et, v in csr.items()}
+    dg = DeviceGraph(graph.edge_types, csr, device, None if shard is None else shard.local)
+    rng = np.random.default_rng(1234)
+    n = graph.n_nodes
+    w1 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, n[et[1]], H1)).to(device)
+                       for et, K in graph.edge_types.items()})
+    w2 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, H1, H2)).to(device)
+                       for et, K in graph.edge_types.items()})
+    plan = ForwardPlan(dg, {j: None for j in n}, w1, w2, H1, H2,
+                       allreduce=None if shard is None else shard.allreduce,
+                       chunk_override=args.chunk, target_waves=args.target_waves)
+    return plan, dg
+
+
+class Decoder:
+    """DEDICOM scoring of B positive + B sampled negative pairs of one drug-drug relation,
+    then the hinge loss — all device launches (dg_unigram_sample, dg_decoder_score_f32 ×2,
+    dg_hinge_loss_f32)."""
+
+    def __init__(self, graph, plan, device, rank):
+        import torch
+
+        from decagon_amd import kernels
+
+        self.k = kernels
+        et = (1, 1)
+        coords = graph.adj[et][0][0]
+        rng = np.random.default_rng(99 + rank)
+        pick = coords[rng.choice(len(coords), BATCH, replace=False)]
+        self.rows = torch.from_numpy(pick[:, 0].astype(np.int32)).to(device)
+        self.cols = torch.from_numpy(pick[:, 1].astype(np.int32)).to(device)
+        deg = graph.degrees[1][0]
+        self.cdf = torch.from_numpy(np.cumsum(np.power(deg, 0.75)).astype(np.float32)).to(device)
+        self.neg = torch.empty(BATCH, dtype=torch.int32, device=device)
+        self.R = torch.from_numpy(glorot_stack(rng, 1, H2, H2)[0]).to(device)
+        self.l = torch.from_numpy(glorot_stack(rng, 1, H2, 1).reshape(-1)).to(device)
+        self.pos = torch.empty(BATCH, device=device)
+        self.negs = torch.empty(BATCH, device=device)
+        self.loss = torch.empty(1, device=device)
+        self.E = plan.embeddings[1]
+
+    def __call__(self):
+        k = self.k
+        k.unigram_sample(self.cdf, BATCH, seed=7, offset=0, out=self.neg)
+        k.decoder_score(self.E, self.E, self.rows, self.cols, self.R, self.l, out=self.pos)
+        k.decoder_score(self.E, self.E, self.neg, self.cols, self.R, self.l, out=self.negs)
+        k.hinge_loss(self.pos, self.negs, MARGIN, out=self.loss)
+
+
+def time_kernel(fn, reps, stream):
+    """Average device duration of one launch of `fn`, from HIP events on the stream the
+    kernel runs on, over `reps` back-to-back launches captured in one hipGraph."""
+    import torch
+
+    with torch.cuda.stream(stream):
+        fn()
+        stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        stream.synchronize()
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        best = None
+        for _ in range(5):
+            t0.record(stream)
+            g.replay()
+            t1.record(stream)
+            t1.synchronize()
+            ms = t0.elapsed_time(t1) / reps
+            best = ms if best is None else min(best, ms)
+    return best
+
+
+def cpu_baseline(graph, seconds):
+    """The oracle's scalar C restatement (fp32, one thread; oracle/gcn_ref.c) of the same
+    two-layer forward in TF's op order, on a bounded number of repetitions."""
+    import ctypes
+
+    from oracle import cpu_forward
+
+    lib = cpu_forward.load()
+    fwd = cpu_forward.Forward(lib, graph, H1, H2)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fwd.run()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or (reps >= 3 and el * (reps + 1) / reps > seconds * 1.5):
+            break
+    edges = 2 * graph.nnz * reps
+    return {"value": edges / el, "unit": "edges/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} full 2-layer forwards of config {graph.name} ({graph.nnz} nnz/layer) in "
+                      f"{el:.1f} s, oracle/gcn_ref.c fp32 scalar, 1 thread"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torchrun --nproc-per-node N")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    graph, shard, scaling, workload = build_workload(args, rank, world)
+    plan, dg = make_plan(args, graph, shard, device)
+    dec = Decoder(graph, plan, device, rank)
+
+    def step():
+        plan.run()
+        dec()
+
+    stream = torch.cuda.Stream(device)
+    use_graph = not args.no_graph and world == 1
+    with torch.cuda.stream(stream):
+        step()
+        stream.synchronize()
+        if use_graph:
+            cg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(cg, stream=stream):
+                step()
+            run = cg.replay
+        else:
+            run = step
+        for _ in range(args.warmup):
+            run()
+        stream.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        stream.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+
+    local_edges = 2 * dg.total_nnz
+    el_max = el
+    tot_edges = local_edges
+    if world > 1:
+        t = torch.tensor([el, float(local_edges)], dtype=torch.float64, device=device)
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        el_max, tot_edges = float(tm[0]), float(t[1])
+    value = tot_edges * args.steps / el_max
+
+    # dominant kernel: layer-1 relation-group SpMM
+    k_ms = time_kernel(lambda: [s() for s in plan._spmm1], args.kernel_reps, stream)
+    k_bytes = plan.layer_bytes(1)
+    achieved = k_bytes / (k_ms * 1e-3) / 1e9
+    k2_ms = time_kernel(lambda: [s() for s in plan._spmm2], args.kernel_reps, stream)
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(graph, args.cpu_seconds)
+        rec = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference-normalised adjacencies (config S) / seeded generator (P); "
+                    "random glorot weights",
+            "config": {"workload": workload, "nnz_per_layer_total": int(tot_edges // 2),
+                       "parallelism": (f"relation-sharded x{world}, RCCL all-reduce per layer" if world > 1
+                                       else "1 GPU"),
+                       "hipgraph": use_graph},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "spmm_groups_kernel (layer 1, d=64)", "kernel_ms": k_ms,
+                         "algorithmic_bytes": k_bytes},
+            "spmm_layer2_ms": k2_ms,
+            "spmm_layer1_edges_per_s": dg.total_nnz / (k_ms * 1e-3),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

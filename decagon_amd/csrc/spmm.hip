@@ -238,7 +238,8 @@ extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, 
         if (s.n_rows < 0 || s.n_rels < 0 || s.chunk < 1 || s.rowptr_rel_stride < 0)
             return DG_EINVAL;
         if (s.n_rows == 0 || s.n_rels == 0) continue;
-        if (!s.rowptr || !s.col || !s.val || !s.x || !s.out) return DG_EINVAL;
+        // col/val may be NULL for a group without nonzeros (rowptr all zero: never read)
+        if (!s.rowptr || !s.x || !s.out) return DG_EINVAL;
         if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || (s.x_ld & 3) || (s.x_rel_stride & 3))
             return DG_EALIGN;
         if (s.x_ld < d) return DG_EINVAL;

@@ -58,8 +58,8 @@ int32_t dg_abi_version(void);
  * -------------------------------------------------------------------------------------- */
 typedef struct dg_rel_group {
     const int32_t* rowptr;      /* device */
-    const int32_t* col;         /* device, [nnz] column indices, 0 <= col < n_cols     */
-    const float* val;           /* device, [nnz] normalized adjacency values           */
+    const int32_t* col;         /* device, [nnz] column indices, 0 <= col < n_cols;    */
+    const float* val;           /* [nnz] values.  Both may be NULL when nnz == 0.      */
     const float* x;             /* device, dense operand of relation 0                 */
     float* out;                 /* device, [n_chunks][n_rows][d]                       */
     const int32_t* rel_map;     /* device, [n_rels] or NULL (identity)                 */

@@ -177,7 +177,7 @@ def test_decoder_score(K, d, diag):
     n_r, n_c, npairs = 300, 200, 1000 + 17
     U = rng.standard_normal((n_r, d)).astype(np.float32)
     V = rng.standard_normal((n_c, d)).astype(np.float32)
-    G = rng.standard_normal((d, d)).astype(np.float32) / np.sqrt(d)
+    G = (rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)
     l = rng.standard_normal(d).astype(np.float32) if diag else None
     ri = rng.integers(0, n_r, npairs).astype(np.int32)
     ci = rng.integers(0, n_c, npairs).astype(np.int32)
