@@ -19,7 +19,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -38,8 +38,15 @@ class DgRelGroup(ctypes.Structure):
         ("n_rows", c_int32),
         ("n_rels", c_int32),
         ("chunk", c_int32),
-        ("reserved", c_int32 * 4),
+        ("n_cols", c_int32),
+        ("x_rels", c_int32),
+        ("reserved", c_int32 * 2),
     ]
+
+
+class DgFusedTarget(ctypes.Structure):
+    _fields_ = [("out", c_void_p), ("n_rows", c_int32), ("g_begin", c_int32), ("g_count", c_int32),
+                ("flags", c_int32)]
 
 
 class DgEpiGroup(ctypes.Structure):
@@ -76,7 +83,12 @@ SIGNATURES = {
     "dg_spmm_groups_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_csr_f32": (
         c_int32,
-        [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p],
+        [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32,
+         c_void_p],
+    ),
+    "dg_gcn_fused_f32": (
+        c_int32,
+        [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32, c_void_p],
     ),
     "dg_gcn_epilogue_f32": (
         c_int32,

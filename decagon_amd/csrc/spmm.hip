@@ -20,6 +20,18 @@
 //   one XCD's L2 while all its rows are processed.
 #include "common.h"
 
+#define DG_LP_SWITCH(LPV, CALL)                     \
+    switch (LPV) {                                  \
+        case 1: CALL(1); break;                     \
+        case 2: CALL(2); break;                     \
+        case 4: CALL(4); break;                     \
+        case 8: CALL(8); break;                     \
+        case 16: CALL(16); break;                   \
+        case 32: CALL(32); break;                   \
+        case 64: CALL(64); break;                   \
+        default: return DG_EINVAL;                  \
+    }
+
 namespace {
 
 struct SpmmGroupK {
@@ -29,8 +41,8 @@ struct SpmmGroupK {
     const float* x;
     float* out;
     const int32_t* rel_map;
-    int64_t x_rel_stride;
-    int64_t x_ld;
+    int32_t x_rel_stride;  // elements (the host guarantees every offset fits in int32)
+    int32_t x_ld;
     int32_t rowptr_rel_stride;
     int32_t n_rows;
     int32_t n_rels;
@@ -47,22 +59,109 @@ struct SpmmArgs {
     int32_t d;
 };
 
-constexpr int kRowsPerBlock = 4;  // 4 waves x 1 row
+constexpr int kRowsPerBlock = 4;  // partial mode: 4 waves x 1 row
+constexpr int kUnroll = 8;        // gathers in flight per lane
 
+// Sum over the nonzeros of row r in relations [k0, k1) of group g:
+//   acc = sum_k sum_{p in row r of A_k} val[p] * X_{rel(k)}[col[p]][:]
+// The row's segments in the (up to 64) relations of a batch are flattened into one index
+// space: lane t holds segment t (begin, length, X offset of its relation); an inclusive
+// wave scan of the lengths gives each segment's flat start.  Every 64 flat positions are
+// then mapped back to (segment, position) by a 6-step binary search over the scan
+// (ds_bpermute), loaded with one coalesced col/val load and consumed G per step by the
+// LP-lane groups with kUnroll 16-byte gathers in flight.  Returns the folded row in lanes
+// 0..LP-1 (lane q holds columns 4q..4q+3).
 template <int LP>
-__global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
-    constexpr int G = dg::kWave / LP;  // nonzeros consumed per wave step
+__device__ __forceinline__ float4 row_sum(const SpmmGroupK& g, int r, int k0, int k1, int d) {
+    constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
     const int sub = lane / LP;
     const int q = lane % LP;
-    const int b = blockIdx.x;
+    const bool qact = q * 4 < d;
+    const float* __restrict__ xq = g.x + q * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int kb = k0; kb < k1; kb += 64) {
+        const int nk = min(64, k1 - kb);
+        int sbeg = 0, slen = 0, xoff = 0;
+        if (lane < nk) {
+            const int32_t* rp = g.rowptr + (int64_t)(kb + lane) * g.rowptr_rel_stride + r;
+            sbeg = rp[0];
+            slen = rp[1] - sbeg;
+            const int rel = g.rel_map ? g.rel_map[kb + lane] : kb + lane;
+            xoff = rel * g.x_rel_stride;
+        }
+        int cum = slen;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(cum, o);
+            if (lane >= o) cum += t;
+        }
+        const int total = __shfl(cum, 63);
+        const int excl = cum - slen;
+#pragma unroll 1
+        for (int base = 0; base < total; base += 64) {
+            const int f = base + lane;
+            int lo = 0, hi = 63;
+#pragma unroll
+            for (int it = 0; it < 6; ++it) {
+                const int mid = (lo + hi) >> 1;
+                if (__shfl(cum, mid) > f)
+                    hi = mid;
+                else
+                    lo = mid + 1;
+            }
+            const int p = __shfl(sbeg, lo) + (f - __shfl(excl, lo));
+            const int xo = __shfl(xoff, lo);
+            int eoff = 0;
+            float v = 0.f;
+            if (f < total) {
+                eoff = xo + g.col[p] * g.x_ld;
+                v = g.val[p];
+            }
+            const int n = min(64, total - base);
+#pragma unroll 1
+            for (int s0 = 0; s0 < n; s0 += kUnroll * G) {
+                int o[kUnroll];
+                float w[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const int src = (s0 + u * G + sub) & 63;
+                    o[u] = __shfl(eoff, src);
+                    w[u] = __shfl(v, src);
+                }
+                float4 xv[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const bool ok = qact && (s0 + u * G + sub) < n;
+                    xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (!ok) w[u] = 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) dg::fma4(acc, w[u], xv[u]);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+    return acc;
+}
 
+template <int LP>
+__device__ __forceinline__ const SpmmGroupK& find_group(const SpmmArgs& args, int b) {
     int gi = 0;
 #pragma unroll 1
     while (gi + 1 < args.n_groups && b >= args.g[gi + 1].block_begin) ++gi;
-    const SpmmGroupK& g = args.g[gi];
+    return args.g[gi];
+}
 
+// Partial mode: one wave per (chunk, row); writes out[c][r][:].
+template <int LP>
+__global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int b = blockIdx.x;
+    const SpmmGroupK& g = find_group<LP>(args, b);
     // XCD-contiguous item map: local block lb runs on XCD label lb % 8.
     const int lb = b - g.block_begin;
     const int per = g.n_blocks >> 3;
@@ -71,71 +170,70 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
     const int c = item / g.row_blocks;
     const int r = (item - c * g.row_blocks) * kRowsPerBlock + wave;
     if (r >= g.n_rows) return;  // wave-uniform; no barriers in this kernel
-
     const int d = args.d;
-    const bool qact = q * 4 < d;
     const int k0 = c * g.chunk;
-    const int k1 = min(k0 + g.chunk, g.n_rels);
-    const float* __restrict__ xq = g.x + q * 4;
-    const int32_t* __restrict__ colp = g.col;
-    const float* __restrict__ valp = g.val;
+    const float4 acc = row_sum<LP>(g, r, k0, min(k0 + g.chunk, g.n_rels), d);
+    if (lane < LP && lane * 4 < d)
+        *reinterpret_cast<float4*>(g.out + ((int64_t)c * g.n_rows + r) * d + lane * 4) = acc;
+}
 
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+// Fused mode (every group of a node type in one chunk): one workgroup per output row r of
+// node type i, one wave per group (i, j); each wave L2-normalises its group's row sum
+// (layers.py:93), the waves meet in LDS and wave 0 adds the groups in order and applies
+// relu (model.py:75) or not (model.py:88).
+struct FusedTargetK {
+    float* out;
+    int32_t n_rows;
+    int32_t g_begin;
+    int32_t g_count;
+    int32_t relu;
+    int32_t block_begin;
+    int32_t pad;
+};
+
+struct FusedArgs {
+    SpmmGroupK g[DG_MAX_GROUPS];
+    FusedTargetK t[DG_MAX_GROUPS];
+    int32_t n_groups;
+    int32_t n_targets;
+    int32_t d;
+    int32_t pad;
+};
+
+template <int LP>
+__global__ __launch_bounds__(512) void gcn_fused_kernel(const FusedArgs a) {
+    __shared__ float4 ybuf[DG_MAX_GROUPS][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int b = blockIdx.x;
+    int ti = 0;
 #pragma unroll 1
-    for (int kb = k0; kb < k1; kb += 64) {
-        const int nk = min(64, k1 - kb);
-        int beg_l = 0, end_l = 0, rel_l = kb + lane;
-        if (lane < nk) {
-            const int32_t* rp = g.rowptr + (int64_t)(kb + lane) * g.rowptr_rel_stride + r;
-            beg_l = rp[0];
-            end_l = rp[1];
-            if (g.rel_map) rel_l = g.rel_map[kb + lane];
-        }
-#pragma unroll 1
-        for (int t = 0; t < nk; ++t) {
-            const int beg = __builtin_amdgcn_readlane(beg_l, t);
-            const int end = __builtin_amdgcn_readlane(end_l, t);
-            const int rel = __builtin_amdgcn_readlane(rel_l, t);
-            const float* __restrict__ X = xq + (int64_t)rel * g.x_rel_stride;
-#pragma unroll 1
-            for (int base = beg; base < end; base += 64) {
-                const int n = min(64, end - base);
-                int cl = 0;
-                float vl = 0.f;
-                if (lane < n) {
-                    cl = colp[base + lane];
-                    vl = valp[base + lane];
-                }
-                // Four steps per trip: all bpermutes, then all gathers, then the FMAs,
-                // so four 16-byte gathers per lane are in flight at once.
-                for (int s0 = 0; s0 < n; s0 += 4 * G) {
-                    int cc[4];
-                    float vv[4];
+    while (ti + 1 < a.n_targets && b >= a.t[ti + 1].block_begin) ++ti;
+    const FusedTargetK& t = a.t[ti];
+    const int r = b - t.block_begin;
+    const int d = a.d;
+    if (wave < t.g_count) {
+        const SpmmGroupK& g = a.g[t.g_begin + wave];
+        float4 s = row_sum<LP>(g, r, 0, g.n_rels, d);
+        // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); lanes >= LP hold copies
+        float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
+        if (lane * 4 >= d) ss = 0.f;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int src = (s0 + u * G + sub) & 63;
-                        cc[u] = __shfl(cl, src);
-                        vv[u] = __shfl(vl, src);
-                    }
-                    float4 xv[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const bool ok = qact && (s0 + u * G + sub) < n;
-                        xv[u] = ok ? *reinterpret_cast<const float4*>(X + (int64_t)cc[u] * g.x_ld)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-                        if (!ok) vv[u] = 0.f;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) dg::fma4(acc, vv[u], xv[u]);
-                }
-            }
-        }
+        for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
+        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+        if (lane < LP) ybuf[wave][lane] = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
     }
-#pragma unroll
-    for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
-    if (sub == 0 && qact) {
-        float* o = g.out + ((int64_t)c * g.n_rows + r) * d + q * 4;
-        *reinterpret_cast<float4*>(o) = acc;
+    __syncthreads();
+    if (wave == 0 && lane < LP && lane * 4 < d) {
+        float4 tot = ybuf[0][lane];
+        for (int w = 1; w < t.g_count; ++w) dg::add4(tot, ybuf[w][lane]);
+        if (t.relu) {
+            tot.x = fmaxf(tot.x, 0.f);
+            tot.y = fmaxf(tot.y, 0.f);
+            tot.z = fmaxf(tot.z, 0.f);
+            tot.w = fmaxf(tot.w, 0.f);
+        }
+        *reinterpret_cast<float4*>(t.out + (int64_t)r * d + lane * 4) = tot;
     }
 }
 
@@ -208,21 +306,42 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
     if (active) *reinterpret_cast<float4*>(a.out + off) = tot;
 }
 
-#define DG_LP_SWITCH(LPV, CALL)                     \
-    switch (LPV) {                                  \
-        case 1: CALL(1); break;                     \
-        case 2: CALL(2); break;                     \
-        case 4: CALL(4); break;                     \
-        case 8: CALL(8); break;                     \
-        case 16: CALL(16); break;                   \
-        case 32: CALL(32); break;                   \
-        case 64: CALL(64); break;                   \
-        default: return DG_EINVAL;                  \
-    }
-
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 2; }
+extern "C" int32_t dg_abi_version(void) { return 3; }
+
+namespace {
+
+// Validate one descriptor and copy it into the kernel form.  Returns DG_OK or an error.
+int convert_group(const dg_rel_group& s, int d, SpmmGroupK& k) {
+    if (s.n_rows < 0 || s.n_rels < 0 || s.chunk < 1 || s.rowptr_rel_stride < 0 || s.n_cols < 0)
+        return DG_EINVAL;
+    // col/val may be NULL for a group without nonzeros (rowptr all zero: never read)
+    if (!s.rowptr || !s.x || !s.out) return DG_EINVAL;
+    if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || (s.x_ld & 3) || (s.x_rel_stride & 3))
+        return DG_EALIGN;
+    if (s.x_ld < d || s.x_rel_stride < 0) return DG_EINVAL;
+    const int64_t x_rels = s.x_rels > 0 ? s.x_rels : s.n_rels;
+    const int64_t span = (x_rels - 1) * s.x_rel_stride + (int64_t)(s.n_cols > 0 ? s.n_cols - 1 : 0) * s.x_ld + d;
+    if (span > 0x7fffffffLL) return DG_EINVAL;  // gathers use 32-bit element offsets
+    k.rowptr = s.rowptr;
+    k.col = s.col;
+    k.val = s.val;
+    k.x = s.x;
+    k.out = s.out;
+    k.rel_map = s.rel_map;
+    k.x_rel_stride = static_cast<int32_t>(s.x_rel_stride);
+    k.x_ld = static_cast<int32_t>(s.x_ld);
+    k.rowptr_rel_stride = s.rowptr_rel_stride;
+    k.n_rows = s.n_rows;
+    k.n_rels = s.n_rels;
+    k.chunk = s.chunk;
+    k.n_chunks = dg::ceil_div(s.n_rels, s.chunk);
+    k.row_blocks = dg::ceil_div(s.n_rows, kRowsPerBlock);
+    return DG_OK;
+}
+
+}  // namespace
 
 extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, int32_t d,
                                   void* stream) {
@@ -235,29 +354,11 @@ extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, 
     int ng = 0;
     for (int i = 0; i < n_groups; ++i) {
         const dg_rel_group& s = groups[i];
-        if (s.n_rows < 0 || s.n_rels < 0 || s.chunk < 1 || s.rowptr_rel_stride < 0)
-            return DG_EINVAL;
         if (s.n_rows == 0 || s.n_rels == 0) continue;
-        // col/val may be NULL for a group without nonzeros (rowptr all zero: never read)
-        if (!s.rowptr || !s.x || !s.out) return DG_EINVAL;
-        if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || (s.x_ld & 3) || (s.x_rel_stride & 3))
-            return DG_EALIGN;
-        if (s.x_ld < d) return DG_EINVAL;
-        SpmmGroupK& k = args.g[ng++];
-        k.rowptr = s.rowptr;
-        k.col = s.col;
-        k.val = s.val;
-        k.x = s.x;
-        k.out = s.out;
-        k.rel_map = s.rel_map;
-        k.x_rel_stride = s.x_rel_stride;
-        k.x_ld = s.x_ld;
-        k.rowptr_rel_stride = s.rowptr_rel_stride;
-        k.n_rows = s.n_rows;
-        k.n_rels = s.n_rels;
-        k.chunk = s.chunk;
-        k.n_chunks = dg::ceil_div(s.n_rels, s.chunk);
-        k.row_blocks = dg::ceil_div(s.n_rows, kRowsPerBlock);
+        SpmmGroupK& k = args.g[ng];
+        const int rc = convert_group(s, d, k);
+        if (rc != DG_OK) return rc;
+        ++ng;
         const int64_t items = (int64_t)k.n_chunks * k.row_blocks;
         k.n_blocks = static_cast<int32_t>(8 * ((items + 7) / 8));
         k.block_begin = static_cast<int32_t>(blocks);
@@ -275,9 +376,56 @@ extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, 
     return dg::launch_status();
 }
 
+extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
+                                const dg_fused_target* targets, int32_t n_targets, int32_t d,
+                                void* stream) {
+    if (n_groups < 1 || !groups || n_targets < 1 || !targets) return DG_EINVAL;
+    if (n_groups > DG_MAX_GROUPS || n_targets > DG_MAX_GROUPS) return DG_ETOOMANY;
+    if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
+    FusedArgs a{};
+    a.d = d;
+    a.n_groups = n_groups;
+    a.n_targets = n_targets;
+    for (int i = 0; i < n_groups; ++i) {
+        dg_rel_group s = groups[i];
+        s.chunk = s.n_rels > 0 ? s.n_rels : 1;
+        if (!s.out) s.out = targets[0].out;  // unused in fused mode
+        const int rc = convert_group(s, d, a.g[i]);
+        if (rc != DG_OK) return rc;
+    }
+    int64_t blocks = 0;
+    int max_waves = 1;
+    for (int t = 0; t < n_targets; ++t) {
+        const dg_fused_target& s = targets[t];
+        if (!s.out || !dg::aligned16(s.out) || s.n_rows < 0 || s.g_count < 1 || s.g_begin < 0 ||
+            s.g_begin + s.g_count > n_groups || (s.flags & ~DG_EPI_RELU))
+            return DG_EINVAL;
+        for (int g = s.g_begin; g < s.g_begin + s.g_count; ++g)
+            if (a.g[g].n_rows != s.n_rows) return DG_EINVAL;
+        FusedTargetK& k = a.t[t];
+        k.out = s.out;
+        k.n_rows = s.n_rows;
+        k.g_begin = s.g_begin;
+        k.g_count = s.g_count;
+        k.relu = (s.flags & DG_EPI_RELU) ? 1 : 0;
+        k.block_begin = static_cast<int32_t>(blocks);
+        blocks += s.n_rows;
+        max_waves = s.g_count > max_waves ? s.g_count : max_waves;
+    }
+    if (blocks == 0) return DG_OK;
+    if (blocks > 0x7fffffff) return DG_EINVAL;
+    const int lp = dg::lanes_per_row(d);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(blocks)), block(64 * max_waves);
+#define DG_LAUNCH_FUSED(L) hipLaunchKernelGGL(gcn_fused_kernel<L>, grid, block, 0, st, a)
+    DG_LP_SWITCH(lp, DG_LAUNCH_FUSED)
+#undef DG_LAUNCH_FUSED
+    return dg::launch_status();
+}
+
 extern "C" int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
-                               int32_t n_rows, const float* x, int64_t ldx, float* y,
-                               int64_t ldy, int32_t d, void* stream) {
+                               int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx,
+                               float* y, int64_t ldy, int32_t d, void* stream) {
     if (ldy != d) return DG_EINVAL;
     dg_rel_group g{};
     g.rowptr = rowptr;
@@ -291,6 +439,7 @@ extern "C" int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const 
     g.n_rows = n_rows;
     g.n_rels = 1;
     g.chunk = 1;
+    g.n_cols = n_cols;
     return dg_spmm_groups_f32(&g, 1, d, stream);
 }
 

@@ -175,33 +175,22 @@ class ForwardPlan:
                 self._pre.append(kernels.PreparedSpmm([spec], h1))
             x1[et] = (xw, n[j] * h1, h1, n_loc)  # local order already applied
 
-        # ---- layer 1 SpMM ----
-        self.partial1: Dict[EdgeType, Tuple[torch.Tensor, int]] = {}
-        specs1 = []
+        self.hidden1 = {i: torch.empty((n[i], h1), **f32) for i in self.targets}
+        self.embeddings = {i: torch.empty((n[i], h2), **f32) for i in self.targets}
+
+        # ---- layer 1: Σ_k Â_k·X_k (+ epilogue) ----
+        x1_specs = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
             xt, xs, xld, x_rels = x1[et]
             local_x = features.get(et[1]) is not None
-            ch = chunk_override or choose_chunk(grp.n_rels, grp.n_rows, grp.nnz, h1, target_waves)
-            nch = max(1, -(-grp.n_rels // ch)) if grp.n_rels else 1
-            part = torch.zeros((nch, grp.n_rows, h1), **f32)
-            self.partial1[et] = (part, nch)
-            if grp.n_rels:
-                specs1.append(kernels.RelGroupSpec(
-                    grp.rowptr, grp.col, grp.val, xt, part, grp.n_rows, grp.n_cols, grp.n_rels, ch,
-                    xs, xld, grp.n_rows,
-                    rel_map=None if local_x else grp.rel_map, x_rels=x_rels,
-                    rel_map_max=None if (local_x or grp.rel_map is None) else int(grp.rel_ids.max())))
-        self._spmm1 = [kernels.PreparedSpmm(specs1[s:s + DG_MAX_GROUPS], h1)
-                       for s in range(0, len(specs1), DG_MAX_GROUPS)]
+            x1_specs[et] = (xt, xs, xld, x_rels, None if local_x else grp.rel_map)
+        self._layer1 = self._build_layer(x1_specs, h1, True, chunk_override, target_waves, f32)
 
-        # ---- layer 2 projection + SpMM ----
+        # ---- layer 2: P_k = H1_j·W2_k, then Σ_k Â_k·P_k (+ epilogue) ----
         self.proj: Dict[EdgeType, torch.Tensor] = {}
-        self.partial2: Dict[EdgeType, Tuple[torch.Tensor, int]] = {}
-        self.hidden1 = {i: torch.empty((n[i], h1), **f32) for i in self.targets}
-        self.embeddings = {i: torch.empty((n[i], h2), **f32) for i in self.targets}
         self._gemm2 = []
-        specs2 = []
+        x2_specs = {}
         for et in self.edge_types:
             i, j = et
             grp = dgraph.groups[et]
@@ -213,90 +202,143 @@ class ForwardPlan:
                 raise ValueError(f"node type {j} has no incoming edge type; layer 2 needs hidden1[{j}]")
             P = torch.empty((max(1, grp.n_rels), n[j], h2), **f32)
             self.proj[et] = P
-            ch = chunk_override or choose_chunk(grp.n_rels, grp.n_rows, grp.nnz, h2, target_waves)
-            nch = max(1, -(-grp.n_rels // ch)) if grp.n_rels else 1
-            part = torch.zeros((nch, grp.n_rows, h2), **f32)
-            self.partial2[et] = (part, nch)
+            x2_specs[et] = (P, n[j] * h2, h2, max(1, grp.n_rels), None)
             if not grp.n_rels:
                 continue
-            H = self.hidden1[j]
             self._gemm2.append(kernels.PreparedGemm(
-                H, (0, h1, 1), W, (h1 * h2, h2, 1), P, (n[j] * h2, h2, 1),
+                self.hidden1[j], (0, h1, 1), W, (h1 * h2, h2, 1), P, (n[j] * h2, h2, 1),
                 n[j], h2, h1, grp.n_rels, b_map=grp.rel_map, b_batches=K,
                 b_map_max=int(grp.rel_ids.max()) if grp.rel_map is not None else None))
-            specs2.append(kernels.RelGroupSpec(
-                grp.rowptr, grp.col, grp.val, P, part, grp.n_rows, grp.n_cols, grp.n_rels, ch,
-                n[j] * h2, h2, grp.n_rows))
-        self._spmm2 = [kernels.PreparedSpmm(specs2[s:s + DG_MAX_GROUPS], h2)
-                       for s in range(0, len(specs2), DG_MAX_GROUPS)]
+        self._layer2 = self._build_layer(x2_specs, h2, False, chunk_override, target_waves, f32)
 
-        # ---- epilogues (and the cross-rank sum when sharded) ----
-        self._epi1 = self._make_epilogue(self.partial1, self.hidden1, h1, DG_EPI_L2NORM | DG_EPI_RELU, f32)
-        self._epi2 = self._make_epilogue(self.partial2, self.embeddings, h2, DG_EPI_L2NORM, f32)
-
-    def _make_epilogue(self, partials, outs, d, flags, f32):
-        """Returns (reduce_launches, flat_sum_buffer or None, epilogue_launches)."""
-        n = self.g.n_nodes
-        if self.allreduce is None:
-            epis = [kernels.PreparedEpilogue([partials[et] for et in self.targets[i]], outs[i], n[i], d, flags)
-                    for i in self.targets]
-            return [], None, epis
-        # sharded: per-group chunk reduce into one flat buffer, all-reduce, then epilogue
-        sizes = [self.g.groups[et].n_rows * d for et in self.edge_types]
-        flat = torch.zeros(int(sum(sizes)), **f32)
-        views, off = {}, 0
-        for et, sz in zip(self.edge_types, sizes):
-            views[et] = flat[off:off + sz]
-            off += sz
-        reds = []
+    # ------------------------------------------------------------------ layer builder
+    def _build_layer(self, x_specs, d, relu, chunk_override, target_waves, f32):
+        """Prepared launches of one layer.  Per node type i: if every group (i, j) fits one
+        chunk and no cross-rank sum is needed, the whole target runs in the fused kernel
+        (SpMM + l2norm + Σ_j + relu, one launch for all such targets); otherwise its groups
+        run in partial mode (chunked sums) followed by the epilogue — with, when sharded,
+        the chunk reduce into the all-reduce buffer and the all-reduce before it."""
+        g = self.g
+        n = g.n_nodes
+        outs = self.hidden1 if relu else self.embeddings
+        chunk, nch = {}, {}
         for et in self.edge_types:
-            if self.g.groups[et].n_rels:
-                reds.append(kernels.PreparedEpilogue([partials[et]], views[et], self.g.groups[et].n_rows, d, 0))
-        epis = [kernels.PreparedEpilogue([(views[et], 1) for et in self.targets[i]], outs[i], n[i], d, flags)
-                for i in self.targets]
-        return reds, flat, epis
+            grp = g.groups[et]
+            c = chunk_override or choose_chunk(grp.n_rels, grp.n_rows, grp.nnz, d, target_waves)
+            chunk[et] = max(1, min(c, max(1, grp.n_rels)))
+            nch[et] = max(1, -(-grp.n_rels // chunk[et])) if grp.n_rels else 1
 
-    def _run_epilogue(self, epi) -> None:
-        reds, flat, epis = epi
-        if flat is not None:
-            if len(reds) < len(self.edge_types):
-                flat.zero_()  # groups without local relations contribute zeros
-            for r in reds:
-                r()
-            self.allreduce(flat)
-        for e in epis:
-            e()
+        def spec(et, out, ch):
+            grp = g.groups[et]
+            xt, xs, xld, x_rels, rmap = x_specs[et]
+            return kernels.RelGroupSpec(
+                grp.rowptr, grp.col, grp.val, xt, out, grp.n_rows, grp.n_cols, grp.n_rels, ch, xs, xld,
+                grp.n_rows, rel_map=rmap, x_rels=x_rels,
+                rel_map_max=int(grp.rel_ids.max()) if rmap is not None else None)
+
+        fused_t = []
+        if self.allreduce is None:
+            fused_t = [i for i, ets in self.targets.items()
+                       if all(nch[et] == 1 and g.groups[et].n_rels > 0 for et in ets)]
+        launches: List[Callable[[], None]] = []
+        if fused_t:
+            launches.append(kernels.PreparedFused(
+                [(outs[i], n[i], [spec(et, None, max(1, g.groups[et].n_rels)) for et in self.targets[i]], relu)
+                 for i in fused_t], d))
+        rest = [et for et in self.edge_types if et[0] not in fused_t]
+        flags = DG_EPI_L2NORM | (DG_EPI_RELU if relu else 0)
+        flat, views = None, {}
+        if self.allreduce is not None and rest:
+            sizes = [g.groups[et].n_rows * d for et in rest]
+            flat = torch.zeros(int(sum(sizes)), **f32)
+            off = 0
+            for et, sz in zip(rest, sizes):
+                views[et] = flat[off:off + sz]
+                off += sz
+        partials, specs, reduces = {}, [], []
+        for et in rest:
+            grp = g.groups[et]
+            if flat is not None and nch[et] == 1:
+                part = views[et]  # single chunk: the SpMM writes the group sum in place
+            else:
+                part = torch.zeros((nch[et], grp.n_rows, d), **f32)
+                if flat is not None and grp.n_rels:
+                    reduces.append(kernels.PreparedEpilogue([(part, nch[et])], views[et], grp.n_rows, d, 0))
+            partials[et] = (part, nch[et])
+            if grp.n_rels:
+                specs.append(spec(et, part, chunk[et]))
+        launches += [kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d)
+                     for s in range(0, len(specs), DG_MAX_GROUPS)]
+        launches += reduces
+        need_zero = flat is not None and any(g.groups[et].n_rels == 0 for et in rest)
+        epis = []
+        for i in self.targets:
+            if i in fused_t:
+                continue
+            src = [(views[et], 1) if flat is not None else partials[et] for et in self.targets[i]]
+            epis.append(kernels.PreparedEpilogue(src, outs[i], n[i], d, flags))
+        return _Layer(launches, flat, need_zero, self.allreduce, epis, chunk, nch, fused_t)
 
     def run_layer1(self) -> None:
         for p in self._pre:
             p()
-        for s in self._spmm1:
-            s()
-        self._run_epilogue(self._epi1)
+        self._layer1.run()
 
     def run_layer2(self) -> None:
         for gm in self._gemm2:
             gm()
-        for s in self._spmm2:
-            s()
-        self._run_epilogue(self._epi2)
+        self._layer2.run()
 
     def run(self) -> None:
         self.run_layer1()
         self.run_layer2()
 
+    @property
+    def spmm_launches(self):
+        """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""
+        pick = lambda L: [l for l in L.launches if isinstance(l, (kernels.PreparedSpmm, kernels.PreparedFused))]
+        return pick(self._layer1), pick(self._layer2)
+
     # ---- accounting (bench / DESIGN.md roofline) ----
     def layer_bytes(self, layer: int) -> int:
-        """Algorithmic (compulsory) HBM bytes of one layer's SpMM launch: every CSR array
-        once (rowptr 4 B/row/relation, col+val 8 B/nonzero), every distinct dense operand
-        X_k once (4·d B per row), every partial written once (4·d B per row)."""
+        """Algorithmic (compulsory) HBM bytes of one layer's SpMM launches: every CSR array
+        once (rowptr 4 B per row per relation, col+val 8 B per nonzero), every distinct
+        dense operand X_k once (4·d B per row of X_k), and the output once — 4·d B per row
+        per chunk partial in partial mode, per output row in fused mode."""
+        L = self._layer1 if layer == 1 else self._layer2
         d = self.h1 if layer == 1 else self.h2
-        parts = self.partial1 if layer == 1 else self.partial2
         tot = 0
         for et, grp in self.g.groups.items():
             if not grp.n_rels:
                 continue
             tot += 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz
             tot += 4 * d * grp.n_cols * grp.n_rels
-            tot += 4 * d * grp.n_rows * parts[et][1]
+            if et[0] not in L.fused_targets:
+                tot += 4 * d * grp.n_rows * L.n_chunks[et]
+        for i in L.fused_targets:
+            tot += 4 * d * self.g.n_nodes[i]
         return tot
+
+
+class _Layer:
+    """The prepared launches of one layer and how to run them."""
+
+    def __init__(self, launches, flat, need_zero, allreduce, epilogues, chunk, n_chunks, fused_targets):
+        self.launches = launches
+        self.flat = flat
+        self.need_zero = need_zero
+        self.allreduce = allreduce
+        self.epilogues = epilogues
+        self.chunk = chunk
+        self.n_chunks = n_chunks
+        self.fused_targets = fused_targets
+
+    def run(self) -> None:
+        if self.need_zero:
+            self.flat.zero_()  # groups without local relations contribute zeros
+        for l in self.launches:
+            l()
+        if self.flat is not None:
+            self.allreduce(self.flat)
+        for e in self.epilogues:
+            e()

@@ -17,7 +17,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import DgEpiGroup, DgGemmDesc, DgRelGroup, check
+from ._lib import DgEpiGroup, DgFusedTarget, DgGemmDesc, DgRelGroup, check
 
 
 def _stream_ptr(stream: Optional[torch.cuda.Stream] = None) -> int:
@@ -40,6 +40,11 @@ def _dev(t: torch.Tensor, dtype: torch.dtype, what: str) -> torch.Tensor:
 # --------------------------------------------------------------------------------------
 # SpMM over relation groups
 # --------------------------------------------------------------------------------------
+def need_x_span(s, d: int) -> int:
+    x_rels = s.n_rels if s.x_rels is None else s.x_rels
+    return (x_rels - 1) * s.x_rel_stride + max(s.n_cols - 1, 0) * s.x_ld + d
+
+
 @dataclass
 class RelGroupSpec:
     """One (i,j) group (or any set of relations sharing n_rows) for dg_spmm_groups_f32."""
@@ -48,7 +53,7 @@ class RelGroupSpec:
     col: torch.Tensor             # int32
     val: torch.Tensor             # float32
     x: torch.Tensor               # float32, dense operand storage
-    out: torch.Tensor             # float32, [n_chunks, n_rows, d]
+    out: Optional[torch.Tensor]   # float32, [n_chunks, n_rows, d] (None in fused mode)
     n_rows: int
     n_cols: int
     n_rels: int
@@ -65,12 +70,13 @@ class RelGroupSpec:
     def n_chunks(self) -> int:
         return -(-self.n_rels // self.chunk)
 
-    def validate(self, d: int) -> None:
+    def validate(self, d: int, need_out: bool = True) -> None:
         _dev(self.rowptr, torch.int32, "rowptr")
         _dev(self.col, torch.int32, "col")
         _dev(self.val, torch.float32, "val")
         _dev(self.x, torch.float32, "x")
-        _dev(self.out, torch.float32, "out")
+        if need_out or self.out is not None:
+            _dev(self.out, torch.float32, "out")
         if self.n_rows == 0 or self.n_rels == 0:
             return
         if self.chunk < 1:
@@ -94,8 +100,27 @@ class RelGroupSpec:
             raise ValueError(f"x has {self.x.numel()} elements, kernel may read {need_x}")
         if self.x_ld < d:
             raise ValueError("x_ld < d")
-        if self.out.numel() < self.n_chunks * self.n_rows * d:
+        if need_out and self.out.numel() < self.n_chunks * self.n_rows * d:
             raise ValueError("out too small for [n_chunks, n_rows, d]")
+        if need_x_span(self, d) >= 2**31:
+            raise ValueError("dense operand too large for 32-bit gather offsets")
+
+
+def _fill_group(g, s: "RelGroupSpec") -> None:
+    g.rowptr = s.rowptr.data_ptr()
+    g.col = s.col.data_ptr()
+    g.val = s.val.data_ptr()
+    g.x = s.x.data_ptr() + 4 * s.x_offset
+    g.out = s.out.data_ptr() if s.out is not None else None
+    g.rel_map = s.rel_map.data_ptr() if s.rel_map is not None else None
+    g.x_rel_stride = s.x_rel_stride
+    g.x_ld = s.x_ld
+    g.rowptr_rel_stride = s.rowptr_rel_stride
+    g.n_rows = s.n_rows
+    g.n_rels = s.n_rels
+    g.chunk = s.chunk
+    g.n_cols = s.n_cols
+    g.x_rels = s.n_rels if s.x_rels is None else s.x_rels
 
 
 class PreparedSpmm:
@@ -111,24 +136,47 @@ class PreparedSpmm:
         arr = (DgRelGroup * max(1, len(specs)))()
         for i, s in enumerate(specs):
             g = arr[i]
-            g.rowptr = s.rowptr.data_ptr()
-            g.col = s.col.data_ptr()
-            g.val = s.val.data_ptr()
-            g.x = s.x.data_ptr() + 4 * s.x_offset
-            g.out = s.out.data_ptr()
-            g.rel_map = s.rel_map.data_ptr() if s.rel_map is not None else None
-            g.x_rel_stride = s.x_rel_stride
-            g.x_ld = s.x_ld
-            g.rowptr_rel_stride = s.rowptr_rel_stride
-            g.n_rows = s.n_rows
-            g.n_rels = s.n_rels
-            g.chunk = s.chunk
+            _fill_group(g, s)
         self._arr = arr
         self._n = len(specs)
         self._fn = _lib.load().dg_spmm_groups_f32
 
     def __call__(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_groups_f32")
+
+
+class PreparedFused:
+    """A fixed dg_gcn_fused_f32 launch: targets = [(out tensor, n_rows, [group specs], relu)]."""
+
+    def __init__(self, targets, d: int):
+        specs, tarr = [], (DgFusedTarget * len(targets))()
+        for t, (out, n_rows, gspecs, relu) in enumerate(targets):
+            _dev(out, torch.float32, "out")
+            if out.numel() < n_rows * d:
+                raise ValueError("fused output too small")
+            tarr[t].out = out.data_ptr()
+            tarr[t].n_rows = n_rows
+            tarr[t].g_begin = len(specs)
+            tarr[t].g_count = len(gspecs)
+            tarr[t].flags = _lib.DG_EPI_RELU if relu else 0
+            for s in gspecs:
+                if s.n_rows != n_rows:
+                    raise ValueError("group rows != target rows")
+                s.validate(d, need_out=False)
+                specs.append(s)
+        if len(specs) > _lib.DG_MAX_GROUPS or len(targets) > _lib.DG_MAX_GROUPS:
+            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups / targets per fused launch")
+        garr = (DgRelGroup * len(specs))()
+        for i, s in enumerate(specs):
+            _fill_group(garr[i], s)
+        self._keep = (specs, [t[0] for t in targets])
+        self._garr, self._tarr = garr, tarr
+        self._ng, self._nt, self.d = len(specs), len(targets), d
+        self._fn = _lib.load().dg_gcn_fused_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(self._garr, self._ng, self._tarr, self._nt, self.d, _stream_ptr(stream)),
+              "dg_gcn_fused_f32")
 
 
 def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:

@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (2); bumped whenever a struct layout or a signature changes. */
+/* ABI version (3); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -54,7 +54,8 @@ int32_t dg_abi_version(void);
  * Replaces: tf.sparse_tensor_dense_matmul(adj_mats[edge_type][k], x)  layers.py:90, :114
  *           tf.sparse_tensor_dense_matmul(x, weights_k) (sparse features) layers.py:89
  *           tf.add_n(outputs)                                         layers.py:92, :116
- * Requirements: d % 4 == 0, 4 <= d <= 256, x and x_ld 16-byte aligned (x_ld % 4 == 0).
+ * Requirements: d % 4 == 0, 4 <= d <= 256, x and x_ld 16-byte aligned (x_ld % 4 == 0), and
+ * (x_rels-1)*x_rel_stride + (n_cols-1)*x_ld + d < 2^31 (gathers use 32-bit offsets).
  * -------------------------------------------------------------------------------------- */
 typedef struct dg_rel_group {
     const int32_t* rowptr;      /* device */
@@ -69,7 +70,9 @@ typedef struct dg_rel_group {
     int32_t n_rows;
     int32_t n_rels;
     int32_t chunk;              /* relations per output chunk, >= 1                    */
-    int32_t reserved[4];        /* zero; filled in by the library                      */
+    int32_t n_cols;             /* columns of A (rows of each X_k)                     */
+    int32_t x_rels;             /* relation slabs addressable in x (0 = n_rels)        */
+    int32_t reserved[2];        /* zero                                                */
 } dg_rel_group;
 
 int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
@@ -78,8 +81,31 @@ int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_gr
 /* Single relation, no chunking: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
  * Replaces one tf.sparse_tensor_dense_matmul (layers.py:90).  ldy must equal d. */
 int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
-                    int32_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
-                    int32_t d, void* stream);
+                    int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx, float* y,
+                    int64_t ldy, int32_t d, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Fused GCN layer (T3 + T4 + T5 + T6 in one launch) for node types whose groups each fit
+ * one chunk: for every target t (a node type i) and row r < n_rows,
+ *
+ *     out_t[r] = act( sum_{g in [g_begin, g_begin+g_count)} l2norm( sum_k A_g,k[r]·X_g,k ) )
+ *
+ * act = relu if flags & DG_EPI_RELU.  The groups' `chunk` and `out` fields are ignored.
+ * One workgroup per output row, one wave per group (g_count <= DG_MAX_GROUPS).
+ * Replaces the per-relation SpMM + add_n + l2_normalize of layers.py:85-94 / 109-118 and the
+ * sum over edge types (+ relu) of model.py:74-75 / 85-88.
+ * -------------------------------------------------------------------------------------- */
+typedef struct dg_fused_target {
+    float* out;                 /* device, [n_rows][d] */
+    int32_t n_rows;
+    int32_t g_begin;
+    int32_t g_count;
+    int32_t flags;              /* 0 or DG_EPI_RELU */
+} dg_fused_target;
+
+int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
+                     const dg_fused_target* targets /* HOST */, int32_t n_targets, int32_t d,
+                     void* stream);
 
 /* --------------------------------------------------------------------------------------
  * GCN epilogue (T4 tail + T5 + T6):  for one node type i with groups g = (i, j_1..j_m),

@@ -1,0 +1,166 @@
+"""CPU: host-side logic of the product — sparse formats, the C-ABI library (loads, exports
+every symbol include/decagon_hip.h declares, rejects bad arguments before touching the
+GPU), the drop-in surface's construction contract, chunk policy and synthetic graphs."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_coo_to_csr_keeps_in_row_order():
+    from decagon_amd.sparse import coo_to_csr
+
+    coords = np.array([[2, 5], [0, 1], [2, 0], [0, 3]])
+    vals = np.array([1.0, 2.0, 3.0, 4.0])
+    h = coo_to_csr(coords, vals, (3, 6))
+    assert h.rowptr.tolist() == [0, 2, 2, 4]
+    assert h.col.tolist() == [1, 3, 5, 0]  # feed order kept inside each row
+    assert h.val.dtype == np.float32 and h.val.tolist() == [2.0, 4.0, 1.0, 3.0]
+
+
+def test_coo_to_csr_rejects_out_of_range():
+    from decagon_amd.sparse import coo_to_csr
+
+    with pytest.raises(ValueError):
+        coo_to_csr(np.array([[0, 7]]), np.array([1.0]), (3, 6))
+
+
+def test_stack_relations_offsets():
+    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, stack_relations
+
+    rng = np.random.default_rng(0)
+    mats = [sp.random(7, 5, density=0.3, random_state=rng, format="csr") for _ in range(3)]
+    st = stack_relations([coo_to_csr(*sparse_to_tuple(m)) for m in mats])
+    assert st.rowptr.shape == (3 * 7 + 1,)
+    for k, m in enumerate(mats):
+        for r in range(7):
+            a, b = st.rowptr[k * 7 + r], st.rowptr[k * 7 + r + 1]
+            assert b - a == m.indptr[r + 1] - m.indptr[r]
+            assert sorted(st.col[a:b].tolist()) == sorted(m.indices[m.indptr[r]:m.indptr[r + 1]].tolist())
+
+
+def test_is_identity():
+    from decagon_amd.sparse import is_identity, sparse_to_tuple
+
+    assert is_identity(*sparse_to_tuple(sp.identity(9).tocoo()))
+    assert not is_identity(*sparse_to_tuple((2 * sp.identity(9)).tocoo()))
+
+
+def _declared_symbols():
+    hdr = (ROOT / "include" / "decagon_hip.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t)\s+(dg_\w+)\s*\(", hdr, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from decagon_amd import _lib
+
+    lib = _lib.load()
+    syms = _declared_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} not bound in _lib.SIGNATURES"
+    assert lib.dg_abi_version() == _lib.ABI_VERSION
+
+
+def test_abi_rejects_bad_arguments_without_a_device():
+    """Argument checks run on the host before any HIP call, so they work here."""
+    from decagon_amd import _lib
+
+    lib = _lib.load()
+    assert lib.dg_spmm_groups_f32(None, 1, 64, None) == _lib.DG_EINVAL
+    g = (_lib.DgRelGroup * 1)()
+    assert lib.dg_spmm_groups_f32(g, 1, 6, None) == _lib.DG_EINVAL  # d % 4 != 0
+    assert lib.dg_spmm_groups_f32(g, 9, 64, None) == _lib.DG_ETOOMANY
+    g[0].n_rows, g[0].n_rels, g[0].chunk = 10, 1, 1
+    g[0].rowptr, g[0].x, g[0].out = 16, 17, 32  # misaligned x
+    g[0].x_ld = 64
+    assert lib.dg_spmm_groups_f32(g, 1, 64, None) == _lib.DG_EALIGN
+    assert lib.dg_decoder_score_f32(None, 32, None, 32, None, None, 4, None, None, 33, None, None) == _lib.DG_EINVAL
+    assert lib.dg_gemm_f32(None, None) == _lib.DG_EINVAL
+    e = (_lib.DgEpiGroup * 1)()
+    assert lib.dg_gcn_epilogue_f32(e, 1, None, 10, 64, 128, None) == _lib.DG_EINVAL  # bad flags
+    assert lib.dg_unigram_sample(None, 0, 5, 0, 0, None, None) == _lib.DG_EINVAL
+
+
+def test_choose_chunk_policy():
+    from decagon_amd.engine import choose_chunk
+
+    assert choose_chunk(6, 400, 55000, 64) == 6            # config S (1,1): one chunk
+    c = choose_chunk(1928, 645, 20_100_000, 64)            # config P (1,1): many chunks
+    assert 8 <= c <= 128
+    assert choose_chunk(1, 100, 10, 64) == 1
+
+
+def test_model_surface_constructs_like_the_reference():
+    import decagon_amd as dg
+
+    et = {(0, 0): 2, (0, 1): 1, (1, 0): 1, (1, 1): 6}
+    dec = {(0, 0): "bilinear", (0, 1): "bilinear", (1, 0): "bilinear", (1, 1): "dedicom"}
+    ph = dg.construct_placeholders(et)
+    assert "adj_mats_1,1,5" in ph and "feat_1" in ph and ph["dropout"].has_default
+    m = dg.DecagonModel(ph, {0: 500, 1: 400}, {0: 500, 1: 400}, et, dec)
+    assert len(m.latent_inters) == len(m.latent_varies) == 10
+    assert len(m.embeddings) == 2 and set(m.hidden1) == {0, 1}
+    # variable layout of layers.py / model.py
+    w = [n for n in m.vars if "graphconvolutionsparsemulti" in n and n.endswith("weights_0:0")]
+    assert w and m.vars[w[0]].shape in {(500, 64), (400, 64)}
+    assert any(n.endswith("global_interaction:0") for n in m.vars)
+    assert sum(1 for n in m.vars if "local_variation_" in n) == 6
+    with pytest.raises(AssertionError):
+        dg.DecagonModel(ph, {0: 500, 1: 400}, {0: 500, 1: 400}, et, dec, bogus=1)
+    with pytest.raises(ValueError):
+        dg.DecagonModel(ph, {0: 500, 1: 400}, {0: 500, 1: 400}, et, {**dec, (1, 1): "nope"})
+    opt = dg.DecagonOptimizer(m.embeddings, m.latent_inters, m.latent_varies,
+                              {0: [np.ones(500)] * 2, 1: [np.ones(400)] * 6}, et,
+                              {e: [(500 if e[0] == 0 else 400, 0)] * k for e, k in et.items()}, ph)
+    for attr in ("outputs", "neg_outputs", "cost", "predictions", "opt_op", "batch_edge_type_idx", "preds"):
+        assert hasattr(opt, attr)
+    assert opt.obj_type2n == {0: 500, 1: 400}
+
+
+def test_session_requires_a_device():
+    import torch
+
+    import decagon_amd as dg
+
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    with pytest.raises(RuntimeError):
+        dg.Session()
+
+
+def test_act_kind_probe():
+    from decagon_amd.layers import act_kind, relu
+
+    assert act_kind(lambda x: x) == "identity"
+    assert act_kind(relu) == "relu"
+    with pytest.raises(ValueError):
+        act_kind(lambda x: 2 * x)
+
+
+def test_synthetic_P_shape_small():
+    from decagon_amd.synthetic import make_P
+
+    g = make_P(seed=1, n_proteins=500, n_drugs=60, n_side_effects=12, ppi_edges=2000, target_edges=300)
+    assert g.edge_types == {(0, 0): 2, (0, 1): 1, (1, 0): 1, (1, 1): 24}
+    c = g.csr()
+    assert c[(1, 0)][0].shape == (60, 500) and c[(0, 1)][0].shape == (500, 60)
+    # every drug-drug relation is symmetric and includes self loops (A + I)
+    r = c[(1, 1)][0]
+    dense = np.zeros((60, 60))
+    for i in range(60):
+        dense[i, r.col[r.rowptr[i]:r.rowptr[i + 1]]] = r.val[r.rowptr[i]:r.rowptr[i + 1]]
+    assert np.allclose(dense, dense.T) and np.all(np.diag(dense) > 0)
+
+
+def test_flags_defaults_match_main_py():
+    from decagon_amd import FLAGS
+
+    assert FLAGS.hidden1 == 64 and FLAGS.hidden2 == 32 and FLAGS.batch_size == 512
+    assert FLAGS.max_margin == 0.1 and FLAGS.learning_rate == 0.001

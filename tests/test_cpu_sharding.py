@@ -1,0 +1,104 @@
+"""CPU: the multi-GPU path's host logic and its collective, with world_size-2 gloo.
+
+The sharded forward computes, per rank, the pre-normalisation group sums of its own
+relations and sum-all-reduces them before the L2 normalisation (layers.py:92-93).  Here
+each rank computes its local sums with the float64 oracle (the checker) and reduces them
+through the product's collective wrapper (decagon_amd.sharding.torch_allreduce) over gloo;
+the result must equal the single-process sum over all relations.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from decagon_amd.sharding import RelationShard, lpt_assign
+
+
+def test_lpt_balances_and_covers():
+    rng = np.random.default_rng(0)
+    costs = rng.integers(1, 1000, 200).tolist() + [50000, 40000]
+    owner = lpt_assign(costs, 8)
+    loads = np.zeros(8)
+    for c, r in zip(costs, owner):
+        loads[r] += c
+    assert sorted(set(owner)) == list(range(8))
+    assert loads.max() <= max(costs) + loads.mean()  # LPT bound
+    assert lpt_assign(costs, 8) == owner  # deterministic
+
+
+def test_relation_shard_lpt_partitions_every_relation():
+    et = {(0, 0): 2, (0, 1): 1, (1, 0): 1, (1, 1): 1928}
+    rng = np.random.default_rng(1)
+    cost = {k: rng.integers(500, 30000, v).tolist() for k, v in et.items()}
+    cost[(0, 0)] = [1_450_000, 1_450_000]
+    seen = {k: [] for k in et}
+    for r in range(8):
+        s = RelationShard.lpt(et, cost, r, 8)
+        for k, v in s.local.items():
+            seen[k] += v
+    for k, v in et.items():
+        assert sorted(seen[k]) == list(range(v))
+
+
+def test_relation_shard_blocks():
+    s = RelationShard.blocks({(0, 0): 2, (1, 1): 6}, 2, 4)
+    assert s.local == {(0, 0): [4, 5], (1, 1): [12, 13, 14, 15, 16, 17]}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from decagon_amd.sharding import RelationShard, torch_allreduce
+    from decagon_amd.synthetic import load_S
+    from oracle import decagon_oracle as orc
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = load_S()
+    nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
+    shard = RelationShard.lpt(g.edge_types, nnz, rank, world, torch_allreduce())
+    rng = np.random.default_rng(7)
+    X = {et: rng.standard_normal((K, g.n_nodes[et[1]], 64)) for et, K in g.edge_types.items()}
+    flat = []
+    for et in g.edge_types:
+        s = np.zeros((g.n_nodes[et[0]], 64))
+        for k in shard.local[et]:
+            s += orc.sparse_dense_matmul(g.adj[et][k], X[et][k])
+        flat.append(s.ravel())
+    buf = torch.from_numpy(np.concatenate(flat))
+    shard.allreduce(buf)
+    q.put((rank, buf.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_rank_group_sums_equal_single_device():
+    from decagon_amd.synthetic import load_S
+    from oracle import decagon_oracle as orc
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = load_S()
+    rng = np.random.default_rng(7)
+    X = {et: rng.standard_normal((K, g.n_nodes[et[1]], 64)) for et, K in g.edge_types.items()}
+    want = np.concatenate([sum(orc.sparse_dense_matmul(g.adj[et][k], X[et][k]) for k in range(K)).ravel()
+                           for et, K in g.edge_types.items()])
+    for r in (0, 1):
+        assert np.allclose(res[r], want, rtol=1e-12, atol=1e-12)
