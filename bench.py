@@ -107,8 +107,7 @@ def make_plan(args, graph, shard, device):
 
 class Decoder:
     """DEDICOM scoring of B positive + B sampled negative pairs of one drug-drug relation,
-    then the hinge loss — all device launches (dg_unigram_sample, dg_decoder_score_f32 ×2,
-    dg_hinge_loss_f32)."""
+    then the hinge loss — one dg_decoder_hinge_f32 launch (sampler + scores + loss)."""
 
     def __init__(self, graph, plan, device, rank):
         import torch
@@ -127,17 +126,12 @@ class Decoder:
         self.neg = torch.empty(BATCH, dtype=torch.int32, device=device)
         self.R = torch.from_numpy(glorot_stack(rng, 1, H2, H2)[0]).to(device)
         self.l = torch.from_numpy(glorot_stack(rng, 1, H2, 1).reshape(-1)).to(device)
-        self.pos = torch.empty(BATCH, device=device)
-        self.negs = torch.empty(BATCH, device=device)
-        self.loss = torch.empty(1, device=device)
         self.E = plan.embeddings[1]
+        self.fused = kernels.PreparedDecoderHinge(self.E, self.E, self.rows, self.cols, self.R, self.l,
+                                                  MARGIN, cdf=self.cdf, seed=7)
 
     def __call__(self):
-        k = self.k
-        k.unigram_sample(self.cdf, BATCH, seed=7, offset=0, out=self.neg)
-        k.decoder_score(self.E, self.E, self.rows, self.cols, self.R, self.l, out=self.pos)
-        k.decoder_score(self.E, self.E, self.neg, self.cols, self.R, self.l, out=self.negs)
-        k.hinge_loss(self.pos, self.negs, MARGIN, out=self.loss)
+        self.fused()
 
 
 def time_kernel(fn, reps, stream):

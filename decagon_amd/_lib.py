@@ -19,7 +19,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -94,7 +94,13 @@ SIGNATURES = {
         c_int32,
         [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     ),
-    "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_void_p]),
+    "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_int32, c_void_p]),
+    "dg_decoder_hinge_f32": (
+        c_int32,
+        [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+         c_uint64, c_uint64, c_int32, c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "dg_decoder_score_f32": (
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,

@@ -16,18 +16,98 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-struct DecArgs {
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Draw #idx of the counter-based unigram sampler: inverse CDF at a 24-bit uniform.
+__device__ __forceinline__ int unigram_draw(const float* cdf, int range, uint64_t seed,
+                                            uint64_t idx) {
+    const uint64_t h = splitmix64(seed ^ splitmix64(idx));
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);  // [0,1), 24 bits
+    const float target = u * cdf[range - 1];
+    int lo = 0, hi = range - 1;  // first c with cdf[c] > target
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] > target)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo;
+}
+
+struct DecTab {
     const float* row_table;
     const float* col_table;
-    const int32_t* row_idx;
-    const int32_t* col_idx;
     const float* G;
     const float* l;
-    float* out;
     int64_t ld_row;
     int64_t ld_col;
-    int32_t n_pairs;
     int32_t d;
+};
+
+// Scores of 32 pairs on one wave: lane i (both halves) names pair i by its row index
+// `ridx` (into row_table) and column index `cidx` (into col_table); `valid` masks pairs
+// past the end.  T = (U∘l)·G runs on v_mfma_f32_32x32x2_f32 in k-blocks of 32 whose A/B
+// fragments are loaded up front (one memory round trip per block, not per k-step); then
+// score[p] = Σ_j T[p][j]·l[j]·V[p][j] is folded over the 32 lanes of each half-wave.
+// Returns the score of pair (r&3)+8(r>>2)+4h in part[r] of lane 0 / 32.
+__device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, bool valid,
+                                           float (&part)[16]) {
+    const int lane = threadIdx.x & 63;
+    const int i = lane & 31;
+    const int h = lane >> 5;
+    const int d = t.d;
+    const float* u = t.row_table + (int64_t)ridx * t.ld_row;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) part[r] = 0.f;
+#pragma unroll 1
+    for (int n0 = 0; n0 < d; n0 += 32) {
+        f32x16 acc = {};
+#pragma unroll 1
+        for (int k0 = 0; k0 < d; k0 += 32) {
+            float av[16], bv[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int kk = k0 + 2 * s + h;
+                float a = valid ? u[kk] : 0.f;
+                if (t.l) a *= t.l[kk];
+                av[s] = a;
+                bv[s] = t.G[(int64_t)kk * d + n0 + i];
+            }
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+        }
+        const int j = n0 + i;
+        const float lj = t.l ? t.l[j] : 1.0f;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int prow = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int c = __shfl(cidx, prow);  // lane prow names pair prow
+            v[r] = t.col_table[(int64_t)c * t.ld_col + j];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) part[r] = fmaf(acc[r] * lj, v[r], part[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+#pragma unroll
+        for (int m = 1; m < 32; m <<= 1) part[r] += __shfl_xor(part[r], m);
+    }
+}
+
+struct DecArgs {
+    DecTab t;
+    const int32_t* row_idx;
+    const int32_t* col_idx;
+    float* out;
+    int32_t n_pairs;
 };
 
 __global__ __launch_bounds__(256) void decoder_score_kernel(const DecArgs a) {
@@ -37,53 +117,98 @@ __global__ __launch_bounds__(256) void decoder_score_kernel(const DecArgs a) {
     if (p0 >= a.n_pairs) return;
     const int i = lane & 31;
     const int h = lane >> 5;
-    const int d = a.d;
     const int p = p0 + i;
-    const bool pvalid = p < a.n_pairs;
-    const float* u = a.row_table + (int64_t)(pvalid ? a.row_idx[p] : 0) * a.ld_row;
-    const int cidx_mine = pvalid ? a.col_idx[p] : 0;
-
+    const bool valid = p < a.n_pairs;
     float part[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) part[r] = 0.f;
-
-#pragma unroll 1
-    for (int n0 = 0; n0 < d; n0 += 32) {
-        f32x16 acc = {};
-#pragma unroll 4
-        for (int k0 = 0; k0 < d; k0 += 2) {
-            const int kk = k0 + h;
-            float av = 0.f;
-            if (pvalid) {
-                av = u[kk];
-                if (a.l) av *= a.l[kk];
-            }
-            const float bv = a.G[(int64_t)kk * d + n0 + i];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-        }
-        const int j = n0 + i;
-        const float lj = a.l ? a.l[j] : 1.0f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int prow = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int cidx = __shfl(cidx_mine, prow);  // lane prow holds pair p0+prow
-            if (p0 + prow < a.n_pairs) {
-                const float v = a.col_table[(int64_t)cidx * a.ld_col + j];
-                part[r] = fmaf(acc[r] * lj, v, part[r]);
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-#pragma unroll
-        for (int m = 1; m < 32; m <<= 1) part[r] += __shfl_xor(part[r], m);
-    }
+    score_tile(a.t, valid ? a.row_idx[p] : 0, valid ? a.col_idx[p] : 0, valid, part);
     if (i == 0) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int pp = p0 + (r & 3) + 8 * (r >> 2) + 4 * h;
             if (pp < a.n_pairs) a.out[pp] = part[r];
         }
+    }
+}
+
+// Fused decoder step (optimizer.py:37-57 + :116-120): for the batch pairs b < n,
+//   neg_row[b] = given[b] or a unigram draw (seed, offset + b),
+//   pos[b] = score(rows[b], cols[b]),  neg[b] = score(neg_row[b], cols[b]),
+//   loss  += relu(neg[b] - (pos[b] - margin))
+// One workgroup of 16 waves per 512 batch pairs (32 tiles: 16 positive, 16 negative).  With
+// one workgroup the loss is written directly; otherwise each block writes its partial and
+// dg_decoder_hinge_f32 reduces them in a second, fixed-order launch.
+constexpr int kHingeBlock = 512;
+
+struct HingeArgs {
+    DecTab t;
+    const int32_t* rows;
+    const int32_t* cols;
+    const int32_t* neg_given;
+    const float* cdf;
+    float* pos;
+    float* neg;
+    int32_t* neg_rows_out;
+    float* loss;        // [1]
+    float* partial;     // [gridDim.x] when gridDim.x > 1
+    uint64_t seed;
+    uint64_t offset;
+    int32_t cdf_range;
+    int32_t n;
+    float margin;
+};
+
+__global__ __launch_bounds__(1024) void decoder_hinge_kernel(const HingeArgs a) {
+    __shared__ float sc[2][kHingeBlock];
+    __shared__ float red[1024];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;  // 0..15
+    const int i = lane & 31;
+    const int h = lane >> 5;
+    const int b0 = blockIdx.x * kHingeBlock;
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {  // 0: positives, 1: negatives
+        const int q0 = wave * 32;           // tile offset inside the block
+        const int b = b0 + q0 + i;
+        const bool valid = b < a.n;
+        int ridx = 0, cidx = 0;
+        if (valid) {
+            cidx = a.cols[b];
+            if (side == 0)
+                ridx = a.rows[b];
+            else if (a.neg_given)
+                ridx = a.neg_given[b];
+            else
+                ridx = unigram_draw(a.cdf, a.cdf_range, a.seed, a.offset + (uint64_t)b);
+            if (side == 1 && a.neg_rows_out && h == 0) a.neg_rows_out[b] = ridx;
+        }
+        float part[16];
+        if (b0 + q0 < a.n) score_tile(a.t, ridx, cidx, valid, part);
+        if (i == 0 && b0 + q0 < a.n) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int q = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float v = (b0 + q < a.n) ? part[r] : 0.f;
+                sc[side][q] = v;
+                if (b0 + q < a.n) (side == 0 ? a.pos : a.neg)[b0 + q] = v;
+            }
+        }
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    float term = 0.f;
+    if (t < kHingeBlock && b0 + t < a.n) term = fmaxf(sc[1][t] - (sc[0][t] - a.margin), 0.f);
+    red[t] = term;
+    __syncthreads();
+#pragma unroll
+    for (int w = 512; w > 0; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    if (t == 0) {
+        if (gridDim.x == 1)
+            a.loss[0] = red[0];
+        else
+            a.partial[blockIdx.x] = red[0];
     }
 }
 
@@ -126,31 +251,17 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* pos, const float
     if (threadIdx.x == 0) loss[0] = sp + w * sn;
 }
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
 __global__ __launch_bounds__(256) void unigram_sample_kernel(const float* cdf, int range, int n,
                                                              uint64_t seed, uint64_t offset,
                                                              int32_t* out) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= n) return;
-    const uint64_t h = splitmix64(seed ^ splitmix64(offset + (uint64_t)idx));
-    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);  // [0,1), 24 bits
-    const float target = u * cdf[range - 1];
-    // first c with cdf[c] > target
-    int lo = 0, hi = range - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (cdf[mid] > target)
-            hi = mid;
-        else
-            lo = mid + 1;
-    }
-    out[idx] = lo;
+    out[idx] = unigram_draw(cdf, range, seed, offset + (uint64_t)idx);
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* partial, int n, float* loss) {
+    const float s = block_sum_256(n, [&](int p) { return partial[p]; });
+    if (threadIdx.x == 0) loss[0] = s;
 }
 
 }  // namespace
@@ -163,7 +274,12 @@ extern "C" int dg_decoder_score_f32(const float* row_table, int64_t ld_row, cons
     if (n_pairs == 0) return DG_OK;
     if (!row_table || !col_table || !row_idx || !col_idx || !G || !out) return DG_EINVAL;
     if (ld_row < d || ld_col < d) return DG_EINVAL;
-    DecArgs a{row_table, col_table, row_idx, col_idx, G, l, out, ld_row, ld_col, n_pairs, d};
+    DecArgs a{};
+    a.t = DecTab{row_table, col_table, G, l, ld_row, ld_col, d};
+    a.row_idx = row_idx;
+    a.col_idx = col_idx;
+    a.out = out;
+    a.n_pairs = n_pairs;
     dim3 grid(dg::ceil_div(n_pairs, 128)), block(256);
     hipLaunchKernelGGL(decoder_score_kernel, grid, block, 0, reinterpret_cast<hipStream_t>(stream), a);
     return dg::launch_status();
@@ -191,5 +307,44 @@ extern "C" int dg_unigram_sample(const float* cdf, int32_t range, int32_t n, uin
     if (n == 0) return DG_OK;
     hipLaunchKernelGGL(unigram_sample_kernel, dim3(dg::ceil_div(n, 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), cdf, range, n, seed, offset, out);
+    return dg::launch_status();
+}
+
+extern "C" int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
+                                    int64_t ld_col, const int32_t* rows, const int32_t* cols,
+                                    const int32_t* neg_rows, const float* cdf, int32_t cdf_range,
+                                    uint64_t seed, uint64_t offset, int32_t n, const float* G,
+                                    const float* l, int32_t d, float margin, float* pos, float* neg,
+                                    int32_t* neg_rows_out, float* loss, float* workspace,
+                                    void* stream) {
+    if (n < 0 || d <= 0 || (d % 32) || d > 256) return DG_EINVAL;
+    if (!row_table || !col_table || !rows || !cols || !G || !pos || !neg || !loss) return DG_EINVAL;
+    if (!neg_rows && (!cdf || cdf_range < 1)) return DG_EINVAL;
+    if (ld_row < d || ld_col < d) return DG_EINVAL;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int blocks = dg::ceil_div(n, kHingeBlock);
+    if (blocks > 1 && !workspace) return DG_EINVAL;
+    if (n == 0) {
+        hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, loss, 0, loss);
+        return dg::launch_status();
+    }
+    HingeArgs a{};
+    a.t = DecTab{row_table, col_table, G, l, ld_row, ld_col, d};
+    a.rows = rows;
+    a.cols = cols;
+    a.neg_given = neg_rows;
+    a.cdf = cdf;
+    a.pos = pos;
+    a.neg = neg;
+    a.neg_rows_out = neg_rows_out;
+    a.loss = loss;
+    a.partial = workspace;
+    a.seed = seed;
+    a.offset = offset;
+    a.cdf_range = cdf_range;
+    a.n = n;
+    a.margin = margin;
+    hipLaunchKernelGGL(decoder_hinge_kernel, dim3(blocks), dim3(1024), 0, st, a);
+    if (blocks > 1) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, workspace, blocks, loss);
     return dg::launch_status();
 }

@@ -20,7 +20,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-struct GemmArgs {
+struct GemmOne {
     const float* a;
     const float* b;
     float* c;
@@ -32,13 +32,35 @@ struct GemmArgs {
     int64_t c_bs, c_sm, c_sn;
     int32_t m, n, k, batch;
     int32_t tiles_m, tiles_n, batch_per_wave;
+    int32_t tile_blocks;   // blocks along the tile dimension (4 tiles each)
+    int32_t block_begin;   // first block of this GEMM in the launch
+    int32_t pad;
 };
 
+struct GemmArgs {
+    GemmOne g[DG_MAX_GROUPS];
+    int32_t n;
+};
+
+// One launch runs up to DG_MAX_GROUPS GEMMs: block b -> (GEMM, tile block, batch block).
+__device__ __forceinline__ const GemmOne& pick(const GemmArgs& A, int b, int& tb, int& bb) {
+    int i = 0;
+#pragma unroll 1
+    while (i + 1 < A.n && b >= A.g[i + 1].block_begin) ++i;
+    const GemmOne& g = A.g[i];
+    const int lb = b - g.block_begin;
+    bb = lb / g.tile_blocks;
+    tb = lb - bb * g.tile_blocks;
+    return g;
+}
+
 // Generic path: any K, A fragment re-loaded per k-step (L1/L2 resident).
-__global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs g) {
+__global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
+    int tb, bblk;
+    const GemmOne& g = pick(args, blockIdx.x, tb, bblk);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int tile = blockIdx.x * 4 + wave;
+    const int tile = tb * 4 + wave;
     if (tile >= g.tiles_m * g.tiles_n) return;
     const int tm = tile / g.tiles_n;
     const int tn = tile - tm * g.tiles_n;
@@ -48,7 +70,7 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs g) {
     const int col = tn * 32 + i;
     const bool row_ok = row < g.m;
     const bool col_ok = col < g.n;
-    const int b0 = blockIdx.y * g.batch_per_wave;
+    const int b0 = bblk * g.batch_per_wave;
     const int b1 = min(b0 + g.batch_per_wave, g.batch);
 #pragma unroll 1
     for (int b = b0; b < b1; ++b) {
@@ -84,11 +106,13 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs g) {
 // Projection path: K == KD (compile-time), the A fragment (KD/2 values per lane) lives in
 // registers for all relations the wave handles.
 template <int KD>
-__global__ __launch_bounds__(256) void gemm_f32_resident_a(const GemmArgs g) {
+__global__ __launch_bounds__(256) void gemm_f32_resident_a(const GemmArgs args) {
     constexpr int S = KD / 2;
+    int tb, bblk;
+    const GemmOne& g = pick(args, blockIdx.x, tb, bblk);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int tile = blockIdx.x * 4 + wave;
+    const int tile = tb * 4 + wave;
     if (tile >= g.tiles_m * g.tiles_n) return;
     const int tm = tile / g.tiles_n;
     const int tn = tile - tm * g.tiles_n;
@@ -98,7 +122,7 @@ __global__ __launch_bounds__(256) void gemm_f32_resident_a(const GemmArgs g) {
     const int col = tn * 32 + i;
     const bool row_ok = row < g.m;
     const bool col_ok = col < g.n;
-    const int b0 = blockIdx.y * g.batch_per_wave;
+    const int b0 = bblk * g.batch_per_wave;
     const int b1 = min(b0 + g.batch_per_wave, g.batch);
     if (b0 >= b1) return;
 
@@ -142,52 +166,60 @@ __global__ __launch_bounds__(256) void gemm_f32_resident_a(const GemmArgs g) {
 
 }  // namespace
 
-extern "C" int dg_gemm_f32(const dg_gemm_desc* d, void* stream) {
-    if (!d) return DG_EINVAL;
-    if (d->m < 0 || d->n < 0 || d->k < 0 || d->batch < 0) return DG_EINVAL;
-    if (d->m == 0 || d->n == 0 || d->batch == 0) return DG_OK;
-    if (!d->c) return DG_EINVAL;
-    if (d->k > 0 && (!d->a || !d->b)) return DG_EINVAL;
-    GemmArgs g{};
-    g.a = d->a;
-    g.b = d->b;
-    g.c = d->c;
-    g.sa = d->sa;
-    g.sc = d->sc;
-    g.b_map = d->b_map;
-    g.a_bs = d->a_bs;
-    g.a_sm = d->a_sm;
-    g.a_sk = d->a_sk;
-    g.b_bs = d->b_bs;
-    g.b_sk = d->b_sk;
-    g.b_sn = d->b_sn;
-    g.c_bs = d->c_bs;
-    g.c_sm = d->c_sm;
-    g.c_sn = d->c_sn;
-    g.m = d->m;
-    g.n = d->n;
-    g.k = d->k;
-    g.batch = d->batch;
-    g.tiles_m = dg::ceil_div(d->m, 32);
-    g.tiles_n = dg::ceil_div(d->n, 32);
-    const int64_t tiles = (int64_t)g.tiles_m * g.tiles_n;
-    const int tile_blocks = dg::ceil_div(tiles, 4);
-    // Relations per wave: enough waves to fill 256 CUs several times over, and each wave
-    // amortises its A fragment over up to 16 relations.
-    int bpw = 1;
-    while (bpw < 16 && (int64_t)tile_blocks * 4 * dg::ceil_div(d->batch, bpw * 2) >= 8192) bpw *= 2;
-    g.batch_per_wave = bpw;
-    const int batch_blocks = dg::ceil_div(d->batch, bpw);
-    if (batch_blocks > 65535) {
-        g.batch_per_wave = dg::ceil_div(d->batch, 65535);
+extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stream) {
+    if (!descs || n_desc < 1) return DG_EINVAL;
+    if (n_desc > DG_MAX_GROUPS) return DG_ETOOMANY;
+    GemmArgs A{};
+    int64_t blocks = 0;
+    int kd = -1;
+    for (int i = 0; i < n_desc; ++i) {
+        const dg_gemm_desc* d = &descs[i];
+        if (d->m < 0 || d->n < 0 || d->k < 0 || d->batch < 0) return DG_EINVAL;
+        if (d->m == 0 || d->n == 0 || d->batch == 0) continue;
+        if (!d->c) return DG_EINVAL;
+        if (d->k > 0 && (!d->a || !d->b)) return DG_EINVAL;
+        GemmOne& g = A.g[A.n++];
+        g.a = d->a;
+        g.b = d->b;
+        g.c = d->c;
+        g.sa = d->sa;
+        g.sc = d->sc;
+        g.b_map = d->b_map;
+        g.a_bs = d->a_bs;
+        g.a_sm = d->a_sm;
+        g.a_sk = d->a_sk;
+        g.b_bs = d->b_bs;
+        g.b_sk = d->b_sk;
+        g.b_sn = d->b_sn;
+        g.c_bs = d->c_bs;
+        g.c_sm = d->c_sm;
+        g.c_sn = d->c_sn;
+        g.m = d->m;
+        g.n = d->n;
+        g.k = d->k;
+        g.batch = d->batch;
+        g.tiles_m = dg::ceil_div(d->m, 32);
+        g.tiles_n = dg::ceil_div(d->n, 32);
+        g.tile_blocks = dg::ceil_div((int64_t)g.tiles_m * g.tiles_n, 4);
+        // Relations per wave: enough waves to fill 256 CUs several times over, and each
+        // wave amortises its A fragment over up to 16 relations.
+        int bpw = 1;
+        while (bpw < 16 && (int64_t)g.tile_blocks * 4 * dg::ceil_div(d->batch, bpw * 2) >= 8192) bpw *= 2;
+        g.batch_per_wave = bpw;
+        g.block_begin = static_cast<int32_t>(blocks);
+        blocks += (int64_t)g.tile_blocks * dg::ceil_div(d->batch, bpw);
+        if (blocks > 0x7fffffff) return DG_EINVAL;
+        const int kk = (d->k == 64 || d->k == 32) ? d->k : 0;
+        kd = (kd < 0 || kd == kk) ? kk : 0;
     }
-    dim3 grid(tile_blocks, dg::ceil_div(d->batch, g.batch_per_wave)), block(256);
+    if (A.n == 0) return DG_OK;
+    dim3 grid(static_cast<unsigned>(blocks)), block(256);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (d->k == 64)
-        hipLaunchKernelGGL(gemm_f32_resident_a<64>, grid, block, 0, st, g);
-    else if (d->k == 32)
-        hipLaunchKernelGGL(gemm_f32_resident_a<32>, grid, block, 0, st, g);
+    if (kd == 64)
+        hipLaunchKernelGGL(gemm_f32_resident_a<64>, grid, block, 0, st, A);
+    else if (kd == 32)
+        hipLaunchKernelGGL(gemm_f32_resident_a<32>, grid, block, 0, st, A);
     else
-        hipLaunchKernelGGL(gemm_f32_generic, grid, block, 0, st, g);
+        hipLaunchKernelGGL(gemm_f32_generic, grid, block, 0, st, A);
     return dg::launch_status();
 }

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 3; }
+extern "C" int32_t dg_abi_version(void) { return 4; }
 
 namespace {
 

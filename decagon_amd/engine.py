@@ -209,6 +209,9 @@ class ForwardPlan:
                 self.hidden1[j], (0, h1, 1), W, (h1 * h2, h2, 1), P, (n[j] * h2, h2, 1),
                 n[j], h2, h1, grp.n_rels, b_map=grp.rel_map, b_batches=K,
                 b_map_max=int(grp.rel_ids.max()) if grp.rel_map is not None else None))
+        # every group's projection in one launch (≤ DG_MAX_GROUPS per launch)
+        self._gemm2 = [kernels.PreparedGemmMulti(self._gemm2[s:s + DG_MAX_GROUPS])
+                       for s in range(0, len(self._gemm2), DG_MAX_GROUPS)]
         self._layer2 = self._build_layer(x2_specs, h2, False, chunk_override, target_waves, f32)
 
     # ------------------------------------------------------------------ layer builder

@@ -281,7 +281,24 @@ class PreparedGemm:
         self._fn = _lib.load().dg_gemm_f32
 
     def __call__(self, stream=None) -> None:
-        check(self._fn(ctypes.byref(self._desc), _stream_ptr(stream)), "dg_gemm_f32")
+        check(self._fn(ctypes.byref(self._desc), 1, _stream_ptr(stream)), "dg_gemm_f32")
+
+
+class PreparedGemmMulti:
+    """Several prepared GEMMs (≤ DG_MAX_GROUPS) in one dg_gemm_f32 launch."""
+
+    def __init__(self, gemms: Sequence[PreparedGemm]):
+        if not 1 <= len(gemms) <= _lib.DG_MAX_GROUPS:
+            raise ValueError(f"1..{_lib.DG_MAX_GROUPS} GEMMs per launch")
+        arr = (DgGemmDesc * len(gemms))()
+        for i, g in enumerate(gemms):
+            ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(g._desc), ctypes.sizeof(DgGemmDesc))
+        self._keep = list(gemms)
+        self._arr, self._n = arr, len(gemms)
+        self._fn = _lib.load().dg_gemm_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(self._arr, self._n, _stream_ptr(stream)), "dg_gemm_f32")
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -368,3 +385,50 @@ def unigram_sample(cdf: torch.Tensor, n: int, seed: int, offset: int,
                                          offset & (2**64 - 1), out.data_ptr(), _stream_ptr(stream)),
           "dg_unigram_sample")
     return out
+
+
+class PreparedDecoderHinge:
+    """dg_decoder_hinge_f32 on fixed buffers: sampled (or given) negatives, positive and
+    negative scores of n pairs and the hinge loss, in one launch (two when n > 512)."""
+
+    def __init__(self, row_table: torch.Tensor, col_table: torch.Tensor, rows: torch.Tensor,
+                 cols: torch.Tensor, G: torch.Tensor, l: Optional[torch.Tensor], margin: float,
+                 cdf: Optional[torch.Tensor] = None, neg_rows: Optional[torch.Tensor] = None,
+                 seed: int = 0, offset: int = 0):
+        for t, nm, dt in ((row_table, "row_table", torch.float32), (col_table, "col_table", torch.float32),
+                          (rows, "rows", torch.int32), (cols, "cols", torch.int32), (G, "G", torch.float32)):
+            _dev(t, dt, nm)
+        d = G.shape[0]
+        n = rows.numel()
+        if G.shape != (d, d) or row_table.shape[1] != d or col_table.shape[1] != d or cols.numel() != n:
+            raise ValueError("decoder_hinge: shape mismatch")
+        if l is not None:
+            _dev(l, torch.float32, "l")
+        if neg_rows is None:
+            if cdf is None:
+                raise ValueError("need either negatives or a sampler CDF")
+            _dev(cdf, torch.float32, "cdf")
+            if cdf.numel() > row_table.shape[0]:
+                raise ValueError("sampler range exceeds the row table")
+        else:
+            _dev(neg_rows, torch.int32, "neg_rows")
+        dev = G.device
+        self.pos = torch.empty(n, device=dev)
+        self.neg = torch.empty(n, device=dev)
+        self.neg_rows = torch.empty(n, device=dev, dtype=torch.int32)
+        self.loss = torch.empty(1, device=dev)
+        self._ws = torch.empty(max(1, -(-n // 512)), device=dev)
+        self._keep = (row_table, col_table, rows, cols, G, l, cdf, neg_rows)
+        self.seed, self.offset = seed, offset
+        self._args = [row_table.data_ptr(), row_table.shape[1], col_table.data_ptr(), col_table.shape[1],
+                      rows.data_ptr(), cols.data_ptr(), neg_rows.data_ptr() if neg_rows is not None else None,
+                      cdf.data_ptr() if cdf is not None else None, cdf.numel() if cdf is not None else 0,
+                      seed, offset, n, G.data_ptr(), l.data_ptr() if l is not None else None, d, float(margin),
+                      self.pos.data_ptr(), self.neg.data_ptr(), self.neg_rows.data_ptr(), self.loss.data_ptr(),
+                      self._ws.data_ptr()]
+        self._fn = _lib.load().dg_decoder_hinge_f32
+
+    def __call__(self, stream=None) -> None:
+        a = list(self._args)
+        a[9], a[10] = self.seed & (2**64 - 1), self.offset & (2**64 - 1)
+        check(self._fn(*a, _stream_ptr(stream)), "dg_decoder_hinge_f32")

@@ -72,9 +72,12 @@ class DecagonOptimizer:
         self.obj_type_lookup_start = np.cumsum([0] + obj_type_n[:-1])
         self.obj_type_lookup_end = np.cumsum(obj_type_n)
 
-        self.neg_samples = Node("optimizer/neg_samples", self._sample_negatives)
-        self.outputs = Node("optimizer/outputs", lambda ctx: self._scores(ctx, self.row_inputs))
-        self.neg_outputs = Node("optimizer/neg_outputs", lambda ctx: self._scores(ctx, self.neg_samples))
+        # One fused launch (dg_decoder_hinge_f32) yields negatives, both score vectors and the
+        # hinge loss; the reference's nodes are views of it.
+        self._decode = Node("optimizer/decode", self._decode_fn)
+        self.neg_samples = Node("optimizer/neg_samples", lambda ctx: ctx.value(self._decode)[3])
+        self.outputs = Node("optimizer/outputs", lambda ctx: ctx.value(self._decode)[0])
+        self.neg_outputs = Node("optimizer/neg_outputs", lambda ctx: ctx.value(self._decode)[1])
         self.preds = Node("optimizer/preds", lambda ctx: self._full(ctx, self.row_inputs))
         self.neg_preds = Node("optimizer/neg_preds", lambda ctx: self._full(ctx, self.neg_samples))
         self.predict()
@@ -123,17 +126,34 @@ class DecagonOptimizer:
         L = runtime.as_device_f32(ctx.value(gv))
         return kernels.matmul(kernels.matmul(L, G), L), None
 
-    def _sample_negatives(self, ctx: RunContext) -> torch.Tensor:
-        e, _, _ = self._edge(ctx)
-        cache = ctx.session.caches
+    def _sampler(self, ctx) -> _Sampler:
         key = ("sampler", id(self))
+        cache = ctx.session.caches
         if key not in cache:
             cache[key] = _Sampler(self._rel_degrees, ctx.session.device)
-        s = cache[key]
-        n = self._batch(ctx).shape[0]
-        out = kernels.unigram_sample(s.cdfs[e], n, self.seed, s.counter)
-        s.counter += n
-        return out
+        return cache[key]
+
+    def _decode_fn(self, ctx: RunContext):
+        """(pos scores, neg scores, hinge loss, negative rows) of the fed batch."""
+        e, rt, ct = self._edge(ctx)
+        row_t, col_t = self._tables(ctx, rt, ct)
+        rows = self._idx_dev(ctx, self.row_inputs, row_t.shape[0])
+        cols = self._idx_dev(ctx, self.col_inputs, col_t.shape[0])
+        G, l = self._latent(ctx, e)
+        if ctx.is_fed(self.neg_samples):
+            negs = self._idx_dev(ctx, self.neg_samples, row_t.shape[0])
+            if negs.numel() != rows.numel():
+                raise InvalidArgumentError("neg_samples must have one entry per batch edge")
+            op = kernels.PreparedDecoderHinge(row_t, col_t, rows, cols, G, l, self.margin, neg_rows=negs)
+        else:
+            s = self._sampler(ctx)
+            if s.cdfs[e].numel() > row_t.shape[0]:
+                raise InvalidArgumentError("degrees list longer than the row embedding table")
+            op = kernels.PreparedDecoderHinge(row_t, col_t, rows, cols, G, l, self.margin, cdf=s.cdfs[e],
+                                              seed=self.seed, offset=s.counter)
+            s.counter += rows.numel()
+        op()
+        return op.pos, op.neg, op.loss[0], op.neg_rows
 
     def _scores(self, ctx: RunContext, rows_node: Node) -> torch.Tensor:
         e, rt, ct = self._edge(ctx)
@@ -181,6 +201,9 @@ class DecagonOptimizer:
     def _hinge_loss(self, aff, neg_aff):
         """optimizer.py:116-120: sum(relu(neg - (pos - margin)))."""
         def fn(ctx):
+            if aff is self.outputs and neg_aff is self.neg_outputs and not (
+                    ctx.is_fed(aff) or ctx.is_fed(neg_aff)):
+                return ctx.value(self._decode)[2]  # computed by the fused decoder launch
             pos = runtime.as_device_f32(ctx.value(aff))
             neg = runtime.as_device_f32(ctx.value(neg_aff))
             return kernels.hinge_loss(pos, neg, self.margin)[0]

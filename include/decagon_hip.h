@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (3); bumped whenever a struct layout or a signature changes. */
+/* ABI version (4); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -159,7 +159,9 @@ typedef struct dg_gemm_desc {
     int32_t m, n, k, batch;
 } dg_gemm_desc;
 
-int dg_gemm_f32(const dg_gemm_desc* desc /* HOST */, void* stream);
+int dg_gemm_f32(const dg_gemm_desc* descs /* HOST array */, int32_t n_desc, void* stream);
+/* n_desc <= DG_MAX_GROUPS independent GEMMs in one launch (e.g. every (i,j) group's
+ * layer-2 projection). */
 
 /* --------------------------------------------------------------------------------------
  * Edge decoder scores (T8 + T9):  for pair p,
@@ -174,6 +176,21 @@ int dg_decoder_score_f32(const float* row_table, int64_t ld_row, const float* co
                          int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
                          int32_t n_pairs, const float* G, const float* l, int32_t d,
                          float* out, void* stream);
+
+/* Fused decoder step (T8 + T9 + T11 + T12 in one launch for batches of <= 512 pairs):
+ *   neg_row[b] = neg_rows[b] if neg_rows != NULL, else draw b of dg_unigram_sample(cdf, seed,
+ *                offset) (same stream of draws), written to neg_rows_out[b] if non-NULL;
+ *   pos[b] = score(rows[b], cols[b]);  neg[b] = score(neg_row[b], cols[b])   (as above)
+ *   loss[0] = sum_b relu(neg[b] - (pos[b] - margin))
+ * For n > 512 a second launch sums per-block partials from `workspace` (ceil(n/512)
+ * floats, device; may be NULL when n <= 512).
+ * Replaces optimizer.py:37-57 (sampler, gathers, pos/neg scores) + :116-120 (hinge). */
+int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
+                         int64_t ld_col, const int32_t* rows, const int32_t* cols,
+                         const int32_t* neg_rows, const float* cdf, int32_t cdf_range,
+                         uint64_t seed, uint64_t offset, int32_t n, const float* G,
+                         const float* l, int32_t d, float margin, float* pos, float* neg,
+                         int32_t* neg_rows_out, float* loss, float* workspace, void* stream);
 
 /* Hinge loss (T12):  loss[0] = sum_p relu(neg[p] - pos[p] + margin).
  * Replaces DecagonOptimizer._hinge_loss  optimizer.py:116-120.  Single workgroup,

@@ -82,7 +82,8 @@ def test_abi_rejects_bad_arguments_without_a_device():
     g[0].x_ld = 64
     assert lib.dg_spmm_groups_f32(g, 1, 64, None) == _lib.DG_EALIGN
     assert lib.dg_decoder_score_f32(None, 32, None, 32, None, None, 4, None, None, 33, None, None) == _lib.DG_EINVAL
-    assert lib.dg_gemm_f32(None, None) == _lib.DG_EINVAL
+    assert lib.dg_gemm_f32(None, 1, None) == _lib.DG_EINVAL
+    assert lib.dg_decoder_hinge_f32(*([None, 32, None, 32, None, None, None, None, 0, 0, 0, 4, None, None, 32, 0.1] + [None] * 6)) == _lib.DG_EINVAL
     e = (_lib.DgEpiGroup * 1)()
     assert lib.dg_gcn_epilogue_f32(e, 1, None, 10, 64, 128, None) == _lib.DG_EINVAL  # bad flags
     assert lib.dg_unigram_sample(None, 0, 5, 0, 0, None, None) == _lib.DG_EINVAL

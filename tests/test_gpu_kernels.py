@@ -225,3 +225,36 @@ def test_shape_checks_fail_before_launch(K):
     x = torch.zeros((5, 32), device="cuda")  # fewer rows than n_cols
     with pytest.raises(ValueError):
         K.RelGroupSpec(rp, cl, vl, x, torch.zeros((1, 10, 32), device="cuda"), 10, 10, 1, 1, 0, 32, 0).validate(32)
+
+
+@pytest.mark.parametrize("n", [512, 100, 1300])
+def test_decoder_hinge_fused(K, n):
+    """dg_decoder_hinge_f32: sampled negatives are exactly dg_unigram_sample's draws, both
+    score vectors match the oracle, the loss is the hinge of optimizer.py:116-120."""
+    rng = np.random.default_rng(n)
+    d, n_r, n_c = 32, 400, 300
+    U = rng.standard_normal((n_r, d)).astype(np.float32)
+    V = rng.standard_normal((n_c, d)).astype(np.float32)
+    G = (rng.standard_normal((d, d)) / 6).astype(np.float32)
+    l = rng.standard_normal(d).astype(np.float32)
+    rows = rng.integers(0, n_r, n).astype(np.int32)
+    cols = rng.integers(0, n_c, n).astype(np.int32)
+    deg = rng.integers(0, 30, n_r).astype(np.float64)
+    cdf = torch.from_numpy(np.cumsum(np.power(deg, 0.75)).astype(np.float32)).cuda()
+    dv = lambda a: torch.from_numpy(a).cuda()
+    op = K.PreparedDecoderHinge(dv(U), dv(V), dv(rows), dv(cols), dv(G), dv(l), 0.1, cdf=cdf, seed=3, offset=77)
+    op()
+    negs = op.neg_rows.cpu().numpy()
+    assert np.array_equal(negs, K.unigram_sample(cdf, n, 3, 77).cpu().numpy())
+    L = np.diag(l.astype(np.float64))
+    emb = [U.astype(np.float64), V.astype(np.float64)]
+    pos = orc.batch_predict(emb, 0, 1, G.astype(np.float64), L, rows, cols)
+    neg = orc.batch_predict(emb, 0, 1, G.astype(np.float64), L, negs, cols)
+    assert rel_err(op.pos.cpu().numpy(), pos) <= 1e-5
+    assert rel_err(op.neg.cpu().numpy(), neg) <= 1e-5
+    want = orc.hinge_loss(pos, neg, 0.1)
+    assert abs(float(op.loss[0]) - want) <= 1e-4 * abs(want)
+    # given negatives
+    op2 = K.PreparedDecoderHinge(dv(U), dv(V), dv(rows), dv(cols), dv(G), dv(l), 0.1, neg_rows=dv(negs))
+    op2()
+    assert np.array_equal(op2.neg.cpu().numpy(), op.neg.cpu().numpy())
