@@ -122,13 +122,12 @@ class Decoder:
         self.rows = torch.from_numpy(pick[:, 0].astype(np.int32)).to(device)
         self.cols = torch.from_numpy(pick[:, 1].astype(np.int32)).to(device)
         deg = graph.degrees[1][0]
-        self.cdf = torch.from_numpy(np.cumsum(np.power(deg, 0.75)).astype(np.float32)).to(device)
-        self.neg = torch.empty(BATCH, dtype=torch.int32, device=device)
+        self.alias = kernels.upload_alias(deg, device)
         self.R = torch.from_numpy(glorot_stack(rng, 1, H2, H2)[0]).to(device)
         self.l = torch.from_numpy(glorot_stack(rng, 1, H2, 1).reshape(-1)).to(device)
         self.E = plan.embeddings[1]
         self.fused = kernels.PreparedDecoderHinge(self.E, self.E, self.rows, self.cols, self.R, self.l,
-                                                  MARGIN, cdf=self.cdf, seed=7)
+                                                  MARGIN, alias=self.alias, seed=7)
 
     def __call__(self):
         self.fused()

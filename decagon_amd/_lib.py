@@ -19,7 +19,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 4
+ABI_VERSION = 6
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -42,6 +42,11 @@ class DgRelGroup(ctypes.Structure):
         ("x_rels", c_int32),
         ("reserved", c_int32 * 2),
     ]
+
+
+class DgProj(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("rel_map", c_void_p), ("out", c_void_p), ("n_rels", c_int32),
+                ("target", c_int32), ("d_out", c_int32), ("reserved", c_int32)]
 
 
 class DgFusedTarget(ctypes.Structure):
@@ -88,7 +93,8 @@ SIGNATURES = {
     ),
     "dg_gcn_fused_f32": (
         c_int32,
-        [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32, c_void_p],
+        [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, POINTER(DgProj), c_int32, c_int32,
+         c_int32, c_void_p],
     ),
     "dg_gcn_epilogue_f32": (
         c_int32,

@@ -23,21 +23,17 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-// Draw #idx of the counter-based unigram sampler: inverse CDF at a 24-bit uniform.
-__device__ __forceinline__ int unigram_draw(const float* cdf, int range, uint64_t seed,
+// Draw #idx of the counter-based unigram sampler from a Walker alias table: entry j holds
+// {acceptance probability (float bits), alias index}.  One 64-bit hash gives the column j
+// (high 32 bits, scaled by range) and the 24-bit acceptance uniform (low bits): one 8-byte
+// load per draw, no search.
+__device__ __forceinline__ int unigram_draw(const uint2* table, int range, uint64_t seed,
                                             uint64_t idx) {
     const uint64_t h = splitmix64(seed ^ splitmix64(idx));
-    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);  // [0,1), 24 bits
-    const float target = u * cdf[range - 1];
-    int lo = 0, hi = range - 1;  // first c with cdf[c] > target
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (cdf[mid] > target)
-            hi = mid;
-        else
-            lo = mid + 1;
-    }
-    return lo;
+    const int j = (int)(((h >> 32) * (uint64_t)range) >> 32);
+    const float u = (float)(h & 0xFFFFFFu) * (1.0f / 16777216.0f);
+    const uint2 e = table[j];
+    return u < __uint_as_float(e.x) ? j : (int)e.y;
 }
 
 struct DecTab {
@@ -131,84 +127,100 @@ __global__ __launch_bounds__(256) void decoder_score_kernel(const DecArgs a) {
 }
 
 // Fused decoder step (optimizer.py:37-57 + :116-120): for the batch pairs b < n,
-//   neg_row[b] = given[b] or a unigram draw (seed, offset + b),
+//   neg_row[b] = given[b] or draw (offset + b) of the alias sampler,
 //   pos[b] = score(rows[b], cols[b]),  neg[b] = score(neg_row[b], cols[b]),
-//   loss  += relu(neg[b] - (pos[b] - margin))
-// One workgroup of 16 waves per 512 batch pairs (32 tiles: 16 positive, 16 negative).  With
-// one workgroup the loss is written directly; otherwise each block writes its partial and
-// dg_decoder_hinge_f32 reduces them in a second, fixed-order launch.
-constexpr int kHingeBlock = 512;
-
+//   loss   = sum_b relu(neg[b] - (pos[b] - margin))
+// One workgroup of two waves per 32 pairs (wave 0 the positive tile, wave 1 the negative
+// tile).  Each workgroup folds its 32 hinge terms, publishes the partial and takes a ticket;
+// the last one (agent-scope release / acquire, cdna_hip_programming.md Guideline 16) adds
+// every partial in block order and resets the ticket counter — fixed order, no float
+// atomics, one launch.
 struct HingeArgs {
     DecTab t;
     const int32_t* rows;
     const int32_t* cols;
     const int32_t* neg_given;
-    const float* cdf;
+    const uint2* alias;
     float* pos;
     float* neg;
     int32_t* neg_rows_out;
     float* loss;        // [1]
-    float* partial;     // [gridDim.x] when gridDim.x > 1
+    float* partial;     // [gridDim.x]
+    uint32_t* ticket;   // zero before the first launch; the last block resets it
     uint64_t seed;
     uint64_t offset;
-    int32_t cdf_range;
+    int32_t range;
     int32_t n;
     float margin;
 };
 
-__global__ __launch_bounds__(1024) void decoder_hinge_kernel(const HingeArgs a) {
-    __shared__ float sc[2][kHingeBlock];
-    __shared__ float red[1024];
+__global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
+    __shared__ float sc[2][32];
+    __shared__ float red[128];
+    __shared__ int last;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;  // 0..15
+    const int side = threadIdx.x >> 6;  // 0: positives, 1: negatives
     const int i = lane & 31;
     const int h = lane >> 5;
-    const int b0 = blockIdx.x * kHingeBlock;
-#pragma unroll 1
-    for (int side = 0; side < 2; ++side) {  // 0: positives, 1: negatives
-        const int q0 = wave * 32;           // tile offset inside the block
-        const int b = b0 + q0 + i;
-        const bool valid = b < a.n;
-        int ridx = 0, cidx = 0;
-        if (valid) {
-            cidx = a.cols[b];
-            if (side == 0)
-                ridx = a.rows[b];
-            else if (a.neg_given)
-                ridx = a.neg_given[b];
-            else
-                ridx = unigram_draw(a.cdf, a.cdf_range, a.seed, a.offset + (uint64_t)b);
-            if (side == 1 && a.neg_rows_out && h == 0) a.neg_rows_out[b] = ridx;
-        }
-        float part[16];
-        if (b0 + q0 < a.n) score_tile(a.t, ridx, cidx, valid, part);
-        if (i == 0 && b0 + q0 < a.n) {
+    const int b0 = blockIdx.x * 32;
+    const int b = b0 + i;
+    const bool valid = b < a.n;
+    int ridx = 0, cidx = 0;
+    if (valid) {
+        cidx = a.cols[b];
+        if (side == 0)
+            ridx = a.rows[b];
+        else if (a.neg_given)
+            ridx = a.neg_given[b];
+        else
+            ridx = unigram_draw(a.alias, a.range, a.seed, a.offset + (uint64_t)b);
+        if (side == 1 && a.neg_rows_out && h == 0) a.neg_rows_out[b] = ridx;
+    }
+    float part[16];
+    score_tile(a.t, ridx, cidx, valid, part);
+    if (i == 0) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int q = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const float v = (b0 + q < a.n) ? part[r] : 0.f;
-                sc[side][q] = v;
-                if (b0 + q < a.n) (side == 0 ? a.pos : a.neg)[b0 + q] = v;
-            }
+        for (int r = 0; r < 16; ++r) {
+            const int q = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float v = (b0 + q < a.n) ? part[r] : 0.f;
+            sc[side][q] = v;
+            if (b0 + q < a.n) (side == 0 ? a.pos : a.neg)[b0 + q] = v;
         }
     }
     __syncthreads();
-    const int t = threadIdx.x;
-    float term = 0.f;
-    if (t < kHingeBlock && b0 + t < a.n) term = fmaxf(sc[1][t] - (sc[0][t] - a.margin), 0.f);
-    red[t] = term;
+    if (threadIdx.x < 64) {
+        float term = 0.f;
+        if (lane < 32 && b0 + lane < a.n) term = fmaxf(sc[1][lane] - (sc[0][lane] - a.margin), 0.f);
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) term += __shfl_xor(term, m);
+        if (lane == 0) {
+            a.partial[blockIdx.x] = term;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t t = atomicAdd(a.ticket, 1u);
+            last = (t == gridDim.x - 1) ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    if (!last) return;  // block-uniform
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    float s = 0.f;
+    for (int k = threadIdx.x; k < (int)gridDim.x; k += 128)
+        s += __hip_atomic_load(a.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    red[threadIdx.x] = s;
     __syncthreads();
 #pragma unroll
-    for (int w = 512; w > 0; w >>= 1) {
-        if (t < w) red[t] += red[t + w];
+    for (int w = 64; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (t == 0) {
-        if (gridDim.x == 1)
-            a.loss[0] = red[0];
-        else
-            a.partial[blockIdx.x] = red[0];
+    if (threadIdx.x == 0) {
+        a.loss[0] = red[0];
+        atomicExch(a.ticket, 0u);
     }
 }
 
@@ -251,17 +263,12 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* pos, const float
     if (threadIdx.x == 0) loss[0] = sp + w * sn;
 }
 
-__global__ __launch_bounds__(256) void unigram_sample_kernel(const float* cdf, int range, int n,
+__global__ __launch_bounds__(256) void unigram_sample_kernel(const uint2* table, int range, int n,
                                                              uint64_t seed, uint64_t offset,
                                                              int32_t* out) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= n) return;
-    out[idx] = unigram_draw(cdf, range, seed, offset + (uint64_t)idx);
-}
-
-__global__ __launch_bounds__(256) void sum_partials_kernel(const float* partial, int n, float* loss) {
-    const float s = block_sum_256(n, [&](int p) { return partial[p]; });
-    if (threadIdx.x == 0) loss[0] = s;
+    out[idx] = unigram_draw(table, range, seed, offset + (uint64_t)idx);
 }
 
 }  // namespace
@@ -301,50 +308,48 @@ extern "C" int dg_xent_loss_f32(const float* pos, const float* neg, int32_t n, f
     return dg::launch_status();
 }
 
-extern "C" int dg_unigram_sample(const float* cdf, int32_t range, int32_t n, uint64_t seed,
-                                 uint64_t offset, int32_t* out, void* stream) {
-    if (range < 1 || n < 0 || !cdf || (n > 0 && !out)) return DG_EINVAL;
+extern "C" int dg_unigram_sample(const uint32_t* alias_table, int32_t range, int32_t n,
+                                 uint64_t seed, uint64_t offset, int32_t* out, void* stream) {
+    if (range < 1 || n < 0 || !alias_table || (n > 0 && !out)) return DG_EINVAL;
     if (n == 0) return DG_OK;
     hipLaunchKernelGGL(unigram_sample_kernel, dim3(dg::ceil_div(n, 256)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), cdf, range, n, seed, offset, out);
+                       reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<const uint2*>(alias_table), range, n, seed, offset, out);
     return dg::launch_status();
 }
 
 extern "C" int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
                                     int64_t ld_col, const int32_t* rows, const int32_t* cols,
-                                    const int32_t* neg_rows, const float* cdf, int32_t cdf_range,
-                                    uint64_t seed, uint64_t offset, int32_t n, const float* G,
-                                    const float* l, int32_t d, float margin, float* pos, float* neg,
-                                    int32_t* neg_rows_out, float* loss, float* workspace,
-                                    void* stream) {
-    if (n < 0 || d <= 0 || (d % 32) || d > 256) return DG_EINVAL;
-    if (!row_table || !col_table || !rows || !cols || !G || !pos || !neg || !loss) return DG_EINVAL;
-    if (!neg_rows && (!cdf || cdf_range < 1)) return DG_EINVAL;
+                                    const int32_t* neg_rows, const uint32_t* alias_table,
+                                    int32_t range, uint64_t seed, uint64_t offset, int32_t n,
+                                    const float* G, const float* l, int32_t d, float margin,
+                                    float* pos, float* neg, int32_t* neg_rows_out, float* loss,
+                                    void* workspace, void* stream) {
+    if (n < 1 || d <= 0 || (d % 32) || d > 256) return DG_EINVAL;
+    if (!row_table || !col_table || !rows || !cols || !G || !pos || !neg || !loss || !workspace)
+        return DG_EINVAL;
+    if (!neg_rows && (!alias_table || range < 1)) return DG_EINVAL;
     if (ld_row < d || ld_col < d) return DG_EINVAL;
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int blocks = dg::ceil_div(n, kHingeBlock);
-    if (blocks > 1 && !workspace) return DG_EINVAL;
-    if (n == 0) {
-        hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, loss, 0, loss);
-        return dg::launch_status();
-    }
+    if (!dg::aligned16(workspace)) return DG_EALIGN;
+    const int blocks = dg::ceil_div(n, 32);
     HingeArgs a{};
     a.t = DecTab{row_table, col_table, G, l, ld_row, ld_col, d};
     a.rows = rows;
     a.cols = cols;
     a.neg_given = neg_rows;
-    a.cdf = cdf;
+    a.alias = reinterpret_cast<const uint2*>(alias_table);
     a.pos = pos;
     a.neg = neg;
     a.neg_rows_out = neg_rows_out;
     a.loss = loss;
-    a.partial = workspace;
+    a.ticket = reinterpret_cast<uint32_t*>(workspace);
+    a.partial = reinterpret_cast<float*>(workspace) + 4;
     a.seed = seed;
     a.offset = offset;
-    a.cdf_range = cdf_range;
+    a.range = range;
     a.n = n;
     a.margin = margin;
-    hipLaunchKernelGGL(decoder_hinge_kernel, dim3(blocks), dim3(1024), 0, st, a);
-    if (blocks > 1) hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, workspace, blocks, loss);
+    hipLaunchKernelGGL(decoder_hinge_kernel, dim3(blocks), dim3(128), 0,
+                       reinterpret_cast<hipStream_t>(stream), a);
     return dg::launch_status();
 }

@@ -69,10 +69,12 @@ constexpr int kUnroll = 8;        // gathers in flight per lane
 // wave scan of the lengths gives each segment's flat start.  Every 64 flat positions are
 // then mapped back to (segment, position) by a 6-step binary search over the scan
 // (ds_bpermute), loaded with one coalesced col/val load and consumed G per step by the
-// LP-lane groups with kUnroll 16-byte gathers in flight.  Returns the folded row in lanes
-// 0..LP-1 (lane q holds columns 4q..4q+3).
+// LP-lane groups with kUnroll 16-byte gathers in flight.  With wcount > 1 the waves of a
+// workgroup share the row: wave part wpart takes every wcount-th batch of 64.  Returns the
+// folded row in every lane (lane l holds columns 4(l%LP)..4(l%LP)+3).
 template <int LP>
-__device__ __forceinline__ float4 row_sum(const SpmmGroupK& g, int r, int k0, int k1, int d) {
+__device__ __forceinline__ float4 row_sum(const SpmmGroupK& g, int r, int k0, int k1, int d,
+                                          int wpart = 0, int wcount = 1) {
     constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
@@ -100,7 +102,7 @@ __device__ __forceinline__ float4 row_sum(const SpmmGroupK& g, int r, int k0, in
         const int total = __shfl(cum, 63);
         const int excl = cum - slen;
 #pragma unroll 1
-        for (int base = 0; base < total; base += 64) {
+        for (int base = wpart * 64; base < total; base += wcount * 64) {
             const int f = base + lane;
             int lo = 0, hi = 63;
 #pragma unroll
@@ -178,9 +180,12 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
 }
 
 // Fused mode (every group of a node type in one chunk): one workgroup per output row r of
-// node type i, one wave per group (i, j); each wave L2-normalises its group's row sum
-// (layers.py:93), the waves meet in LDS and wave 0 adds the groups in order and applies
-// relu (model.py:75) or not (model.py:88).
+// node type i; W waves per group (i, j) share the row's nonzeros.  The waves of a group
+// meet in LDS, the group's first wave L2-normalises the group sum (layers.py:93), then
+// wave 0 adds the groups in order and applies relu (model.py:75) or not (model.py:88).
+// Optional projection epilogue (layer 1 only): for every layer-2 group whose source node
+// type is i, P_k[r][:] = out[r][:] · W2_k — the next layer's H_j·W_k (layers.py:113) for
+// this row, a k-ordered fmaf chain exactly like the MFMA path — so layer 2 needs no GEMM.
 struct FusedTargetK {
     float* out;
     int32_t n_rows;
@@ -191,18 +196,33 @@ struct FusedTargetK {
     int32_t pad;
 };
 
+struct ProjK {
+    const float* w;
+    const int32_t* rel_map;
+    float* out;
+    int32_t n_rels;
+    int32_t target;
+    int32_t d_out;
+    int32_t pad;
+};
+
 struct FusedArgs {
     SpmmGroupK g[DG_MAX_GROUPS];
     FusedTargetK t[DG_MAX_GROUPS];
+    ProjK p[DG_MAX_GROUPS];
     int32_t n_groups;
     int32_t n_targets;
+    int32_t n_projs;
     int32_t d;
+    int32_t wpg;  // waves per group
     int32_t pad;
 };
 
 template <int LP>
-__global__ __launch_bounds__(512) void gcn_fused_kernel(const FusedArgs a) {
-    __shared__ float4 ybuf[DG_MAX_GROUPS][64];
+__global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
+    __shared__ float4 pbuf[16][LP];
+    __shared__ float4 ybuf[DG_MAX_GROUPS][LP];
+    __shared__ float hrow[4 * LP];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int b = blockIdx.x;
@@ -212,28 +232,57 @@ __global__ __launch_bounds__(512) void gcn_fused_kernel(const FusedArgs a) {
     const FusedTargetK& t = a.t[ti];
     const int r = b - t.block_begin;
     const int d = a.d;
-    if (wave < t.g_count) {
-        const SpmmGroupK& g = a.g[t.g_begin + wave];
-        float4 s = row_sum<LP>(g, r, 0, g.n_rels, d);
-        // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); lanes >= LP hold copies
+    const int W = a.wpg;
+    const int gl = wave / W;
+    const int part = wave - gl * W;
+    const int q = lane % LP;
+    if (gl < t.g_count) {
+        const SpmmGroupK& g = a.g[t.g_begin + gl];
+        const float4 s = row_sum<LP>(g, r, 0, g.n_rels, d, part, W);
+        if (lane < LP) pbuf[wave][lane] = s;
+    }
+    __syncthreads();
+    if (gl < t.g_count && part == 0) {
+        float4 s = pbuf[wave][q];
+        for (int w = 1; w < W; ++w) dg::add4(s, pbuf[wave + w][q]);
+        // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); columns >= d hold zeros
         float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
-        if (lane * 4 >= d) ss = 0.f;
 #pragma unroll
         for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
         const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
-        if (lane < LP) ybuf[wave][lane] = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+        if (lane < LP) ybuf[gl][lane] = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
     }
     __syncthreads();
-    if (wave == 0 && lane < LP && lane * 4 < d) {
+    if (wave == 0 && lane < LP) {
         float4 tot = ybuf[0][lane];
-        for (int w = 1; w < t.g_count; ++w) dg::add4(tot, ybuf[w][lane]);
+        for (int g = 1; g < t.g_count; ++g) dg::add4(tot, ybuf[g][lane]);
         if (t.relu) {
             tot.x = fmaxf(tot.x, 0.f);
             tot.y = fmaxf(tot.y, 0.f);
             tot.z = fmaxf(tot.z, 0.f);
             tot.w = fmaxf(tot.w, 0.f);
         }
-        *reinterpret_cast<float4*>(t.out + (int64_t)r * d + lane * 4) = tot;
+        if (lane * 4 < d) *reinterpret_cast<float4*>(t.out + (int64_t)r * d + lane * 4) = tot;
+        reinterpret_cast<float4*>(hrow)[lane] = tot;
+    }
+    if (a.n_projs == 0) return;  // launch-uniform
+    __syncthreads();
+#pragma unroll 1
+    for (int pi = 0; pi < a.n_projs; ++pi) {
+        const ProjK& pj = a.p[pi];
+        if (pj.target != ti) continue;
+        const int dout = pj.d_out;
+        const int total = pj.n_rels * dout;
+        for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+            const int kk = idx / dout;
+            const int c = idx - kk * dout;
+            const int rel = pj.rel_map ? pj.rel_map[kk] : kk;
+            const float* __restrict__ wcol = pj.w + (int64_t)rel * d * dout + c;
+            float acc = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < d; ++k) acc = fmaf(hrow[k], wcol[(int64_t)k * dout], acc);
+            pj.out[((int64_t)kk * t.n_rows + r) * dout + c] = acc;
+        }
     }
 }
 
@@ -308,7 +357,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 4; }
+extern "C" int32_t dg_abi_version(void) { return 6; }
 
 namespace {
 
@@ -377,15 +426,21 @@ extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, 
 }
 
 extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
-                                const dg_fused_target* targets, int32_t n_targets, int32_t d,
-                                void* stream) {
+                                const dg_fused_target* targets, int32_t n_targets,
+                                const dg_proj* projs, int32_t n_projs, int32_t waves_per_group,
+                                int32_t d, void* stream) {
     if (n_groups < 1 || !groups || n_targets < 1 || !targets) return DG_EINVAL;
-    if (n_groups > DG_MAX_GROUPS || n_targets > DG_MAX_GROUPS) return DG_ETOOMANY;
+    if (n_groups > DG_MAX_GROUPS || n_targets > DG_MAX_GROUPS || n_projs > DG_MAX_GROUPS)
+        return DG_ETOOMANY;
+    if (n_projs < 0 || (n_projs > 0 && !projs)) return DG_EINVAL;
     if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
+    if (waves_per_group < 1) return DG_EINVAL;
     FusedArgs a{};
     a.d = d;
     a.n_groups = n_groups;
     a.n_targets = n_targets;
+    a.n_projs = n_projs;
+    a.wpg = waves_per_group;
     for (int i = 0; i < n_groups; ++i) {
         dg_rel_group s = groups[i];
         s.chunk = s.n_rels > 0 ? s.n_rels : 1;
@@ -394,7 +449,7 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
         if (rc != DG_OK) return rc;
     }
     int64_t blocks = 0;
-    int max_waves = 1;
+    int max_groups = 1;
     for (int t = 0; t < n_targets; ++t) {
         const dg_fused_target& s = targets[t];
         if (!s.out || !dg::aligned16(s.out) || s.n_rows < 0 || s.g_count < 1 || s.g_begin < 0 ||
@@ -410,13 +465,20 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
         k.relu = (s.flags & DG_EPI_RELU) ? 1 : 0;
         k.block_begin = static_cast<int32_t>(blocks);
         blocks += s.n_rows;
-        max_waves = s.g_count > max_waves ? s.g_count : max_waves;
+        max_groups = s.g_count > max_groups ? s.g_count : max_groups;
+    }
+    if (max_groups * waves_per_group > 16) return DG_EINVAL;  // 1024 threads per workgroup
+    for (int i = 0; i < n_projs; ++i) {
+        const dg_proj& s = projs[i];
+        if (!s.w || !s.out || s.n_rels < 0 || s.d_out < 1 || s.target < 0 || s.target >= n_targets)
+            return DG_EINVAL;
+        a.p[i] = ProjK{s.w, s.rel_map, s.out, s.n_rels, s.target, s.d_out, 0};
     }
     if (blocks == 0) return DG_OK;
     if (blocks > 0x7fffffff) return DG_EINVAL;
     const int lp = dg::lanes_per_row(d);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    dim3 grid(static_cast<unsigned>(blocks)), block(64 * max_waves);
+    dim3 grid(static_cast<unsigned>(blocks)), block(64 * max_groups * waves_per_group);
 #define DG_LAUNCH_FUSED(L) hipLaunchKernelGGL(gcn_fused_kernel<L>, grid, block, 0, st, a)
     DG_LP_SWITCH(lp, DG_LAUNCH_FUSED)
 #undef DG_LAUNCH_FUSED

@@ -178,24 +178,13 @@ class ForwardPlan:
         self.hidden1 = {i: torch.empty((n[i], h1), **f32) for i in self.targets}
         self.embeddings = {i: torch.empty((n[i], h2), **f32) for i in self.targets}
 
-        # ---- layer 1: Σ_k Â_k·X_k (+ epilogue) ----
-        x1_specs = {}
-        for et in self.edge_types:
-            grp = dgraph.groups[et]
-            xt, xs, xld, x_rels = x1[et]
-            local_x = features.get(et[1]) is not None
-            x1_specs[et] = (xt, xs, xld, x_rels, None if local_x else grp.rel_map)
-        self._layer1 = self._build_layer(x1_specs, h1, True, chunk_override, target_waves, f32)
-
-        # ---- layer 2: P_k = H1_j·W2_k, then Σ_k Â_k·P_k (+ epilogue) ----
+        # ---- layer-2 projection buffers P_k = H1_j·W2_k ----
         self.proj: Dict[EdgeType, torch.Tensor] = {}
-        self._gemm2 = []
         x2_specs = {}
         for et in self.edge_types:
             i, j = et
             grp = dgraph.groups[et]
-            W = w2.stacks[et]
-            K, din, dout = W.shape
+            K, din, dout = w2.stacks[et].shape
             if din != h1 or dout != h2:
                 raise ValueError("layer-2 weight shape != (hidden1, hidden2)")
             if j not in self.hidden1:
@@ -203,19 +192,69 @@ class ForwardPlan:
             P = torch.empty((max(1, grp.n_rels), n[j], h2), **f32)
             self.proj[et] = P
             x2_specs[et] = (P, n[j] * h2, h2, max(1, grp.n_rels), None)
-            if not grp.n_rels:
+
+        # ---- layer 1: Σ_k Â_k·X_k (+ epilogue, + the layer-2 projections of fused rows) ----
+        x1_specs = {}
+        for et in self.edge_types:
+            grp = dgraph.groups[et]
+            xt, xs, xld, x_rels = x1[et]
+            local_x = features.get(et[1]) is not None
+            x1_specs[et] = (xt, xs, xld, x_rels, None if local_x else grp.rel_map)
+        fused1 = self._fused_targets(h1, chunk_override, target_waves)
+        rels_from = {}
+        for et in self.edge_types:
+            rels_from[et[1]] = rels_from.get(et[1], 0) + dgraph.groups[et].n_rels
+        proj_fused = [et for et in self.edge_types
+                      if dgraph.groups[et].n_rels and et[1] in fused1
+                      and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS]
+        if len(proj_fused) > DG_MAX_GROUPS:
+            proj_fused = []
+        projs = []
+        for et in proj_fused:
+            grp = dgraph.groups[et]
+            projs.append((et[1], kernels.ProjSpec(
+                w2.stacks[et], self.proj[et], grp.n_rels, -1, rel_map=grp.rel_map,
+                rel_map_max=int(grp.rel_ids.max()) if grp.rel_map is not None else None)))
+        self._layer1 = self._build_layer(x1_specs, h1, True, chunk_override, target_waves, f32, projs)
+
+        # ---- layer 2: remaining projections as one batched MFMA GEMM launch, then SpMM ----
+        gemms = []
+        for et in self.edge_types:
+            grp = dgraph.groups[et]
+            if not grp.n_rels or et in proj_fused:
                 continue
-            self._gemm2.append(kernels.PreparedGemm(
-                self.hidden1[j], (0, h1, 1), W, (h1 * h2, h2, 1), P, (n[j] * h2, h2, 1),
-                n[j], h2, h1, grp.n_rels, b_map=grp.rel_map, b_batches=K,
+            j = et[1]
+            W = w2.stacks[et]
+            gemms.append(kernels.PreparedGemm(
+                self.hidden1[j], (0, h1, 1), W, (h1 * h2, h2, 1), self.proj[et], (n[j] * h2, h2, 1),
+                n[j], h2, h1, grp.n_rels, b_map=grp.rel_map, b_batches=W.shape[0],
                 b_map_max=int(grp.rel_ids.max()) if grp.rel_map is not None else None))
-        # every group's projection in one launch (≤ DG_MAX_GROUPS per launch)
-        self._gemm2 = [kernels.PreparedGemmMulti(self._gemm2[s:s + DG_MAX_GROUPS])
-                       for s in range(0, len(self._gemm2), DG_MAX_GROUPS)]
+        self._gemm2 = [kernels.PreparedGemmMulti(gemms[s:s + DG_MAX_GROUPS])
+                       for s in range(0, len(gemms), DG_MAX_GROUPS)]
         self._layer2 = self._build_layer(x2_specs, h2, False, chunk_override, target_waves, f32)
 
+    # a fused launch projects a row onto at most this many layer-2 relations (VALU epilogue);
+    # beyond it the batched MFMA GEMM is used
+    FUSED_PROJ_MAX_RELS = 64
+
+    def _chunks(self, d, chunk_override, target_waves):
+        chunk, nch = {}, {}
+        for et in self.edge_types:
+            grp = self.g.groups[et]
+            c = chunk_override or choose_chunk(grp.n_rels, grp.n_rows, grp.nnz, d, target_waves)
+            chunk[et] = max(1, min(c, max(1, grp.n_rels)))
+            nch[et] = max(1, -(-grp.n_rels // chunk[et])) if grp.n_rels else 1
+        return chunk, nch
+
+    def _fused_targets(self, d, chunk_override, target_waves):
+        if self.allreduce is not None:
+            return []
+        _, nch = self._chunks(d, chunk_override, target_waves)
+        return [i for i, ets in self.targets.items()
+                if all(nch[et] == 1 and self.g.groups[et].n_rels > 0 for et in ets)]
+
     # ------------------------------------------------------------------ layer builder
-    def _build_layer(self, x_specs, d, relu, chunk_override, target_waves, f32):
+    def _build_layer(self, x_specs, d, relu, chunk_override, target_waves, f32, projs=()):
         """Prepared launches of one layer.  Per node type i: if every group (i, j) fits one
         chunk and no cross-rank sum is needed, the whole target runs in the fused kernel
         (SpMM + l2norm + Σ_j + relu, one launch for all such targets); otherwise its groups
@@ -224,12 +263,7 @@ class ForwardPlan:
         g = self.g
         n = g.n_nodes
         outs = self.hidden1 if relu else self.embeddings
-        chunk, nch = {}, {}
-        for et in self.edge_types:
-            grp = g.groups[et]
-            c = chunk_override or choose_chunk(grp.n_rels, grp.n_rows, grp.nnz, d, target_waves)
-            chunk[et] = max(1, min(c, max(1, grp.n_rels)))
-            nch[et] = max(1, -(-grp.n_rels // chunk[et])) if grp.n_rels else 1
+        chunk, nch = self._chunks(d, chunk_override, target_waves)
 
         def spec(et, out, ch):
             grp = g.groups[et]
@@ -239,15 +273,20 @@ class ForwardPlan:
                 grp.n_rows, rel_map=rmap, x_rels=x_rels,
                 rel_map_max=int(grp.rel_ids.max()) if rmap is not None else None)
 
-        fused_t = []
-        if self.allreduce is None:
-            fused_t = [i for i, ets in self.targets.items()
-                       if all(nch[et] == 1 and g.groups[et].n_rels > 0 for et in ets)]
+        fused_t = self._fused_targets(d, chunk_override, target_waves)
         launches: List[Callable[[], None]] = []
         if fused_t:
+            # waves per group: one batch of 64 nonzeros per wave for the densest row group
+            avg = max(g.groups[et].nnz / max(1, g.groups[et].n_rows) for i in fused_t for et in self.targets[i])
+            max_groups = max(len(self.targets[i]) for i in fused_t)
+            wpg = int(max(1, min(4, 16 // max_groups, math.ceil(avg / 64.0))))
+            pspecs = []
+            for tgt_node, pj in projs:
+                pj.target = fused_t.index(tgt_node)
+                pspecs.append(pj)
             launches.append(kernels.PreparedFused(
                 [(outs[i], n[i], [spec(et, None, max(1, g.groups[et].n_rels)) for et in self.targets[i]], relu)
-                 for i in fused_t], d))
+                 for i in fused_t], d, pspecs, wpg))
         rest = [et for et in self.edge_types if et[0] not in fused_t]
         flags = DG_EPI_L2NORM | (DG_EPI_RELU if relu else 0)
         flat, views = None, {}

@@ -14,10 +14,11 @@ import ctypes
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib
-from ._lib import DgEpiGroup, DgFusedTarget, DgGemmDesc, DgRelGroup, check
+from ._lib import DgEpiGroup, DgFusedTarget, DgGemmDesc, DgProj, DgRelGroup, check
 
 
 def _stream_ptr(stream: Optional[torch.cuda.Stream] = None) -> int:
@@ -145,11 +146,26 @@ class PreparedSpmm:
         check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_groups_f32")
 
 
-class PreparedFused:
-    """A fixed dg_gcn_fused_f32 launch: targets = [(out tensor, n_rows, [group specs], relu)]."""
+@dataclass
+class ProjSpec:
+    """Projection epilogue of a fused launch: out[kk] = row · w[rel_map[kk] or kk]."""
 
-    def __init__(self, targets, d: int):
+    w: torch.Tensor                     # float32 [K, d, d_out]
+    out: torch.Tensor                   # float32 [n_rels, n_rows, d_out]
+    n_rels: int
+    target: int                         # index into the fused launch's targets
+    rel_map: Optional[torch.Tensor] = None
+    rel_map_max: Optional[int] = None
+
+
+class PreparedFused:
+    """A fixed dg_gcn_fused_f32 launch.
+
+    targets = [(out tensor, n_rows, [group specs], relu)], projs = [ProjSpec]."""
+
+    def __init__(self, targets, d: int, projs: Sequence[ProjSpec] = (), waves_per_group: int = 1):
         specs, tarr = [], (DgFusedTarget * len(targets))()
+        max_groups = 1
         for t, (out, n_rows, gspecs, relu) in enumerate(targets):
             _dev(out, torch.float32, "out")
             if out.numel() < n_rows * d:
@@ -159,6 +175,7 @@ class PreparedFused:
             tarr[t].g_begin = len(specs)
             tarr[t].g_count = len(gspecs)
             tarr[t].flags = _lib.DG_EPI_RELU if relu else 0
+            max_groups = max(max_groups, len(gspecs))
             for s in gspecs:
                 if s.n_rows != n_rows:
                     raise ValueError("group rows != target rows")
@@ -166,17 +183,42 @@ class PreparedFused:
                 specs.append(s)
         if len(specs) > _lib.DG_MAX_GROUPS or len(targets) > _lib.DG_MAX_GROUPS:
             raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups / targets per fused launch")
+        if not 1 <= waves_per_group or max_groups * waves_per_group > 16:
+            raise ValueError("groups x waves_per_group must be <= 16")
+        if len(projs) > _lib.DG_MAX_GROUPS:
+            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} projections per fused launch")
+        parr = (DgProj * max(1, len(projs)))()
+        for i, pj in enumerate(projs):
+            _dev(pj.w, torch.float32, "proj w")
+            _dev(pj.out, torch.float32, "proj out")
+            K, din, dout = pj.w.shape
+            n_rows = targets[pj.target][1]
+            if din != d or pj.out.numel() < pj.n_rels * n_rows * dout:
+                raise ValueError("projection shapes do not match the fused layer")
+            if pj.rel_map is not None:
+                _dev(pj.rel_map, torch.int32, "proj rel_map")
+                if pj.rel_map_max is None or not 0 <= pj.rel_map_max < K:
+                    raise ValueError("proj rel_map_max must index inside w")
+            elif pj.n_rels > K:
+                raise ValueError("projection n_rels > K")
+            parr[i].w = pj.w.data_ptr()
+            parr[i].rel_map = pj.rel_map.data_ptr() if pj.rel_map is not None else None
+            parr[i].out = pj.out.data_ptr()
+            parr[i].n_rels = pj.n_rels
+            parr[i].target = pj.target
+            parr[i].d_out = dout
         garr = (DgRelGroup * len(specs))()
         for i, s in enumerate(specs):
             _fill_group(garr[i], s)
-        self._keep = (specs, [t[0] for t in targets])
-        self._garr, self._tarr = garr, tarr
-        self._ng, self._nt, self.d = len(specs), len(targets), d
+        self._keep = (specs, [t[0] for t in targets], list(projs))
+        self._garr, self._tarr, self._parr = garr, tarr, parr
+        self._ng, self._nt, self._np, self.d = len(specs), len(targets), len(projs), d
+        self.wpg = waves_per_group
         self._fn = _lib.load().dg_gcn_fused_f32
 
     def __call__(self, stream=None) -> None:
-        check(self._fn(self._garr, self._ng, self._tarr, self._nt, self.d, _stream_ptr(stream)),
-              "dg_gcn_fused_f32")
+        check(self._fn(self._garr, self._ng, self._tarr, self._nt, self._parr if self._np else None, self._np,
+                       self.wpg, self.d, _stream_ptr(stream)), "dg_gcn_fused_f32")
 
 
 def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:
@@ -373,42 +415,53 @@ def xent_loss(pos: torch.Tensor, neg: torch.Tensor, neg_weight: float,
     return out
 
 
-def unigram_sample(cdf: torch.Tensor, n: int, seed: int, offset: int,
+def unigram_sample(table: torch.Tensor, n: int, seed: int, offset: int,
                    out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-    _dev(cdf, torch.float32, "cdf")
+    """n draws from an alias table (sampling.alias_table, uploaded as int32 [range, 2])."""
+    _dev(table, torch.int32, "alias table")
+    if table.dim() != 2 or table.shape[1] != 2:
+        raise ValueError("alias table must be [range, 2]")
     if out is None:
-        out = torch.empty(n, device=cdf.device, dtype=torch.int32)
+        out = torch.empty(n, device=table.device, dtype=torch.int32)
     _dev(out, torch.int32, "out")
     if out.numel() < n:
         raise ValueError("out too small")
-    check(_lib.load().dg_unigram_sample(cdf.data_ptr(), cdf.numel(), n, seed & (2**64 - 1),
+    check(_lib.load().dg_unigram_sample(table.data_ptr(), table.shape[0], n, seed & (2**64 - 1),
                                          offset & (2**64 - 1), out.data_ptr(), _stream_ptr(stream)),
           "dg_unigram_sample")
     return out
 
 
+def upload_alias(degrees, device) -> torch.Tensor:
+    from .sampling import alias_table
+
+    return torch.from_numpy(alias_table(degrees).view(np.int32)).to(device)
+
+
 class PreparedDecoderHinge:
     """dg_decoder_hinge_f32 on fixed buffers: sampled (or given) negatives, positive and
-    negative scores of n pairs and the hinge loss, in one launch (two when n > 512)."""
+    negative scores of n pairs and the hinge loss, in one launch."""
 
     def __init__(self, row_table: torch.Tensor, col_table: torch.Tensor, rows: torch.Tensor,
                  cols: torch.Tensor, G: torch.Tensor, l: Optional[torch.Tensor], margin: float,
-                 cdf: Optional[torch.Tensor] = None, neg_rows: Optional[torch.Tensor] = None,
+                 alias: Optional[torch.Tensor] = None, neg_rows: Optional[torch.Tensor] = None,
                  seed: int = 0, offset: int = 0):
         for t, nm, dt in ((row_table, "row_table", torch.float32), (col_table, "col_table", torch.float32),
                           (rows, "rows", torch.int32), (cols, "cols", torch.int32), (G, "G", torch.float32)):
             _dev(t, dt, nm)
         d = G.shape[0]
         n = rows.numel()
+        if n < 1:
+            raise ValueError("empty batch")
         if G.shape != (d, d) or row_table.shape[1] != d or col_table.shape[1] != d or cols.numel() != n:
             raise ValueError("decoder_hinge: shape mismatch")
         if l is not None:
             _dev(l, torch.float32, "l")
         if neg_rows is None:
-            if cdf is None:
-                raise ValueError("need either negatives or a sampler CDF")
-            _dev(cdf, torch.float32, "cdf")
-            if cdf.numel() > row_table.shape[0]:
+            if alias is None:
+                raise ValueError("need either negatives or a sampler alias table")
+            _dev(alias, torch.int32, "alias")
+            if alias.shape[0] > row_table.shape[0]:
                 raise ValueError("sampler range exceeds the row table")
         else:
             _dev(neg_rows, torch.int32, "neg_rows")
@@ -417,12 +470,12 @@ class PreparedDecoderHinge:
         self.neg = torch.empty(n, device=dev)
         self.neg_rows = torch.empty(n, device=dev, dtype=torch.int32)
         self.loss = torch.empty(1, device=dev)
-        self._ws = torch.empty(max(1, -(-n // 512)), device=dev)
-        self._keep = (row_table, col_table, rows, cols, G, l, cdf, neg_rows)
+        self._ws = torch.zeros(4 + -(-n // 32), device=dev)  # ticket word + partials
+        self._keep = (row_table, col_table, rows, cols, G, l, alias, neg_rows)
         self.seed, self.offset = seed, offset
         self._args = [row_table.data_ptr(), row_table.shape[1], col_table.data_ptr(), col_table.shape[1],
                       rows.data_ptr(), cols.data_ptr(), neg_rows.data_ptr() if neg_rows is not None else None,
-                      cdf.data_ptr() if cdf is not None else None, cdf.numel() if cdf is not None else 0,
+                      alias.data_ptr() if alias is not None else None, alias.shape[0] if alias is not None else 0,
                       seed, offset, n, G.data_ptr(), l.data_ptr() if l is not None else None, d, float(margin),
                       self.pos.data_ptr(), self.neg.data_ptr(), self.neg_rows.data_ptr(), self.loss.data_ptr(),
                       self._ws.data_ptr()]

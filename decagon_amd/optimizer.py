@@ -24,16 +24,10 @@ from .graph import InvalidArgumentError, Node, Operation, RunContext
 
 
 class _Sampler:
-    """Per-relation device CDFs of degree^0.75 (built once per session)."""
+    """Per-relation device alias tables of degree^0.75 (built once per session)."""
 
     def __init__(self, degrees_list, device):
-        self.cdfs = []
-        for deg in degrees_list:
-            w = np.power(np.asarray(deg, np.float64), 0.75)
-            cdf = np.cumsum(w).astype(np.float32)
-            if cdf.size == 0 or cdf[-1] <= 0:
-                raise ValueError("unigram sampler needs a positive total degree")
-            self.cdfs.append(torch.from_numpy(cdf).to(device))
+        self.tables = [kernels.upload_alias(deg, device) for deg in degrees_list]
         self.counter = 0
 
 
@@ -147,9 +141,9 @@ class DecagonOptimizer:
             op = kernels.PreparedDecoderHinge(row_t, col_t, rows, cols, G, l, self.margin, neg_rows=negs)
         else:
             s = self._sampler(ctx)
-            if s.cdfs[e].numel() > row_t.shape[0]:
+            if s.tables[e].shape[0] > row_t.shape[0]:
                 raise InvalidArgumentError("degrees list longer than the row embedding table")
-            op = kernels.PreparedDecoderHinge(row_t, col_t, rows, cols, G, l, self.margin, cdf=s.cdfs[e],
+            op = kernels.PreparedDecoderHinge(row_t, col_t, rows, cols, G, l, self.margin, alias=s.tables[e],
                                               seed=self.seed, offset=s.counter)
             s.counter += rows.numel()
         op()

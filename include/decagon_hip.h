@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (4); bumped whenever a struct layout or a signature changes. */
+/* ABI version (6); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -85,13 +85,18 @@ int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                     int64_t ldy, int32_t d, void* stream);
 
 /* --------------------------------------------------------------------------------------
- * Fused GCN layer (T3 + T4 + T5 + T6 in one launch) for node types whose groups each fit
- * one chunk: for every target t (a node type i) and row r < n_rows,
+ * Fused GCN layer (T3 + T4 + T5 + T6, optionally T7 of the next layer, in one launch) for
+ * node types whose groups each fit one chunk: for every target t (a node type i), r < n_rows,
  *
  *     out_t[r] = act( sum_{g in [g_begin, g_begin+g_count)} l2norm( sum_k A_g,k[r]·X_g,k ) )
  *
  * act = relu if flags & DG_EPI_RELU.  The groups' `chunk` and `out` fields are ignored.
- * One workgroup per output row, one wave per group (g_count <= DG_MAX_GROUPS).
+ * One workgroup per output row, `waves_per_group` waves per group sharing the row's nonzeros
+ * (g_count * waves_per_group <= 16).
+ * Projection epilogue: for each dg_proj p with p.target == t,
+ *     p.out[kk][r][c] = sum_k out_t[r][k] * p.w[rel(kk)][k][c]     kk < p.n_rels, c < d_out
+ * (rel(kk) = p.rel_map[kk] or kk; p.w is a [K][d][d_out] stack; p.out is [n_rels][n_rows][d_out])
+ * — the next layer's H_j·W_k (layers.py:113) for the rows just produced.
  * Replaces the per-relation SpMM + add_n + l2_normalize of layers.py:85-94 / 109-118 and the
  * sum over edge types (+ relu) of model.py:74-75 / 85-88.
  * -------------------------------------------------------------------------------------- */
@@ -103,9 +108,20 @@ typedef struct dg_fused_target {
     int32_t flags;              /* 0 or DG_EPI_RELU */
 } dg_fused_target;
 
+typedef struct dg_proj {
+    const float* w;             /* device, [K][d][d_out] weight stack        */
+    const int32_t* rel_map;     /* device, [n_rels] or NULL                  */
+    float* out;                 /* device, [n_rels][n_rows of target][d_out] */
+    int32_t n_rels;
+    int32_t target;             /* index into the targets array              */
+    int32_t d_out;
+    int32_t reserved;
+} dg_proj;
+
 int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
-                     const dg_fused_target* targets /* HOST */, int32_t n_targets, int32_t d,
-                     void* stream);
+                     const dg_fused_target* targets /* HOST */, int32_t n_targets,
+                     const dg_proj* projs /* HOST, may be NULL */, int32_t n_projs,
+                     int32_t waves_per_group, int32_t d, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * GCN epilogue (T4 tail + T5 + T6):  for one node type i with groups g = (i, j_1..j_m),
@@ -177,20 +193,21 @@ int dg_decoder_score_f32(const float* row_table, int64_t ld_row, const float* co
                          int32_t n_pairs, const float* G, const float* l, int32_t d,
                          float* out, void* stream);
 
-/* Fused decoder step (T8 + T9 + T11 + T12 in one launch for batches of <= 512 pairs):
- *   neg_row[b] = neg_rows[b] if neg_rows != NULL, else draw b of dg_unigram_sample(cdf, seed,
- *                offset) (same stream of draws), written to neg_rows_out[b] if non-NULL;
+/* Fused decoder step (T8 + T9 + T11 + T12 in one launch):
+ *   neg_row[b] = neg_rows[b] if neg_rows != NULL, else draw (offset + b) of the alias
+ *                sampler — the same draws as dg_unigram_sample — written to neg_rows_out[b]
+ *                if non-NULL;
  *   pos[b] = score(rows[b], cols[b]);  neg[b] = score(neg_row[b], cols[b])   (as above)
- *   loss[0] = sum_b relu(neg[b] - (pos[b] - margin))
- * For n > 512 a second launch sums per-block partials from `workspace` (ceil(n/512)
- * floats, device; may be NULL when n <= 512).
+ *   loss[0] = sum_b relu(neg[b] - (pos[b] - margin))   (fixed block order)
+ * workspace: device, 16-byte aligned, 16 + 4*ceil(n/32) bytes, its first word zero before
+ * the first call (the kernel leaves it zero again).  n >= 1.
  * Replaces optimizer.py:37-57 (sampler, gathers, pos/neg scores) + :116-120 (hinge). */
 int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
                          int64_t ld_col, const int32_t* rows, const int32_t* cols,
-                         const int32_t* neg_rows, const float* cdf, int32_t cdf_range,
+                         const int32_t* neg_rows, const uint32_t* alias_table, int32_t range,
                          uint64_t seed, uint64_t offset, int32_t n, const float* G,
                          const float* l, int32_t d, float margin, float* pos, float* neg,
-                         int32_t* neg_rows_out, float* loss, float* workspace, void* stream);
+                         int32_t* neg_rows_out, float* loss, void* workspace, void* stream);
 
 /* Hinge loss (T12):  loss[0] = sum_p relu(neg[p] - pos[p] + margin).
  * Replaces DecagonOptimizer._hinge_loss  optimizer.py:116-120.  Single workgroup,
@@ -204,13 +221,14 @@ int dg_xent_loss_f32(const float* pos, const float* neg, int32_t n, float neg_we
                      float* loss, void* stream);
 
 /* --------------------------------------------------------------------------------------
- * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, drawn by
- * inverse CDF from a counter-based hash (seed, offset + i).  cdf is the inclusive prefix
- * sum of the (distorted) weights, cdf[range-1] > 0.
+ * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, draw
+ * (offset + i) of a counter-based hash stream, through a Walker alias table of `range`
+ * entries {acceptance probability as float bits, alias index} (uint32 pairs, built once on
+ * the host: decagon_amd/sampling.py).
  * Replaces tf.nn.fixed_unigram_candidate_sampler(distortion=0.75, unique=False)
  * optimizer.py:40-47 (distribution only — TF's RNG stream is not reproducible).
  * -------------------------------------------------------------------------------------- */
-int dg_unigram_sample(const float* cdf, int32_t range, int32_t n, uint64_t seed,
+int dg_unigram_sample(const uint32_t* alias_table, int32_t range, int32_t n, uint64_t seed,
                       uint64_t offset, int32_t* out, void* stream);
 
 #ifdef __cplusplus

@@ -165,3 +165,16 @@ def test_flags_defaults_match_main_py():
 
     assert FLAGS.hidden1 == 64 and FLAGS.hidden2 == 32 and FLAGS.batch_size == 512
     assert FLAGS.max_margin == 0.1 and FLAGS.learning_rate == 0.001
+
+
+def test_alias_table_encodes_the_unigram_distribution():
+    from decagon_amd.sampling import alias_table, table_distribution
+    from oracle.decagon_oracle import unigram_distribution
+
+    rng = np.random.default_rng(3)
+    for deg in (rng.integers(0, 100, 645).astype(float), np.array([0.0, 0.0, 5.0]), np.ones(7)):
+        tab = alias_table(deg)
+        assert tab.shape == (deg.shape[0], 2)
+        assert np.max(np.abs(table_distribution(tab) - unigram_distribution(deg))) < 1e-7
+    with pytest.raises(ValueError):
+        alias_table(np.zeros(4))

@@ -203,18 +203,22 @@ def test_losses(K):
 
 
 def test_unigram_sampler_distribution(K):
+    from decagon_amd.sampling import alias_table, table_distribution
+
     rng = np.random.default_rng(9)
     deg = rng.integers(0, 50, 400).astype(np.float64)
     deg[:10] = 0
     p = orc.unigram_distribution(deg)
-    cdf = torch.from_numpy(np.cumsum(np.power(deg, 0.75)).astype(np.float32)).cuda()
+    tab = alias_table(deg)
+    assert np.max(np.abs(table_distribution(tab) - p)) < 1e-7  # the table encodes p exactly
+    dt = torch.from_numpy(tab.view(np.int32)).cuda()
     n = 400000
-    s = K.unigram_sample(cdf, n, seed=1, offset=0).cpu().numpy()
+    s = K.unigram_sample(dt, n, seed=1, offset=0).cpu().numpy()
     assert s.min() >= 0 and s.max() < 400
     assert np.all(np.bincount(s, minlength=400)[:10] == 0)  # zero degree never drawn
     freq = np.bincount(s, minlength=400) / n
     assert np.max(np.abs(freq - p)) < 5e-3
-    s2 = K.unigram_sample(cdf, n, seed=1, offset=0).cpu().numpy()
+    s2 = K.unigram_sample(dt, n, seed=1, offset=0).cpu().numpy()
     assert np.array_equal(s, s2)  # counter-based: reproducible
 
 
@@ -240,12 +244,17 @@ def test_decoder_hinge_fused(K, n):
     rows = rng.integers(0, n_r, n).astype(np.int32)
     cols = rng.integers(0, n_c, n).astype(np.int32)
     deg = rng.integers(0, 30, n_r).astype(np.float64)
-    cdf = torch.from_numpy(np.cumsum(np.power(deg, 0.75)).astype(np.float32)).cuda()
+    tab = K.upload_alias(deg, "cuda")
     dv = lambda a: torch.from_numpy(a).cuda()
-    op = K.PreparedDecoderHinge(dv(U), dv(V), dv(rows), dv(cols), dv(G), dv(l), 0.1, cdf=cdf, seed=3, offset=77)
+    op = K.PreparedDecoderHinge(dv(U), dv(V), dv(rows), dv(cols), dv(G), dv(l), 0.1, alias=tab, seed=3, offset=77)
     op()
     negs = op.neg_rows.cpu().numpy()
-    assert np.array_equal(negs, K.unigram_sample(cdf, n, 3, 77).cpu().numpy())
+    assert np.array_equal(negs, K.unigram_sample(tab, n, 3, 77).cpu().numpy())
+    op()  # a second launch reuses the ticket counter the first one reset
+    assert abs(float(op.loss[0]) - orc.hinge_loss(orc.batch_predict([U.astype(np.float64), V.astype(np.float64)], 0, 1,
+               G.astype(np.float64), np.diag(l.astype(np.float64)), rows, cols),
+               orc.batch_predict([U.astype(np.float64), V.astype(np.float64)], 0, 1, G.astype(np.float64),
+               np.diag(l.astype(np.float64)), negs, cols), 0.1)) <= 1e-3
     L = np.diag(l.astype(np.float64))
     emb = [U.astype(np.float64), V.astype(np.float64)]
     pos = orc.batch_predict(emb, 0, 1, G.astype(np.float64), L, rows, cols)
