@@ -92,7 +92,8 @@ def make_plan(args, graph, shard, device):
     csr = graph.csr()
     if shard is not None:  # only local relations need host CSR / upload
         csr = {et: [c if k in set(shard.local[et]) else None for k, c in enumerate(v)] for et, v in csr.items()}
-    dg = DeviceGraph(graph.edge_types, csr, device, None if shard is None else shard.local)
+    dg = DeviceGraph(graph.edge_types, csr, device, None if shard is None else shard.local,
+                     chunk=args.chunk, target_waves=args.target_waves)
     rng = np.random.default_rng(1234)
     n = graph.n_nodes
     w1 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, n[et[1]], H1)).to(device)
@@ -100,8 +101,7 @@ def make_plan(args, graph, shard, device):
     w2 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, H1, H2)).to(device)
                        for et, K in graph.edge_types.items()})
     plan = ForwardPlan(dg, {j: None for j in n}, w1, w2, H1, H2,
-                       allreduce=None if shard is None else shard.allreduce,
-                       chunk_override=args.chunk, target_waves=args.target_waves)
+                       allreduce=None if shard is None else shard.allreduce)
     return plan, dg
 
 

@@ -19,7 +19,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -27,20 +27,15 @@ _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMA
 class DgRelGroup(ctypes.Structure):
     _fields_ = [
         ("rowptr", c_void_p),
-        ("col", c_void_p),
+        ("vcol", c_void_p),
         ("val", c_void_p),
         ("x", c_void_p),
         ("out", c_void_p),
-        ("rel_map", c_void_p),
-        ("x_rel_stride", c_int64),
         ("x_ld", c_int64),
-        ("rowptr_rel_stride", c_int32),
         ("n_rows", c_int32),
-        ("n_rels", c_int32),
-        ("chunk", c_int32),
-        ("n_cols", c_int32),
-        ("x_rels", c_int32),
-        ("reserved", c_int32 * 2),
+        ("n_chunks", c_int32),
+        ("x_rows", c_int32),
+        ("reserved", c_int32 * 3),
     ]
 
 

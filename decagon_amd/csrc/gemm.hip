@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
         }
         if (col_ok) {
             const float s = g.sc ? g.sc[col] : 1.0f;
-            float* C = g.c + b * g.c_bs + (int64_t)col * g.c_sn;
+            float* C = g.c + bb * g.c_bs + (int64_t)col * g.c_sn;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void gemm_f32_resident_a(const GemmArgs args) 
         for (int s = 0; s < S; ++s)
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(afrag[s], bfrag[s], acc, 0, 0, 0);
         if (col_ok) {
-            float* C = g.c + b * g.c_bs + (int64_t)col * g.c_sn;
+            float* C = g.c + bb * g.c_bs + (int64_t)col * g.c_sn;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;

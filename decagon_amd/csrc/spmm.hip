@@ -1,4 +1,4 @@
-// Relation-group CSR SpMM and the fused GCN epilogue for gfx950 (MI355X).
+// Relation-group CSR SpMM and the fused GCN layer for gfx950 (MI355X).
 //
 // Reference ops replaced (paths relative to the reference root):
 //   tf.sparse_tensor_dense_matmul(adj_mats[edge_type][k], x)  decagon/deep/layers.py:90, :114
@@ -6,18 +6,23 @@
 //   tf.add_n(outputs) / tf.nn.l2_normalize(outputs, dim=1)     decagon/deep/layers.py:92-93, :116-117
 //   tf.nn.relu(tf.add_n(hid1)) / tf.add_n(embeds)              decagon/deep/model.py:75, :88
 //
-// Work decomposition:
-//   one launch covers every (i,j) group of a layer; a wave owns one output row r of one
-//   relation chunk c and walks the nonzeros of row r in every relation of the chunk.
-//   A dense row of width d is covered by LP = d/4 lanes holding one float4 each, so a wave
-//   consumes G = 64/LP nonzeros per step (d=64: 16 lanes x 4 nonzeros; d=32: 8 x 8).
-//   The (col,val) pairs of up to 64 nonzeros are loaded by one coalesced load and handed to
-//   the lane groups with ds_bpermute; row pointers of up to 64 relations likewise with one
-//   load, read back with v_readlane (wave-uniform).  The G partial sums are folded with a
-//   shuffle butterfly and written once per (chunk, row): no atomics, fixed order.
-//   Blocks are dealt to XCDs round-robin; the block->work-item map gives each XCD a
-//   contiguous run of items (chunk-major), so the dense operands X_k of one chunk stay in
-//   one XCD's L2 while all its rows are processed.
+// Data layout: a group's relations are stored as a chunk-merged CSR.
+// For chunk c (a run of consecutive relations) and row r, the nonzeros of every relation of
+// the chunk in row r are contiguous, [rowptr[c*n_rows + r], rowptr[c*n_rows + r + 1]), and
+// each carries a virtual column v = k*n_cols + col: the row of the relation-stacked dense
+// operand X = [X_0; X_1; ...] it multiplies.  Σ_{k in chunk} Â_k[r]·X_k is then one sparse
+// dot product over one contiguous range — built once at upload, so no kernel ever looks up
+// per-relation row pointers.
+//
+// Work decomposition: a wave owns one (chunk, row) range.  A dense row of width d is held by
+// LP = d/4 lanes (one float4 each), so a wave consumes G = 64/LP nonzeros per step (d=64:
+// 16 lanes x 4; d=32: 8 x 8).  64 (vcol, val) pairs come in with one coalesced load (the next
+// 64 are prefetched while the current ones are consumed), are handed to the lane groups with
+// ds_bpermute, and kUnroll 16-byte gathers per lane are kept in flight.  The G partial sums
+// are folded with a shuffle butterfly: fixed order, no atomics.
+// Partial mode writes out[c][r][:]; fused mode (one chunk per group) finishes the layer in
+// the same workgroup: L2 norm per group, Σ over the node type's groups, relu, and optionally
+// the next layer's projection of the finished row.
 #include "common.h"
 
 #define DG_LP_SWITCH(LPV, CALL)                     \
@@ -36,17 +41,12 @@ namespace {
 
 struct SpmmGroupK {
     const int32_t* rowptr;
-    const int32_t* col;
+    const int32_t* vcol;
     const float* val;
     const float* x;
     float* out;
-    const int32_t* rel_map;
-    int32_t x_rel_stride;  // elements (the host guarantees every offset fits in int32)
-    int32_t x_ld;
-    int32_t rowptr_rel_stride;
+    int32_t x_ld;  // elements; the host guarantees x_rows * x_ld < 2^31
     int32_t n_rows;
-    int32_t n_rels;
-    int32_t chunk;
     int32_t n_chunks;
     int32_t row_blocks;
     int32_t block_begin;
@@ -59,102 +59,68 @@ struct SpmmArgs {
     int32_t d;
 };
 
-constexpr int kRowsPerBlock = 4;  // partial mode: 4 waves x 1 row
+constexpr int kRowsPerBlock = 4;  // partial mode: 4 waves x 1 (chunk, row)
 constexpr int kUnroll = 8;        // gathers in flight per lane
 
-// Sum over the nonzeros of row r in relations [k0, k1) of group g:
-//   acc = sum_k sum_{p in row r of A_k} val[p] * X_{rel(k)}[col[p]][:]
-// The row's segments in the (up to 64) relations of a batch are flattened into one index
-// space: lane t holds segment t (begin, length, X offset of its relation); an inclusive
-// wave scan of the lengths gives each segment's flat start.  Every 64 flat positions are
-// then mapped back to (segment, position) by a 6-step binary search over the scan
-// (ds_bpermute), loaded with one coalesced col/val load and consumed G per step by the
-// LP-lane groups with kUnroll 16-byte gathers in flight.  With wcount > 1 the waves of a
-// workgroup share the row: wave part wpart takes every wcount-th batch of 64.  Returns the
-// folded row in every lane (lane l holds columns 4(l%LP)..4(l%LP)+3).
+// acc = Σ_{p in [beg, end)} val[p] * X[vcol[p]][:], over every wcount-th batch of 64
+// starting at batch wpart.  Returns the folded row in every lane (lane l holds columns
+// 4(l%LP) .. 4(l%LP)+3).
 template <int LP>
-__device__ __forceinline__ float4 row_sum(const SpmmGroupK& g, int r, int k0, int k1, int d,
-                                          int wpart = 0, int wcount = 1) {
+__device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, int beg, int end, int d,
+                                            int wpart = 0, int wcount = 1) {
     constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const int q = lane % LP;
     const bool qact = q * 4 < d;
     const float* __restrict__ xq = g.x + q * 4;
+    const int32_t* __restrict__ vcolp = g.vcol;
+    const float* __restrict__ valp = g.val;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int stride = wcount * 64;
+    int base = beg + wpart * 64;
+    int vc = 0;
+    float vv = 0.f;
+    if (base + lane < end) {
+        vc = vcolp[base + lane];
+        vv = valp[base + lane];
+    }
 #pragma unroll 1
-    for (int kb = k0; kb < k1; kb += 64) {
-        const int nk = min(64, k1 - kb);
-        int sbeg = 0, slen = 0, xoff = 0;
-        if (lane < nk) {
-            const int32_t* rp = g.rowptr + (int64_t)(kb + lane) * g.rowptr_rel_stride + r;
-            sbeg = rp[0];
-            slen = rp[1] - sbeg;
-            const int rel = g.rel_map ? g.rel_map[kb + lane] : kb + lane;
-            xoff = rel * g.x_rel_stride;
+    for (; base < end; base += stride) {
+        const int n = min(64, end - base);
+        const int eoff = vc * g.x_ld;
+        const float v = vv;
+        const int nb = base + stride;  // prefetch the next batch of this wave
+        vc = 0;
+        vv = 0.f;
+        if (nb + lane < end) {
+            vc = vcolp[nb + lane];
+            vv = valp[nb + lane];
         }
-        int cum = slen;  // inclusive scan over the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(cum, o);
-            if (lane >= o) cum += t;
-        }
-        const int total = __shfl(cum, 63);
-        const int excl = cum - slen;
 #pragma unroll 1
-        for (int base = wpart * 64; base < total; base += wcount * 64) {
-            const int f = base + lane;
-            int lo = 0, hi = 63;
+        for (int s0 = 0; s0 < n; s0 += kUnroll * G) {
+            int o[kUnroll];
+            float w[kUnroll];
 #pragma unroll
-            for (int it = 0; it < 6; ++it) {
-                const int mid = (lo + hi) >> 1;
-                if (__shfl(cum, mid) > f)
-                    hi = mid;
-                else
-                    lo = mid + 1;
+            for (int u = 0; u < kUnroll; ++u) {
+                const int src = (s0 + u * G + sub) & 63;
+                o[u] = __shfl(eoff, src);
+                w[u] = __shfl(v, src);
             }
-            const int p = __shfl(sbeg, lo) + (f - __shfl(excl, lo));
-            const int xo = __shfl(xoff, lo);
-            int eoff = 0;
-            float v = 0.f;
-            if (f < total) {
-                eoff = xo + g.col[p] * g.x_ld;
-                v = g.val[p];
+            float4 xv[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const bool ok = qact && (s0 + u * G + sub) < n;
+                xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (!ok) w[u] = 0.f;
             }
-            const int n = min(64, total - base);
-#pragma unroll 1
-            for (int s0 = 0; s0 < n; s0 += kUnroll * G) {
-                int o[kUnroll];
-                float w[kUnroll];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const int src = (s0 + u * G + sub) & 63;
-                    o[u] = __shfl(eoff, src);
-                    w[u] = __shfl(v, src);
-                }
-                float4 xv[kUnroll];
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const bool ok = qact && (s0 + u * G + sub) < n;
-                    xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (!ok) w[u] = 0.f;
-                }
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) dg::fma4(acc, w[u], xv[u]);
-            }
+            for (int u = 0; u < kUnroll; ++u) dg::fma4(acc, w[u], xv[u]);
         }
     }
 #pragma unroll
     for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
     return acc;
-}
-
-template <int LP>
-__device__ __forceinline__ const SpmmGroupK& find_group(const SpmmArgs& args, int b) {
-    int gi = 0;
-#pragma unroll 1
-    while (gi + 1 < args.n_groups && b >= args.g[gi + 1].block_begin) ++gi;
-    return args.g[gi];
 }
 
 // Partial mode: one wave per (chunk, row); writes out[c][r][:].
@@ -163,8 +129,12 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int b = blockIdx.x;
-    const SpmmGroupK& g = find_group<LP>(args, b);
-    // XCD-contiguous item map: local block lb runs on XCD label lb % 8.
+    int gi = 0;
+#pragma unroll 1
+    while (gi + 1 < args.n_groups && b >= args.g[gi + 1].block_begin) ++gi;
+    const SpmmGroupK& g = args.g[gi];
+    // XCD-contiguous item map: local block lb runs on XCD label lb % 8, and each XCD takes a
+    // contiguous, chunk-major run of items, so one chunk's dense rows stay in one L2.
     const int lb = b - g.block_begin;
     const int per = g.n_blocks >> 3;
     const int item = (lb & 7) * per + (lb >> 3);
@@ -173,10 +143,9 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
     const int r = (item - c * g.row_blocks) * kRowsPerBlock + wave;
     if (r >= g.n_rows) return;  // wave-uniform; no barriers in this kernel
     const int d = args.d;
-    const int k0 = c * g.chunk;
-    const float4 acc = row_sum<LP>(g, r, k0, min(k0 + g.chunk, g.n_rels), d);
-    if (lane < LP && lane * 4 < d)
-        *reinterpret_cast<float4*>(g.out + ((int64_t)c * g.n_rows + r) * d + lane * 4) = acc;
+    const int64_t slot = (int64_t)c * g.n_rows + r;
+    const float4 acc = range_sum<LP>(g, g.rowptr[slot], g.rowptr[slot + 1], d);
+    if (lane < LP && lane * 4 < d) *reinterpret_cast<float4*>(g.out + slot * d + lane * 4) = acc;
 }
 
 // Fused mode (every group of a node type in one chunk): one workgroup per output row r of
@@ -238,7 +207,7 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
     const int q = lane % LP;
     if (gl < t.g_count) {
         const SpmmGroupK& g = a.g[t.g_begin + gl];
-        const float4 s = row_sum<LP>(g, r, 0, g.n_rels, d, part, W);
+        const float4 s = range_sum<LP>(g, g.rowptr[r], g.rowptr[r + 1], d, part, W);
         if (lane < LP) pbuf[wave][lane] = s;
     }
     __syncthreads();
@@ -281,7 +250,7 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
             float acc = 0.f;
 #pragma unroll 8
             for (int k = 0; k < d; ++k) acc = fmaf(hrow[k], wcol[(int64_t)k * dout], acc);
-            pj.out[((int64_t)kk * t.n_rows + r) * dout + c] = acc;
+            pj.out[((int64_t)rel * t.n_rows + r) * dout + c] = acc;
         }
     }
 }
@@ -357,35 +326,26 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 6; }
+extern "C" int32_t dg_abi_version(void) { return 7; }
 
 namespace {
 
 // Validate one descriptor and copy it into the kernel form.  Returns DG_OK or an error.
-int convert_group(const dg_rel_group& s, int d, SpmmGroupK& k) {
-    if (s.n_rows < 0 || s.n_rels < 0 || s.chunk < 1 || s.rowptr_rel_stride < 0 || s.n_cols < 0)
-        return DG_EINVAL;
-    // col/val may be NULL for a group without nonzeros (rowptr all zero: never read)
-    if (!s.rowptr || !s.x || !s.out) return DG_EINVAL;
-    if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || (s.x_ld & 3) || (s.x_rel_stride & 3))
-        return DG_EALIGN;
-    if (s.x_ld < d || s.x_rel_stride < 0) return DG_EINVAL;
-    const int64_t x_rels = s.x_rels > 0 ? s.x_rels : s.n_rels;
-    const int64_t span = (x_rels - 1) * s.x_rel_stride + (int64_t)(s.n_cols > 0 ? s.n_cols - 1 : 0) * s.x_ld + d;
-    if (span > 0x7fffffffLL) return DG_EINVAL;  // gathers use 32-bit element offsets
+int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k) {
+    if (s.n_rows < 0 || s.n_chunks < 1 || s.x_rows < 0) return DG_EINVAL;
+    // vcol/val may be NULL for a group without nonzeros (rowptr all zero: never read)
+    if (!s.rowptr || !s.x || (need_out && !s.out)) return DG_EINVAL;
+    if (!dg::aligned16(s.x) || (need_out && !dg::aligned16(s.out)) || (s.x_ld & 3)) return DG_EALIGN;
+    if (s.x_ld < d) return DG_EINVAL;
+    if ((int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;  // 32-bit gather offsets
     k.rowptr = s.rowptr;
-    k.col = s.col;
+    k.vcol = s.vcol;
     k.val = s.val;
     k.x = s.x;
     k.out = s.out;
-    k.rel_map = s.rel_map;
-    k.x_rel_stride = static_cast<int32_t>(s.x_rel_stride);
     k.x_ld = static_cast<int32_t>(s.x_ld);
-    k.rowptr_rel_stride = s.rowptr_rel_stride;
     k.n_rows = s.n_rows;
-    k.n_rels = s.n_rels;
-    k.chunk = s.chunk;
-    k.n_chunks = dg::ceil_div(s.n_rels, s.chunk);
+    k.n_chunks = s.n_chunks;
     k.row_blocks = dg::ceil_div(s.n_rows, kRowsPerBlock);
     return DG_OK;
 }
@@ -403,9 +363,9 @@ extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, 
     int ng = 0;
     for (int i = 0; i < n_groups; ++i) {
         const dg_rel_group& s = groups[i];
-        if (s.n_rows == 0 || s.n_rels == 0) continue;
+        if (s.n_rows == 0) continue;
         SpmmGroupK& k = args.g[ng];
-        const int rc = convert_group(s, d, k);
+        const int rc = convert_group(s, d, true, k);
         if (rc != DG_OK) return rc;
         ++ng;
         const int64_t items = (int64_t)k.n_chunks * k.row_blocks;
@@ -442,10 +402,8 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
     a.n_projs = n_projs;
     a.wpg = waves_per_group;
     for (int i = 0; i < n_groups; ++i) {
-        dg_rel_group s = groups[i];
-        s.chunk = s.n_rels > 0 ? s.n_rels : 1;
-        if (!s.out) s.out = targets[0].out;  // unused in fused mode
-        const int rc = convert_group(s, d, a.g[i]);
+        if (groups[i].n_chunks != 1) return DG_EINVAL;  // fused mode: the whole group is one chunk
+        const int rc = convert_group(groups[i], d, false, a.g[i]);
         if (rc != DG_OK) return rc;
     }
     int64_t blocks = 0;
@@ -491,17 +449,14 @@ extern "C" int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const 
     if (ldy != d) return DG_EINVAL;
     dg_rel_group g{};
     g.rowptr = rowptr;
-    g.col = col;
+    g.vcol = col;
     g.val = val;
     g.x = x;
     g.out = y;
-    g.x_rel_stride = 0;
     g.x_ld = ldx;
-    g.rowptr_rel_stride = 0;
     g.n_rows = n_rows;
-    g.n_rels = 1;
-    g.chunk = 1;
-    g.n_cols = n_cols;
+    g.n_chunks = 1;
+    g.x_rows = n_cols;
     return dg_spmm_groups_f32(&g, 1, d, stream);
 }
 

@@ -41,87 +41,58 @@ def _dev(t: torch.Tensor, dtype: torch.dtype, what: str) -> torch.Tensor:
 # --------------------------------------------------------------------------------------
 # SpMM over relation groups
 # --------------------------------------------------------------------------------------
-def need_x_span(s, d: int) -> int:
-    x_rels = s.n_rels if s.x_rels is None else s.x_rels
-    return (x_rels - 1) * s.x_rel_stride + max(s.n_cols - 1, 0) * s.x_ld + d
-
-
 @dataclass
 class RelGroupSpec:
-    """One (i,j) group (or any set of relations sharing n_rows) for dg_spmm_groups_f32."""
+    """One relation group in the chunk-merged layout of dg_rel_group (decagon_hip.h)."""
 
-    rowptr: torch.Tensor          # int32
-    col: torch.Tensor             # int32
-    val: torch.Tensor             # float32
-    x: torch.Tensor               # float32, dense operand storage
-    out: Optional[torch.Tensor]   # float32, [n_chunks, n_rows, d] (None in fused mode)
+    rowptr: torch.Tensor          # int32 [n_chunks*n_rows + 1]
+    vcol: torch.Tensor            # int32 [nnz] virtual columns (rows of x)
+    val: torch.Tensor             # float32 [nnz]
+    x: torch.Tensor               # float32, relation-stacked dense operand, row v at v*x_ld
+    out: Optional[torch.Tensor]   # float32 [n_chunks, n_rows, d] (None in fused mode)
     n_rows: int
-    n_cols: int
-    n_rels: int
-    chunk: int
-    x_rel_stride: int
+    n_chunks: int
     x_ld: int
-    rowptr_rel_stride: int
-    x_offset: int = 0             # element offset of X_0 inside x
-    rel_map: Optional[torch.Tensor] = None   # int32 [n_rels]: X_k = X_{rel_map[k]}
-    x_rels: Optional[int] = None  # relation slabs addressable in x (default n_rels)
-    rel_map_max: Optional[int] = None  # host-known max(rel_map), checked against x_rels
-
-    @property
-    def n_chunks(self) -> int:
-        return -(-self.n_rels // self.chunk)
+    x_rows: int                   # rows of x the kernel may address
+    vcol_max: int = -1            # host-known max(vcol) (-1: no nonzeros)
 
     def validate(self, d: int, need_out: bool = True) -> None:
         _dev(self.rowptr, torch.int32, "rowptr")
-        _dev(self.col, torch.int32, "col")
+        _dev(self.vcol, torch.int32, "vcol")
         _dev(self.val, torch.float32, "val")
         _dev(self.x, torch.float32, "x")
         if need_out or self.out is not None:
             _dev(self.out, torch.float32, "out")
-        if self.n_rows == 0 or self.n_rels == 0:
+        if self.n_rows == 0:
             return
-        if self.chunk < 1:
-            raise ValueError("chunk must be >= 1")
-        need_rp = (self.n_rels - 1) * self.rowptr_rel_stride + self.n_rows + 1
-        if self.rowptr.numel() < need_rp:
-            raise ValueError(f"rowptr has {self.rowptr.numel()} entries, kernel reads {need_rp}")
-        if self.col.numel() != self.val.numel():
-            raise ValueError("col/val length mismatch")
-        x_rels = self.n_rels if self.x_rels is None else self.x_rels
-        if self.rel_map is not None:
-            _dev(self.rel_map, torch.int32, "rel_map")
-            if self.rel_map.numel() < self.n_rels:
-                raise ValueError("rel_map shorter than n_rels")
-            if self.rel_map_max is None or not (0 <= self.rel_map_max < x_rels):
-                raise ValueError("rel_map_max must be given and index inside x")
-        elif x_rels < self.n_rels:
-            raise ValueError("x holds fewer relation slabs than n_rels")
-        need_x = self.x_offset + (x_rels - 1) * self.x_rel_stride + (self.n_cols - 1) * self.x_ld + d
-        if self.n_cols > 0 and self.x.numel() < need_x:
-            raise ValueError(f"x has {self.x.numel()} elements, kernel may read {need_x}")
-        if self.x_ld < d:
-            raise ValueError("x_ld < d")
+        if self.n_chunks < 1:
+            raise ValueError("n_chunks must be >= 1")
+        if self.rowptr.numel() < self.n_chunks * self.n_rows + 1:
+            raise ValueError(f"rowptr has {self.rowptr.numel()} entries, kernel reads {self.n_chunks * self.n_rows + 1}")
+        if self.vcol.numel() != self.val.numel():
+            raise ValueError("vcol/val length mismatch")
+        if self.x_ld < d or self.x_ld % 4:
+            raise ValueError("x_ld must be >= d and a multiple of 4")
+        if self.vcol_max >= self.x_rows:
+            raise ValueError(f"vcol reaches row {self.vcol_max} of a {self.x_rows}-row operand")
+        if self.x_rows > 0 and self.x.numel() < (self.x_rows - 1) * self.x_ld + d:
+            raise ValueError(f"x has {self.x.numel()} elements, kernel may read {(self.x_rows - 1) * self.x_ld + d}")
+        if self.x_rows * self.x_ld >= 2**31:
+            raise ValueError("dense operand too large for 32-bit gather offsets")
         if need_out and self.out.numel() < self.n_chunks * self.n_rows * d:
             raise ValueError("out too small for [n_chunks, n_rows, d]")
-        if need_x_span(self, d) >= 2**31:
-            raise ValueError("dense operand too large for 32-bit gather offsets")
 
 
-def _fill_group(g, s: "RelGroupSpec") -> None:
+def _fill_group(g, s: RelGroupSpec) -> None:
     g.rowptr = s.rowptr.data_ptr()
-    g.col = s.col.data_ptr()
-    g.val = s.val.data_ptr()
-    g.x = s.x.data_ptr() + 4 * s.x_offset
+    g.vcol = s.vcol.data_ptr() if s.vcol.numel() else None
+    g.val = s.val.data_ptr() if s.val.numel() else None
+    g.x = s.x.data_ptr()
     g.out = s.out.data_ptr() if s.out is not None else None
-    g.rel_map = s.rel_map.data_ptr() if s.rel_map is not None else None
-    g.x_rel_stride = s.x_rel_stride
     g.x_ld = s.x_ld
-    g.rowptr_rel_stride = s.rowptr_rel_stride
     g.n_rows = s.n_rows
-    g.n_rels = s.n_rels
-    g.chunk = s.chunk
-    g.n_cols = s.n_cols
-    g.x_rels = s.n_rels if s.x_rels is None else s.x_rels
+    g.n_chunks = s.n_chunks
+    g.x_rows = s.x_rows
 
 
 class PreparedSpmm:
@@ -227,13 +198,16 @@ def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:
 
 def spmm_csr(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x: torch.Tensor,
              n_rows: int, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-    """Y = A·X for one CSR relation (tf.sparse_tensor_dense_matmul, layers.py:90)."""
+    """Y = A·X for one CSR relation (tf.sparse_tensor_dense_matmul, layers.py:90): a plain
+    CSR is the merged layout with one chunk and vcol = col."""
     if x.dim() != 2:
         raise ValueError("x must be 2-D")
+    x = x.contiguous()
     n_cols, d = x.shape
     if out is None:
         out = torch.empty((n_rows, d), device=x.device, dtype=torch.float32)
-    spec = RelGroupSpec(rowptr, col, val, x.contiguous(), out, n_rows, n_cols, 1, 1, 0, d, 0)
+    vmax = int(col.max()) if col.numel() else -1
+    spec = RelGroupSpec(rowptr, col, val, x, out, n_rows, 1, d, n_cols, vcol_max=vmax)
     PreparedSpmm([spec], d)(stream)
     return out
 

@@ -118,10 +118,11 @@ class _GraphConvBase(MultiLayer):
         for k in range(self.num_types):
             self.vars["weights_%d" % k] = Variable(self.weights_stack[k], f"{scope}/weights_{k}:0")
 
-    def _adj_group(self, ctx):
-        """Upload (cached) this layer's adjacency feeds as one device group."""
+    def _adj_group(self, ctx, per_rel: bool):
+        """Upload (cached) this layer's adjacency feeds as one device group: one chunk for
+        the whole group, or one per relation when the activation precedes add_n."""
         nodes = self.adj_mats[self.edge_type]
-        return runtime.device_group(ctx, nodes)
+        return runtime.device_group(ctx, nodes, chunk=1 if per_rel else len(nodes))
 
 
 class GraphConvolutionSparseMulti(_GraphConvBase):
@@ -146,7 +147,7 @@ class GraphConvolutionSparseMulti(_GraphConvBase):
 
         def fn(ctx):
             _check_dropout(ctx, self.dropout)
-            grp = self._adj_group(ctx)
+            grp = self._adj_group(ctx, kind == "relu")
             feat = runtime.feature_csr(ctx, inputs)
             return runtime.gcn_layer(grp, self.weights_stack, feat, self.output_dim, kind == "relu")
 
@@ -173,7 +174,7 @@ class GraphConvolutionMulti(_GraphConvBase):
 
         def fn(ctx):
             _check_dropout(ctx, self.dropout)
-            grp = self._adj_group(ctx)
+            grp = self._adj_group(ctx, kind == "relu")
             h = ctx.value(inputs)
             h = runtime.as_device_f32(h)
             return runtime.gcn_layer_dense(grp, self.weights_stack, h, self.output_dim, kind == "relu")

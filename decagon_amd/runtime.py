@@ -86,21 +86,21 @@ def feature_csr(ctx: RunContext, node: Node):
 
 def device_graph(ctx: RunContext, edge_types: Dict[Tuple[int, int], int],
                  adj_nodes: Dict[Tuple[int, int], Sequence[Node]],
-                 local: Optional[Dict] = None) -> DeviceGraph:
+                 local: Optional[Dict] = None, chunk=None) -> DeviceGraph:
     csrs = {et: [host_csr(ctx, n) for n in adj_nodes[et]] for et in edge_types}
     key = ("dgraph", tuple((et, tuple(id(c) for c in csrs[et])) for et in edge_types),
-           None if local is None else tuple((et, tuple(v)) for et, v in local.items()))
+           None if local is None else tuple((et, tuple(v)) for et, v in local.items()), chunk)
     cache = ctx.session.caches.setdefault("dgraph", {})
     hit = cache.get(key)
     if hit is None:
-        hit = (csrs, DeviceGraph(edge_types, csrs, ctx.session.device, local))
+        hit = (csrs, DeviceGraph(edge_types, csrs, ctx.session.device, local, chunk=chunk))
         cache[key] = hit
     return hit[1]
 
 
-def device_group(ctx: RunContext, nodes: Sequence[Node]) -> DeviceGroup:
+def device_group(ctx: RunContext, nodes: Sequence[Node], chunk: Optional[int] = None) -> DeviceGroup:
     et = (0, 1)  # label only
-    g = device_graph(ctx, {et: len(nodes)}, {et: list(nodes)})
+    g = device_graph(ctx, {et: len(nodes)}, {et: list(nodes)}, chunk=chunk)
     return g.groups[et]
 
 
@@ -109,40 +109,40 @@ def invalidate(session) -> None:
 
 
 # ---------------------------------------------------------------- standalone layer forward
-def _feature_product(grp: DeviceGroup, W: torch.Tensor, feat: Optional[HostCSR], d_out: int):
-    """X_j·W_k for all k: returns (x tensor, rel stride, ld)."""
-    K, F, _ = W.shape
-    if feat is None:
-        if F != grp.n_cols:
-            raise ValueError("identity features need one weight row per node")
-        return W, F * d_out, d_out
-    dev = W.device
-    rp, cl, vl = (torch.from_numpy(a).to(dev) for a in (feat.rowptr, feat.col, feat.val))
-    xw = torch.empty((K, feat.shape[0], d_out), device=dev, dtype=torch.float32)
-    kernels.spmm_groups([kernels.RelGroupSpec(rp, cl, vl, W, xw, feat.shape[0], F, K, 1, F * d_out,
-                                              d_out, 0)], d_out)
-    return xw, feat.shape[0] * d_out, d_out
-
-
-def _conv(grp: DeviceGroup, x, xs, xld, d_out, per_rel_relu: bool) -> torch.Tensor:
+def _conv(grp: DeviceGroup, x: torch.Tensor, d_out: int, per_rel_relu: bool) -> torch.Tensor:
+    """l2norm(Σ_k act(Â_k·X_k)) for one group; per-relation relu needs one chunk per
+    relation (the epilogue applies it to each chunk partial before the sum)."""
     dev = x.device
-    K = grp.n_rels
-    chunk = 1 if per_rel_relu else K
-    nch = -(-K // chunk)
-    part = torch.empty((nch, grp.n_rows, d_out), device=dev, dtype=torch.float32)
-    kernels.spmm_groups([kernels.RelGroupSpec(grp.rowptr, grp.col, grp.val, x, part, grp.n_rows,
-                                              grp.n_cols, K, chunk, xs, xld, grp.n_rows)], d_out)
+    if per_rel_relu and grp.n_chunks != grp.n_rels:
+        raise ValueError("per-relation activation needs a one-relation-per-chunk layout")
+    part = torch.empty((grp.n_chunks, grp.n_rows, d_out), device=dev, dtype=torch.float32)
+    kernels.spmm_groups([kernels.RelGroupSpec(grp.rowptr, grp.vcol, grp.val, x, part, grp.n_rows, grp.n_chunks,
+                                              d_out, grp.K * grp.n_cols, vcol_max=grp.vcol_max)], d_out)
     out = torch.empty((grp.n_rows, d_out), device=dev, dtype=torch.float32)
     flags = DG_EPI_L2NORM | (DG_EPI_CHUNK_RELU if per_rel_relu else 0)
-    kernels.gcn_epilogue([(part, nch)], out, grp.n_rows, d_out, flags)
+    kernels.gcn_epilogue([(part, grp.n_chunks)], out, grp.n_rows, d_out, flags)
     return out
 
 
 def gcn_layer(grp: DeviceGroup, W: torch.Tensor, feat: Optional[HostCSR], d_out: int,
               per_rel_relu: bool) -> torch.Tensor:
     """GraphConvolutionSparseMulti._call (layers.py:85-94) for one edge type."""
-    x, xs, xld = _feature_product(grp, W, feat, d_out)
-    return _conv(grp, x, xs, xld, d_out, per_rel_relu)
+    K, F, _ = W.shape
+    if feat is None:
+        if F != grp.n_cols:
+            raise ValueError("identity features need one weight row per node")
+        x = W
+    else:
+        from .sparse import merge_chunks
+
+        fm = merge_chunks([feat] * K, np.arange(K), 1, K)
+        dev = W.device
+        x = torch.empty((K, feat.shape[0], d_out), device=dev, dtype=torch.float32)
+        kernels.spmm_groups([kernels.RelGroupSpec(
+            torch.from_numpy(fm.rowptr).to(dev), torch.from_numpy(fm.vcol).to(dev),
+            torch.from_numpy(fm.val).to(dev), W, x, feat.shape[0], K, d_out, K * F,
+            vcol_max=int(fm.vcol.max()) if fm.nnz else -1)], d_out)
+    return _conv(grp, x, d_out, per_rel_relu)
 
 
 def gcn_layer_dense(grp: DeviceGroup, W: torch.Tensor, h: torch.Tensor, d_out: int,
@@ -154,7 +154,7 @@ def gcn_layer_dense(grp: DeviceGroup, W: torch.Tensor, h: torch.Tensor, d_out: i
     P = torch.empty((K, grp.n_cols, d_out), device=h.device, dtype=torch.float32)
     kernels.PreparedGemm(h, (0, d_in, 1), W, (d_in * d_out, d_out, 1), P, (grp.n_cols * d_out, d_out, 1),
                          grp.n_cols, d_out, d_in, K)()
-    return _conv(grp, P, grp.n_cols * d_out, d_out, d_out, per_rel_relu)
+    return _conv(grp, P, d_out, per_rel_relu)
 
 
 # ---------------------------------------------------------------- decoders

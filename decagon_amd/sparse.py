@@ -165,3 +165,64 @@ def stack_relations(csrs: Sequence[HostCSR]) -> StackedCSR:
     val = np.concatenate([c.val for c in csrs]) if total else np.zeros(0, np.float32)
     return StackedCSR(rowptr.astype(np.int32), col.astype(np.int32), val.astype(np.float32),
                       n_r, n_c, len(csrs), np.asarray(nnz, np.int64))
+
+
+@dataclass
+class MergedCSR:
+    """A group's relations in the chunk-merged layout of dg_rel_group (decagon_hip.h):
+    for chunk c and row r the nonzeros of every relation of the chunk, contiguous, at
+    [rowptr[c*n_rows + r], rowptr[c*n_rows + r + 1]); vcol = k_x * n_cols + col where k_x is
+    the relation's slab in the relation-stacked dense operand."""
+
+    rowptr: np.ndarray
+    vcol: np.ndarray
+    val: np.ndarray
+    n_rows: int
+    n_cols: int
+    n_chunks: int
+    chunk: int
+    x_rows: int
+
+    @property
+    def nnz(self) -> int:
+        return int(self.vcol.shape[0])
+
+
+def merge_chunks(csrs: Sequence[HostCSR], slabs: Sequence[int], chunk: int, n_slabs: int) -> MergedCSR:
+    """Build the chunk-merged layout.  `csrs` are the (local) relations in order, `slabs[k]`
+    the slab of relation k in the stacked operand (its global relation index), `chunk`
+    relations per chunk, `n_slabs` slabs in the operand.  Inside a (chunk, row) range the
+    nonzeros run relation by relation, each relation's in-row (feed) order kept."""
+    if not csrs:
+        raise ValueError("empty relation group")
+    n_r, n_c = csrs[0].shape
+    K = len(csrs)
+    chunk = max(1, min(int(chunk), K))
+    n_chunks = -(-K // chunk)
+    counts = np.zeros(n_chunks * n_r, np.int64)
+    for k, c in enumerate(csrs):
+        if c.shape != (n_r, n_c):
+            raise ValueError("all relations of a group must share one shape")
+        counts[(k // chunk) * n_r:(k // chunk + 1) * n_r] += np.diff(c.rowptr.astype(np.int64))
+    total = int(counts.sum())
+    if total >= 2**31 or n_slabs * n_c >= 2**31:
+        raise ValueError("group exceeds int32 indexing")
+    rowptr = np.zeros(n_chunks * n_r + 1, np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    vcol = np.empty(total, np.int32)
+    val = np.empty(total, np.float32)
+    fill = rowptr[:-1].copy()  # next free position of each (chunk, row) range
+    for k, c in enumerate(csrs):
+        cb = (k // chunk) * n_r
+        lens = np.diff(c.rowptr.astype(np.int64))
+        if c.nnz == 0:
+            continue
+        starts = fill[cb:cb + n_r]
+        # destination of each nonzero: its row's next free slot + its rank within the row
+        rows = np.repeat(np.arange(n_r), lens)
+        rank = np.arange(c.nnz, dtype=np.int64) - np.repeat(c.rowptr[:-1].astype(np.int64), lens)
+        dst = starts[rows] + rank
+        vcol[dst] = int(slabs[k]) * n_c + c.col
+        val[dst] = c.val
+        fill[cb:cb + n_r] += lens
+    return MergedCSR(rowptr.astype(np.int32), vcol, val, n_r, n_c, n_chunks, chunk, n_slabs * n_c)

@@ -34,51 +34,46 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (6); bumped whenever a struct layout or a signature changes. */
+/* ABI version (7); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
- * Relation group SpMM (T3 + T4 of SURVEY §2.2):  for every group g and chunk c,
+ * Relation-group SpMM (T3 + T4 of SURVEY §2.2) over a chunk-merged CSR.
  *
- *     out_g[c][r][:] = sum_{k in chunk c} sum_{p in row r of A_g,k} val[p] * X_g,k[col[p]][:]
+ * A group's relations A_k (k < K, all n_rows x n_cols) are split into chunks of consecutive
+ * relations; for chunk c and row r the nonzeros of every relation in the chunk are stored
+ * contiguously, [rowptr[c*n_rows + r], rowptr[c*n_rows + r + 1]), each with a virtual
+ * column vcol = k*n_cols + col — the row of the relation-stacked dense operand
+ * X = [X_0; X_1; ...] (row v at x + v*x_ld) that it multiplies.  Then
  *
- * A_g,k is relation k of the group, stored as stacked CSR: relation k's row pointer for row
- * r is rowptr[k*rowptr_rel_stride + r] (rowptr_rel_stride = n_rows for K stacked CSRs whose
- * offsets are global into col/val, or 0 when all K relations share one CSR, the T2 case
- * X_j * W_k of layers.py:89).  X_g,k = x + k*x_rel_stride, row stride x_ld (elements).
- * If rel_map is non-NULL, X_g,k = x + rel_map[k]*x_rel_stride instead (a rank's shard of
- * the relations, picked out of the full weight stack without a copy).
- * Chunks hold `chunk` consecutive relations; n_chunks = ceil(n_rels/chunk).  out_g is dense
- * [n_chunks][n_rows][d].  With chunk == n_rels the output is the add_n of layers.py:92/116.
+ *     out[c][r][:] = sum_{p in range(c, r)} val[p] * X[vcol[p]][:]
+ *                  = sum_{k in chunk c} (A_k · X_k)[r][:]
  *
+ * With one chunk this is the add_n of layers.py:92/116.  The layout is built once at upload
+ * (decagon_amd/sparse.py: merge_chunks).
  * Replaces: tf.sparse_tensor_dense_matmul(adj_mats[edge_type][k], x)  layers.py:90, :114
  *           tf.sparse_tensor_dense_matmul(x, weights_k) (sparse features) layers.py:89
  *           tf.add_n(outputs)                                         layers.py:92, :116
- * Requirements: d % 4 == 0, 4 <= d <= 256, x and x_ld 16-byte aligned (x_ld % 4 == 0), and
- * (x_rels-1)*x_rel_stride + (n_cols-1)*x_ld + d < 2^31 (gathers use 32-bit offsets).
+ * Requirements: d % 4 == 0, 4 <= d <= 256, x and x_ld 16-byte aligned (x_ld % 4 == 0),
+ * x_rows * x_ld < 2^31 (gathers use 32-bit offsets), 0 <= vcol < x_rows.
  * -------------------------------------------------------------------------------------- */
 typedef struct dg_rel_group {
-    const int32_t* rowptr;      /* device */
-    const int32_t* col;         /* device, [nnz] column indices, 0 <= col < n_cols;    */
-    const float* val;           /* [nnz] values.  Both may be NULL when nnz == 0.      */
-    const float* x;             /* device, dense operand of relation 0                 */
-    float* out;                 /* device, [n_chunks][n_rows][d]                       */
-    const int32_t* rel_map;     /* device, [n_rels] or NULL (identity)                 */
-    int64_t x_rel_stride;       /* elements between X_k and X_{k+1}                    */
-    int64_t x_ld;               /* elements between consecutive rows of X_k            */
-    int32_t rowptr_rel_stride;  /* n_rows (stacked) or 0 (shared CSR)                  */
+    const int32_t* rowptr;      /* device, [n_chunks*n_rows + 1]                          */
+    const int32_t* vcol;        /* device, [nnz] virtual columns (rows of X)              */
+    const float* val;           /* device, [nnz].  vcol/val may be NULL when nnz == 0.    */
+    const float* x;             /* device, relation-stacked dense operand                 */
+    float* out;                 /* device, [n_chunks][n_rows][d] (unused in fused mode)   */
+    int64_t x_ld;               /* elements between consecutive rows of X                 */
     int32_t n_rows;
-    int32_t n_rels;
-    int32_t chunk;              /* relations per output chunk, >= 1                    */
-    int32_t n_cols;             /* columns of A (rows of each X_k)                     */
-    int32_t x_rels;             /* relation slabs addressable in x (0 = n_rels)        */
-    int32_t reserved[2];        /* zero                                                */
+    int32_t n_chunks;
+    int32_t x_rows;             /* rows of X addressable (bound on vcol)                  */
+    int32_t reserved[3];        /* zero                                                   */
 } dg_rel_group;
 
 int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
                        int32_t d, void* stream);
 
-/* Single relation, no chunking: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
+/* Single relation, plain CSR: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
  * Replaces one tf.sparse_tensor_dense_matmul (layers.py:90).  ldy must equal d. */
 int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                     int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx, float* y,
@@ -90,12 +85,12 @@ int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
  *
  *     out_t[r] = act( sum_{g in [g_begin, g_begin+g_count)} l2norm( sum_k A_g,k[r]·X_g,k ) )
  *
- * act = relu if flags & DG_EPI_RELU.  The groups' `chunk` and `out` fields are ignored.
+ * act = relu if flags & DG_EPI_RELU.  Every group must have n_chunks == 1; `out` is ignored.
  * One workgroup per output row, `waves_per_group` waves per group sharing the row's nonzeros
  * (g_count * waves_per_group <= 16).
  * Projection epilogue: for each dg_proj p with p.target == t,
- *     p.out[kk][r][c] = sum_k out_t[r][k] * p.w[rel(kk)][k][c]     kk < p.n_rels, c < d_out
- * (rel(kk) = p.rel_map[kk] or kk; p.w is a [K][d][d_out] stack; p.out is [n_rels][n_rows][d_out])
+ *     p.out[rel(kk)][r][c] = sum_k out_t[r][k] * p.w[rel(kk)][k][c]   kk < p.n_rels, c < d_out
+ * (rel(kk) = p.rel_map[kk] or kk; p.w is a [K][d][d_out] stack, p.out [K][n_rows][d_out])
  * — the next layer's H_j·W_k (layers.py:113) for the rows just produced.
  * Replaces the per-relation SpMM + add_n + l2_normalize of layers.py:85-94 / 109-118 and the
  * sum over edge types (+ relu) of model.py:74-75 / 85-88.
@@ -111,7 +106,7 @@ typedef struct dg_fused_target {
 typedef struct dg_proj {
     const float* w;             /* device, [K][d][d_out] weight stack        */
     const int32_t* rel_map;     /* device, [n_rels] or NULL                  */
-    float* out;                 /* device, [n_rels][n_rows of target][d_out] */
+    float* out;                 /* device, [K][n_rows of target][d_out]      */
     int32_t n_rels;
     int32_t target;             /* index into the targets array              */
     int32_t d_out;
@@ -157,8 +152,9 @@ int dg_gcn_epilogue_f32(const dg_epi_group* groups /* HOST array */, int32_t n_g
  *   C_b[m][n] = sc[n] * sum_k (sa[k] * A_b[m][k]) * B_b[k][n]        b < batch
  *
  * Element (m,k) of A_b is A[b*a_bs + m*a_sm + k*a_sk]; likewise B (k,n) and C (m,n).
- * sa / sc are optional (NULL = ones).  If b_map is non-NULL, B_b starts at
- * b + b_map[b]*b_bs (relation shard of a weight stack).  No alignment requirement.
+ * sa / sc are optional (NULL = ones).  If b_map is non-NULL, batch b reads B at
+ * b + b_map[b]*b_bs and writes C at c + b_map[b]*c_bs (a rank's relation shard of a
+ * relation-indexed stack).  No alignment requirement.
  * Replaces: tf.matmul(x, weights_k)                          layers.py:113 (batched over k)
  *           tf.matmul chain row·L·G·L·colᵀ (predict)         optimizer.py:87-106
  * -------------------------------------------------------------------------------------- */

@@ -77,7 +77,7 @@ def test_abi_rejects_bad_arguments_without_a_device():
     g = (_lib.DgRelGroup * 1)()
     assert lib.dg_spmm_groups_f32(g, 1, 6, None) == _lib.DG_EINVAL  # d % 4 != 0
     assert lib.dg_spmm_groups_f32(g, 9, 64, None) == _lib.DG_ETOOMANY
-    g[0].n_rows, g[0].n_rels, g[0].chunk = 10, 1, 1
+    g[0].n_rows, g[0].n_chunks, g[0].x_rows = 10, 1, 10
     g[0].rowptr, g[0].x, g[0].out = 16, 17, 32  # misaligned x
     g[0].x_ld = 64
     assert lib.dg_spmm_groups_f32(g, 1, 64, None) == _lib.DG_EALIGN
@@ -87,6 +87,23 @@ def test_abi_rejects_bad_arguments_without_a_device():
     e = (_lib.DgEpiGroup * 1)()
     assert lib.dg_gcn_epilogue_f32(e, 1, None, 10, 64, 128, None) == _lib.DG_EINVAL  # bad flags
     assert lib.dg_unigram_sample(None, 0, 5, 0, 0, None, None) == _lib.DG_EINVAL
+
+
+def test_merge_chunks_layout():
+    from decagon_amd.sparse import coo_to_csr, merge_chunks, sparse_to_tuple
+
+    rng = np.random.default_rng(2)
+    mats = [sp.random(8, 6, density=0.4, random_state=rng, format="csr") for _ in range(5)]
+    slabs = [3, 0, 1, 6, 2]
+    m = merge_chunks([coo_to_csr(*sparse_to_tuple(x)) for x in mats], slabs, 2, 7)
+    assert m.n_chunks == 3 and m.rowptr.shape == (3 * 8 + 1,) and m.x_rows == 42
+    X = rng.standard_normal((42, 4))
+    for c in range(3):
+        for r in range(8):
+            a, b = m.rowptr[c * 8 + r], m.rowptr[c * 8 + r + 1]
+            got = (m.val[a:b, None] * X[m.vcol[a:b]]).sum(0)
+            want = sum((mats[k] @ X[slabs[k] * 6:(slabs[k] + 1) * 6])[r] for k in range(2 * c, min(5, 2 * c + 2)))
+            assert np.allclose(got, want)
 
 
 def test_choose_chunk_policy():

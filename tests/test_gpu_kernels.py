@@ -82,33 +82,68 @@ def test_spmm_empty_matrix(K):
 
 @pytest.mark.parametrize("chunk", [1, 2, 3, 7])
 @pytest.mark.parametrize("d", [32, 64])
-def test_spmm_groups_chunks_and_relmap(K, chunk, d):
-    """Stacked relations, chunked partial sums, a relation map into a bigger weight stack,
-    and two groups in one launch."""
-    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, stack_relations
+def test_spmm_groups_chunks_and_slabs(K, chunk, d):
+    """Chunk-merged relations, chunked partial sums, relations living in arbitrary slabs of
+    a bigger stacked operand (a rank's shard), and two groups in one launch."""
+    from decagon_amd.sparse import coo_to_csr, merge_chunks, sparse_to_tuple
 
     rng = np.random.default_rng(chunk * 100 + d)
-    groups, wants, specs = [], [], []
+    wants, specs = [], []
     for (n_r, n_c, nrel) in ((120, 90, 7), (90, 120, 3)):
         mats = [_rand_csr(rng, n_r, n_c, 0.04, empty_rows=0.1) for _ in range(nrel)]
-        st = stack_relations([coo_to_csr(*sparse_to_tuple(m)) for m in mats])
         total = nrel + 4
+        slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
+        m = merge_chunks([coo_to_csr(*sparse_to_tuple(x)) for x in mats], slabs, chunk, total)
         X = rng.standard_normal((total, n_c, d)).astype(np.float32)
-        rel_ids = rng.choice(total, size=nrel, replace=False).astype(np.int32)
-        nch = -(-nrel // chunk)
+        nch = m.n_chunks
         out = torch.zeros((nch, n_r, d), device="cuda")
-        spec = K.RelGroupSpec(torch.from_numpy(st.rowptr).cuda(), torch.from_numpy(st.col).cuda(),
-                              torch.from_numpy(st.val).cuda(), torch.from_numpy(X).cuda(), out, n_r, n_c,
-                              nrel, chunk, n_c * d, d, n_r, rel_map=torch.from_numpy(rel_ids).cuda(),
-                              x_rels=total, rel_map_max=int(rel_ids.max()))
+        spec = K.RelGroupSpec(torch.from_numpy(m.rowptr).cuda(), torch.from_numpy(m.vcol).cuda(),
+                              torch.from_numpy(m.val).cuda(), torch.from_numpy(X).cuda(), out, n_r, nch, d,
+                              total * n_c, vcol_max=int(m.vcol.max()))
         specs.append(spec)
         want = np.zeros((nch, n_r, d))
-        for k, m in enumerate(mats):
-            want[k // chunk] += m @ X[rel_ids[k]].astype(np.float64)
+        for k, x in enumerate(mats):
+            want[k // m.chunk] += x @ X[slabs[k]].astype(np.float64)
         wants.append(want)
     K.spmm_groups(specs, d)
     for s, w in zip(specs, wants):
         assert rel_err(s.out.cpu().numpy(), w) <= 1e-5
+
+
+def test_fused_kernel_matches_oracle(K):
+    """dg_gcn_fused_f32 with two targets, several groups each, waves_per_group 1..3 and a
+    projection epilogue against the float64 restatement."""
+    from decagon_amd.sparse import coo_to_csr, merge_chunks, sparse_to_tuple
+
+    rng = np.random.default_rng(42)
+    n = {0: 150, 1: 90}
+    ets = {(0, 0): 2, (0, 1): 1, (1, 0): 1, (1, 1): 3}
+    mats, X, specs_by_t, want = {}, {}, {0: [], 1: []}, {}
+    for et, Kr in ets.items():
+        mats[et] = [_rand_csr(rng, n[et[0]], n[et[1]], 0.08, empty_rows=0.1) for _ in range(Kr)]
+        X[et] = rng.standard_normal((Kr, n[et[1]], 64)).astype(np.float32)
+        m = merge_chunks([coo_to_csr(*sparse_to_tuple(x)) for x in mats[et]], np.arange(Kr), Kr, Kr)
+        specs_by_t[et[0]].append(K.RelGroupSpec(
+            torch.from_numpy(m.rowptr).cuda(), torch.from_numpy(m.vcol).cuda(), torch.from_numpy(m.val).cuda(),
+            torch.from_numpy(X[et]).cuda(), None, n[et[0]], 1, 64, Kr * n[et[1]], vcol_max=int(m.vcol.max())))
+    for t in (0, 1):
+        tot = 0
+        for et in ets:
+            if et[0] == t:
+                s = sum(mats[et][k] @ X[et][k].astype(np.float64) for k in range(ets[et]))
+                tot = tot + orc.l2_normalize_rows(s)
+        want[t] = np.maximum(tot, 0)
+    W2 = rng.standard_normal((5, 64, 32)).astype(np.float32)
+    P = torch.zeros((5, n[1], 32), device="cuda")
+    rmap = torch.tensor([4, 0, 2], dtype=torch.int32, device="cuda")
+    for wpg in (1, 2, 3):
+        outs = {t: torch.empty((n[t], 64), device="cuda") for t in (0, 1)}
+        proj = K.ProjSpec(torch.from_numpy(W2).cuda(), P, 3, 1, rel_map=rmap, rel_map_max=4)
+        K.PreparedFused([(outs[t], n[t], specs_by_t[t], True) for t in (0, 1)], 64, [proj], wpg)()
+        for t in (0, 1):
+            assert rel_err(outs[t].cpu().numpy(), want[t]) <= 1e-5
+        for kk, rel in enumerate([4, 0, 2]):
+            assert rel_err(P[rel].cpu().numpy(), want[1] @ W2[rel].astype(np.float64)) <= 1e-5
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2, 3, 5])
@@ -228,7 +263,8 @@ def test_shape_checks_fail_before_launch(K):
     rp, cl, vl, _ = _dev_csr(m)
     x = torch.zeros((5, 32), device="cuda")  # fewer rows than n_cols
     with pytest.raises(ValueError):
-        K.RelGroupSpec(rp, cl, vl, x, torch.zeros((1, 10, 32), device="cuda"), 10, 10, 1, 1, 0, 32, 0).validate(32)
+        K.RelGroupSpec(rp, cl, vl, x, torch.zeros((1, 10, 32), device="cuda"), 10, 1, 32, 10,
+                       vcol_max=int(cl.max())).validate(32)
 
 
 @pytest.mark.parametrize("n", [512, 100, 1300])

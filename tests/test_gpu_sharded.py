@@ -25,7 +25,7 @@ def _plan(g, shard, device):
     csr = g.csr()
     dg = DeviceGraph(g.edge_types, csr, device, None if shard is None else shard.local)
     return ForwardPlan(dg, {0: None, 1: None}, w1, w2, 64, 32,
-                       allreduce=None if shard is None else shard.allreduce, chunk_override=None)
+                       allreduce=None if shard is None else shard.allreduce)
 
 
 def _worker(rank, world, port, q, chunk_small):
