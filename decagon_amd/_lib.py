@@ -19,7 +19,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -36,6 +36,24 @@ class DgRelGroup(ctypes.Structure):
         ("n_chunks", c_int32),
         ("x_rows", c_int32),
         ("reserved", c_int32 * 3),
+    ]
+
+
+class DgStagedGroup(ctypes.Structure):
+    _fields_ = [
+        ("rowptr", c_void_p),
+        ("vcol", c_void_p),
+        ("val", c_void_p),
+        ("slab", c_void_p),
+        ("x", c_void_p),
+        ("out", c_void_p),
+        ("x_ld", c_int64),
+        ("n_rows", c_int32),
+        ("n_cols", c_int32),
+        ("n_rels", c_int32),
+        ("out_chunk", c_int32),
+        ("x_rows", c_int32),
+        ("reserved", c_int32),
     ]
 
 
@@ -96,6 +114,7 @@ SIGNATURES = {
         [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     ),
     "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_int32, c_void_p]),
+    "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_int32, c_void_p]),
     "dg_decoder_hinge_f32": (
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,

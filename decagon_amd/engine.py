@@ -35,6 +35,35 @@ from .sparse import HostCSR, MergedCSR, merge_chunks
 EdgeType = Tuple[int, int]
 
 
+# LDS-staged groups: many relations over a column space narrow enough that one relation's
+# column slice (16 floats, rows padded to 20) fits LDS next to two more workgroups.
+STAGED_MIN_RELS = int(os.environ.get("DG_STAGED_MIN_RELS", "32"))
+STAGED_MAX_COLS = 2048
+STAGED_MAX_ROWS = 2048
+STAGED_BINS = 128
+
+
+def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
+    return (os.environ.get("DG_STAGED", "1") != "0" and n_rels >= STAGED_MIN_RELS
+            and n_cols <= STAGED_MAX_COLS and n_rows <= STAGED_MAX_ROWS)
+
+
+def snake_bins(costs: Sequence[float], bin_size: int) -> np.ndarray:
+    """An order of the items in which every run of `bin_size` consecutive items has about
+    the same total cost: sort by cost, deal in snake order to ceil(n/bin_size) bins."""
+    n = len(costs)
+    n_bins = max(1, -(-n // bin_size))
+    order = np.argsort(-np.asarray(costs, np.float64), kind="stable")
+    bins: List[List[int]] = [[] for _ in range(n_bins)]
+    for pos, item in enumerate(order):
+        rnd, k = divmod(pos, n_bins)
+        b = k if rnd % 2 == 0 else n_bins - 1 - k
+        if len(bins[b]) >= bin_size:  # last round is partial: fill the first free bin
+            b = next(i for i in range(n_bins) if len(bins[i]) < bin_size)
+        bins[b].append(int(item))
+    return np.asarray([i for b in bins for i in b], np.int64)
+
+
 def choose_chunk(n_rels: int, n_rows: int, nnz: int, d: int, target_waves: int = 32768) -> int:
     """Relations per chunk.  Partials cost 8·d bytes per (chunk, row) against ≈8 bytes per
     nonzero of CSR reads; keep them under a quarter of it, but keep at least `target_waves`
@@ -66,6 +95,8 @@ class DeviceGroup:
     nnz: int
     vcol_max: int
     rel_map: Optional[torch.Tensor] = None   # device rel_ids, when not 0..K-1
+    staged: bool = False           # runs through dg_spmm_staged_f32 (layout: chunk = 1)
+    out_chunk: int = 1             # staged: relations summed per output chunk
 
     @property
     def n_rels(self) -> int:
@@ -104,6 +135,16 @@ class DeviceGraph:
             loc = [rels[k] for k in ids]
             nnz = int(sum(c.nnz for c in loc))
             ch = chunk.get(et) if isinstance(chunk, dict) else chunk
+            staged = ch is None and stageable(len(loc), n_r, n_c)
+            out_chunk = 1
+            if staged:
+                # one chunk per relation; output chunks of out_chunk relations with balanced
+                # nonzero counts (relation sizes are Zipf-skewed)
+                out_chunk = max(1, -(-len(loc) // STAGED_BINS))
+                perm = snake_bins([c.nnz for c in loc], out_chunk)
+                ids = ids[perm]
+                loc = [loc[i] for i in perm]
+                ch = 1
             if ch is None:
                 ch = choose_chunk(len(loc), n_r, nnz, d_policy, target_waves)
             if loc:
@@ -118,6 +159,7 @@ class DeviceGraph:
                 int(m.vcol.max()) if m.nnz else -1)
             if ids.size and not np.array_equal(ids, np.arange(K)):
                 g.rel_map = torch.from_numpy(ids).to(device)
+            g.staged, g.out_chunk = staged, out_chunk
             self.groups[et] = g
 
     @property
@@ -236,7 +278,8 @@ class ForwardPlan:
         if self.allreduce is not None:
             return []
         return [i for i, ets in self.targets.items()
-                if all(self.g.groups[et].n_chunks == 1 and self.g.groups[et].n_rels > 0 for et in ets)]
+                if all(self.g.groups[et].n_chunks == 1 and self.g.groups[et].n_rels > 0
+                       and not self.g.groups[et].staged for et in ets)]
 
     def _spec(self, et, x: torch.Tensor, out, d) -> kernels.RelGroupSpec:
         grp = self.g.groups[et]
@@ -253,10 +296,12 @@ class ForwardPlan:
         launches: List[Callable[[], None]] = []
         fused_t = self.fused
         if fused_t:
-            # waves per group: the densest row group gets about one batch of 64 per wave
+            # waves per group: small launches (latency-bound) split the densest row group's
+            # batches of 64 over up to two waves; big launches have parallelism to spare
             avg = max(g.groups[et].nnz / max(1, g.groups[et].n_rows) for i in fused_t for et in self.targets[i])
             max_groups = max(len(self.targets[i]) for i in fused_t)
-            wpg = int(max(1, min(2, 16 // max_groups, math.ceil(avg / 64.0))))
+            rows = sum(n[i] for i in fused_t)
+            wpg = 1 if rows >= 4096 else int(max(1, min(2, 16 // max_groups, math.ceil(avg / 64.0))))
             if os.environ.get("DG_WPG"):  # tuning override
                 wpg = max(1, min(int(os.environ["DG_WPG"]), 16 // max_groups))
             pspecs = []
@@ -276,18 +321,28 @@ class ForwardPlan:
             for et, sz in zip(rest, sizes):
                 views[et] = flat[off:off + sz]
                 off += sz
-        partials, specs, reduces = {}, [], []
+        partials, specs, staged, reduces = {}, [], [], []
         for et in rest:
             grp = g.groups[et]
-            if flat is not None and grp.n_chunks == 1:
+            n_out = -(-grp.n_rels // grp.out_chunk) if grp.staged else grp.n_chunks
+            if flat is not None and n_out == 1:
                 part = views[et]  # single chunk: the SpMM writes the group sum in place
             else:
-                part = torch.zeros((grp.n_chunks, grp.n_rows, d), **f32)
+                part = torch.zeros((max(1, n_out), grp.n_rows, d), **f32)
                 if flat is not None and grp.n_rels:
-                    reduces.append(kernels.PreparedEpilogue([(part, grp.n_chunks)], views[et], grp.n_rows, d, 0))
-            partials[et] = (part, grp.n_chunks)
-            if grp.n_rels:
+                    reduces.append(kernels.PreparedEpilogue([(part, n_out)], views[et], grp.n_rows, d, 0))
+            partials[et] = (part, max(1, n_out))
+            if not grp.n_rels:
+                continue
+            if grp.staged:
+                staged.append(kernels.StagedSpec(
+                    grp.rowptr, grp.vcol, grp.val, grp.rel_map, xs[et], part, grp.n_rows, grp.n_cols,
+                    grp.n_rels, grp.out_chunk, d, grp.K * grp.n_cols, vcol_max=grp.vcol_max))
+            else:
                 specs.append(self._spec(et, xs[et], part, d))
+        slice_ = int(os.environ.get("DG_STAGED_SLICE", "16"))
+        launches += [kernels.PreparedStaged(staged[s:s + DG_MAX_GROUPS], d, slice_)
+                     for s in range(0, len(staged), DG_MAX_GROUPS)]
         launches += [kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d)
                      for s in range(0, len(specs), DG_MAX_GROUPS)]
         launches += reduces
@@ -317,7 +372,8 @@ class ForwardPlan:
     @property
     def spmm_launches(self):
         """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""
-        pick = lambda L: [l for l in L.launches if isinstance(l, (kernels.PreparedSpmm, kernels.PreparedFused))]
+        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged)
+        pick = lambda L: [l for l in L.launches if isinstance(l, kinds)]
         return pick(self._layer1), pick(self._layer2)
 
     # ---- accounting (bench / DESIGN.md roofline) ----
@@ -336,7 +392,8 @@ class ForwardPlan:
             tot += 4 * (grp.n_chunks * grp.n_rows + 1) + 8 * grp.nnz
             tot += 4 * d * grp.n_cols * grp.n_rels
             if et[0] not in L.fused_targets:
-                tot += 4 * d * grp.n_rows * grp.n_chunks
+                n_out = -(-grp.n_rels // grp.out_chunk) if grp.staged else grp.n_chunks
+                tot += 4 * d * grp.n_rows * n_out
         for i in L.fused_targets:
             tot += 4 * d * self.g.n_nodes[i]
         if layer == 1:

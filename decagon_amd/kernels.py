@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import DgEpiGroup, DgFusedTarget, DgGemmDesc, DgProj, DgRelGroup, check
+from ._lib import DgEpiGroup, DgFusedTarget, DgGemmDesc, DgProj, DgRelGroup, DgStagedGroup, check
 
 
 def _stream_ptr(stream: Optional[torch.cuda.Stream] = None) -> int:
@@ -192,6 +192,71 @@ class PreparedFused:
                        self.wpg, self.d, _stream_ptr(stream)), "dg_gcn_fused_f32")
 
 
+@dataclass
+class StagedSpec:
+    """One group for dg_spmm_staged_f32 (one chunk per relation in the merged layout)."""
+
+    rowptr: torch.Tensor          # int32 [n_rels*n_rows + 1]
+    vcol: torch.Tensor            # int32 [nnz]
+    val: torch.Tensor             # float32 [nnz]
+    slab: Optional[torch.Tensor]  # int32 [n_rels] or None
+    x: torch.Tensor
+    out: torch.Tensor             # float32 [ceil(n_rels/out_chunk), n_rows, d]
+    n_rows: int
+    n_cols: int
+    n_rels: int
+    out_chunk: int
+    x_ld: int
+    x_rows: int
+    vcol_max: int = -1
+
+    def validate(self, d: int) -> None:
+        for t, nm, dt in ((self.rowptr, "rowptr", torch.int32), (self.vcol, "vcol", torch.int32),
+                          (self.val, "val", torch.float32), (self.x, "x", torch.float32),
+                          (self.out, "out", torch.float32)):
+            _dev(t, dt, nm)
+        if self.slab is not None:
+            _dev(self.slab, torch.int32, "slab")
+            if self.slab.numel() < self.n_rels:
+                raise ValueError("slab shorter than n_rels")
+        if self.rowptr.numel() < self.n_rels * self.n_rows + 1:
+            raise ValueError("staged rowptr must hold one chunk per relation")
+        if self.vcol_max >= self.x_rows or self.x.numel() < (self.x_rows - 1) * self.x_ld + d:
+            raise ValueError("dense operand smaller than the indices address")
+        if self.x_rows * self.x_ld >= 2**31:
+            raise ValueError("dense operand too large for 32-bit gather offsets")
+        n_out = -(-self.n_rels // self.out_chunk)
+        if self.out.numel() < n_out * self.n_rows * d:
+            raise ValueError("staged out too small")
+
+
+class PreparedStaged:
+    """A fixed dg_spmm_staged_f32 launch."""
+
+    def __init__(self, specs: Sequence[StagedSpec], d: int, slice_: int = 16):
+        if not 1 <= len(specs) <= _lib.DG_MAX_GROUPS:
+            raise ValueError(f"1..{_lib.DG_MAX_GROUPS} groups per launch")
+        arr = (DgStagedGroup * len(specs))()
+        for i, s in enumerate(specs):
+            s.validate(d)
+            g = arr[i]
+            g.rowptr = s.rowptr.data_ptr()
+            g.vcol = s.vcol.data_ptr() if s.vcol.numel() else None
+            g.val = s.val.data_ptr() if s.val.numel() else None
+            g.slab = s.slab.data_ptr() if s.slab is not None else None
+            g.x = s.x.data_ptr()
+            g.out = s.out.data_ptr()
+            g.x_ld = s.x_ld
+            g.n_rows, g.n_cols, g.n_rels = s.n_rows, s.n_cols, s.n_rels
+            g.out_chunk, g.x_rows = s.out_chunk, s.x_rows
+        self._keep = list(specs)
+        self._arr, self._n, self.d, self.slice = arr, len(specs), d, slice_
+        self._fn = _lib.load().dg_spmm_staged_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(self._arr, self._n, self.d, self.slice, _stream_ptr(stream)), "dg_spmm_staged_f32")
+
+
 def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:
     PreparedSpmm(specs, d)(stream)
 
@@ -277,7 +342,7 @@ class PreparedGemm:
         if m and n and k and batch:
             if a.numel() < span(a_strides, m, k) or b.numel() < span(b_strides, k, n, nb_b):
                 raise ValueError("gemm operand too small for its strides")
-        if m and n and batch and c.numel() < span(c_strides, m, n):
+        if m and n and batch and c.numel() < span(c_strides, m, n, nb_b):
             raise ValueError("gemm output too small for its strides")
         if sa is not None and (sa.numel() < k or sa.dtype != torch.float32 or not sa.is_cuda):
             raise ValueError("sa must be a float32 device vector of length k")

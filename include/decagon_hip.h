@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (7); bumped whenever a struct layout or a signature changes. */
+/* ABI version (8); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -117,6 +117,39 @@ int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
                      const dg_fused_target* targets /* HOST */, int32_t n_targets,
                      const dg_proj* projs /* HOST, may be NULL */, int32_t n_projs,
                      int32_t waves_per_group, int32_t d, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * LDS-staged relation SpMM (T3 + T4) for groups with many relations over few columns
+ * (polypharmacy drug×drug: 1,928 relations of 645×645).  Layout: one chunk per relation
+ * (merge_chunks with chunk = 1, i.e. stacked CSR with rowptr [n_rels*n_rows + 1]) and
+ * vcol = slab(k)*n_cols + col.  For output chunk c (out_chunk consecutive relations):
+ *
+ *     out[c][r][:] = sum_{k in chunk c} sum_{p in row r of A_k} val[p] * X[vcol[p]][:]
+ *
+ * One workgroup per (c, column slice of `slice` floats); each relation's slab
+ * X[slab(k)*n_cols .. +n_cols][slice] is streamed into LDS once and every nonzero gathers
+ * from LDS.  Requirements: slice ∈ {16, 32}; n_cols * (slice + 4) * 4 <= 160 KiB;
+ * n_rows <= 8 * 16 * (256 / slice); d % 4 == 0; x, x_ld 16-byte aligned.
+ * Replaces layers.py:90-92 / :114-116 for such groups.
+ * -------------------------------------------------------------------------------------- */
+typedef struct dg_staged_group {
+    const int32_t* rowptr;      /* device, [n_rels*n_rows + 1]                   */
+    const int32_t* vcol;        /* device, [nnz] slab(k)*n_cols + col            */
+    const float* val;           /* device, [nnz]                                 */
+    const int32_t* slab;        /* device, [n_rels] slab of relation k, or NULL  */
+    const float* x;             /* device, relation-stacked dense operand        */
+    float* out;                 /* device, [ceil(n_rels/out_chunk)][n_rows][d]   */
+    int64_t x_ld;
+    int32_t n_rows;
+    int32_t n_cols;
+    int32_t n_rels;
+    int32_t out_chunk;          /* relations summed into one output chunk        */
+    int32_t x_rows;             /* rows of x addressable                         */
+    int32_t reserved;
+} dg_staged_group;
+
+int dg_spmm_staged_f32(const dg_staged_group* groups /* HOST */, int32_t n_groups, int32_t d,
+                       int32_t slice, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * GCN epilogue (T4 tail + T5 + T6):  for one node type i with groups g = (i, j_1..j_m),

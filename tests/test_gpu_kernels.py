@@ -183,13 +183,13 @@ def test_gemm(K, m, n, k, batch):
     bmap = rng.permutation(batch + 2)[:batch].astype(np.int32)
     sa = rng.standard_normal(k).astype(np.float32)
     sc = rng.standard_normal(n).astype(np.float32)
-    C = torch.empty((batch, m, n), device="cuda")
+    C = torch.zeros((batch + 2, m, n), device="cuda")  # C is indexed by the map too
     K.PreparedGemm(torch.from_numpy(A).cuda(), (0, k, 1), torch.from_numpy(B).cuda(), (k * n, n, 1), C,
                    (m * n, n, 1), m, n, k, batch, torch.from_numpy(sa).cuda(), torch.from_numpy(sc).cuda(),
                    b_map=torch.from_numpy(bmap).cuda(), b_batches=batch + 2, b_map_max=int(bmap.max()))()
     for b in range(batch):
         want = ((A.astype(np.float64) * sa) @ B[bmap[b]].astype(np.float64)) * sc
-        got = C[b].cpu().numpy()
+        got = C[bmap[b]].cpu().numpy()
         if k == 0:
             assert np.all(got == 0)
         else:
@@ -303,3 +303,29 @@ def test_decoder_hinge_fused(K, n):
     op2 = K.PreparedDecoderHinge(dv(U), dv(V), dv(rows), dv(cols), dv(G), dv(l), 0.1, neg_rows=dv(negs))
     op2()
     assert np.array_equal(op2.neg.cpu().numpy(), op.neg.cpu().numpy())
+
+
+@pytest.mark.parametrize("slice_", [16, 32])
+@pytest.mark.parametrize("d", [32, 64])
+@pytest.mark.parametrize("n_rows", [150, 1100])
+def test_spmm_staged(K, slice_, d, n_rows):
+    """LDS-staged SpMM: relations in permuted slabs, output chunks of 5 relations, rows
+    beyond one pass, empty rows."""
+    from decagon_amd.sparse import coo_to_csr, merge_chunks, sparse_to_tuple
+
+    rng = np.random.default_rng(slice_ + d + n_rows)
+    n_cols, nrel, total, out_chunk = 137, 23, 30, 5
+    mats = [_rand_csr(rng, n_rows, n_cols, 0.03, empty_rows=0.1) for _ in range(nrel)]
+    slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
+    m = merge_chunks([coo_to_csr(*sparse_to_tuple(x)) for x in mats], slabs, 1, total)
+    X = rng.standard_normal((total, n_cols, d)).astype(np.float32)
+    n_out = -(-nrel // out_chunk)
+    out = torch.zeros((n_out, n_rows, d), device="cuda")
+    spec = K.StagedSpec(torch.from_numpy(m.rowptr).cuda(), torch.from_numpy(m.vcol).cuda(),
+                        torch.from_numpy(m.val).cuda(), torch.from_numpy(slabs).cuda(), torch.from_numpy(X).cuda(),
+                        out, n_rows, n_cols, nrel, out_chunk, d, total * n_cols, vcol_max=int(m.vcol.max()))
+    K.PreparedStaged([spec], d, slice_)()
+    want = np.zeros((n_out, n_rows, d))
+    for k, x in enumerate(mats):
+        want[k // out_chunk] += x @ X[slabs[k]].astype(np.float64)
+    assert rel_err(out.cpu().numpy(), want) <= 1e-5

@@ -203,3 +203,38 @@ def test_dedicom_kat_reference_parameters(golden_kat):
         from decagon_amd import runtime
         full = runtime.full_scores(E, E, R, l).cpu().numpy()
         assert rel_err(full, want) <= TOL
+
+
+@pytest.mark.parametrize("staged", ["1", "0"])
+def test_polypharmacy_shaped_plan_matches_oracle(monkeypatch, staged):
+    """A scaled-down config P (drug×drug group large enough for the LDS-staged kernel and
+    for partial mode + epilogue; proteins fused) against the float64 restatement."""
+    import importlib
+
+    from oracle import decagon_oracle as orc
+    from decagon_amd import engine, synthetic
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    monkeypatch.setenv("DG_STAGED", staged)
+    g = synthetic.make_P(seed=3, n_proteins=900, n_drugs=120, n_side_effects=40, ppi_edges=6000,
+                         target_edges=700)
+    rng = np.random.default_rng(1)
+    n = g.n_nodes
+    w1 = {et: rng.uniform(-0.2, 0.2, (K, n[et[1]], 64)).astype(np.float32) for et, K in g.edge_types.items()}
+    w2 = {et: rng.uniform(-0.3, 0.3, (K, 64, 32)).astype(np.float32) for et, K in g.edge_types.items()}
+    dev = torch.device("cuda")
+    dg = engine.DeviceGraph(g.edge_types, g.csr(), dev)
+    assert dg.groups[(1, 1)].staged == (staged == "1")
+    plan = engine.ForwardPlan(dg, {0: None, 1: None},
+                              engine.LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
+                              engine.LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, 32)
+    plan.run()
+    torch.cuda.synchronize()
+    feats = {t: (np.stack([np.arange(n[t])] * 2, 1), np.ones(n[t]), (n[t], n[t])) for t in n}
+    h1, emb = orc.decagon_forward(g.edge_types, g.adj, feats,
+                                  {et: [x.astype(np.float64) for x in w] for et, w in w1.items()},
+                                  {et: [x.astype(np.float64) for x in w] for et, w in w2.items()})
+    assert rel_err(plan.hidden1[1].cpu().numpy(), h1[1]) <= TOL
+    assert rel_err(plan.embeddings[0].cpu().numpy(), emb[0]) <= TOL
+    assert rel_err(plan.embeddings[1].cpu().numpy(), emb[1]) <= TOL
