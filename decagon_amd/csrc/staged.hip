@@ -12,10 +12,12 @@
 // registers across the relations of an output chunk.
 //
 // Workgroup = 1024 threads, one per (output chunk c, column slice s):
-//   for k in chunk c:   stage X_slab(k)[:, s*W .. s*W+W) → LDS (rows padded by 16 B)
-//                       rows r = pass*RP + wave*(64/LPW) + lane/LPW, LPW lanes per row:
-//                       8 nonzeros (vcol, val) loaded per lane-group round, handed out with
-//                       ds_bpermute, 16-byte LDS gathers, fmaf into acc[pass]
+//   for k in chunk c:   issue at once: the CSR of every row this thread owns (LPW*NPF
+//                       nonzeros per row in registers), the slab X_slab(k)[:, s*W .. s*W+W)
+//                       and relation k+1's row pointers; barrier; slab -> LDS (rows padded
+//                       by 16 B); barrier; rows r = pass*RP + wave*(64/LPW) + lane/LPW, LPW
+//                       lanes per row, (vcol, val) handed out with ds_bpermute, 16-byte LDS
+//                       gathers, fmaf into acc[pass]
 //   write out[c][r][s*W .. s*W+W)
 // Fixed summation order, no atomics.
 #include "common.h"
@@ -50,7 +52,10 @@ struct StagedArgs {
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
 
-template <int LPW, int MAXP>
+// LPW lanes per row (slice = 4*LPW floats); MAXP passes of RP rows; NPF nonzeros per lane
+// prefetched per row and relation (rows longer than LPW*NPF finish in a tail loop); SR
+// 16-byte staging loads per thread.
+template <int LPW, int MAXP, int NPF, int SR>
 __global__ __launch_bounds__(kThreads) void spmm_staged_kernel(const StagedArgs a) {
     extern __shared__ float4 xs[];  // [n_cols][LPW + 1] float4 (one float4 of padding per row)
     constexpr int RPW = 64 / LPW;          // rows per wave per pass
@@ -60,7 +65,7 @@ __global__ __launch_bounds__(kThreads) void spmm_staged_kernel(const StagedArgs 
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int q = lane % LPW;
-    const int gsub = lane / LPW;           // row slot of this lane group within the wave
+    const int gbase = lane - q;            // first lane of this lane group
     const int b = blockIdx.x;
     int gi = 0;
 #pragma unroll 1
@@ -79,85 +84,132 @@ __global__ __launch_bounds__(kThreads) void spmm_staged_kernel(const StagedArgs 
     const bool qact = col0 + q * 4 < d;
     const int n_rows = g.n_rows;
     const int n_cols = g.n_cols;
+    const int row0 = wave * RPW + lane / LPW;  // this lane group's row in pass 0
+    const int k0 = c * g.out_chunk;
+    const int k1 = min(k0 + g.out_chunk, g.n_rels);
 
     float4 acc[MAXP];
 #pragma unroll
     for (int p = 0; p < MAXP; ++p) acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-    const int k0 = c * g.out_chunk;
-    const int k1 = min(k0 + g.out_chunk, g.n_rels);
+    // row extents of relation k for every pass (prefetched one relation ahead)
+    int beg[MAXP], len[MAXP];
+    auto load_rows = [&](int k, int (&bg)[MAXP], int (&ln)[MAXP]) {
+        const int32_t* __restrict__ rp = g.rowptr + (int64_t)k * n_rows;
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p) {
+            const int r = p * RP + row0;
+            bg[p] = 0;
+            ln[p] = 0;
+            if (k < k1 && r < n_rows) {
+                bg[p] = rp[r];
+                ln[p] = rp[r + 1] - bg[p];
+            }
+        }
+    };
+    load_rows(k0, beg, len);
+
 #pragma unroll 1
     for (int k = k0; k < k1; ++k) {
         const int slab = g.slab ? g.slab[k] : k;
         const int vbase = slab * n_cols;
-        // ---- stage X_slab[:, col0 .. col0+4*LPW) into LDS ----
-        __syncthreads();  // the previous relation's gathers are done
-        const float* __restrict__ xk = g.x + (int64_t)vbase * g.x_ld + col0;
-        for (int idx = tid; idx < n_cols * LPW; idx += kThreads) {
-            const int v = idx / LPW;
-            const int qq = idx - v * LPW;
-            float4 val4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (col0 + qq * 4 < d) val4 = *reinterpret_cast<const float4*>(xk + (int64_t)v * g.x_ld + qq * 4);
-            xs[v * LDR + qq] = val4;
-        }
-        __syncthreads();
-        // ---- every row's nonzeros of relation k, gathered from LDS ----
-        const int32_t* __restrict__ rp = g.rowptr + (int64_t)k * n_rows;
+        // ---- 1. issue every load of relation k: its CSR for this thread's rows ----
+        int vc[MAXP][NPF];
+        float vv[MAXP][NPF];
 #pragma unroll
         for (int p = 0; p < MAXP; ++p) {
-            const int r = p * RP + wave * RPW + gsub;
-            if (p * RP >= n_rows) break;  // uniform
-            int beg = 0, end = 0;
-            if (r < n_rows) {
-                beg = rp[r];
-                end = rp[r + 1];
+#pragma unroll
+            for (int i = 0; i < NPF; ++i) {
+                const int o = q + LPW * i;
+                vc[p][i] = 0;
+                vv[p][i] = 0.f;
+                if (o < len[p]) {
+                    vc[p][i] = g.vcol[beg[p] + o];
+                    vv[p][i] = g.val[beg[p] + o];
+                }
             }
-            // lane groups of one wave walk their rows in lock-step, LPW nonzeros per round
-            int len = end - beg;
-            int maxlen = len;
+        }
+        // ---- ... its dense slab X_slab[:, col0 .. col0+4*LPW) ----
+        const float* __restrict__ xk = g.x + (int64_t)vbase * g.x_ld + col0;
+        float4 st[SR];
+#pragma unroll
+        for (int j = 0; j < SR; ++j) {
+            const int idx = tid + j * kThreads;
+            const int v = idx / LPW;
+            const int qq = idx - v * LPW;
+            st[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (v < n_cols && col0 + qq * 4 < d)
+                st[j] = *reinterpret_cast<const float4*>(xk + (int64_t)v * g.x_ld + qq * 4);
+        }
+        // ---- ... and the next relation's row extents ----
+        int nbeg[MAXP], nlen[MAXP];
+        load_rows(k + 1, nbeg, nlen);
+        __syncthreads();  // the previous relation's gathers are done with the slab buffer
+#pragma unroll
+        for (int j = 0; j < SR; ++j) {
+            const int idx = tid + j * kThreads;
+            const int v = idx / LPW;
+            if (v < n_cols) xs[v * LDR + (idx - v * LPW)] = st[j];
+        }
+        __syncthreads();
+        // ---- 2. gather from LDS: lane group walks its row, LPW nonzeros per round ----
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p) {
+            if (p * RP >= n_rows) break;  // uniform
+#pragma unroll
+            for (int i = 0; i < NPF; ++i) {
+#pragma unroll
+                for (int t = 0; t < LPW; ++t) {
+                    const int vct = __shfl(vc[p][i], gbase + t) - vbase;
+                    const float vvt = __shfl(vv[p][i], gbase + t);
+                    if (LPW * i + t < len[p]) dg::fma4(acc[p], vvt, xs[vct * LDR + q]);
+                }
+            }
+            // rows longer than the prefetch: finish from global memory (rare)
+            int maxlen = len[p];
 #pragma unroll
             for (int m = LPW; m < 64; m <<= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m));
 #pragma unroll 1
-            for (int o = 0; o < maxlen; o += LPW) {
-                const int e = beg + o + q;
-                int vc = 0;
-                float vv = 0.f;
-                if (o + q < len) {
-                    vc = g.vcol[e] - vbase;
-                    vv = g.val[e];
+            for (int o = LPW * NPF; o < maxlen; o += LPW) {
+                int vcl = 0;
+                float vvl = 0.f;
+                if (o + q < len[p]) {
+                    vcl = g.vcol[beg[p] + o + q] - vbase;
+                    vvl = g.val[beg[p] + o + q];
                 }
 #pragma unroll
                 for (int t = 0; t < LPW; ++t) {
-                    const int src = (lane - q) + t;  // lane t of this lane group
-                    const int vct = __shfl(vc, src);
-                    const float vvt = __shfl(vv, src);
-                    if (o + t < len) {
-                        const float4 xv = xs[vct * LDR + q];
-                        dg::fma4(acc[p], vvt, xv);
-                    }
+                    const int vct = __shfl(vcl, gbase + t);
+                    const float vvt = __shfl(vvl, gbase + t);
+                    if (o + t < len[p]) dg::fma4(acc[p], vvt, xs[vct * LDR + q]);
                 }
             }
+        }
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p) {
+            beg[p] = nbeg[p];
+            len[p] = nlen[p];
         }
     }
     // ---- write the chunk partial ----
 #pragma unroll
     for (int p = 0; p < MAXP; ++p) {
-        const int r = p * RP + wave * RPW + gsub;
+        const int r = p * RP + row0;
         if (p * RP >= n_rows) break;
         if (r < n_rows && qact)
             *reinterpret_cast<float4*>(g.out + ((int64_t)c * n_rows + r) * d + col0 + q * 4) = acc[p];
     }
 }
 
-template <int LPW, int MAXP>
+template <int LPW, int MAXP, int NPF, int SR>
 int launch_staged(const StagedArgs& a, int64_t blocks, int lds_bytes, hipStream_t st) {
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmm_staged_kernel<LPW, MAXP>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmm_staged_kernel<LPW, MAXP, NPF, SR>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         configured = true;
     }
-    hipLaunchKernelGGL((spmm_staged_kernel<LPW, MAXP>), dim3(static_cast<unsigned>(blocks)),
+    hipLaunchKernelGGL((spmm_staged_kernel<LPW, MAXP, NPF, SR>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kThreads), lds_bytes, st, a);
     return dg::launch_status();
 }
@@ -209,14 +261,16 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
     const int64_t lds = (int64_t)max_cols * (lpw + 1) * 16;
     if (lds > 160 * 1024) return DG_EINVAL;           // the slab must fit in LDS
     const int passes = dg::ceil_div(max_rows, rows_per_pass);
+    const int sr = dg::ceil_div((int64_t)max_cols * lpw, kThreads);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int L = static_cast<int>(lds);
-    if (lpw == 8) {
-        if (passes <= 4) return launch_staged<8, 4>(a, blocks, L, st);
-        if (passes <= 8) return launch_staged<8, 8>(a, blocks, L, st);
-    } else {
-        if (passes <= 4) return launch_staged<4, 4>(a, blocks, L, st);
-        if (passes <= 8) return launch_staged<4, 8>(a, blocks, L, st);
+    // register budget: passes x prefetch and staging loads per thread are compile-time
+    // (every variant below stays within 128 VGPRs without scratch)
+    if (lpw == 4 && sr <= 4) {
+        if (passes <= 4) return launch_staged<4, 4, 4, 4>(a, blocks, L, st);
+        if (passes <= 8) return launch_staged<4, 8, 1, 4>(a, blocks, L, st);
+    } else if (lpw == 8 && sr <= 8 && passes <= 4) {
+        return launch_staged<8, 4, 2, 8>(a, blocks, L, st);
     }
-    return DG_EINVAL;  // too many rows for one workgroup's registers
+    return DG_EINVAL;  // too many rows or columns for one workgroup
 }

@@ -43,9 +43,17 @@ STAGED_MAX_ROWS = 2048
 STAGED_BINS = 128
 
 
+def staged_slice() -> int:
+    return int(os.environ.get("DG_STAGED_SLICE", "16"))
+
+
 def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
-    return (os.environ.get("DG_STAGED", "1") != "0" and n_rels >= STAGED_MIN_RELS
-            and n_cols <= STAGED_MAX_COLS and n_rows <= STAGED_MAX_ROWS)
+    sl = staged_slice()
+    # kernel variants (staged.hip): slice 16 up to 8 passes, slice 32 up to 4 passes of
+    # 16 waves x (256 / slice) rows; staging registers cover 1024 slab rows
+    max_rows = (8 if sl == 16 else 4) * 16 * (256 // sl)
+    return (os.environ.get("DG_STAGED", "0") != "0" and n_rels >= STAGED_MIN_RELS
+            and n_cols <= 1024 and n_rows <= min(STAGED_MAX_ROWS, max_rows))
 
 
 def snake_bins(costs: Sequence[float], bin_size: int) -> np.ndarray:
@@ -340,7 +348,7 @@ class ForwardPlan:
                     grp.n_rels, grp.out_chunk, d, grp.K * grp.n_cols, vcol_max=grp.vcol_max))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
-        slice_ = int(os.environ.get("DG_STAGED_SLICE", "16"))
+        slice_ = staged_slice()
         launches += [kernels.PreparedStaged(staged[s:s + DG_MAX_GROUPS], d, slice_)
                      for s in range(0, len(staged), DG_MAX_GROUPS)]
         launches += [kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d)

@@ -307,15 +307,15 @@ def test_decoder_hinge_fused(K, n):
 
 @pytest.mark.parametrize("slice_", [16, 32])
 @pytest.mark.parametrize("d", [32, 64])
-@pytest.mark.parametrize("n_rows", [150, 1100])
-def test_spmm_staged(K, slice_, d, n_rows):
+@pytest.mark.parametrize("n_rows,density", [(150, 0.03), (1100, 0.03), (300, 0.45)])
+def test_spmm_staged(K, slice_, d, n_rows, density):
     """LDS-staged SpMM: relations in permuted slabs, output chunks of 5 relations, rows
-    beyond one pass, empty rows."""
+    beyond one pass, empty rows, rows longer than the per-row register prefetch."""
     from decagon_amd.sparse import coo_to_csr, merge_chunks, sparse_to_tuple
 
     rng = np.random.default_rng(slice_ + d + n_rows)
     n_cols, nrel, total, out_chunk = 137, 23, 30, 5
-    mats = [_rand_csr(rng, n_rows, n_cols, 0.03, empty_rows=0.1) for _ in range(nrel)]
+    mats = [_rand_csr(rng, n_rows, n_cols, density, empty_rows=0.1) for _ in range(nrel)]
     slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
     m = merge_chunks([coo_to_csr(*sparse_to_tuple(x)) for x in mats], slabs, 1, total)
     X = rng.standard_normal((total, n_cols, d)).astype(np.float32)
@@ -324,6 +324,10 @@ def test_spmm_staged(K, slice_, d, n_rows):
     spec = K.StagedSpec(torch.from_numpy(m.rowptr).cuda(), torch.from_numpy(m.vcol).cuda(),
                         torch.from_numpy(m.val).cuda(), torch.from_numpy(slabs).cuda(), torch.from_numpy(X).cuda(),
                         out, n_rows, n_cols, nrel, out_chunk, d, total * n_cols, vcol_max=int(m.vcol.max()))
+    if slice_ == 32 and n_rows > 512:  # 4 passes x 128 rows: beyond one workgroup's registers
+        with pytest.raises(K._lib.KernelError if hasattr(K, "_lib") else Exception):
+            K.PreparedStaged([spec], d, slice_)()
+        return
     K.PreparedStaged([spec], d, slice_)()
     want = np.zeros((n_out, n_rows, d))
     for k, x in enumerate(mats):
