@@ -11,8 +11,8 @@ __version__ = "0.1.0"
 from . import flags  # noqa: F401
 from .flags import FLAGS  # noqa: F401
 from .graph import (InvalidArgumentError, Node, Operation, Placeholder, Session, Variable,  # noqa: F401
-                    global_variables_initializer, placeholder, placeholder_with_default,
-                    sparse_placeholder)
+                    float32, global_variables_initializer, int32, name_scope, placeholder,
+                    placeholder_with_default, sparse_placeholder)
 from .inits import set_random_seed  # noqa: F401
 from .layers import (BilinearDecoder, DEDICOMDecoder, DistMultDecoder,  # noqa: F401
                      GraphConvolutionMulti, GraphConvolutionSparseMulti, InnerProductDecoder,

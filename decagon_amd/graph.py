@@ -12,6 +12,8 @@ any node — not only a placeholder — may be fed, which overrides its computat
 """
 from __future__ import annotations
 
+import contextlib
+
 import itertools
 from typing import Any, Callable, Dict, Optional
 
@@ -192,6 +194,18 @@ class Session:
             return _to_numpy(v)
 
         return conv(out)
+
+
+# dtype names accepted by placeholder() (the reference passes tf.int32 / tf.float32,
+# main.py:93-106); only used for documentation, values are converted at feed time
+int32 = "int32"
+float32 = "float32"
+
+
+@contextlib.contextmanager
+def name_scope(name: str):
+    """tf.name_scope (main.py:268): a naming scope; node names are not part of the contract."""
+    yield name
 
 
 def global_variables_initializer() -> Operation:

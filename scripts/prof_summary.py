@@ -1,0 +1,90 @@
+"""Summarise a scripts/profile_round.sh output directory: per-kernel launch count and mean
+duration (kernel-trace stats) and per-launch mean FETCH_SIZE / WRITE_SIZE (PMC passes).
+
+    python3 scripts/prof_summary.py gpurun_out/prof_r01 > profiles/r01_summary.md
+    python3 scripts/prof_summary.py gpurun_out/prof_r01 --json profiles/r01_traffic.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(")[0] if "(" in name else name
+
+
+def stats(d):
+    f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    if not f:
+        return []
+    return list(csv.DictReader(open(f[0])))
+
+
+def pmc(d):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = defaultdict(list)
+    if not f:
+        return acc
+    for r in csv.DictReader(open(f[0])):
+        acc[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return acc
+
+
+def traffic_json(root, out):
+    """Per-kernel mean FETCH_SIZE / WRITE_SIZE per launch (KiB, raw counter values) for each
+    config, plus mean durations — what bench.py reads to fill roofline.traffic."""
+    rec = {}
+    for cfg in ("S", "P"):
+        counters = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            counters.update(pmc(os.path.join(root, f"{cfg}_{ctr}")))
+        kern = {}
+        for (k, c), v in counters.items():
+            kern.setdefault(k, {})[c.lower() + "_kib"] = sum(v) / len(v)
+        for r in stats(os.path.join(root, f"{cfg}_trace")):
+            kern.setdefault(short(r["Name"]), {})["avg_us"] = float(r["AverageNs"]) / 1e3
+        rec[cfg] = kern
+    json.dump(rec, open(out, "w"), indent=1, sort_keys=True)
+
+
+def main(root):
+    if len(sys.argv) > 3 and sys.argv[2] == "--json":
+        traffic_json(root, sys.argv[3])
+        return
+    print(f"# rocprofv3 summary: {os.path.basename(root.rstrip('/'))}\n")
+    for cfg in ("S", "P"):
+        st = stats(os.path.join(root, f"{cfg}_trace"))
+        if not st:
+            continue
+        bj = os.path.join(root, f"{cfg}_bench.json")
+        if os.path.exists(bj):
+            try:
+                rec = json.loads(open(bj).read().strip().splitlines()[-1])
+                print(f"## config {cfg}: bench line under the profiler\n")
+                print(f"value {rec['value']:.4g} edges/s, {rec['ms_per_step']*1e3:.1f} us/step; "
+                      f"layer-1 SpMM {rec['roofline']['kernel_ms']*1e3:.2f} us, "
+                      f"{rec['roofline']['algorithmic_bytes']} algorithmic B\n")
+            except Exception:
+                pass
+        counters = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            counters.update(pmc(os.path.join(root, f"{cfg}_{ctr}")))
+        print(f"## config {cfg}: kernels (kernel-trace --stats)\n")
+        print("| kernel | calls | avg us | total % | FETCH_SIZE/launch (raw) | WRITE_SIZE/launch (raw) |")
+        print("|---|---|---|---|---|---|")
+        for r in st[:14]:
+            k = short(r["Name"])
+            f = counters.get((k, "FETCH_SIZE"), [])
+            w = counters.get((k, "WRITE_SIZE"), [])
+            fs = f"{sum(f)/len(f):.1f}" if f else "-"
+            ws = f"{sum(w)/len(w):.1f}" if w else "-"
+            print(f"| `{k}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | {fs} | {ws} |")
+        print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,0 +1,23 @@
+# Round profile: rocprofv3 kernel-trace stats of the default bench (config S) and of config P,
+# then one PMC pass per TCC counter (FETCH_SIZE, WRITE_SIZE: they do not fit one pass).
+# Usage on the GPU box:  bash scripts/profile_round.sh <tag>      (outputs: gpurun_out/prof_<tag>/)
+set -e
+tag=${1:-r01}
+cd "$GRAFT_REPO_ROOT"
+out=gpurun_out/prof_$tag
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for cfg in S P; do
+  if [ $cfg = S ]; then steps="--steps 200 --warmup 20 --kernel-reps 200"; else steps="--steps 20 --warmup 3 --kernel-reps 20"; fi
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${cfg}_trace -o run -- \
+    python3 bench.py --config $cfg $steps --no-cpu-baseline > $out/${cfg}_bench.json 2> $out/${cfg}_trace.log
+  echo "$cfg trace done"
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $out/${cfg}_$ctr -o run -- \
+      python3 bench.py --config $cfg --no-graph --steps 5 --warmup 1 --kernel-reps 3 --no-cpu-baseline \
+      > /dev/null 2> $out/${cfg}_$ctr.log
+    echo "$cfg $ctr done"
+  done
+done
+python3 scripts/prof_summary.py $out > $out/summary.md
+echo summary done
