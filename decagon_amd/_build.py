@@ -24,7 +24,7 @@ def lib_path() -> Path:
 
 
 def _sources():
-    return sorted(CSRC.glob("*.hip"))
+    return sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
 
 
 def _deps():

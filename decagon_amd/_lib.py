@@ -7,6 +7,8 @@ package fails loudly instead of silently running on the CPU.
 from __future__ import annotations
 
 import ctypes
+import os
+from pathlib import Path
 from ctypes import POINTER, c_float, c_int32, c_int64, c_uint64, c_void_p
 
 from . import _build
@@ -19,7 +21,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 8
+ABI_VERSION = 11
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -41,9 +43,9 @@ class DgRelGroup(ctypes.Structure):
 
 class DgStagedGroup(ctypes.Structure):
     _fields_ = [
-        ("rowptr", c_void_p),
-        ("vcol", c_void_p),
-        ("val", c_void_p),
+        ("pairs", c_void_p),
+        ("jm", c_void_p),
+        ("jmoff", c_void_p),
         ("slab", c_void_p),
         ("x", c_void_p),
         ("out", c_void_p),
@@ -114,7 +116,8 @@ SIGNATURES = {
         [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     ),
     "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_int32, c_void_p]),
-    "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_int32, c_void_p]),
+    "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
+    "dg_staged_order": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "dg_decoder_hinge_f32": (
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
@@ -146,8 +149,9 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = _build.lib_path()
-    if not path.exists() or (build_if_missing and _build.needs_build()):
+    override = os.environ.get("DG_LIB")  # an instrumented build (scripts/staged_prof.py)
+    path = Path(override) if override else _build.lib_path()
+    if not override and (not path.exists() or (build_if_missing and _build.needs_build())):
         if not build_if_missing:
             raise ImportError(f"{path} missing: run __graft_entry__.build() or python -m decagon_amd._build")
         _build.build()

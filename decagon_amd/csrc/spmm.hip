@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 8; }
+extern "C" int32_t dg_abi_version(void) { return 11; }
 
 namespace {
 

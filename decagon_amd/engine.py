@@ -30,30 +30,22 @@ import torch
 
 from . import kernels
 from ._lib import DG_EPI_L2NORM, DG_EPI_RELU, DG_MAX_GROUPS
-from .sparse import HostCSR, MergedCSR, merge_chunks
+from .sparse import HostCSR, MergedCSR, merge_chunks, staged_layout
 
 EdgeType = Tuple[int, int]
 
 
-# LDS-staged groups: many relations over a column space narrow enough that one relation's
-# column slice (16 floats, rows padded to 20) fits LDS next to two more workgroups.
+# LDS-staged groups (staged.hip): many relations over a column space narrow enough that one
+# relation's 16-float column slice and the output rows' accumulators fit LDS.
 STAGED_MIN_RELS = int(os.environ.get("DG_STAGED_MIN_RELS", "32"))
-STAGED_MAX_COLS = 2048
-STAGED_MAX_ROWS = 2048
-STAGED_BINS = 128
-
-
-def staged_slice() -> int:
-    return int(os.environ.get("DG_STAGED_SLICE", "16"))
+STAGED_MAX_COLS = 1024
+STAGED_MAX_ROWS = 1023
+STAGED_BINS = int(os.environ.get("DG_STAGED_BINS", "128"))
 
 
 def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
-    sl = staged_slice()
-    # kernel variants (staged.hip): slice 16 up to 8 passes, slice 32 up to 4 passes of
-    # 16 waves x (256 / slice) rows; staging registers cover 1024 slab rows
-    max_rows = (8 if sl == 16 else 4) * 16 * (256 // sl)
-    return (os.environ.get("DG_STAGED", "0") != "0" and n_rels >= STAGED_MIN_RELS
-            and n_cols <= 1024 and n_rows <= min(STAGED_MAX_ROWS, max_rows))
+    return (os.environ.get("DG_STAGED", "1") != "0" and n_rels >= STAGED_MIN_RELS
+            and 0 < n_cols <= STAGED_MAX_COLS and 0 < n_rows <= STAGED_MAX_ROWS)
 
 
 def snake_bins(costs: Sequence[float], bin_size: int) -> np.ndarray:
@@ -105,6 +97,7 @@ class DeviceGroup:
     rel_map: Optional[torch.Tensor] = None   # device rel_ids, when not 0..K-1
     staged: bool = False           # runs through dg_spmm_staged_f32 (layout: chunk = 1)
     out_chunk: int = 1             # staged: relations summed per output chunk
+    layout: Optional["kernels.StagedDevice"] = None  # staged: the diagonal-major layout
 
     @property
     def n_rels(self) -> int:
@@ -168,6 +161,10 @@ class DeviceGraph:
             if ids.size and not np.array_equal(ids, np.arange(K)):
                 g.rel_map = torch.from_numpy(ids).to(device)
             g.staged, g.out_chunk = staged, out_chunk
+            if staged:
+                lay = staged_layout(loc, kernels.staged_order,
+                                    split=os.environ.get("DG_STAGED_SPLIT", "1") != "0")
+                g.layout = kernels.StagedDevice.upload(lay, device)
             self.groups[et] = g
 
     @property
@@ -344,12 +341,11 @@ class ForwardPlan:
                 continue
             if grp.staged:
                 staged.append(kernels.StagedSpec(
-                    grp.rowptr, grp.vcol, grp.val, grp.rel_map, xs[et], part, grp.n_rows, grp.n_cols,
-                    grp.n_rels, grp.out_chunk, d, grp.K * grp.n_cols, vcol_max=grp.vcol_max))
+                    grp.layout, grp.rel_map, xs[et], part, grp.out_chunk, d, grp.K * grp.n_cols,
+                    slab_max=int(grp.rel_ids.max())))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
-        slice_ = staged_slice()
-        launches += [kernels.PreparedStaged(staged[s:s + DG_MAX_GROUPS], d, slice_)
+        launches += [kernels.PreparedStaged(staged[s:s + DG_MAX_GROUPS], d)
                      for s in range(0, len(staged), DG_MAX_GROUPS)]
         launches += [kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d)
                      for s in range(0, len(specs), DG_MAX_GROUPS)]

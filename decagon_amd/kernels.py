@@ -192,69 +192,98 @@ class PreparedFused:
                        self.wpg, self.d, _stream_ptr(stream)), "dg_gcn_fused_f32")
 
 
-@dataclass
-class StagedSpec:
-    """One group for dg_spmm_staged_f32 (one chunk per relation in the merged layout)."""
+def staged_order(csr, perm: np.ndarray) -> np.ndarray:
+    """Diagonal of each nonzero of one relation (CSR order) for the staged layout: the
+    library's bank-conflict-avoiding order (dg_staged_order, host-only)."""
+    rowptr = np.ascontiguousarray(csr.rowptr, np.int32)
+    col = np.ascontiguousarray(csr.col, np.int32)
+    perm = np.ascontiguousarray(perm, np.int32)
+    rank = np.zeros(len(col), np.int32)
+    check(_lib.load().dg_staged_order(rowptr.ctypes.data, col.ctypes.data, len(rowptr) - 1,
+                                      perm.ctypes.data, rank.ctypes.data), "dg_staged_order")
+    return rank
 
-    rowptr: torch.Tensor          # int32 [n_rels*n_rows + 1]
-    vcol: torch.Tensor            # int32 [nnz]
-    val: torch.Tensor             # float32 [nnz]
-    slab: Optional[torch.Tensor]  # int32 [n_rels] or None
-    x: torch.Tensor
-    out: torch.Tensor             # float32 [ceil(n_rels/out_chunk), n_rows, d]
+
+@dataclass
+class StagedDevice:
+    """A StagedLayout (sparse.py) uploaded to the device."""
+
+    pairs: torch.Tensor
+    jm: torch.Tensor
+    jmoff: torch.Tensor
     n_rows: int
     n_cols: int
     n_rels: int
+
+    @classmethod
+    def upload(cls, layout, device) -> "StagedDevice":
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        return cls(t(layout.pairs), t(layout.jm), t(layout.jmoff), layout.n_rows, layout.n_cols,
+                   len(layout.jmoff) - 1)
+
+
+@dataclass
+class StagedSpec:
+    """One group for dg_spmm_staged_f32."""
+
+    layout: StagedDevice
+    slab: Optional[torch.Tensor]  # int32 [n_rels] or None
+    x: torch.Tensor
+    out: torch.Tensor             # float32 [ceil(n_rels/out_chunk), n_rows, d]
     out_chunk: int
     x_ld: int
     x_rows: int
-    vcol_max: int = -1
+    slab_max: int = -1            # host-known max(slab) (or n_rels-1 without slab), for checks
 
     def validate(self, d: int) -> None:
-        for t, nm, dt in ((self.rowptr, "rowptr", torch.int32), (self.vcol, "vcol", torch.int32),
-                          (self.val, "val", torch.float32), (self.x, "x", torch.float32),
+        L = self.layout
+        for t, nm, dt in ((L.pairs, "pairs", torch.int32), (L.jm, "jm", torch.int32),
+                          (L.jmoff, "jmoff", torch.int32), (self.x, "x", torch.float32),
                           (self.out, "out", torch.float32)):
             _dev(t, dt, nm)
+        if L.pairs.data_ptr() % 16:
+            raise ValueError("pairs must be 16-byte aligned")
+        if not (0 < L.n_rows < 1024 and 0 < L.n_cols <= 1024):
+            raise ValueError("staged groups need n_rows < 1024, n_cols <= 1024")
+        if not 1 <= self.out_chunk <= 64:
+            raise ValueError("staged out_chunk must be 1..64")
         if self.slab is not None:
             _dev(self.slab, torch.int32, "slab")
-            if self.slab.numel() < self.n_rels:
+            if self.slab.numel() < L.n_rels:
                 raise ValueError("slab shorter than n_rels")
-        if self.rowptr.numel() < self.n_rels * self.n_rows + 1:
-            raise ValueError("staged rowptr must hold one chunk per relation")
-        if self.vcol_max >= self.x_rows or self.x.numel() < (self.x_rows - 1) * self.x_ld + d:
-            raise ValueError("dense operand smaller than the indices address")
+        smax = self.slab_max if self.slab_max >= 0 else L.n_rels - 1
+        if (smax + 1) * L.n_cols > self.x_rows or self.x.numel() < (self.x_rows - 1) * self.x_ld + d:
+            raise ValueError("dense operand smaller than the slabs address")
         if self.x_rows * self.x_ld >= 2**31:
             raise ValueError("dense operand too large for 32-bit gather offsets")
-        n_out = -(-self.n_rels // self.out_chunk)
-        if self.out.numel() < n_out * self.n_rows * d:
+        n_out = -(-L.n_rels // self.out_chunk)
+        if self.out.numel() < n_out * L.n_rows * d:
             raise ValueError("staged out too small")
 
 
 class PreparedStaged:
     """A fixed dg_spmm_staged_f32 launch."""
 
-    def __init__(self, specs: Sequence[StagedSpec], d: int, slice_: int = 16):
+    def __init__(self, specs: Sequence[StagedSpec], d: int):
         if not 1 <= len(specs) <= _lib.DG_MAX_GROUPS:
             raise ValueError(f"1..{_lib.DG_MAX_GROUPS} groups per launch")
         arr = (DgStagedGroup * len(specs))()
         for i, s in enumerate(specs):
             s.validate(d)
-            g = arr[i]
-            g.rowptr = s.rowptr.data_ptr()
-            g.vcol = s.vcol.data_ptr() if s.vcol.numel() else None
-            g.val = s.val.data_ptr() if s.val.numel() else None
+            L, g = s.layout, arr[i]
+            g.pairs, g.jm, g.jmoff = L.pairs.data_ptr(), L.jm.data_ptr(), L.jmoff.data_ptr()
             g.slab = s.slab.data_ptr() if s.slab is not None else None
             g.x = s.x.data_ptr()
             g.out = s.out.data_ptr()
             g.x_ld = s.x_ld
-            g.n_rows, g.n_cols, g.n_rels = s.n_rows, s.n_cols, s.n_rels
+            g.n_rows, g.n_cols, g.n_rels = L.n_rows, L.n_cols, L.n_rels
             g.out_chunk, g.x_rows = s.out_chunk, s.x_rows
         self._keep = list(specs)
-        self._arr, self._n, self.d, self.slice = arr, len(specs), d, slice_
+        self._arr, self._n, self.d = arr, len(specs), d
         self._fn = _lib.load().dg_spmm_staged_f32
 
     def __call__(self, stream=None) -> None:
-        check(self._fn(self._arr, self._n, self.d, self.slice, _stream_ptr(stream)), "dg_spmm_staged_f32")
+        check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_f32")
 
 
 def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 from collections import namedtuple
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import scipy.sparse as sp
@@ -226,3 +226,100 @@ def merge_chunks(csrs: Sequence[HostCSR], slabs: Sequence[int], chunk: int, n_sl
         val[dst] = c.val
         fill[cb:cb + n_r] += lens
     return MergedCSR(rowptr.astype(np.int32), vcol, val, n_r, n_c, n_chunks, chunk, n_slabs * n_c)
+
+
+@dataclass
+class StagedLayout:
+    """Device layout of a group for dg_spmm_staged_f32 (include/decagon_hip.h).
+
+    Per relation, rows longer than a segment length L are split into virtual rows of at most
+    L consecutive nonzeros (L the smallest that leaves at most `lanes` virtual rows); the
+    virtual rows are sorted by length (descending, stable) and the nonzeros stored
+    diagonal-major — the m-th nonzero of every virtual row that has one, in sorted order — so
+    thread i of a workgroup owns sorted virtual row i and a wave's pairs at diagonal m are
+    one contiguous run.
+
+      pairs [nnz + 1, 2] int32   (column, fp32 value bits), relations back to back, + 1 pad pair
+      jm    int32                per relation at jmoff[k]: [n_virt, n_rounds, 0, 0]
+                                 (n_rounds = most segments of a row), vinfo[n_virt] =
+                                 row | seg << 10 | len << 16 per sorted virtual row,
+                                 doff[maxlen + 1] (absolute pair offset of diagonal m)
+    """
+
+    pairs: np.ndarray
+    jm: np.ndarray
+    jmoff: np.ndarray
+    n_rows: int
+    n_cols: int
+    nnz: int
+
+
+def _segment_length(lens: np.ndarray, lanes: int) -> int:
+    """Smallest L with sum(ceil(lens / L)) <= lanes."""
+    nnz = int(lens.sum())
+    L = max(1, -(-nnz // lanes))
+    while int((-(-lens // L)).sum()) > lanes:
+        L += 1
+    return L
+
+
+def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
+                  lanes: int = 1024, split: bool = True) -> StagedLayout:
+    """Build the staged layout of relations `csrs` (all one shape, local columns) with at
+    most `lanes` virtual rows per relation (split=False: one virtual row per nonempty row).
+    `order(csr, perm) -> rank` places each nonzero of a (virtual-row) CSR on a diagonal
+    (default: feed order); the device path passes the library's bank-conflict-avoiding
+    order (kernels.staged_order)."""
+    if not csrs:
+        raise ValueError("empty relation group")
+    n_r, n_c = csrs[0].shape
+    if n_r >= 1024 or n_c > 1024 or lanes > 1024:
+        raise ValueError("staged groups need n_rows < 1024, n_cols <= 1024")
+    total = int(sum(c.nnz for c in csrs))
+    if total + 1 >= 2**31:
+        raise ValueError("group exceeds int32 indexing")
+    pairs = np.zeros((total + 1, 2), np.int32)
+    jm_parts, jmoff = [], [0]
+    base = 0
+    for c in csrs:
+        if c.shape != (n_r, n_c):
+            raise ValueError("all relations of a group must share one shape")
+        lens = np.diff(c.rowptr.astype(np.int64))
+        L = (_segment_length(lens, lanes) if split else int(lens.max())) if c.nnz else 1
+        nseg = -(-lens // L)                                   # segments per row (0: empty row)
+        vrow = np.repeat(np.arange(n_r), nseg)                 # virtual row -> row
+        vseg = np.arange(len(vrow)) - np.repeat(np.cumsum(nseg) - nseg, nseg)
+        vstart = c.rowptr[:-1].astype(np.int64)[vrow] + vseg * L
+        vlen = np.minimum(L, lens[vrow] - vseg * L)
+        n_v = len(vrow)
+        vrowptr = np.zeros(n_v + 1, np.int64)
+        np.cumsum(vlen, out=vrowptr[1:])                       # virtual CSR = same nonzero order
+        perm = np.argsort(-vlen, kind="stable")
+        rl = vlen[perm]
+        maxlen = int(rl[0]) if n_v else 0
+        cnt = n_v - np.cumsum(np.bincount(rl, minlength=maxlen + 1))[:maxlen]
+        doff = np.empty(maxlen + 1, np.int64)
+        doff[0] = base
+        np.cumsum(cnt, out=doff[1:])
+        doff[1:] += base
+        if c.nnz:
+            inv = np.empty(n_v, np.int64)
+            inv[perm] = np.arange(n_v)
+            vr = np.repeat(np.arange(n_v), vlen)
+            if order is None:
+                rank = np.arange(c.nnz, dtype=np.int64) - vrowptr[:-1][vr]
+            else:
+                vcsr = HostCSR(vrowptr.astype(np.int32), c.col, c.val, (n_v, n_c))
+                rank = np.asarray(order(vcsr, perm), np.int64)
+            dst = doff[rank] + inv[vr]
+            pairs[dst, 0] = c.col
+            pairs[dst, 1] = np.ascontiguousarray(c.val, np.float32).view(np.int32)
+        rounds = int(nseg.max()) if n_r else 0
+        vinfo = vrow[perm] | (vseg[perm] << 10) | (rl << 16)
+        seg = np.concatenate([[n_v, rounds, 0, 0], vinfo, doff]).astype(np.int64)
+        pad = (-len(seg)) % 4
+        jm_parts.append(np.concatenate([seg.astype(np.int32), np.zeros(pad, np.int32)]))
+        jmoff.append(jmoff[-1] + len(seg) + pad)
+        base += c.nnz
+    return StagedLayout(pairs, np.concatenate(jm_parts) if jm_parts else np.zeros(0, np.int32),
+                        np.asarray(jmoff, np.int32), n_r, n_c, total)

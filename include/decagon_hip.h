@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (8); bumped whenever a struct layout or a signature changes. */
+/* ABI version (11); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -119,37 +119,54 @@ int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
                      int32_t waves_per_group, int32_t d, void* stream);
 
 /* --------------------------------------------------------------------------------------
- * LDS-staged relation SpMM (T3 + T4) for groups with many relations over few columns
- * (polypharmacy drug×drug: 1,928 relations of 645×645).  Layout: one chunk per relation
- * (merge_chunks with chunk = 1, i.e. stacked CSR with rowptr [n_rels*n_rows + 1]) and
- * vcol = slab(k)*n_cols + col.  For output chunk c (out_chunk consecutive relations):
+ * LDS-staged relation SpMM for groups of many relations over a narrow column space
+ * (polypharmacy drug x drug: 1,928 relations of 645 x 645).  For output chunk c (out_chunk
+ * consecutive relations):
  *
- *     out[c][r][:] = sum_{k in chunk c} sum_{p in row r of A_k} val[p] * X[vcol[p]][:]
+ *     out[c][r][:] = sum_{k in chunk c} sum_{p in row r of A_k} val[p] * X[slab(k)*n_cols + col[p]][:]
  *
- * One workgroup per (c, column slice of `slice` floats); each relation's slab
- * X[slab(k)*n_cols .. +n_cols][slice] is streamed into LDS once and every nonzero gathers
- * from LDS.  Requirements: slice ∈ {16, 32}; n_cols * (slice + 4) * 4 <= 160 KiB;
- * n_rows <= 8 * 16 * (256 / slice); d % 4 == 0; x, x_ld 16-byte aligned.
+ * Layout (built on the host by decagon_amd/sparse.py: staged_layout): per relation, rows are
+ * split into virtual rows of at most L consecutive nonzeros (at most 1024 virtual rows),
+ * sorted by length, and the nonzeros stored diagonal-major (the m-th nonzero of every
+ * virtual row that has one, in sorted order):
+ *   pairs      [nnz + 1][2] int32: (column, fp32 value bits), relations back to back, plus one
+ *              padding pair; 16-byte aligned
+ *   jm, jmoff  relation k's tables at jm[jmoff[k] .. jmoff[k+1]) (at most 3072 ints):
+ *              [n_virt, n_rounds, 0, 0], vinfo[n_virt] = row | segment << 10 | length << 16,
+ *              doff[maxlen + 1] (absolute pair offset of diagonal m)
+ * One workgroup of 1024 threads per (c, 16-float column slice); thread i owns sorted virtual
+ * row i and streams its pairs from global memory (one coalesced load per wave and diagonal);
+ * the slab slice is in LDS and every nonzero gathers from it; the segments of a row are
+ * summed in segment order.  Requirements: n_rows < 1024; n_cols <= 1024; out_chunk <= 64;
+ * d % 4 == 0; x, x_ld 16-byte aligned.
  * Replaces layers.py:90-92 / :114-116 for such groups.
  * -------------------------------------------------------------------------------------- */
 typedef struct dg_staged_group {
-    const int32_t* rowptr;      /* device, [n_rels*n_rows + 1]                   */
-    const int32_t* vcol;        /* device, [nnz] slab(k)*n_cols + col            */
-    const float* val;           /* device, [nnz]                                 */
-    const int32_t* slab;        /* device, [n_rels] slab of relation k, or NULL  */
-    const float* x;             /* device, relation-stacked dense operand        */
-    float* out;                 /* device, [ceil(n_rels/out_chunk)][n_rows][d]   */
+    const int32_t* pairs;       /* device, [nnz + 1][2]                                  */
+    const int32_t* jm;          /* device                                                */
+    const int32_t* jmoff;       /* device, [n_rels + 1]                                  */
+    const int32_t* slab;        /* device, [n_rels] slab of relation k, or NULL (= k)    */
+    const float* x;             /* device, relation-stacked dense operand                */
+    float* out;                 /* device, [ceil(n_rels/out_chunk)][n_rows][d]           */
     int64_t x_ld;
     int32_t n_rows;
     int32_t n_cols;
     int32_t n_rels;
-    int32_t out_chunk;          /* relations summed into one output chunk        */
-    int32_t x_rows;             /* rows of x addressable                         */
+    int32_t out_chunk;          /* relations summed into one output chunk (<= 64)        */
+    int32_t x_rows;             /* rows of x addressable                                 */
     int32_t reserved;
 } dg_staged_group;
 
 int dg_spmm_staged_f32(const dg_staged_group* groups /* HOST */, int32_t n_groups, int32_t d,
-                       int32_t slice, void* stream);
+                       void* stream);
+
+/* Host-only layout helper: for one relation in CSR (HOST arrays) and its sorted-row order
+ * perm[n_rows] (sorted index -> row, lengths descending), rank_out[p] = the diagonal nonzero
+ * p is placed on.  Each row's nonzeros are ordered so that the rows sharing a ds_read_b128
+ * lane group in the staged kernel read different LDS bank slots at every diagonal where
+ * possible (a fixed order: the row sums change only by rounding, deterministically). */
+int dg_staged_order(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                    const int32_t* perm, int32_t* rank_out);
 
 /* --------------------------------------------------------------------------------------
  * GCN epilogue (T4 tail + T5 + T6):  for one node type i with groups g = (i, j_1..j_m),

@@ -1,0 +1,65 @@
+"""Cycle breakdown of dg_spmm_staged_f32 on config P (profiling aid).
+
+Build (here):   python scripts/staged_prof.py build     -> scripts/prof_build/libdecagon_hip_prof.so
+Run (GPU box):  python scripts/staged_prof.py run [bins]
+Per workgroup: cycles waiting at the stage barrier (copies), at relation starts (slab write),
+gathering, and the stage count; printed as means over blocks for layer 1 and layer 2.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+OUT = ROOT / "scripts" / "prof_build" / "libdecagon_hip_prof.so"
+
+
+def build():
+    sys.path.insert(0, str(ROOT))
+    from decagon_amd import _build
+    OUT.parent.mkdir(exist_ok=True)
+    cmd = [_build.hipcc(), "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared", "-DDG_STAGED_PROF",
+           f"-I{ROOT / 'include'}", f"-I{_build.CSRC}", "-o", str(OUT), *map(str, _build._sources())]
+    subprocess.run(cmd, check=True)
+
+
+def run():
+    os.environ["DG_LIB"] = str(OUT)
+    os.environ["DG_STAGED"] = "1"
+    if len(sys.argv) > 2:
+        os.environ["DG_STAGED_BINS"] = sys.argv[2]
+    sys.path.insert(0, str(ROOT))
+    import numpy as np
+    import torch
+
+    import bench
+    from decagon_amd import _lib, kernels
+
+    lib = _lib.load()
+    lib.dg_staged_prof_copy.restype = ctypes.c_int64
+    lib.dg_staged_prof_copy.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    args = bench.parse.__wrapped__() if hasattr(bench.parse, "__wrapped__") else None
+    sys.argv = [sys.argv[0], "--config", "P"]
+    args = bench.parse()
+    graph, shard, _, _ = bench.build_workload(args, 0, 1)
+    plan, dg = bench.make_plan(args, graph, shard, torch.device("cuda", 0))
+    l1, l2 = plan.spmm_launches
+    clock = 100e6  # s_memtime/readcyclecounter ticks (shader clock): report raw and per stage
+    for name, launches in (("layer1", l1), ("layer2", l2)):
+        st = [x for x in launches if isinstance(x, kernels.PreparedStaged)]
+        for rep in range(3):
+            st[0]()
+        torch.cuda.synchronize()
+        buf = np.zeros((1 << 16, 4), np.uint64)
+        n = lib.dg_staged_prof_copy(buf.ctypes.data, 1 << 16)
+        b = buf[:n]
+        b = b[b[:, 3] > 0]
+        tot = b[:, :3].sum(1).astype(np.float64)
+        print(f"{name}: blocks {len(b)}  relations/block {b[:, 3].mean():.1f}  cycles/block mean {tot.mean():.0f} max {tot.max():.0f}")
+        for j, nm in enumerate(("start", "gather", "accum")):
+            print(f"   {nm:7s} mean {b[:, j].mean():10.0f}  ({100 * b[:, j].sum() / tot.sum():.1f} %)  per stage {b[:, j].mean() / b[:, 3].mean():.0f}")
+
+
+if __name__ == "__main__":
+    {"build": build, "run": run}[sys.argv[1]]()

@@ -195,3 +195,35 @@ def test_alias_table_encodes_the_unigram_distribution():
         assert np.max(np.abs(table_distribution(tab) - unigram_distribution(deg))) < 1e-7
     with pytest.raises(ValueError):
         alias_table(np.zeros(4))
+
+
+def test_staged_layout_reproduces_every_relation():
+    """The staged layout (sparse.staged_layout) holds each relation exactly: rebuilding A_k
+    from vinfo / doff / pairs gives the matrix back, with long rows split into virtual rows
+    of at most L nonzeros (at most `lanes` of them) sorted by length."""
+    import scipy.sparse as sp
+
+    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, staged_layout
+
+    rng = np.random.default_rng(3)
+    mats = [sp.random(40, 30, density=dn, random_state=int(rng.integers(1 << 30)), format="csr",
+                      dtype=np.float32) for dn in (0.3, 0.0, 0.05, 0.9)]
+    lanes = 64
+    lay = staged_layout([coo_to_csr(*sparse_to_tuple(m)) for m in mats], lanes=lanes)
+    vals = lay.pairs[:, 1].view(np.float32)
+    for k, m in enumerate(mats):
+        jm = lay.jm[lay.jmoff[k]:lay.jmoff[k + 1]]
+        n_v, rounds = jm[0], jm[1]
+        vinfo = jm[4:4 + n_v]
+        row, seg, vlen = vinfo & 1023, (vinfo >> 10) & 63, vinfo >> 16
+        maxlen = int(vlen.max()) if n_v else 0
+        doff = jm[4 + n_v:4 + n_v + maxlen + 1]
+        assert n_v <= lanes and np.all(np.diff(vlen) <= 0)     # sorted by length
+        assert rounds == (seg.max() + 1 if n_v else 0)
+        got = np.zeros((40, 30), np.float32)
+        for i in range(n_v):
+            for mm in range(vlen[i]):
+                p = doff[mm] + i
+                assert got[row[i], lay.pairs[p, 0]] == 0
+                got[row[i], lay.pairs[p, 0]] = vals[p]
+        np.testing.assert_array_equal(got, m.toarray())

@@ -305,31 +305,39 @@ def test_decoder_hinge_fused(K, n):
     assert np.array_equal(op2.neg.cpu().numpy(), op.neg.cpu().numpy())
 
 
-@pytest.mark.parametrize("slice_", [16, 32])
-@pytest.mark.parametrize("d", [32, 64])
-@pytest.mark.parametrize("n_rows,density", [(150, 0.03), (1100, 0.03), (300, 0.45)])
-def test_spmm_staged(K, slice_, d, n_rows, density):
-    """LDS-staged SpMM: relations in permuted slabs, output chunks of 5 relations, rows
-    beyond one pass, empty rows, rows longer than the per-row register prefetch."""
-    from decagon_amd.sparse import coo_to_csr, merge_chunks, sparse_to_tuple
+@pytest.mark.parametrize("d", [16, 32, 64, 40])
+@pytest.mark.parametrize("n_rows,n_cols,density,out_chunk", [
+    (150, 137, 0.03, 5),     # several relations per output chunk, empty rows
+    (1000, 137, 0.03, 7),    # rows up to the 1024-thread workgroup
+    (300, 137, 0.45, 4),     # long rows, split into segments
+    (645, 645, 0.3, 3),      # ~125k nonzeros per relation
+    (900, 50, 0.9, 2),       # 45 nonzeros per row: many segments per row
+    (64, 1024, 0.01, 23),    # widest column space, one output chunk
+])
+def test_spmm_staged(K, d, n_rows, n_cols, density, out_chunk):
+    """LDS-staged SpMM against the float64 product: relations in permuted slabs, output
+    chunks, split rows, a partial last column slice (d=40), an empty relation."""
+    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, staged_layout
 
-    rng = np.random.default_rng(slice_ + d + n_rows)
-    n_cols, nrel, total, out_chunk = 137, 23, 30, 5
+    rng = np.random.default_rng(d + n_rows + n_cols)
+    nrel, total = 23, 30
     mats = [_rand_csr(rng, n_rows, n_cols, density, empty_rows=0.1) for _ in range(nrel)]
+    mats[3] = sp.csr_matrix((n_rows, n_cols), dtype=np.float32)  # an empty relation
     slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
-    m = merge_chunks([coo_to_csr(*sparse_to_tuple(x)) for x in mats], slabs, 1, total)
+    lay = staged_layout([coo_to_csr(*sparse_to_tuple(x)) for x in mats], K.staged_order)
+    dev = K.StagedDevice.upload(lay, "cuda")
     X = rng.standard_normal((total, n_cols, d)).astype(np.float32)
     n_out = -(-nrel // out_chunk)
     out = torch.zeros((n_out, n_rows, d), device="cuda")
-    spec = K.StagedSpec(torch.from_numpy(m.rowptr).cuda(), torch.from_numpy(m.vcol).cuda(),
-                        torch.from_numpy(m.val).cuda(), torch.from_numpy(slabs).cuda(), torch.from_numpy(X).cuda(),
-                        out, n_rows, n_cols, nrel, out_chunk, d, total * n_cols, vcol_max=int(m.vcol.max()))
-    if slice_ == 32 and n_rows > 512:  # 4 passes x 128 rows: beyond one workgroup's registers
-        with pytest.raises(K._lib.KernelError if hasattr(K, "_lib") else Exception):
-            K.PreparedStaged([spec], d, slice_)()
-        return
-    K.PreparedStaged([spec], d, slice_)()
+    spec = K.StagedSpec(dev, torch.from_numpy(slabs).cuda(), torch.from_numpy(X).cuda(), out, out_chunk, d,
+                        total * n_cols, slab_max=int(slabs.max()))
+    K.PreparedStaged([spec], d)()
     want = np.zeros((n_out, n_rows, d))
     for k, x in enumerate(mats):
         want[k // out_chunk] += x @ X[slabs[k]].astype(np.float64)
     assert rel_err(out.cpu().numpy(), want) <= 1e-5
+    # bitwise reproducible
+    out2 = torch.zeros_like(out)
+    spec.out = out2
+    K.PreparedStaged([spec], d)()
+    assert torch.equal(out, out2)
