@@ -164,6 +164,104 @@ __global__ __launch_bounds__(256) void gemm_f32_resident_a(const GemmArgs args) 
     }
 }
 
+// Relation-batched projection C_b = A · B_map(b) with A shared by every batch (H_j,
+// a_bs == 0), n <= 32, K == KD, no scaling: the transposed product on the matrix pipe,
+//   D[n][m] = sum_k B[k][n] * A[m][k] = C[m][n],
+// so lane l ends with row m0 + (l&31) and columns 8q + 4(l>>5) .. +3 of it for q < 4: four
+// 16-byte stores per lane.  One wave per 32-row tile of A (its fragment in registers for the
+// block's run of batches); B_map(b) (KD×32 floats) is staged through LDS once per block and
+// batch, double-buffered, in the fragment order [n][k&1][k>>1] (rows padded by 4 floats),
+// its float4 loads issued two batches ahead and before the previous batch's stores (vmcnt
+// counts stores too: a wait for a load issued after a store would drain the store).  The
+// k-steps run in order on one accumulator: the result is bitwise a k-ordered fmaf chain.
+template <int KD>
+__global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
+    constexpr int S = KD / 2;
+    constexpr int LDW = S + 4;               // floats per (n, k&1) row of the staged B
+    constexpr int WB = 32 * 2 * LDW;         // floats per staged B buffer
+    constexpr int NF4 = KD * 8;              // float4s of one [KD][32] B
+    __shared__ float wl[2 * WB];
+    int tb, bblk;
+    const GemmOne& g = pick(args, blockIdx.x, tb, bblk);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int nw = blockDim.x >> 6;
+    const int tm = tb * nw + wave;           // this wave's 32-row tile
+    const int i = lane & 31;
+    const int h = lane >> 5;
+    const int b0 = bblk * g.batch_per_wave;
+    const int b1 = min(b0 + g.batch_per_wave, g.batch);
+    const int row = tm * 32 + i;
+    const bool row_ok = tm < g.tiles_m && row < g.m;
+
+    float hf[S];  // B operand of the transposed product: A[row][2s + h]
+    {
+        const float* A = g.a + (int64_t)row * g.a_sm;
+#pragma unroll
+        for (int s = 0; s < S; ++s) hf[s] = row_ok ? A[(2 * s + h) * g.a_sk] : 0.f;
+    }
+    // the block's batch map in one register (<= 64 batches): lane j holds map(b0 + j), read
+    // with readlane — no vector load (and no vmcnt wait, which would also drain the stores)
+    // inside the loop
+    const int bm = b0 + lane < b1 ? (g.b_map ? g.b_map[b0 + lane] : b0 + lane) : 0;
+    auto map_of = [&](int b) { return __builtin_amdgcn_readlane(bm, b - b0); };
+    // B_map(b) in float4s of [KD][32]: thread t holds float4s t and t + blockDim (blockDim >= 256)
+    float4 wr0 = make_float4(0.f, 0.f, 0.f, 0.f), wr1 = wr0;
+    auto load_b = [&](int b) {
+        const float* B = g.b + map_of(b) * g.b_bs;
+        const int f0 = threadIdx.x, f1 = threadIdx.x + blockDim.x;
+        if (f0 < NF4 && 4 * (f0 & 7) < g.n) wr0 = *reinterpret_cast<const float4*>(B + (f0 >> 3) * g.b_sk + 4 * (f0 & 7));
+        if (f1 < NF4 && 4 * (f1 & 7) < g.n) wr1 = *reinterpret_cast<const float4*>(B + (f1 >> 3) * g.b_sk + 4 * (f1 & 7));
+    };
+    auto put_b = [&](int u) {
+        float* w = wl + u * WB;
+        auto put4 = [&](int f, float4 v) {
+            if (f >= NF4) return;
+            const int k = f >> 3, n = 4 * (f & 7);
+            float* d = w + (n * 2 + (k & 1)) * LDW + (k >> 1);
+            d[0] = v.x;
+            d[2 * LDW] = v.y;
+            d[4 * LDW] = v.z;
+            d[6 * LDW] = v.w;
+        };
+        put4(threadIdx.x, wr0);
+        put4(threadIdx.x + blockDim.x, wr1);
+    };
+    if (b0 < b1) {
+        load_b(b0);
+        put_b(0);
+        if (b0 + 1 < b1) load_b(b0 + 1);
+    }
+    // iteration b: barrier | MFMAs on buffer b | B(b+1) registers -> the other buffer (its loads
+    // were issued before batch b-1's stores) | loads of B(b+2) | stores of batch b
+#pragma unroll 1
+    for (int b = b0; b < b1; ++b) {
+        __syncthreads();  // buffer (b - b0) & 1 staged; the other one is free
+        const float* w = wl + ((b - b0) & 1) * WB + (i * 2 + h) * LDW;
+        f32x16 acc = {};
+#pragma unroll
+        for (int s4 = 0; s4 < S; s4 += 4) {
+            const float4 af = *reinterpret_cast<const float4*>(w + s4);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.x, hf[s4 + 0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.y, hf[s4 + 1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.z, hf[s4 + 2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, hf[s4 + 3], acc, 0, 0, 0);
+        }
+        if (b + 1 < b1) put_b((b + 1 - b0) & 1);
+        if (b + 2 < b1) load_b(b + 2);
+        if (row_ok) {
+            float* C = g.c + map_of(b) * g.c_bs + (int64_t)row * g.c_sm;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = 8 * q + 4 * h;
+                if (n < g.n)
+                    *reinterpret_cast<float4*>(C + n) =
+                        make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stream) {
@@ -213,8 +311,41 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
         kd = (kd < 0 || kd == kk) ? kk : 0;
     }
     if (A.n == 0) return DG_OK;
-    dim3 grid(static_cast<unsigned>(blocks)), block(256);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // the projection shape (every descriptor): shared A, n <= 32 (a multiple of 4), K in
+    // {32, 64}, unscaled, C rows 16-byte aligned and contiguous
+    bool proj = kd > 0;
+    for (int i = 0; i < A.n && proj; ++i) {
+        const GemmOne& g = A.g[i];
+        proj = g.a_bs == 0 && g.n <= 32 && (g.n & 3) == 0 && !g.sa && !g.sc && g.c_sn == 1 && (g.c_sm & 3) == 0 &&
+               (g.c_bs & 3) == 0 && dg::aligned16(g.c) && g.b_sn == 1 && (g.b_sk & 3) == 0 && (g.b_bs & 3) == 0 &&
+               dg::aligned16(g.b);
+    }
+    if (proj) {
+        // waves per block: the m tiles split evenly over ceil(tiles/8) blocks (>= 4 waves)
+        int tiles_m_max = 0;
+        for (int i = 0; i < A.n; ++i) tiles_m_max = A.g[i].tiles_m > tiles_m_max ? A.g[i].tiles_m : tiles_m_max;
+        const int nbm = dg::ceil_div(tiles_m_max, 8);
+        const int wpb = dg::ceil_div(tiles_m_max, nbm) < 4 ? 4 : dg::ceil_div(tiles_m_max, nbm);
+        int64_t pblocks = 0;
+        for (int i = 0; i < A.n; ++i) {
+            GemmOne& g = A.g[i];
+            g.tile_blocks = dg::ceil_div(g.tiles_m, wpb);
+            // batches per block: about 4 blocks per CU of 256
+            int bpb = 1;
+            while (bpb < 64 && (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb * 2) >= 1024) bpb *= 2;  // <= 64: one map register
+            g.batch_per_wave = bpb;
+            g.block_begin = static_cast<int32_t>(pblocks);
+            pblocks += (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb);
+        }
+        dim3 pgrid(static_cast<unsigned>(pblocks)), pblock(64 * wpb);
+        if (kd == 64)
+            hipLaunchKernelGGL(gemm_f32_proj<64>, pgrid, pblock, 0, st, A);
+        else
+            hipLaunchKernelGGL(gemm_f32_proj<32>, pgrid, pblock, 0, st, A);
+        return dg::launch_status();
+    }
+    dim3 grid(static_cast<unsigned>(blocks)), block(256);
     if (kd == 64)
         hipLaunchKernelGGL(gemm_f32_resident_a<64>, grid, block, 0, st, A);
     else if (kd == 32)

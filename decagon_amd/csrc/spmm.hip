@@ -270,18 +270,27 @@ struct EpiArgs {
     int32_t flags;
 };
 
+// One wave per output row: LP lanes cover the row's d floats (a float4 each) and the
+// wave's CG = 64/LP lane groups split the chunks (group cg sums chunks cg, cg+CG, ... with four
+// loads in flight), combined by an xor butterfly — every lane ends with the same bits, so the
+// result is deterministic; then the L2 norm over the row's LP lanes.
 template <int LP>
 __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
-    constexpr int G = dg::kWave / LP;  // rows per wave
+    constexpr int CG = dg::kWave / LP;  // chunk groups per wave
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int sub = lane / LP;
+    const int cg = lane / LP;
     const int q = lane % LP;
-    const int r = (blockIdx.x * 4 + wave) * G + sub;
+    const int r = blockIdx.x * 4 + wave;
+    if (r >= a.n_rows) return;  // wave-uniform; no barriers
     const int d = a.d;
-    const bool active = r < a.n_rows && q * 4 < d;
+    const bool qok = q * 4 < d;
     const int64_t plane = (int64_t)a.n_rows * d;
     const int64_t off = (int64_t)r * d + q * 4;
+    const bool crelu = a.flags & DG_EPI_CHUNK_RELU;
+    auto relu4 = [](float4 v) {
+        return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+    };
 
     float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 1
@@ -289,19 +298,24 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
         const float* __restrict__ p = a.g[gi].partial + off;
         const int nc = a.g[gi].n_chunks;
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (active) {
+        if (qok) {
+            int c = cg;
 #pragma unroll 1
-            for (int c = 0; c < nc; ++c) {
-                float4 v = *reinterpret_cast<const float4*>(p + c * plane);
-                if (a.flags & DG_EPI_CHUNK_RELU) {
-                    v.x = fmaxf(v.x, 0.f);
-                    v.y = fmaxf(v.y, 0.f);
-                    v.z = fmaxf(v.z, 0.f);
-                    v.w = fmaxf(v.w, 0.f);
-                }
-                dg::add4(s, v);
+            for (; c + 3 * CG < nc; c += 4 * CG) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (c + u * CG) * plane);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) dg::add4(s, crelu ? relu4(v[u]) : v[u]);
+            }
+#pragma unroll 1
+            for (; c < nc; c += CG) {
+                const float4 v = *reinterpret_cast<const float4*>(p + c * plane);
+                dg::add4(s, crelu ? relu4(v) : v);
             }
         }
+#pragma unroll
+        for (int m = LP; m < dg::kWave; m <<= 1) dg::add4(s, dg::shfl_xor4(s, m));
         if (a.flags & DG_EPI_L2NORM) {
             // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); all-zero rows stay zero.
             float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
@@ -315,13 +329,8 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
         }
         dg::add4(tot, s);
     }
-    if (a.flags & DG_EPI_RELU) {
-        tot.x = fmaxf(tot.x, 0.f);
-        tot.y = fmaxf(tot.y, 0.f);
-        tot.z = fmaxf(tot.z, 0.f);
-        tot.w = fmaxf(tot.w, 0.f);
-    }
-    if (active) *reinterpret_cast<float4*>(a.out + off) = tot;
+    if (a.flags & DG_EPI_RELU) tot = relu4(tot);
+    if (qok && cg == 0) *reinterpret_cast<float4*>(a.out + off) = tot;
 }
 
 }  // namespace
@@ -481,8 +490,7 @@ extern "C" int dg_gcn_epilogue_f32(const dg_epi_group* groups, int32_t n_groups,
     a.d = d;
     a.flags = flags;
     const int lp = dg::lanes_per_row(d);
-    const int rows_per_block = 4 * (dg::kWave / lp);
-    dim3 grid(dg::ceil_div(n_rows, rows_per_block)), block(256);
+    dim3 grid(dg::ceil_div(n_rows, 4)), block(256);  // one wave per row
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define DG_LAUNCH_EPI(L) hipLaunchKernelGGL(epilogue_kernel<L>, grid, block, 0, st, a)
     DG_LP_SWITCH(lp, DG_LAUNCH_EPI)

@@ -196,6 +196,27 @@ def test_gemm(K, m, n, k, batch):
             assert rel_err(got, want) <= 1e-5
 
 
+@pytest.mark.parametrize("m,n,k,batch", [(645, 32, 64, 37), (100, 32, 32, 5), (33, 16, 64, 300),
+                                         (1000, 32, 64, 1)])
+def test_gemm_projection(K, m, n, k, batch):
+    """The relation-batched projection path (shared A, n <= 32, unscaled): C[bmap[b]] =
+    A · B[bmap[b]], float4 stores of the transposed MFMA product, partial row tiles."""
+    rng = np.random.default_rng(m + n + k + batch)
+    A = rng.standard_normal((m, k)).astype(np.float32)
+    B = rng.standard_normal((batch + 3, k, n)).astype(np.float32)
+    bmap = rng.permutation(batch + 3)[:batch].astype(np.int32)
+    C = torch.full((batch + 3, m, n), 7.0, device="cuda")
+    K.PreparedGemm(torch.from_numpy(A).cuda(), (0, k, 1), torch.from_numpy(B).cuda(), (k * n, n, 1), C,
+                   (m * n, n, 1), m, n, k, batch, b_map=torch.from_numpy(bmap).cuda(), b_batches=batch + 3,
+                   b_map_max=int(bmap.max()))()
+    got = C.cpu().numpy()
+    for b in range(batch):
+        want = A.astype(np.float64) @ B[bmap[b]].astype(np.float64)
+        assert rel_err(got[bmap[b]], want) <= 1e-5
+    untouched = np.setdiff1d(np.arange(batch + 3), bmap)
+    assert np.all(got[untouched] == 7.0)
+
+
 def test_gemm_transposed_strides(K):
     rng = np.random.default_rng(11)
     A = rng.standard_normal((50, 32)).astype(np.float32)
