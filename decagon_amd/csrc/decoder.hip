@@ -61,8 +61,31 @@ __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, 
     const float* u = t.row_table + (int64_t)ridx * t.ld_row;
 #pragma unroll
     for (int r = 0; r < 16; ++r) part[r] = 0.f;
+    if (d == 32) {
+        // one k-block, one n-block: every load (G, l, U row, V rows) in flight together, then
+        // the 16 MFMAs — the same k-ordered chain as the general loop below
+        float av[16], bv[16], v[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int kk = 2 * s + h;
+            bv[s] = t.G[kk * 32 + i];
+            const float a = valid ? u[kk] : 0.f;
+            av[s] = t.l ? a * t.l[kk] : a;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int prow = (r & 3) + 8 * (r >> 2) + 4 * h;
+            v[r] = t.col_table[(int64_t)__shfl(cidx, prow) * t.ld_col + i];
+        }
+        const float lj = t.l ? t.l[i] : 1.0f;
+        f32x16 acc = {};
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) part[r] = fmaf(acc[r] * lj, v[r], 0.f);
+    }
 #pragma unroll 1
-    for (int n0 = 0; n0 < d; n0 += 32) {
+    for (int n0 = 0; d != 32 && n0 < d; n0 += 32) {
         f32x16 acc = {};
 #pragma unroll 1
         for (int k0 = 0; k0 < d; k0 += 32) {

@@ -196,9 +196,14 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
 
     float hf[S];  // B operand of the transposed product: A[row][2s + h]
     {
-        const float* A = g.a + (int64_t)row * g.a_sm;
+        const int64_t a_sk = g.a_sk;  // one kernel-argument read, not one per element
+        const float* A = g.a + (int64_t)(row_ok ? row : 0) * g.a_sm + h * a_sk;
 #pragma unroll
-        for (int s = 0; s < S; ++s) hf[s] = row_ok ? A[(2 * s + h) * g.a_sk] : 0.f;
+        for (int s = 0; s < S; ++s) hf[s] = A[2 * s * a_sk];
+        if (!row_ok) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) hf[s] = 0.f;
+        }
     }
     // the block's batch map in one register (<= 64 batches): lane j holds map(b0 + j), read
     // with readlane — no vector load (and no vmcnt wait, which would also drain the stores)
@@ -331,9 +336,9 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
         for (int i = 0; i < A.n; ++i) {
             GemmOne& g = A.g[i];
             g.tile_blocks = dg::ceil_div(g.tiles_m, wpb);
-            // batches per block: about 4 blocks per CU of 256
+            // batches per block: about 2 blocks per CU of 256, amortising each wave's A fragment
             int bpb = 1;
-            while (bpb < 64 && (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb * 2) >= 1024) bpb *= 2;  // <= 64: one map register
+            while (bpb < 64 && (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb * 2) >= 512) bpb *= 2;  // <= 64: one map register
             g.batch_per_wave = bpb;
             g.block_begin = static_cast<int32_t>(pblocks);
             pblocks += (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb);

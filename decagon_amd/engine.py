@@ -48,6 +48,20 @@ def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
             and 0 < n_cols <= STAGED_MAX_COLS and 0 < n_rows <= STAGED_MAX_ROWS)
 
 
+STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "512"))  # ~2 rounds on 256 CUs
+
+
+def staged_out_chunk(grp, d: int) -> int:
+    """Relations per output chunk of a staged group for a layer of width d: a multiple of the
+    group's snake-bin size (so chunks stay balanced) giving about STAGED_TARGET_BLOCKS
+    workgroups of (chunk, 16-float slice) — one round on the chip, one LDS-full workgroup per CU."""
+    n_slices = -(-d // 16)
+    want = max(1, STAGED_TARGET_BLOCKS // n_slices)        # output chunks
+    per = max(1, -(-grp.n_rels // want))
+    oc = grp.out_chunk * max(1, -(-per // grp.out_chunk))
+    return min(oc, 64)
+
+
 def snake_bins(costs: Sequence[float], bin_size: int) -> np.ndarray:
     """An order of the items in which every run of `bin_size` consecutive items has about
     the same total cost: sort by cost, deal in snake order to ceil(n/bin_size) bins."""
@@ -96,7 +110,7 @@ class DeviceGroup:
     vcol_max: int
     rel_map: Optional[torch.Tensor] = None   # device rel_ids, when not 0..K-1
     staged: bool = False           # runs through dg_spmm_staged_f32 (layout: chunk = 1)
-    out_chunk: int = 1             # staged: relations summed per output chunk
+    out_chunk: int = 1             # staged: snake-bin size (a layer's output chunk is a multiple)
     layout: Optional["kernels.StagedDevice"] = None  # staged: the diagonal-major layout
 
     @property
@@ -329,7 +343,7 @@ class ForwardPlan:
         partials, specs, staged, reduces = {}, [], [], []
         for et in rest:
             grp = g.groups[et]
-            n_out = -(-grp.n_rels // grp.out_chunk) if grp.staged else grp.n_chunks
+            n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
             if flat is not None and n_out == 1:
                 part = views[et]  # single chunk: the SpMM writes the group sum in place
             else:
@@ -341,7 +355,7 @@ class ForwardPlan:
                 continue
             if grp.staged:
                 staged.append(kernels.StagedSpec(
-                    grp.layout, grp.rel_map, xs[et], part, grp.out_chunk, d, grp.K * grp.n_cols,
+                    grp.layout, grp.rel_map, xs[et], part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
                     slab_max=int(grp.rel_ids.max())))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
@@ -396,7 +410,7 @@ class ForwardPlan:
             tot += 4 * (grp.n_chunks * grp.n_rows + 1) + 8 * grp.nnz
             tot += 4 * d * grp.n_cols * grp.n_rels
             if et[0] not in L.fused_targets:
-                n_out = -(-grp.n_rels // grp.out_chunk) if grp.staged else grp.n_chunks
+                n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
                 tot += 4 * d * grp.n_rows * n_out
         for i in L.fused_targets:
             tot += 4 * d * self.g.n_nodes[i]
