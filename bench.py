@@ -163,7 +163,10 @@ def time_kernel(fn, reps, stream):
 
 
 KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm_groups_kernel<{lp}>",
-                "PreparedStaged": "spmm_staged_kernel<"}
+                "PreparedStaged": "spmm_staged_kernel"}
+
+
+PreparedStagedT = type(None)  # set in main() once decagon_amd is imported
 
 
 def pmc_traffic(config, launches, d):
@@ -184,7 +187,13 @@ def pmc_traffic(config, launches, d):
         hit = [v for k, v in rec.items() if k.replace("void ", "").startswith(pat)]
         if not hit or "fetch_size_kib" not in hit[0] or "write_size_kib" not in hit[0]:
             return None, src, None
-        tot += (2.0 * hit[0]["fetch_size_kib"] + hit[0]["write_size_kib"]) * 1024.0
+        e = hit[0]
+        if isinstance(l, PreparedStagedT) and e.get("by_grid"):
+            # both layers launch this kernel; layer 1 (d=64: 4 column slices) has the largest grid
+            e = e["by_grid"][max(e["by_grid"], key=int)]
+            if "fetch_size_kib" not in e or "write_size_kib" not in e:
+                return None, src, None
+        tot += (2.0 * e["fetch_size_kib"] + e["write_size_kib"]) * 1024.0
         us += hit[0].get("avg_us", 0.0)
     return tot, src, us * 1e-3
 
@@ -285,6 +294,9 @@ def main():
     k_bytes = plan.layer_bytes(1)
     achieved = k_bytes / (k_ms * 1e-3) / 1e9
     k2_ms = time_kernel(lambda: [s() for s in l2], args.kernel_reps, stream)
+    global PreparedStagedT
+    from decagon_amd.kernels import PreparedStaged
+    PreparedStagedT = PreparedStaged
     traffic, traffic_src, traffic_ms = pmc_traffic(args.config, l1, H1)
 
     if rank == 0:

@@ -24,13 +24,17 @@ def stats(d):
     return list(csv.DictReader(open(f[0])))
 
 
-def pmc(d):
+def pmc(d, by_grid=False):
+    """(kernel, counter) -> values per dispatch (or (kernel, counter, grid) with by_grid)."""
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     acc = defaultdict(list)
     if not f:
         return acc
     for r in csv.DictReader(open(f[0])):
-        acc[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+        key = (short(r["Kernel_Name"]), r["Counter_Name"])
+        if by_grid:
+            key = key + (int(r.get("Grid_Size", 0) or 0),)
+        acc[key].append(float(r["Counter_Value"]))
     return acc
 
 
@@ -39,12 +43,15 @@ def traffic_json(root, out):
     config, plus mean durations — what bench.py reads to fill roofline.traffic."""
     rec = {}
     for cfg in ("S", "P"):
-        counters = {}
+        counters, grids = {}, {}
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             counters.update(pmc(os.path.join(root, f"{cfg}_{ctr}")))
+            grids.update(pmc(os.path.join(root, f"{cfg}_{ctr}"), by_grid=True))
         kern = {}
         for (k, c), v in counters.items():
             kern.setdefault(k, {})[c.lower() + "_kib"] = sum(v) / len(v)
+        for (k, c, gsz), v in grids.items():  # one kernel launched with several grids (layers)
+            kern.setdefault(k, {}).setdefault("by_grid", {}).setdefault(str(gsz), {})[c.lower() + "_kib"] = sum(v) / len(v)
         for r in stats(os.path.join(root, f"{cfg}_trace")):
             kern.setdefault(short(r["Name"]), {})["avg_us"] = float(r["AverageNs"]) / 1e3
         rec[cfg] = kern
