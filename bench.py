@@ -52,6 +52,8 @@ def parse():
                     help="steps captured back to back in one hipGraph (must divide --steps and --warmup)")
     ap.add_argument("--target-waves", type=int, default=32768)
     ap.add_argument("--chunk", type=int, default=None)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
+                    "gloo only to exercise the multi-rank path on a single-GPU box)")
     return ap.parse_args()
 
 
@@ -231,10 +233,14 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torchrun --nproc-per-node N")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(1, torch.cuda.device_count())  # ranks share a GPU only in a gloo rehearsal
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.backend)
 
     graph, shard, scaling, workload = build_workload(args, rank, world)
     plan, dg = make_plan(args, graph, shard, device)
@@ -245,21 +251,42 @@ def main():
         dec()
 
     stream = torch.cuda.Stream(device)
-    use_graph = not args.no_graph and world == 1
-    # G complete steps per hipGraph replay (each replay runs exactly G steps, so the timed
-    # region still runs exactly --steps steps); G = 1 when it does not divide both counts
-    G = args.graph_steps if use_graph else 1
+    use_graph = not args.no_graph
+    # N = 1: G complete steps per hipGraph replay (each replay runs exactly G steps, so the
+    # timed region still runs exactly --steps steps); G = 1 when it does not divide both counts.
+    # N > 1: the compute between the two per-layer all-reduces is captured (one hipGraph per
+    # phase); the RCCL collectives run eagerly between the replays.
+    G = args.graph_steps if use_graph and world == 1 else 1
     if G < 1 or args.steps % G or args.warmup % G:
         G = 1
     with torch.cuda.stream(stream):
         step()
         stream.synchronize()
-        if use_graph:
+        if use_graph and world == 1:
             cg = torch.cuda.CUDAGraph()
             with torch.cuda.graph(cg, stream=stream):
                 for _ in range(G):
                     step()
             run = cg.replay
+        elif use_graph:
+            phases = plan.phases()
+            last = max(i for i, (kind, _) in enumerate(phases) if kind == "compute")
+            seq = []
+            for i, (kind, fn) in enumerate(phases):
+                if kind == "exchange":
+                    seq.append(fn)
+                    continue
+                body = (lambda fn=fn: (fn(), dec())) if i == last else fn
+                body()
+                stream.synchronize()
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph, stream=stream):
+                    body()
+                seq.append(gph.replay)
+
+            def run():
+                for f in seq:
+                    f()
         else:
             run = step
         for _ in range(args.warmup // G):
@@ -318,9 +345,10 @@ def main():
             "data": "synthetic: reference-normalised adjacencies (config S) / seeded generator (P); "
                     "random glorot weights",
             "config": {"workload": workload, "nnz_per_layer_total": int(tot_edges // 2),
-                       "parallelism": (f"relation-sharded x{world}, RCCL all-reduce per layer" if world > 1
-                                       else "1 GPU"),
-                       "hipgraph": use_graph, "steps_per_graph": G},
+                       "parallelism": (f"relation-sharded x{world}, "
+                                       f"{'RCCL' if args.backend == 'nccl' else args.backend} all-reduce per layer"
+                                       if world > 1 else "1 GPU"),
+                       "hipgraph": use_graph, "steps_per_graph": G if world == 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src, "traffic_profiled_kernel_ms": traffic_ms,

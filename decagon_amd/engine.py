@@ -387,6 +387,33 @@ class ForwardPlan:
         self.run_layer1()
         self.run_layer2()
 
+    def phases(self) -> List[Tuple[str, Callable[[], None]]]:
+        """The forward as alternating ("compute", fn) / ("exchange", fn) phases: the device
+        launches between two collectives form one compute phase (capturable into one
+        hipGraph), each layer's all-reduce of its pre-normalisation sums is an exchange."""
+        out: List[Tuple[str, Callable[[], None]]] = []
+        cur: List[Callable[[], None]] = []
+
+        def close():
+            if cur:
+                fns = list(cur)
+                out.append(("compute", lambda: [f() for f in fns]))
+                cur.clear()
+
+        cur.extend(self._pre)
+        for layer, before in ((self._layer1, []), (self._layer2, self._gemm2)):
+            cur.extend(before)
+            if layer.need_zero:
+                cur.append(layer.flat.zero_)
+            cur.extend(layer.launches)
+            if layer.flat is not None:
+                close()
+                flat, ar = layer.flat, layer.allreduce
+                out.append(("exchange", lambda flat=flat, ar=ar: ar(flat)))
+            cur.extend(layer.epilogues)
+        close()
+        return out
+
     @property
     def spmm_launches(self):
         """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""

@@ -42,8 +42,30 @@ def _worker(rank, world, port, q, chunk_small):
     plan = _plan(g, shard, torch.device("cuda", 0))
     plan.run()
     torch.cuda.synchronize()
-    q.put((rank, plan.hidden1[1].cpu().numpy(), plan.embeddings[0].cpu().numpy(),
-           plan.embeddings[1].cpu().numpy()))
+    eager = (plan.hidden1[1].cpu().numpy(), plan.embeddings[0].cpu().numpy(), plan.embeddings[1].cpu().numpy())
+    # the bench's N > 1 form: each compute phase captured in a hipGraph, exchanges eager
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        seq = []
+        for kind, fn in plan.phases():
+            if kind == "exchange":
+                seq.append(fn)
+                continue
+            fn()
+            stream.synchronize()
+            gph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gph, stream=stream):
+                fn()
+            seq.append(gph.replay)
+        for h in list(plan.hidden1.values()) + list(plan.embeddings.values()):
+            h.fill_(float("nan"))
+        for f in seq:
+            f()
+        stream.synchronize()
+    graphed = (plan.hidden1[1].cpu().numpy(), plan.embeddings[0].cpu().numpy(), plan.embeddings[1].cpu().numpy())
+    for x, y in zip(eager, graphed):
+        assert np.array_equal(x, y), "graph-captured phases differ from the eager forward"
+    q.put((rank,) + eager)
     dist.barrier()
     dist.destroy_process_group()
 
