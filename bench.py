@@ -43,7 +43,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["S", "P"], default="S")
+    ap.add_argument("--config", choices=["S", "P", "D"], default="S",
+                    help="S / P: the GCN forward step (metric: edges/s); D: config 5, bf16 DEDICOM "
+                         "scoring of every drug-drug slot's batch (metric: scored pairs/s)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -222,8 +224,97 @@ def cpu_baseline(graph, seconds):
                       f"{el:.1f} s, oracle/gcn_ref.c fp32 scalar, 1 thread"}
 
 
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: no sparsity)
+
+
+def main_decoder(args):
+    """Config 5 (BASELINE configs[4]): d = 256 bf16 embeddings / R / D_k, DEDICOM decoder on
+    MFMA, every one of the 1,928 drug-drug relation slots scoring B = 512 positives and 512
+    negatives drawn on the device from the degree^0.75 alias table, in one launch per step.
+    One GPU; the 8-GPU form shards the slots (no collective but the scalar loss)."""
+    import torch
+
+    from decagon_amd import kernels
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    d, n_drugs, slots, B = 256, 645, 1928, BATCH
+    rng = np.random.default_rng(5)
+    bf = torch.bfloat16
+    E = torch.from_numpy(rng.standard_normal((n_drugs, d)).astype(np.float32) / 4).to(bf).to(dev)
+    R = torch.from_numpy(glorot_stack(rng, 1, d, d)[0]).to(bf).to(dev)
+    Dk = torch.from_numpy(glorot_stack(rng, slots, d, 1).reshape(slots, d)).to(bf).to(dev)
+    n = slots * B
+    # positives: synthetic drug pairs of the P shape (uniform ids); negatives: device draws
+    rows = torch.empty(2 * n, dtype=torch.int32, device=dev)
+    rows[:n] = torch.from_numpy(rng.integers(0, n_drugs, n).astype(np.int32)).to(dev)
+    cols1 = torch.from_numpy(rng.integers(0, n_drugs, n).astype(np.int32)).to(dev)
+    cols = torch.cat([cols1, cols1])
+    rel1 = torch.arange(slots, dtype=torch.int32, device=dev).repeat_interleave(B)
+    rel = torch.cat([rel1, rel1])
+    alias = kernels.upload_alias(rng.integers(1, 200, n_drugs).astype(np.float64), dev)
+    out = torch.empty(2 * n, dtype=torch.float32, device=dev)
+    neg_rows = rows[n:]
+
+    def sample():
+        kernels.unigram_sample(alias, n, 11, 0, out=neg_rows)
+
+    def score():
+        kernels.decoder_score_bf16(E, E, rows, cols, R, Dk, rel, out=out)
+
+    def step():
+        sample()
+        score()
+
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        step()
+        stream.synchronize()
+        G = args.graph_steps if args.steps % max(1, args.graph_steps) == 0 and args.warmup % max(1, args.graph_steps) == 0 else 1
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg, stream=stream):
+            for _ in range(G):
+                step()
+        for _ in range(args.warmup // G):
+            cg.replay()
+        stream.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps // G):
+            cg.replay()
+        stream.synchronize()
+        el = time.perf_counter() - t0
+    k_ms = time_kernel(score, args.kernel_reps, stream)
+    flop_pair = 2 * d * d + 4 * d
+    tflops = 2 * n * flop_pair / (k_ms * 1e-3) / 1e12
+    rec = {
+        "metric": "DEDICOM scored pairs/sec (config 5: d=256 bf16, all 1,928 drug-drug slots)",
+        "value": 2 * n * args.steps / el,
+        "unit": "pairs/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16 (fp32 accumulation)",
+        "data": "synthetic drug pairs (uniform ids, 645 drugs), device-sampled negatives, random bf16 R / D_k",
+        "config": {"workload": f"config 5: {slots} relation slots x ({B} pos + {B} neg) pairs, d={d}, "
+                               "DEDICOM uT.D_k.R.D_k.v on v_mfma_f32_32x32x16_bf16",
+                   "pairs_per_step": 2 * n, "hipgraph": True},
+        "roofline": {"bound": "mfma", "achieved": tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tflops / BF16_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "decoder_bf16_kernel<256>", "kernel_ms": k_ms,
+                     "algorithmic_flops": 2 * n * flop_pair},
+        "cpu_baseline": None,
+    }
+    print(json.dumps(rec))
+
+
 def main():
     args = parse()
+    if args.config == "D":
+        return main_decoder(args)
     import torch
     import torch.distributed as dist
 

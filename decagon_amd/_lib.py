@@ -118,6 +118,8 @@ SIGNATURES = {
     "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_int32, c_void_p]),
     "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
     "dg_staged_order": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                        c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "dg_decoder_hinge_f32": (
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,

@@ -1,0 +1,179 @@
+// bf16 DEDICOM edge scores on gfx950's bf16 MFMA (BASELINE config 5: d = 256 bf16 embeddings
+// and parameters, fp32 accumulation, every drug-drug relation slot's positive and negative
+// batch in one launch).
+//
+// Replaces (paths relative to the reference root):
+//   DecagonOptimizer.batch_predict for DEDICOM relations     decagon/deep/optimizer.py:63-85
+//   (G = R global, L = D_k diagonal: model.py:130-134)
+//
+// For pair p of relation k = rel[p], u = row_table[row[p]], v = col_table[col[p]]:
+//     score[p] = Σ_n ( Σ_i u_i D_k[i] R[i][n] ) D_k[n] v_n         (uᵀ·D_k·R·D_k·v)
+//
+// Workgroup (1024 threads, 512 at d = 256; one per CU: Rᵀ fills LDS) keeps Rᵀ in LDS — 16-byte slots XOR-
+// swizzled by row, so the 32 lanes reading one k-slot of 32 consecutive rows hit 32 distinct
+// slots — and its 16 waves loop over tiles of 32 pairs.  A tile is the transposed product
+//     Tᵀ[n][p] = Σ_i Rᵀ[n][i] · (u_p ∘ D_k)[i]     on v_mfma_f32_32x32x16_bf16
+// (A = Rᵀ from LDS, B = the pairs' scaled rows, built in registers once per tile and reused by
+// all d/32 column tiles), so each lane ends owning ONE pair (its column p) and 16 n's of each
+// column tile: the D_k·v epilogue reads 8-byte runs of the lane's own v and D_k rows.  The
+// lane halves (n mod 8 < 4 or not) meet in one shuffle.  Pairs need not share a relation.
+#include "common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+
+__device__ __forceinline__ float bf2f(uint16_t x) { return __uint_as_float(static_cast<uint32_t>(x) << 16); }
+
+// round-to-nearest-even fp32 -> bf16 (finite inputs)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+struct Bf16DecArgs {
+    const uint16_t* row_table;
+    const uint16_t* col_table;
+    const uint16_t* R;      // [d][d] row-major (R[i][n])
+    const uint16_t* L;      // [n_rel][d] diagonals, or NULL (identity)
+    const int32_t* rows;
+    const int32_t* cols;
+    const int32_t* rel;     // per pair, or NULL (relation 0)
+    float* out;
+    int64_t ld_row, ld_col;
+    int32_t n_pairs, d;
+};
+
+// threads per workgroup: 16 waves, but 8 at d = 256 (its 16 B-operand fragments need the
+// registers of a 2-waves-per-SIMD allocation); one workgroup per CU either way (Rᵀ in LDS)
+template <int D>
+constexpr int threads_for() { return D == 256 ? 512 : 1024; }
+
+template <int D>
+__global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf16DecArgs a) {
+    constexpr int kThreads = threads_for<D>();
+    constexpr int KS = D / 16;  // k-steps of 16
+    constexpr int NT = D / 32;  // column tiles of 32
+    constexpr int SL = D / 8;   // 16-byte slots per Rᵀ row
+    extern __shared__ uint4 rt[];  // Rᵀ: row n, slot q (k = 8q .. 8q+7) at rt[n*SL + (q ^ (n % SL))]
+    const int tid = threadIdx.x;
+    // stage Rᵀ: thread handles (n, q) slots; reads R[8q + j][n], j < 8 (column gather, once)
+    for (int e = tid; e < D * SL; e += kThreads) {
+        const int n = e / SL, q = e - n * SL;
+        uint16_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a.R[(int64_t)(8 * q + j) * D + n];
+        uint4 w;
+        w.x = v[0] | (uint32_t)v[1] << 16;
+        w.y = v[2] | (uint32_t)v[3] << 16;
+        w.z = v[4] | (uint32_t)v[5] << 16;
+        w.w = v[6] | (uint32_t)v[7] << 16;
+        rt[n * SL + (q ^ (n % SL))] = w;
+    }
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int r = lane & 31;
+    const int h = lane >> 5;
+    const int n_tiles = (a.n_pairs + 31) / 32;
+    const int stride = gridDim.x * (kThreads / 64);
+#pragma unroll 1
+    for (int tile = blockIdx.x * (kThreads / 64) + wave; tile < n_tiles; tile += stride) {
+        const int p = tile * 32 + r;
+        const bool valid = p < a.n_pairs;
+        const int pr = valid ? a.rows[p] : 0;
+        const int pc = valid ? a.cols[p] : 0;
+        const int pk = (valid && a.rel) ? a.rel[p] : 0;
+        const uint16_t* u = a.row_table + (int64_t)pr * a.ld_row;
+        const uint16_t* v = a.col_table + (int64_t)pc * a.ld_col;
+        const uint16_t* lk = a.L ? a.L + (int64_t)pk * D : nullptr;
+        // B operand: (u ∘ D_k)[16s + 8h + j] in bf16, s < KS
+        bf16x8 bf[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const uint4 uu = *reinterpret_cast<const uint4*>(u + 16 * s + 8 * h);
+            uint4 ll = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
+            if (lk) ll = *reinterpret_cast<const uint4*>(lk + 16 * s + 8 * h);
+            const uint32_t uw[4] = {uu.x, uu.y, uu.z, uu.w}, lw[4] = {ll.x, ll.y, ll.z, ll.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float x0 = bf2f(uw[j] & 0xffff) * bf2f(lw[j] & 0xffff);
+                const float x1 = bf2f(uw[j] >> 16) * bf2f(lw[j] >> 16);
+                bf[s][2 * j] = valid ? (short)f2bf(x0) : (short)0;
+                bf[s][2 * j + 1] = valid ? (short)f2bf(x1) : (short)0;
+            }
+        }
+        float part = 0.f;
+#pragma unroll 1
+        for (int t = 0; t < NT; ++t) {
+            const int n = 32 * t + r;  // A-operand row of this lane
+            f32x16 acc = {};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int q = 2 * s + h;  // slot of k = 16s + 8h .. +7
+                const uint4 w = rt[n * SL + (q ^ (n % SL))];
+                bf16x8 af;
+                af[0] = (short)(w.x & 0xffff);
+                af[1] = (short)(w.x >> 16);
+                af[2] = (short)(w.y & 0xffff);
+                af[3] = (short)(w.y >> 16);
+                af[4] = (short)(w.z & 0xffff);
+                af[5] = (short)(w.z >> 16);
+                af[6] = (short)(w.w & 0xffff);
+                af[7] = (short)(w.w >> 16);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[s], acc, 0, 0, 0);
+            }
+            // lane owns pair r: acc[reg] = T[n = 32t + (reg&3) + 8(reg>>2) + 4h][p]
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = 32 * t + 8 * g + 4 * h;
+                const uint2 vv = *reinterpret_cast<const uint2*>(v + n0);
+                uint2 ll = make_uint2(0x3f803f80u, 0x3f803f80u);
+                if (lk) ll = *reinterpret_cast<const uint2*>(lk + n0);
+                part = fmaf(acc[4 * g + 0], bf2f(ll.x & 0xffff) * bf2f(vv.x & 0xffff), part);
+                part = fmaf(acc[4 * g + 1], bf2f(ll.x >> 16) * bf2f(vv.x >> 16), part);
+                part = fmaf(acc[4 * g + 2], bf2f(ll.y & 0xffff) * bf2f(vv.y & 0xffff), part);
+                part = fmaf(acc[4 * g + 3], bf2f(ll.y >> 16) * bf2f(vv.y >> 16), part);
+            }
+        }
+        part += __shfl_xor(part, 32);
+        if (h == 0 && valid) a.out[p] = part;
+    }
+}
+
+}  // namespace
+
+extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
+                                     int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
+                                     const int32_t* rel_idx, int32_t n_pairs, const uint16_t* G,
+                                     const uint16_t* l_table, int32_t d, float* out, void* stream) {
+    if (n_pairs < 0 || !row_table || !col_table || !row_idx || !col_idx || !G || !out) return DG_EINVAL;
+    if (d != 64 && d != 128 && d != 256) return DG_EINVAL;
+    if (ld_row < d || ld_col < d || (ld_row & 7) || (ld_col & 7)) return DG_EALIGN;
+    if (!dg::aligned16(row_table) || !dg::aligned16(col_table) || (l_table && !dg::aligned16(l_table)))
+        return DG_EALIGN;
+    if (n_pairs == 0) return DG_OK;
+    Bf16DecArgs a{row_table, col_table, G, l_table, row_idx, col_idx, rel_idx, out, ld_row, ld_col, n_pairs, d};
+    const int n_tiles = (n_pairs + 31) / 32;
+    const int waves = (d == 256 ? 512 : 1024) / 64;
+    int blocks = (n_tiles + waves - 1) / waves;
+    if (blocks > 256) blocks = 256;  // persistent: one Rᵀ-holding workgroup per CU
+    const int lds = d * d * 2;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    static bool configured = false;
+    if (!configured) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&decoder_bf16_kernel<256>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        configured = true;
+    }
+    if (d == 256)
+        hipLaunchKernelGGL(decoder_bf16_kernel<256>, dim3(blocks), dim3(threads_for<256>()), lds, st, a);
+    else if (d == 128)
+        hipLaunchKernelGGL(decoder_bf16_kernel<128>, dim3(blocks), dim3(threads_for<128>()), lds, st, a);
+    else
+        hipLaunchKernelGGL(decoder_bf16_kernel<64>, dim3(blocks), dim3(threads_for<64>()), lds, st, a);
+    return dg::launch_status();
+}

@@ -457,6 +457,38 @@ def decoder_score(row_table: torch.Tensor, col_table: torch.Tensor, row_idx: tor
     return out
 
 
+def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: torch.Tensor,
+                       cols: torch.Tensor, G: torch.Tensor, l_table: Optional[torch.Tensor] = None,
+                       rel: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                       stream=None) -> torch.Tensor:
+    """bf16 DEDICOM scores of pairs (rows[p], cols[p]) of relations rel[p] (dg_decoder_score_bf16):
+    uᵀ·D_k·G·D_k·v with bf16 tables / G / diagonals and fp32 accumulation (config 5)."""
+    n = rows.numel()
+    d = G.shape[0]
+    for t, nm in ((row_table, "row_table"), (col_table, "col_table"), (G, "G")):
+        _dev(t, torch.bfloat16, nm)
+    if l_table is not None:
+        _dev(l_table, torch.bfloat16, "l_table")
+        if l_table.shape[-1] != d or l_table.stride(-1) != 1 or (l_table.dim() == 2 and l_table.stride(0) != d):
+            raise ValueError("l_table must be a contiguous [n_rel, d] bf16 tensor")
+    for t, nm in ((rows, "rows"), (cols, "cols")):
+        _dev(t, torch.int32, nm)
+    if rel is not None:
+        _dev(rel, torch.int32, "rel")
+    if G.shape != (d, d) or not G.is_contiguous():
+        raise ValueError("G must be a contiguous d×d bf16 matrix")
+    if row_table.shape[1] != d or col_table.shape[1] != d or row_table.stride(1) != 1 or col_table.stride(1) != 1:
+        raise ValueError("tables must have d contiguous columns")
+    if out is None:
+        out = torch.empty(n, device=rows.device, dtype=torch.float32)
+    check(_lib.load().dg_decoder_score_bf16(
+        row_table.data_ptr(), row_table.stride(0), col_table.data_ptr(), col_table.stride(0), rows.data_ptr(),
+        cols.data_ptr(), rel.data_ptr() if rel is not None else None, n, G.data_ptr(),
+        l_table.data_ptr() if l_table is not None else None, d, out.data_ptr(), _stream_ptr(stream)),
+        "dg_decoder_score_bf16")
+    return out
+
+
 def hinge_loss(pos: torch.Tensor, neg: torch.Tensor, margin: float,
                out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
     _dev(pos, torch.float32, "pos")

@@ -239,6 +239,17 @@ int dg_decoder_score_f32(const float* row_table, int64_t ld_row, const float* co
                          int32_t n_pairs, const float* G, const float* l, int32_t d,
                          float* out, void* stream);
 
+/* bf16 DEDICOM scores (BASELINE config 5): for pair p of relation k = rel_idx[p] (rel_idx
+ * NULL: k = 0), u = row_table[row_idx[p]], v = col_table[col_idx[p]] (bf16 rows),
+ *     out[p] = sum_n ( sum_i bf16(u_i * l_k[i]) * G[i][n] ) * l_k[n] * v_n     (fp32 accumulation)
+ * G: bf16 d×d row-major (DEDICOM's global R); l_table: bf16 [n_rel][d] diagonals D_k (NULL =
+ * identity).  Pairs may mix relations.  d ∈ {64, 128, 256}; tables 16-byte aligned rows.
+ * Replaces batch_predict (optimizer.py:63-85) for DEDICOM relations (model.py:130-134). */
+int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
+                          int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
+                          const int32_t* rel_idx, int32_t n_pairs, const uint16_t* G,
+                          const uint16_t* l_table, int32_t d, float* out, void* stream);
+
 /* Fused decoder step (T8 + T9 + T11 + T12 in one launch):
  *   neg_row[b] = neg_rows[b] if neg_rows != NULL, else draw (offset + b) of the alias
  *                sampler — the same draws as dg_unigram_sample — written to neg_rows_out[b]

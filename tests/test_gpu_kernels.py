@@ -245,6 +245,36 @@ def test_decoder_score(K, d, diag):
     assert rel_err(got, want) <= 1e-5
 
 
+@pytest.mark.parametrize("d", [64, 128, 256])
+def test_decoder_score_bf16(K, d):
+    """Config 5's bf16 DEDICOM scorer against float64 on the same bf16 inputs: the kernel
+    rounds u∘D_k to bf16 (the MFMA operand) and accumulates in fp32 — tolerance 1e-4 against
+    a reference that applies the same operand rounding.  Pairs mix relations; ragged tail."""
+    rng = np.random.default_rng(d)
+    n_r, n_c, n_rel, n = 300, 200, 7, 32 * 40 + 13
+    bf = torch.bfloat16
+    E_r = torch.from_numpy(rng.standard_normal((n_r, d)).astype(np.float32)).to(bf)
+    E_c = torch.from_numpy(rng.standard_normal((n_c, d)).astype(np.float32)).to(bf)
+    R = torch.from_numpy((rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)).to(bf)
+    Dk = torch.from_numpy(rng.standard_normal((n_rel, d)).astype(np.float32)).to(bf)
+    rows = rng.integers(0, n_r, n).astype(np.int32)
+    cols = rng.integers(0, n_c, n).astype(np.int32)
+    rel = rng.integers(0, n_rel, n).astype(np.int32)
+    got = K.decoder_score_bf16(E_r.cuda(), E_c.cuda(), torch.from_numpy(rows).cuda(), torch.from_numpy(cols).cuda(),
+                               R.cuda(), Dk.cuda(), torch.from_numpy(rel).cuda()).cpu().numpy()
+    u = E_r.float().numpy()[rows]
+    v = E_c.float().numpy()[cols]
+    dk = Dk.float().numpy()[rel]
+    a = torch.from_numpy((u * dk).astype(np.float32)).to(bf).double().numpy()  # the bf16 operand
+    want = np.einsum("pi,in,pn->p", a, R.double().numpy(), dk.astype(np.float64) * v.astype(np.float64))
+    assert rel_err(got, want) <= 1e-4
+    # identity diagonal, single relation
+    got2 = K.decoder_score_bf16(E_r.cuda(), E_c.cuda(), torch.from_numpy(rows).cuda(), torch.from_numpy(cols).cuda(),
+                                R.cuda()).cpu().numpy()
+    want2 = np.einsum("pi,in,pn->p", u.astype(np.float64), R.double().numpy(), v.astype(np.float64))
+    assert rel_err(got2, want2) <= 1e-4
+
+
 def test_losses(K):
     rng = np.random.default_rng(5)
     pos = rng.standard_normal(1000).astype(np.float32)
