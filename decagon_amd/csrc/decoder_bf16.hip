@@ -9,7 +9,7 @@
 // For pair p of relation k = rel[p], u = row_table[row[p]], v = col_table[col[p]]:
 //     score[p] = Σ_n ( Σ_i u_i D_k[i] R[i][n] ) D_k[n] v_n         (uᵀ·D_k·R·D_k·v)
 //
-// Workgroup (1024 threads, 512 at d = 256; one per CU: Rᵀ fills LDS) keeps Rᵀ in LDS — 16-byte slots XOR-
+// Workgroup (1024 threads, 768 at d = 256; one per CU: Rᵀ fills LDS) keeps Rᵀ in LDS — 16-byte slots XOR-
 // swizzled by row, so the 32 lanes reading one k-slot of 32 consecutive rows hit 32 distinct
 // slots — and its 16 waves loop over tiles of 32 pairs.  A tile is the transposed product
 //     Tᵀ[n][p] = Σ_i Rᵀ[n][i] · (u_p ∘ D_k)[i]     on v_mfma_f32_32x32x16_bf16
@@ -23,15 +23,12 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 
 
-__device__ __forceinline__ float bf2f(uint16_t x) { return __uint_as_float(static_cast<uint32_t>(x) << 16); }
 
-// round-to-nearest-even fp32 -> bf16 (finite inputs)
-__device__ __forceinline__ uint16_t f2bf(float f) {
-    const uint32_t u = __float_as_uint(f);
-    return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
 struct Bf16DecArgs {
     const uint16_t* row_table;
@@ -46,10 +43,10 @@ struct Bf16DecArgs {
     int32_t n_pairs, d;
 };
 
-// threads per workgroup: 16 waves, but 8 at d = 256 (its 16 B-operand fragments need the
-// registers of a 2-waves-per-SIMD allocation); one workgroup per CU either way (Rᵀ in LDS)
+// threads per workgroup: 16 waves, but 12 at d = 256 (its 16 B-operand fragments need the
+// registers of a 3-waves-per-SIMD allocation); one workgroup per CU either way (Rᵀ in LDS)
 template <int D>
-constexpr int threads_for() { return D == 256 ? 512 : 1024; }
+constexpr int threads_for() { return D == 256 ? 768 : 1024; }
 
 template <int D>
 __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf16DecArgs a) {
@@ -98,45 +95,44 @@ __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf
             uint4 ll = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
             if (lk) ll = *reinterpret_cast<const uint4*>(lk + 16 * s + 8 * h);
             const uint32_t uw[4] = {uu.x, uu.y, uu.z, uu.w}, lw[4] = {ll.x, ll.y, ll.z, ll.w};
+            bf16v8 x;  // round-to-nearest-even by the cast (v_cvt_pk_bf16_f32)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float x0 = bf2f(uw[j] & 0xffff) * bf2f(lw[j] & 0xffff);
-                const float x1 = bf2f(uw[j] >> 16) * bf2f(lw[j] >> 16);
-                bf[s][2 * j] = valid ? (short)f2bf(x0) : (short)0;
-                bf[s][2 * j + 1] = valid ? (short)f2bf(x1) : (short)0;
+                x[2 * j] = (__bf16)(bf_lo(uw[j]) * bf_lo(lw[j]));
+                x[2 * j + 1] = (__bf16)(bf_hi(uw[j]) * bf_hi(lw[j]));
             }
+            bf[s] = valid ? __builtin_bit_cast(bf16x8, x) : bf16x8{};
         }
         float part = 0.f;
+        // two column tiles at a time: two independent accumulator chains, so each MFMA's
+        // operand read and its predecessor's result are not on one serial path
 #pragma unroll 1
-        for (int t = 0; t < NT; ++t) {
-            const int n = 32 * t + r;  // A-operand row of this lane
-            f32x16 acc = {};
+        for (int t = 0; t < NT; t += 2) {
+            const int na = 32 * t + r, nb = na + 32;  // A-operand rows of this lane
+            f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const int q = 2 * s + h;  // slot of k = 16s + 8h .. +7
-                const uint4 w = rt[n * SL + (q ^ (n % SL))];
-                bf16x8 af;
-                af[0] = (short)(w.x & 0xffff);
-                af[1] = (short)(w.x >> 16);
-                af[2] = (short)(w.y & 0xffff);
-                af[3] = (short)(w.y >> 16);
-                af[4] = (short)(w.z & 0xffff);
-                af[5] = (short)(w.z >> 16);
-                af[6] = (short)(w.w & 0xffff);
-                af[7] = (short)(w.w >> 16);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[s], acc, 0, 0, 0);
+                const uint4 wa = rt[na * SL + (q ^ (na % SL))];
+                const uint4 wb = rt[nb * SL + (q ^ (nb % SL))];
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa), bf[s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wb), bf[s], acc1, 0, 0, 0);
             }
-            // lane owns pair r: acc[reg] = T[n = 32t + (reg&3) + 8(reg>>2) + 4h][p]
+            // lane owns pair r: acc[reg] = T[n = 32t' + (reg&3) + 8(reg>>2) + 4h][p]
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n0 = 32 * t + 8 * g + 4 * h;
-                const uint2 vv = *reinterpret_cast<const uint2*>(v + n0);
-                uint2 ll = make_uint2(0x3f803f80u, 0x3f803f80u);
-                if (lk) ll = *reinterpret_cast<const uint2*>(lk + n0);
-                part = fmaf(acc[4 * g + 0], bf2f(ll.x & 0xffff) * bf2f(vv.x & 0xffff), part);
-                part = fmaf(acc[4 * g + 1], bf2f(ll.x >> 16) * bf2f(vv.x >> 16), part);
-                part = fmaf(acc[4 * g + 2], bf2f(ll.y & 0xffff) * bf2f(vv.y & 0xffff), part);
-                part = fmaf(acc[4 * g + 3], bf2f(ll.y >> 16) * bf2f(vv.y >> 16), part);
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n0 = 32 * (t + u) + 8 * g + 4 * h;
+                    const uint2 vv = *reinterpret_cast<const uint2*>(v + n0);
+                    uint2 ll = make_uint2(0x3f803f80u, 0x3f803f80u);
+                    if (lk) ll = *reinterpret_cast<const uint2*>(lk + n0);
+                    const f32x16& acc = u ? acc1 : acc0;
+                    part = fmaf(acc[4 * g + 0], bf_lo(ll.x) * bf_lo(vv.x), part);
+                    part = fmaf(acc[4 * g + 1], bf_hi(ll.x) * bf_hi(vv.x), part);
+                    part = fmaf(acc[4 * g + 2], bf_lo(ll.y) * bf_lo(vv.y), part);
+                    part = fmaf(acc[4 * g + 3], bf_hi(ll.y) * bf_hi(vv.y), part);
+                }
             }
         }
         part += __shfl_xor(part, 32);
@@ -158,7 +154,7 @@ extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, 
     if (n_pairs == 0) return DG_OK;
     Bf16DecArgs a{row_table, col_table, G, l_table, row_idx, col_idx, rel_idx, out, ld_row, ld_col, n_pairs, d};
     const int n_tiles = (n_pairs + 31) / 32;
-    const int waves = (d == 256 ? 512 : 1024) / 64;
+    const int waves = (d == 256 ? 768 : 1024) / 64;
     int blocks = (n_tiles + waves - 1) / waves;
     if (blocks > 256) blocks = 256;  // persistent: one Rᵀ-holding workgroup per CU
     const int lds = d * d * 2;
