@@ -236,22 +236,32 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
     }
     if (a.n_projs == 0) return;  // launch-uniform
     __syncthreads();
+    // every projection output (entry, relation, column) of this target in one index space, so
+    // the block's threads run a single load/fmaf chain each instead of one chain per entry
+    int total = 0;
 #pragma unroll 1
-    for (int pi = 0; pi < a.n_projs; ++pi) {
-        const ProjK& pj = a.p[pi];
-        if (pj.target != ti) continue;
-        const int dout = pj.d_out;
-        const int total = pj.n_rels * dout;
-        for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
-            const int kk = idx / dout;
-            const int c = idx - kk * dout;
-            const int rel = pj.rel_map ? pj.rel_map[kk] : kk;
-            const float* __restrict__ wcol = pj.w + (int64_t)rel * d * dout + c;
-            float acc = 0.f;
-#pragma unroll 8
-            for (int k = 0; k < d; ++k) acc = fmaf(hrow[k], wcol[(int64_t)k * dout], acc);
-            pj.out[((int64_t)rel * t.n_rows + r) * dout + c] = acc;
+    for (int pi = 0; pi < a.n_projs; ++pi)
+        if (a.p[pi].target == ti) total += a.p[pi].n_rels * a.p[pi].d_out;
+#pragma unroll 1
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+        int pi = 0, rem = idx;
+#pragma unroll 1
+        for (;; ++pi) {
+            if (a.p[pi].target != ti) continue;
+            const int n = a.p[pi].n_rels * a.p[pi].d_out;
+            if (rem < n) break;
+            rem -= n;
         }
+        const ProjK& pj = a.p[pi];
+        const int dout = pj.d_out;
+        const int kk = rem / dout;
+        const int c = rem - kk * dout;
+        const int rel = pj.rel_map ? pj.rel_map[kk] : kk;
+        const float* __restrict__ wcol = pj.w + (int64_t)rel * d * dout + c;
+        float acc = 0.f;
+#pragma unroll 8
+        for (int k = 0; k < d; ++k) acc = fmaf(hrow[k], wcol[(int64_t)k * dout], acc);
+        pj.out[((int64_t)rel * t.n_rows + r) * dout + c] = acc;
     }
 }
 
