@@ -25,6 +25,10 @@
 // the next layer's projection of the finished row.
 #include "common.h"
 
+#ifndef DG_PROJ_UNROLL
+#define DG_PROJ_UNROLL 16  // W loads per batch of the projection chain (measured: 8 → 16 −0.4 µs at S)
+#endif
+
 #define DG_LP_SWITCH(LPV, CALL)                     \
     switch (LPV) {                                  \
         case 1: CALL(1); break;                     \
@@ -259,7 +263,7 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
         const int rel = pj.rel_map ? pj.rel_map[kk] : kk;
         const float* __restrict__ wcol = pj.w + (int64_t)rel * d * dout + c;
         float acc = 0.f;
-#pragma unroll 8
+#pragma unroll DG_PROJ_UNROLL
         for (int k = 0; k < d; ++k) acc = fmaf(hrow[k], wcol[(int64_t)k * dout], acc);
         pj.out[((int64_t)rel * t.n_rows + r) * dout + c] = acc;
     }
