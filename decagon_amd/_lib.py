@@ -21,7 +21,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 11
+ABI_VERSION = 13
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -55,7 +55,7 @@ class DgStagedGroup(ctypes.Structure):
         ("n_rels", c_int32),
         ("out_chunk", c_int32),
         ("x_rows", c_int32),
-        ("reserved", c_int32),
+        ("jm_len", c_int32),
     ]
 
 

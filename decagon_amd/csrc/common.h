@@ -43,6 +43,10 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
     a.w += b.w;
 }
 
+__device__ __forceinline__ float4 shfl4(const float4& v, int src) {
+    return make_float4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+}
+
 __device__ __forceinline__ float4 shfl_xor4(const float4& v, int m) {
     return make_float4(__shfl_xor(v.x, m), __shfl_xor(v.y, m), __shfl_xor(v.z, m),
                        __shfl_xor(v.w, m));

@@ -9,22 +9,28 @@
 // and every nonzero gathers a full row.  Here a workgroup copies each relation's dense
 // operand slice into LDS once and every nonzero gathers from LDS (ds_read_b128).
 //
-// Layout (decagon_amd/sparse.py: staged_layout): per relation, rows are split into virtual
-// rows of at most L nonzeros (L the smallest leaving ≤ 1024 of them), sorted by length, and
-// the nonzeros stored diagonal-major: the m-th nonzero of every virtual row that has one, in
-// sorted order.  Thread i owns sorted virtual row i, so at diagonal m the 64 threads of a
-// wave read 64 consecutive (col, value) pairs — one coalesced 512-byte load straight from
-// global memory, prefetched four diagonals ahead in registers — and no thread walks a long
-// row while the others wait.  Each row's nonzeros are ordered on the host (layout.cpp) so the
-// 16 lanes of a ds_read_b128 group mostly gather from distinct bank slots.
+// Layout (decagon_amd/sparse.py: staged_layout): per relation, a long row becomes a group of
+// ≤ 8 equal-length segments ("virtual rows", zero-padded), groups sorted by length and kept
+// inside one 64-lane wave, and each wave's nonzeros a dense diagonal-major block [rlw][64]
+// (rlw a multiple of 4, holes zero pairs).  Thread i owns virtual row i, so at diagonal m the
+// 64 threads of a wave read 64 consecutive (col, value) pairs — one coalesced 512-byte load
+// straight from global memory at woff + 64m + lane, no table and no test, prefetched four
+// diagonals ahead in registers (the next relation's first four before the barrier).  The
+// relation tables (woff, rlw, vinfo) come from global memory a relation ahead.  Each row's
+// nonzeros are ordered on the host (layout.cpp) so the 16 lanes of a ds_read_b128 group mostly
+// gather from distinct bank slots.
 //
-// Workgroup = 1024 threads, one per (output chunk c, 16-float column slice s):
+// Workgroup = 1024 threads, one per (output chunk c, 16-float column slice s), ONE barrier per
+// relation: the slab slice X_slab(k)[:, 16s .. +16) and k's tables live in one of two LDS
+// buffers (columns 80 B apart: the bank slot of float4 j of column v is (5v+j) mod 16, plus
+// an all-zero column n_cols for padding pairs):
 //   for relation k of the chunk:
-//     barrier; the slab slice X_slab(k)[:, 16s .. +16) and k's tables (vinfo, doff), both
-//     prefetched into registers during relation k-1, → LDS (columns 80 B apart: the bank slot
-//     of float4 j of column v is (5v+j) mod 16); barrier; prefetch relation k+1's
-//     thread i: part = Σ_{m < len[i]} val · xs[col]   (pairs from global, 4 × ds_read_b128 per nonzero)
-//     acc[row[i]] += part, in rounds by segment index (a row's segments in order)
+//     [barrier: relation k-1's gathers are done, relation k's slab buffer is complete]
+//     relation k+1's slab slice (prefetched into registers during k-1) → the other buffer;
+//     prefetch relation k+2's; load relation k+1's tables
+//     thread i: part = Σ_{m < len[i]} val · xs[col]   (4 × ds_read_b128 + 16 fmaf per nonzero)
+//     a group's segments are summed in lane order by shuffles; its first lane does
+//     acc[row] += part (one writer per row per relation)
 //   out[c][r][16s .. +16) = acc[r]
 // Fixed summation order, no atomics: bitwise reproducible.
 #include "common.h"
@@ -34,7 +40,10 @@ namespace {
 constexpr int kMaxThreads = 1024;
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kMetaInts = 256;  // a chunk's tables: jm offsets (nk + 1) and slabs (nk), nk <= 64
-constexpr int kJmRegs = 3;      // jm words per thread: 4 + 1024 + (n_cols + 1) + pad <= 3 * 1024
+constexpr int kDummyRow = 1023;
+#ifdef DG_STAGED_PROF
+constexpr int kProfSlots = 6;  // per wave: barrier, put+prefetch, tables, gather, accumulate, relations
+#endif
 
 struct StagedGroupK {
     const int2* pairs;
@@ -59,22 +68,22 @@ struct StagedArgs {
     StagedGroupK g[DG_MAX_GROUPS];
     int32_t n_groups;
     int32_t d;
-    int32_t xs_f4;     // float4 slots of the slab slice (+ the zero column)
+    int32_t xs_f4;     // float4 slots of one slab buffer (+ the zero column)
     int32_t acc_f4;    // float4 slots of the accumulator
-    int32_t jm_ints;   // ints of the jm buffer
 #ifdef DG_STAGED_PROF
-    unsigned long long* prof;  // per block: [relation start, gather, accumulate, relations] cycles
+    unsigned long long* prof;  // per block, per wave: kProfSlots counters (see DG_TICK below)
 #endif
 };
 
-// float4 j = q & 3 of column v = q >> 2 of the slab slice (zero past the slice; a partial last
-// slice loads any valid float4); it lives at xs[5v + j] — columns 80 B apart, so the 16-byte
-// bank slot of float4 j of column v is (5v + j) mod 16, a bijection of v & 15 for every j
-__device__ __forceinline__ float4 slab_slot(const float* xk, int q, int n_cols, int x_ld, int col0, int d) {
-    if (q >= n_cols * 4) return make_float4(0.f, 0.f, 0.f, 0.f);
-    const int v = q >> 2;
-    const int cj = min(col0 + 4 * (q & 3), d - 4) - col0;
-    return *reinterpret_cast<const float4*>(xk + (int64_t)v * x_ld + cj);
+// offset (floats, from the slice's first column of slab row 0) of float4 j = q & 3 of column
+// v = q >> 2 of the slab slice; it lives at xs[5v + j] — columns 80 B apart, so the 16-byte
+// bank slot of float4 j of column v is (5v + j) mod 16, a bijection of v & 15 for every j.
+// Past the slice (q >= 4 n_cols) the offset is clamped to a valid float4 that put() skips, and
+// a partial last slice reads any valid float4: every prefetch load is unconditional, so the
+// compiler's vmcnt accounting needs no path-conservative waits.
+__device__ __forceinline__ int slab_off(int q, int n_cols, int x_ld, int col0, int d) {
+    const int v = min(q >> 2, n_cols - 1);
+    return __umul24(v, x_ld) + min(col0 + 4 * (q & 3), d - 4) - col0;
 }
 
 __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedArgs a) {
@@ -101,73 +110,85 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     const int k0 = c * g.out_chunk;
     const int nk = min(g.out_chunk, g.n_rels - k0);  // relations of this chunk
 
-    // LDS: xs (columns 0..n_cols-1, then the zero column n_cols) | meta | acc | jm
-    float4* xs = lds;  // at offset 0: gather addresses need no base
-    int* jof = reinterpret_cast<int*>(xs + a.xs_f4);
+    // LDS: xs[2] (columns 0..n_cols-1, then the zero column) | meta | acc
+    float4* xs0 = lds;  // buffer 0 at offset 0
+    int* jof = reinterpret_cast<int*>(xs0 + 2 * a.xs_f4);
     int* slb = jof + (nk + 1);
     float4* acc = reinterpret_cast<float4*>(jof + kMetaInts);
-    int* jm = reinterpret_cast<int*>(acc + a.acc_f4);
 
     for (int i = tid; i <= nk; i += T) jof[i] = g.jmoff[k0 + i];
     for (int i = tid; i < nk; i += T) slb[i] = g.slab ? g.slab[k0 + i] : k0 + i;
     for (int i = tid; i < n_rows * 4; i += T) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < 4) xs[n_cols * 5 + tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < 8) xs0[(tid >> 2) * a.xs_f4 + n_cols * 5 + (tid & 3)] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
 
-    // relation i's slab slice and tables into registers (T >= n_cols: 4 slots per thread)
+    // relation i's slab slice into registers (T >= n_cols: 4 slots per thread)
     float4 xr0, xr1, xr2, xr3;
-    int jr[kJmRegs];
     auto prefetch = [&](int i) {
-        const float* xk = g.x + (int64_t)slb[i] * n_cols * g.x_ld + col0;
-        xr0 = slab_slot(xk, tid, n_cols, g.x_ld, col0, d);
-        xr1 = slab_slot(xk, tid + T, n_cols, g.x_ld, col0, d);
-        xr2 = slab_slot(xk, tid + 2 * T, n_cols, g.x_ld, col0, d);
-        xr3 = slab_slot(xk, tid + 3 * T, n_cols, g.x_ld, col0, d);
-        const int j0 = jof[i], jn = jof[i + 1] - j0;
-#pragma unroll
-        for (int u = 0; u < kJmRegs; ++u) jr[u] = tid + u * T < jn ? g.jm[j0 + tid + u * T] : 0;
+        const float* xk = g.x + (int64_t)__builtin_amdgcn_readfirstlane(slb[i]) * n_cols * g.x_ld + col0;
+        xr0 = *reinterpret_cast<const float4*>(xk + slab_off(tid, n_cols, g.x_ld, col0, d));
+        xr1 = *reinterpret_cast<const float4*>(xk + slab_off(tid + T, n_cols, g.x_ld, col0, d));
+        xr2 = *reinterpret_cast<const float4*>(xk + slab_off(tid + 2 * T, n_cols, g.x_ld, col0, d));
+        xr3 = *reinterpret_cast<const float4*>(xk + slab_off(tid + 3 * T, n_cols, g.x_ld, col0, d));
+    };
+    auto put = [&](int i) {  // registers of relation i -> slab buffer i & 1
+        float4* xs = xs0 + (i & 1) * a.xs_f4;
+        const int n4 = n_cols * 4;
+        auto put4 = [&](int q, float4 v) {
+            if (q < n4) xs[(q >> 2) * 5 + (q & 3)] = v;
+        };
+        put4(tid, xr0);
+        put4(tid + T, xr1);
+        put4(tid + 2 * T, xr2);
+        put4(tid + 3 * T, xr3);
     };
     prefetch(0);
+    put(0);
+    prefetch(min(1, nk - 1));
+
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // relation i's tables, straight from global memory (L2-resident, read a relation ahead):
+    // this wave's pair block (woff, rlw diagonals), the largest group, this lane's vinfo
+    // (read unconditionally — jm ends with 1024 spare ints; used only by waves with rlw > 0)
+    auto tables = [&](int i, int& woff, int& rlw, int& big, int& vi) {
+        const int32_t* t = g.jm + __builtin_amdgcn_readfirstlane(jof[i]);
+        big = t[1];
+        woff = t[4 + wave];
+        rlw = t[20 + wave];
+        vi = t[36 + tid];
+    };
+    // the pairs of diagonals m .. m+3 of this lane: one coalesced 512-byte load per diagonal
+    auto pairs4 = [&](int base, int2 (&u)[4]) {
+        const int2* p = g.pairs + base + lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) u[q] = p[64 * q];
+    };
+    int woff, rlw, big, vi;
+    tables(0, woff, rlw, big, vi);
+    woff = __builtin_amdgcn_readfirstlane(woff);
+    rlw = __builtin_amdgcn_readfirstlane(rlw);
+    int2 un[4];
+    pairs4(woff, un);  // waves without pairs read block 0 (valid: a group has >= 256 pairs)
 
 #ifdef DG_STAGED_PROF
-    unsigned long long c_start = 0, c_gather = 0, c_acc = 0, c0 = __builtin_readcyclecounter(), c1;
+    unsigned long long c_bar = 0, c_put = 0, c_start = 0, c_gather = 0, c_acc = 0,
+                       c0 = __builtin_readcyclecounter(), c1;
 #define DG_TICK(acc_) (c1 = __builtin_readcyclecounter(), acc_ += c1 - c0, c0 = c1)
 #else
 #define DG_TICK(acc_) ((void)0)
 #endif
-    const int2 zero_pair = make_int2(n_cols, 0);  // the zero column, value 0: adds +0
 #pragma unroll 1
     for (int i = 0; i < nk; ++i) {
-        __syncthreads();  // relation i-1's gathers and accumulation are done with xs / jm
-        {
-            const int n4 = n_cols * 4;
-            auto put = [&](int q, float4 v) {
-                if (q < n4) xs[(q >> 2) * 5 + (q & 3)] = v;
-            };
-            put(tid, xr0);
-            put(tid + T, xr1);
-            put(tid + 2 * T, xr2);
-            put(tid + 3 * T, xr3);
-            const int jn = jof[i + 1] - jof[i];
-#pragma unroll
-            for (int u = 0; u < kJmRegs; ++u)
-                if (tid + u * T < jn) jm[tid + u * T] = jr[u];
-        }
-        __syncthreads();
-        const int n_virt = jm[0], rounds = jm[1];
-        const int vi = tid < n_virt ? jm[4 + tid] : 0;  // row | seg << 10 | len << 16
-        const int rl = vi >> 16;
-        const int* doff = jm + 4 + n_virt;
-        // the wave's longest virtual row is its first (sorted descending)
-        const int rlw = __builtin_amdgcn_readfirstlane(rl);
-        const int2* pr = g.pairs + tid;
-        auto pairs4 = [&](int m, int2 (&u)[4]) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) u[q] = m + q < rl ? pr[doff[m + q]] : zero_pair;
-        };
-        int2 un[4];
-        pairs4(0, un);  // issued before the next relation's prefetch: waiting for it does not
-        if (i + 1 < nk) prefetch(i + 1);  // wait for those
+        __syncthreads();  // relation i-1's gathers done; relation i's slab buffer complete
+        DG_TICK(c_bar);
+        if (i + 1 < nk) put(i + 1);       // the other buffer: last read by relation i-1
+        // unconditional (clamped) loads past the chunk's end: see slab_off
+        prefetch(min(i + 2, nk - 1));
+        DG_TICK(c_put);
+        int nwoff, nrlw, nbig, nvi;
+        tables(min(i + 1, nk - 1), nwoff, nrlw, nbig, nvi);
+        const float4* xs = xs0 + (i & 1) * a.xs_f4;
         DG_TICK(c_start);
         float4 part[4];
 #pragma unroll
@@ -177,7 +198,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
             int2 u[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) u[q] = un[q];
-            if (m + 4 < rlw) pairs4(m + 4, un);
+            if (m + 4 < rlw) pairs4(woff + 64 * (m + 4), un);
             float4 gx[4][4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -192,32 +213,52 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
                 for (int j = 0; j < 4; ++j) dg::fma4(part[j], v, gx[q][j]);
             }
         }
+        // the next relation's first diagonals: their latency hides behind the accumulation,
+        // the barrier and the slab copy
+        nwoff = __builtin_amdgcn_readfirstlane(nwoff);
+        nrlw = __builtin_amdgcn_readfirstlane(nrlw);
+        pairs4(nwoff, un);
         DG_TICK(c_gather);
-        // a row's segments meet in the accumulator in segment order, one round each
-        float4* ar = acc + (vi & 1023) * 4;
+        if (rlw > 0) {
+            // a group's segments (consecutive lanes of this wave) summed in lane order
+            const int seg = (vi >> 10) & 7, gsz = ((vi >> 13) & 7) + 1;
+            const int bg = __builtin_amdgcn_readfirstlane(big);
 #pragma unroll 1
-        for (int rd = 0; rd < rounds; ++rd) {
-            if (rl > 0 && ((vi >> 10) & 63) == rd) {
+            for (int j = 1; j < bg; ++j) {
+                float4 o[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q] = dg::shfl4(part[q], min(lane + j, 63));
+                if (seg == 0 && j < gsz) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dg::add4(part[q], o[q]);
+                }
+            }
+            const int row = vi & 1023;
+            if (seg == 0 && row != kDummyRow) {
+                float4* ar = acc + row * 4;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float4 o = ar[j];
-                    o.x += part[j].x;
-                    o.y += part[j].y;
-                    o.z += part[j].z;
-                    o.w += part[j].w;
+                    dg::add4(o, part[j]);
                     ar[j] = o;
                 }
             }
-            if (rd + 1 < rounds) __syncthreads();
         }
+        woff = nwoff;
+        rlw = nrlw;
+        big = nbig;
+        vi = nvi;
         DG_TICK(c_acc);
     }
 #ifdef DG_STAGED_PROF
-    if (tid == 0) {
-        a.prof[4 * b + 0] = c_start;
-        a.prof[4 * b + 1] = c_gather;
-        a.prof[4 * b + 2] = c_acc;
-        a.prof[4 * b + 3] = nk;
+    if (lane == 0) {
+        unsigned long long* pw = a.prof + ((int64_t)b * (kMaxThreads / 64) + (tid >> 6)) * kProfSlots;
+        pw[0] = c_bar;
+        pw[1] = c_put;
+        pw[2] = c_start;
+        pw[3] = c_gather;
+        pw[4] = c_acc;
+        pw[5] = nk;
     }
 #endif
 #undef DG_TICK
@@ -238,7 +279,7 @@ extern "C" int64_t dg_staged_prof_copy(unsigned long long* host, int64_t max_blo
     const int64_t n = dg_staged_prof_blocks < max_blocks ? dg_staged_prof_blocks : max_blocks;
     if (!dg_staged_prof_last || n <= 0) return 0;
     (void)hipDeviceSynchronize();
-    (void)hipMemcpy(host, dg_staged_prof_last, n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(host, dg_staged_prof_last, n * 16 * kProfSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost);
     return n;
 }
 #endif
@@ -254,8 +295,9 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
     int max_cols = 0, max_rows = 0;
     for (int i = 0; i < n_groups; ++i) {
         const dg_staged_group& s = groups[i];
+        if (s.jm_len < 36 + kMaxThreads) return DG_EINVAL;  // one table + the spare ints
         if (s.n_rows < 0 || s.n_cols < 0 || s.n_rels < 0 || s.out_chunk < 1 || s.out_chunk > 64) return DG_EINVAL;
-        if (s.n_rows >= kMaxThreads || s.n_cols > kMaxThreads) return DG_EINVAL;  // rows fit 10 bits
+        if (s.n_rows >= kDummyRow || s.n_cols > kMaxThreads) return DG_EINVAL;  // rows fit 10 bits
         if (s.n_rows == 0 || s.n_rels == 0) continue;
         if (!s.pairs || !s.jm || !s.jmoff || !s.x || !s.out) return DG_EINVAL;
         if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || !dg::aligned16(s.pairs) || (s.x_ld & 3) || s.x_ld < d)
@@ -287,8 +329,7 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
     const int threads = kMaxThreads;  // one thread per virtual row (staged_layout: at most 1024)
     a.xs_f4 = (max_cols + 1) * 5;     // + the zero column
     a.acc_f4 = max_rows * 4;
-    a.jm_ints = kJmRegs * kMaxThreads;
-    const int64_t lds = (int64_t)a.xs_f4 * 16 + kMetaInts * 4 + (int64_t)a.acc_f4 * 16 + (int64_t)a.jm_ints * 4;
+    const int64_t lds = 2 * (int64_t)a.xs_f4 * 16 + kMetaInts * 4 + (int64_t)a.acc_f4 * 16;
     if (lds > kLdsBytes) return DG_EINVAL;
 #ifdef DG_STAGED_PROF
     {
@@ -296,10 +337,10 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
         static int64_t have_blocks = 0;
         if (have_blocks < blocks) {
             if (buf) (void)hipFree(buf);
-            (void)hipMalloc(&buf, blocks * 4 * sizeof(unsigned long long));
+            (void)hipMalloc(&buf, blocks * 16 * kProfSlots * sizeof(unsigned long long));
             have_blocks = blocks;
         }
-        (void)hipMemset(buf, 0, blocks * 4 * sizeof(unsigned long long));
+        (void)hipMemset(buf, 0, blocks * 16 * kProfSlots * sizeof(unsigned long long));
         a.prof = buf;
         dg_staged_prof_last = buf;
         dg_staged_prof_blocks = blocks;

@@ -39,13 +39,14 @@ EdgeType = Tuple[int, int]
 # relation's 16-float column slice and the output rows' accumulators fit LDS.
 STAGED_MIN_RELS = int(os.environ.get("DG_STAGED_MIN_RELS", "32"))
 STAGED_MAX_COLS = 1024
-STAGED_MAX_ROWS = 1023
+STAGED_MAX_ROWS = 1022
 STAGED_BINS = int(os.environ.get("DG_STAGED_BINS", "128"))
 
 
 def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
     return (os.environ.get("DG_STAGED", "1") != "0" and n_rels >= STAGED_MIN_RELS
-            and 0 < n_cols <= STAGED_MAX_COLS and 0 < n_rows <= STAGED_MAX_ROWS)
+            and 0 < n_cols <= STAGED_MAX_COLS and 0 < n_rows <= STAGED_MAX_ROWS
+            and kernels.staged_lds_bytes(n_rows, n_cols) <= kernels.STAGED_LDS_BYTES)
 
 
 STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "512"))  # ~2 rounds on 256 CUs

@@ -214,12 +214,24 @@ class StagedDevice:
     n_rows: int
     n_cols: int
     n_rels: int
+    jm_len: int                   # ints in jm (tables + spare)
+    jm_end: int                   # jmoff[n_rels]
 
     @classmethod
     def upload(cls, layout, device) -> "StagedDevice":
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
         return cls(t(layout.pairs), t(layout.jm), t(layout.jmoff), layout.n_rows, layout.n_cols,
-                   len(layout.jmoff) - 1)
+                   len(layout.jmoff) - 1, layout.jm_len, int(layout.jmoff[-1]))
+
+
+STAGED_LDS_BYTES = 160 * 1024
+STAGED_JM_SPARE = 1024
+
+
+def staged_lds_bytes(n_rows: int, n_cols: int) -> int:
+    """LDS of one staged workgroup (mirrors dg_spmm_staged_f32): two slab buffers of n_cols + 1
+    columns 80 B apart, 1 KiB of chunk tables, n_rows 64-byte accumulators."""
+    return 2 * (n_cols + 1) * 80 + 1024 + n_rows * 64
 
 
 @dataclass
@@ -243,8 +255,12 @@ class StagedSpec:
             _dev(t, dt, nm)
         if L.pairs.data_ptr() % 16:
             raise ValueError("pairs must be 16-byte aligned")
-        if not (0 < L.n_rows < 1024 and 0 < L.n_cols <= 1024):
-            raise ValueError("staged groups need n_rows < 1024, n_cols <= 1024")
+        if not (0 < L.n_rows < 1023 and 0 < L.n_cols <= 1024):
+            raise ValueError("staged groups need n_rows < 1023, n_cols <= 1024")
+        if L.jm_len < L.jm_end + STAGED_JM_SPARE or L.jm.numel() < L.jm_len:
+            raise ValueError("staged jm must end with 1024 spare ints")
+        if staged_lds_bytes(L.n_rows, L.n_cols) > STAGED_LDS_BYTES:
+            raise ValueError("staged group does not fit LDS (two slab buffers + accumulators)")
         if not 1 <= self.out_chunk <= 64:
             raise ValueError("staged out_chunk must be 1..64")
         if self.slab is not None:
@@ -277,7 +293,7 @@ class PreparedStaged:
             g.out = s.out.data_ptr()
             g.x_ld = s.x_ld
             g.n_rows, g.n_cols, g.n_rels = L.n_rows, L.n_cols, L.n_rels
-            g.out_chunk, g.x_rows = s.out_chunk, s.x_rows
+            g.out_chunk, g.x_rows, g.jm_len = s.out_chunk, s.x_rows, L.jm_len
         self._keep = list(specs)
         self._arr, self._n, self.d = arr, len(specs), d
         self._fn = _lib.load().dg_spmm_staged_f32

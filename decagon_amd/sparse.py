@@ -232,18 +232,23 @@ def merge_chunks(csrs: Sequence[HostCSR], slabs: Sequence[int], chunk: int, n_sl
 class StagedLayout:
     """Device layout of a group for dg_spmm_staged_f32 (include/decagon_hip.h).
 
-    Per relation, rows longer than a segment length L are split into virtual rows of at most
-    L consecutive nonzeros (L the smallest that leaves at most `lanes` virtual rows); the
-    virtual rows are sorted by length (descending, stable) and the nonzeros stored
-    diagonal-major — the m-th nonzero of every virtual row that has one, in sorted order — so
-    thread i of a workgroup owns sorted virtual row i and a wave's pairs at diagonal m are
-    one contiguous run.
+    Per relation, a row of len nonzeros becomes a group of S = ceil(len / L) virtual rows of
+    equal length ceil(len / S) (the last padded with zero pairs: column n_cols, value 0), S <= 8,
+    L the smallest segment length leaving at most `lanes` virtual rows.  Virtual rows are
+    sorted by length (descending) with each group on consecutive lanes of one 64-lane wave
+    (dummy lanes — all zero pairs — pad where a group would straddle a wave boundary).  Lane
+    l = 64w + j owns virtual row l; wave w's pairs are a dense block [rlw_w][64] (rlw_w = its
+    longest lane rounded up to a multiple of 4, holes filled with zero pairs), so the pair of
+    lane j at diagonal m sits at woff_w + 64m + j and the kernel loads it with no table or test.
+    A group's segments are summed within the wave in lane order.
 
-      pairs [nnz + 1, 2] int32   (column, fp32 value bits), relations back to back, + 1 pad pair
-      jm    int32                per relation at jmoff[k]: [n_virt, n_rounds, 0, 0]
-                                 (n_rounds = most segments of a row), vinfo[n_virt] =
-                                 row | seg << 10 | len << 16 per sorted virtual row,
-                                 doff[maxlen + 1] (absolute pair offset of diagonal m)
+      pairs [n_pairs, 2] int32   (column, fp32 value bits), relations and waves back to back
+      jm    int32                per relation at jmoff[k]: [n_waves, largest group, 0, 0],
+                                 (then STAGED_JM_SPARE zeros ending the array)
+                                 woff[16] (absolute pair offset of each wave's block),
+                                 rlw[16] (diagonals per wave, 0 past n_waves),
+                                 vinfo[64 n_waves] = row | seg << 10 | (group size - 1) << 13 |
+                                 len << 16 (row 1023: dummy lane)
     """
 
     pairs: np.ndarray
@@ -253,14 +258,58 @@ class StagedLayout:
     n_cols: int
     nnz: int
 
+    @property
+    def jm_len(self) -> int:
+        """Ints in jm: the relation tables plus STAGED_JM_SPARE zeros (the kernel reads every
+        lane's vinfo slot unconditionally)."""
+        return len(self.jm)
+
+
+STAGED_MAX_GROUP = 8     # segments per row (3 bits of vinfo)
+STAGED_DUMMY_ROW = 1023  # vinfo row of a dummy (padding) lane
+STAGED_JM_SPARE = 1024   # zero ints ending jm
+
 
 def _segment_length(lens: np.ndarray, lanes: int) -> int:
-    """Smallest L with sum(ceil(lens / L)) <= lanes."""
+    """Smallest L >= ceil(max / 8) leaving sum(ceil(lens / L)) virtual rows, with room for
+    the padding lanes of wave boundaries, within `lanes`."""
     nnz = int(lens.sum())
-    L = max(1, -(-nnz // lanes))
-    while int((-(-lens // L)).sum()) > lanes:
+    L = max(1, -(-nnz // lanes), -(-int(lens.max()) // STAGED_MAX_GROUP))
+    budget = lanes - (STAGED_MAX_GROUP - 1) * (-(-lanes // 64))
+    floor = int((lens > 0).sum())
+    while int((-(-lens // L)).sum()) > max(budget, floor):
         L += 1
     return L
+
+
+def _place_groups(glen: np.ndarray, gsize: np.ndarray, lanes: int) -> List[Tuple[int, int]]:
+    """Lane order of groups: descending length, each group inside one 64-lane wave.  Returns
+    [(group index, or -1 for a dummy lane, length)] in lane order — a dummy pads a wave's tail
+    where the next group (of the same length) does not fit and no single of that length is
+    left to fill it."""
+    order = np.lexsort((-gsize, -glen))     # by length desc, then bigger groups first
+    out: List[Tuple[int, int]] = []
+    pos, i, n = 0, 0, len(order)
+    while i < n:
+        ln = int(glen[order[i]])
+        j = i
+        while j < n and glen[order[j]] == ln:
+            j += 1
+        multi = [int(g) for g in order[i:j] if gsize[g] > 1]
+        single = [int(g) for g in order[i:j] if gsize[g] == 1]
+        for g in multi:
+            while int(gsize[g]) > 64 - pos % 64:
+                out.append((single.pop() if single else -1, ln))
+                pos += 1
+            out.append((g, ln))
+            pos += int(gsize[g])
+        for g in single:
+            out.append((g, ln))
+            pos += 1
+        i = j
+    if pos > lanes:
+        raise ValueError("staged layout needs more than %d lanes" % lanes)
+    return out
 
 
 def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
@@ -273,53 +322,86 @@ def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
     if not csrs:
         raise ValueError("empty relation group")
     n_r, n_c = csrs[0].shape
-    if n_r >= 1024 or n_c > 1024 or lanes > 1024:
-        raise ValueError("staged groups need n_rows < 1024, n_cols <= 1024")
-    total = int(sum(c.nnz for c in csrs))
-    if total + 1 >= 2**31:
-        raise ValueError("group exceeds int32 indexing")
-    pairs = np.zeros((total + 1, 2), np.int32)
-    jm_parts, jmoff = [], [0]
+    if n_r >= STAGED_DUMMY_ROW or n_c > 1024 or lanes > 1024:
+        raise ValueError("staged groups need n_rows < 1023, n_cols <= 1024")
+    pairs_parts, jm_parts, jmoff = [], [], [0]
     base = 0
     for c in csrs:
         if c.shape != (n_r, n_c):
             raise ValueError("all relations of a group must share one shape")
         lens = np.diff(c.rowptr.astype(np.int64))
-        L = (_segment_length(lens, lanes) if split else int(lens.max())) if c.nnz else 1
-        nseg = -(-lens // L)                                   # segments per row (0: empty row)
-        vrow = np.repeat(np.arange(n_r), nseg)                 # virtual row -> row
-        vseg = np.arange(len(vrow)) - np.repeat(np.cumsum(nseg) - nseg, nseg)
-        vstart = c.rowptr[:-1].astype(np.int64)[vrow] + vseg * L
-        vlen = np.minimum(L, lens[vrow] - vseg * L)
-        n_v = len(vrow)
-        vrowptr = np.zeros(n_v + 1, np.int64)
-        np.cumsum(vlen, out=vrowptr[1:])                       # virtual CSR = same nonzero order
-        perm = np.argsort(-vlen, kind="stable")
-        rl = vlen[perm]
-        maxlen = int(rl[0]) if n_v else 0
-        cnt = n_v - np.cumsum(np.bincount(rl, minlength=maxlen + 1))[:maxlen]
-        doff = np.empty(maxlen + 1, np.int64)
-        doff[0] = base
-        np.cumsum(cnt, out=doff[1:])
-        doff[1:] += base
+        rows_nz = np.nonzero(lens)[0]
+        if len(rows_nz) > lanes:
+            raise ValueError("more nonempty rows than lanes")
+        L = (_segment_length(lens, lanes) if split else int(lens.max())) if len(rows_nz) else 1
+        while True:
+            S = -(-lens[rows_nz] // L)                        # group size per nonempty row
+            E = -(-lens[rows_nz] // np.maximum(S, 1))         # segment length (padded)
+            try:
+                placed = _place_groups(E, S, lanes)
+                break
+            except ValueError:                                # boundary padding overflowed
+                L += 1
+        # lanes in order: row, segment, group size, length, first real nonzero, real count
+        lrow, lseg, lgs, llen, lst, lcnt = [], [], [], [], [], []
+        for g, ln in placed:
+            if g < 0:
+                lrow.append(STAGED_DUMMY_ROW); lseg.append(0); lgs.append(1)
+                llen.append(ln); lst.append(0); lcnt.append(0)
+                continue
+            r, sz = int(rows_nz[g]), int(S[g])
+            r0, total_r = int(c.rowptr[r]), int(lens[r])
+            for q in range(sz):
+                lrow.append(r); lseg.append(q); lgs.append(sz); llen.append(ln)
+                lst.append(r0 + q * ln); lcnt.append(max(0, min(ln, total_r - q * ln)))
+        n_v = len(lrow)
+        n_w = -(-n_v // 64)
+        pad_l = n_w * 64 - n_v                                # dummy lanes ending the last wave
+        llen = np.asarray(llen + [0] * pad_l, np.int64)
+        lcnt = np.asarray(lcnt + [0] * pad_l, np.int64)
+        lrow = lrow + [STAGED_DUMMY_ROW] * pad_l
+        lseg = lseg + [0] * pad_l
+        lgs = lgs + [1] * pad_l
+        # wave w: a dense [rlw_w][64] block of pairs, rlw_w = its longest lane rounded up to 4
+        rlw = ((llen[::64] + 3) // 4 * 4) if n_w else np.zeros(0, np.int64)
+        woff = np.zeros(16, np.int64)
+        woff[:n_w] = base + np.concatenate([[0], np.cumsum(rlw * 64)[:-1]]) if n_w else 0
+        n_pairs = int(rlw.sum()) * 64
+        rel_pairs = np.zeros((n_pairs, 2), np.int32)
+        rel_pairs[:, 0] = n_c  # padding: the zero column, value 0
         if c.nnz:
-            inv = np.empty(n_v, np.int64)
-            inv[perm] = np.arange(n_v)
-            vr = np.repeat(np.arange(n_v), vlen)
+            # the lanes' real nonzeros as a CSR over lanes (each a contiguous piece of its row)
+            n_l = n_w * 64
+            vrowptr = np.zeros(n_l + 1, np.int64)
+            np.cumsum(lcnt, out=vrowptr[1:])
+            vr = np.repeat(np.arange(n_l), lcnt)
+            src = np.repeat(np.asarray(lst + [0] * pad_l, np.int64), lcnt) + (np.arange(len(vr)) - vrowptr[:-1][vr])
+            vcol = np.ascontiguousarray(c.col[src], np.int32)
+            vval = np.ascontiguousarray(np.asarray(c.val, np.float32)[src])
             if order is None:
-                rank = np.arange(c.nnz, dtype=np.int64) - vrowptr[:-1][vr]
+                rank = np.arange(len(src), dtype=np.int64) - vrowptr[:-1][vr]
             else:
-                vcsr = HostCSR(vrowptr.astype(np.int32), c.col, c.val, (n_v, n_c))
-                rank = np.asarray(order(vcsr, perm), np.int64)
-            dst = doff[rank] + inv[vr]
-            pairs[dst, 0] = c.col
-            pairs[dst, 1] = np.ascontiguousarray(c.val, np.float32).view(np.int32)
-        rounds = int(nseg.max()) if n_r else 0
-        vinfo = vrow[perm] | (vseg[perm] << 10) | (rl << 16)
-        seg = np.concatenate([[n_v, rounds, 0, 0], vinfo, doff]).astype(np.int64)
-        pad = (-len(seg)) % 4
-        jm_parts.append(np.concatenate([seg.astype(np.int32), np.zeros(pad, np.int32)]))
-        jmoff.append(jmoff[-1] + len(seg) + pad)
-        base += c.nnz
-    return StagedLayout(pairs, np.concatenate(jm_parts) if jm_parts else np.zeros(0, np.int32),
-                        np.asarray(jmoff, np.int32), n_r, n_c, total)
+                rank = np.asarray(order(HostCSR(vrowptr.astype(np.int32), vcol, vval, (n_l, n_c)),
+                                        np.arange(n_l)), np.int64)
+            dst = woff[vr >> 6] - base + rank * 64 + (vr & 63)
+            rel_pairs[dst, 0] = vcol
+            rel_pairs[dst, 1] = vval.view(np.int32)
+        pairs_parts.append(rel_pairs)
+        big = int(max(lgs)) if n_v else 1
+        rl16 = np.zeros(16, np.int64)
+        rl16[:n_w] = rlw
+        vinfo = (np.asarray(lrow, np.int64) | (np.asarray(lseg, np.int64) << 10)
+                 | ((np.asarray(lgs, np.int64) - 1) << 13) | (llen << 16))
+        seg = np.concatenate([[n_w, big, 0, 0], woff, rl16, vinfo]).astype(np.int64)
+        jm_parts.append(seg.astype(np.int32))
+        jmoff.append(jmoff[-1] + len(seg))
+        base += n_pairs
+    if base >= 2**31:
+        raise ValueError("group exceeds int32 indexing")
+    # at least one 4-diagonal block: waves without pairs read block 0 unconditionally
+    pairs = np.concatenate(pairs_parts) if base else np.zeros((256, 2), np.int32)
+    if not base:
+        pairs[:, 0] = n_c
+    jm = np.concatenate(jm_parts + [np.zeros(STAGED_JM_SPARE, np.int32)])
+    return StagedLayout(pairs, jm,
+                        np.asarray(jmoff, np.int32), n_r, n_c, int(sum(c.nnz for c in csrs)))

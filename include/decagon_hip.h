@@ -125,24 +125,26 @@ int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
  *
  *     out[c][r][:] = sum_{k in chunk c} sum_{p in row r of A_k} val[p] * X[slab(k)*n_cols + col[p]][:]
  *
- * Layout (built on the host by decagon_amd/sparse.py: staged_layout): per relation, rows are
- * split into virtual rows of at most L consecutive nonzeros (at most 1024 virtual rows),
- * sorted by length, and the nonzeros stored diagonal-major (the m-th nonzero of every
- * virtual row that has one, in sorted order):
- *   pairs      [nnz + 1][2] int32: (column, fp32 value bits), relations back to back, plus one
- *              padding pair; 16-byte aligned
- *   jm, jmoff  relation k's tables at jm[jmoff[k] .. jmoff[k+1]) (at most 3072 ints):
- *              [n_virt, n_rounds, 0, 0], vinfo[n_virt] = row | segment << 10 | length << 16,
- *              doff[maxlen + 1] (absolute pair offset of diagonal m)
+ * Layout (built on the host by decagon_amd/sparse.py: staged_layout): per relation, a long
+ * row becomes a group of <= 8 equal-length segments (virtual rows; padding pairs have column
+ * n_cols and value 0), at most 1024 virtual rows (16 waves of 64 lanes) sorted by length
+ * with each group inside one wave; wave w's pairs form a dense block [rlw_w][64] (rlw_w a
+ * multiple of 4; holes are padding pairs), lane j's pair at diagonal m at woff_w + 64 m + j:
+ *   pairs      [n_pairs][2] int32: (column, fp32 value bits), relations and waves back to
+ *              back; 16-byte aligned
+ *   jm, jmoff  relation k's tables at jm[jmoff[k] .. jmoff[k+1]): [n_waves, largest group,
+ *              0, 0], woff[16], rlw[16] (0 past n_waves), vinfo[64 n_waves] = row |
+ *              segment << 10 | (group size - 1) << 13 | length << 16 (row 1023: padding
+ *              lane); jm ends with 1024 spare ints (jm_len >= jmoff[n_rels] + 1024)
  * One workgroup of 1024 threads per (c, 16-float column slice); thread i owns sorted virtual
  * row i and streams its pairs from global memory (one coalesced load per wave and diagonal);
  * the slab slice is in LDS and every nonzero gathers from it; the segments of a row are
- * summed in segment order.  Requirements: n_rows < 1024; n_cols <= 1024; out_chunk <= 64;
+ * summed in segment order.  Requirements: n_rows < 1023; n_cols <= 1024; out_chunk <= 64;
  * d % 4 == 0; x, x_ld 16-byte aligned.
  * Replaces layers.py:90-92 / :114-116 for such groups.
  * -------------------------------------------------------------------------------------- */
 typedef struct dg_staged_group {
-    const int32_t* pairs;       /* device, [nnz + 1][2]                                  */
+    const int32_t* pairs;       /* device, [n_pairs][2]                                  */
     const int32_t* jm;          /* device                                                */
     const int32_t* jmoff;       /* device, [n_rels + 1]                                  */
     const int32_t* slab;        /* device, [n_rels] slab of relation k, or NULL (= k)    */
@@ -154,7 +156,7 @@ typedef struct dg_staged_group {
     int32_t n_rels;
     int32_t out_chunk;          /* relations summed into one output chunk (<= 64)        */
     int32_t x_rows;             /* rows of x addressable                                 */
-    int32_t reserved;
+    int32_t jm_len;             /* ints in jm, including the 1024 spare                  */
 } dg_staged_group;
 
 int dg_spmm_staged_f32(const dg_staged_group* groups /* HOST */, int32_t n_groups, int32_t d,

@@ -2,8 +2,9 @@
 
 Build (here):   python scripts/staged_prof.py build     -> scripts/prof_build/libdecagon_hip_prof.so
 Run (GPU box):  python scripts/staged_prof.py run [bins]
-Per workgroup: cycles waiting at the stage barrier (copies), at relation starts (slab write),
-gathering, and the stage count; printed as means over blocks for layer 1 and layer 2.
+Per wave of each workgroup: cycles at the relation barrier, filling the other buffers and
+issuing the next prefetch, reading the relation tables, gathering, and accumulating; printed
+per relation as means over blocks, one column per wave, for layer 1 and layer 2.
 """
 import ctypes
 import os
@@ -51,15 +52,18 @@ def run():
         for rep in range(3):
             st[0]()
         torch.cuda.synchronize()
-        buf = np.zeros((1 << 16, 4), np.uint64)
-        n = lib.dg_staged_prof_copy(buf.ctypes.data, 1 << 16)
+        buf = np.zeros((1 << 12, 16, 6), np.uint64)   # [block][wave][slot]
+        n = lib.dg_staged_prof_copy(buf.ctypes.data, 1 << 12)
         b = buf[:n]
-        b = b[b[:, 3] > 0]
-        tot = b[:, :3].sum(1).astype(np.float64)
-        print(f"{name}: blocks {len(b)}  relations/block {b[:, 3].mean():.1f}  cycles/block mean {tot.mean():.0f} max {tot.max():.0f}")
-        for j, nm in enumerate(("start", "gather", "accum")):
-            print(f"   {nm:7s} mean {b[:, j].mean():10.0f}  ({100 * b[:, j].sum() / tot.sum():.1f} %)  per stage {b[:, j].mean() / b[:, 3].mean():.0f}")
-
+        b = b[b[:, 0, 5] > 0].astype(np.float64)
+        nk = b[:, 0, 5].mean()
+        tot = b[:, 0, :5].sum(1)
+        print(f"{name}: blocks {len(b)}  relations/block {nk:.1f}  cycles/block mean {tot.mean():.0f} max {tot.max():.0f}")
+        names = ("barrier", "put", "tables", "gather", "accum")
+        print("   per relation, mean over blocks; columns = waves 0..15")
+        for j, nm in enumerate(names):
+            row = " ".join(f"{v:6.0f}" for v in b[:, :, j].mean(0) / nk)
+            print(f"   {nm:8s} {row}")
 
 if __name__ == "__main__":
     {"build": build, "run": run}[sys.argv[1]]()

@@ -199,31 +199,62 @@ def test_alias_table_encodes_the_unigram_distribution():
 
 def test_staged_layout_reproduces_every_relation():
     """The staged layout (sparse.staged_layout) holds each relation exactly: rebuilding A_k
-    from vinfo / doff / pairs gives the matrix back, with long rows split into virtual rows
-    of at most L nonzeros (at most `lanes` of them) sorted by length."""
+    from vinfo / woff / rlw / pairs gives the matrix back.  Long rows become groups of at most
+    8 equal-length segments (zero-column padding), groups sit on consecutive lanes of one
+    64-lane wave, lanes are sorted by length, at most `lanes` of them, and every wave's block
+    is dense: lane j's pair at diagonal m sits at woff + 64 m + j (holes are zero pairs)."""
     import scipy.sparse as sp
 
     from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, staged_layout
 
     rng = np.random.default_rng(3)
-    mats = [sp.random(40, 30, density=dn, random_state=int(rng.integers(1 << 30)), format="csr",
+    n_r, n_c = 150, 30
+    mats = [sp.random(n_r, n_c, density=dn, random_state=int(rng.integers(1 << 30)), format="csr",
                       dtype=np.float32) for dn in (0.3, 0.0, 0.05, 0.9)]
-    lanes = 64
+    lanes = 256
     lay = staged_layout([coo_to_csr(*sparse_to_tuple(m)) for m in mats], lanes=lanes)
     vals = lay.pairs[:, 1].view(np.float32)
+    covered = np.zeros(len(lay.pairs), bool)
     for k, m in enumerate(mats):
         jm = lay.jm[lay.jmoff[k]:lay.jmoff[k + 1]]
-        n_v, rounds = jm[0], jm[1]
-        vinfo = jm[4:4 + n_v]
-        row, seg, vlen = vinfo & 1023, (vinfo >> 10) & 63, vinfo >> 16
-        maxlen = int(vlen.max()) if n_v else 0
-        doff = jm[4 + n_v:4 + n_v + maxlen + 1]
-        assert n_v <= lanes and np.all(np.diff(vlen) <= 0)     # sorted by length
-        assert rounds == (seg.max() + 1 if n_v else 0)
-        got = np.zeros((40, 30), np.float32)
-        for i in range(n_v):
-            for mm in range(vlen[i]):
-                p = doff[mm] + i
-                assert got[row[i], lay.pairs[p, 0]] == 0
-                got[row[i], lay.pairs[p, 0]] = vals[p]
+        n_w, big = int(jm[0]), int(jm[1])
+        woff, rlw = jm[4:20].astype(np.int64), jm[20:36].astype(np.int64)
+        vinfo = jm[36:].astype(np.int64)
+        assert len(vinfo) == 64 * n_w and 64 * n_w <= lanes
+        assert np.all(rlw[n_w:] == 0) and np.all(rlw % 4 == 0)
+        row, seg, gsz, vlen = vinfo & 1023, (vinfo >> 10) & 7, ((vinfo >> 13) & 7) + 1, vinfo >> 16
+        assert np.all(np.diff(vlen) <= 0)                                 # sorted by length
+        assert big == (gsz.max() if n_w else 1)
+        for i in range(64 * n_w):                                         # groups inside a wave
+            if row[i] != 1023 and seg[i] == 0:
+                assert i // 64 == (i + gsz[i] - 1) // 64
+                assert np.all(row[i:i + gsz[i]] == row[i]) and np.all(seg[i:i + gsz[i]] == np.arange(gsz[i]))
+        got = np.zeros((n_r, n_c), np.float64)
+        for w in range(n_w):
+            assert woff[w] % 64 == 0 and vlen[64 * w] <= rlw[w]
+            blk = slice(woff[w], woff[w] + 64 * rlw[w])
+            assert not covered[blk].any()
+            covered[blk] = True
+            for j in range(64):
+                i = 64 * w + j
+                for mm in range(rlw[w]):
+                    p = woff[w] + 64 * mm + j
+                    c = lay.pairs[p, 0]
+                    if c == n_c:
+                        assert vals[p] == 0.0                             # padding pair
+                        continue
+                    assert mm < vlen[i] and row[i] != 1023 and got[row[i], c] == 0
+                    got[row[i], c] = vals[p]
         np.testing.assert_array_equal(got, m.toarray())
+    assert covered.all()
+
+
+def test_stageable_respects_the_lds_budget():
+    """The engine only stages groups whose two slab buffers, accumulators and relation
+    tables fit one workgroup's LDS (the launcher refuses the rest with DG_EINVAL)."""
+    from decagon_amd import engine, kernels
+    assert engine.stageable(1928, 645, 645)                   # polypharmacy drug x drug
+    assert kernels.staged_lds_bytes(645, 645) <= kernels.STAGED_LDS_BYTES
+    assert not engine.stageable(64, 64, 1024)                 # slabs alone overflow
+    assert not engine.stageable(64, 1023, 16)                 # rows beyond the 10-bit row id
+    assert not engine.stageable(8, 645, 645)                  # too few relations to pay off

@@ -363,7 +363,7 @@ def test_decoder_hinge_fused(K, n):
     (300, 137, 0.45, 4),     # long rows, split into segments
     (645, 645, 0.3, 3),      # ~125k nonzeros per relation
     (900, 50, 0.9, 2),       # 45 nonzeros per row: many segments per row
-    (64, 1024, 0.01, 23),    # widest column space, one output chunk
+    (64, 880, 0.01, 23),     # widest column space that fits LDS at 64 rows, one output chunk
 ])
 def test_spmm_staged(K, d, n_rows, n_cols, density, out_chunk):
     """LDS-staged SpMM against the float64 product: relations in permuted slabs, output
