@@ -75,15 +75,23 @@ struct StagedArgs {
 #endif
 };
 
-// offset (floats, from the slice's first column of slab row 0) of float4 j = q & 3 of column
-// v = q >> 2 of the slab slice; it lives at xs[5v + j] — columns 80 B apart, so the 16-byte
-// bank slot of float4 j of column v is (5v + j) mod 16, a bijection of v & 15 for every j.
-// Past the slice (q >= 4 n_cols) the offset is clamped to a valid float4 that put() skips, and
-// a partial last slice reads any valid float4: every prefetch load is unconditional, so the
-// compiler's vmcnt accounting needs no path-conservative waits.
-__device__ __forceinline__ int slab_off(int q, int n_cols, int x_ld, int col0, int d) {
-    const int v = min(q >> 2, n_cols - 1);
-    return __umul24(v, x_ld) + min(col0 + 4 * (q & 3), d - 4) - col0;
+// Async global->LDS copy of 16 bytes per lane (global_load_lds_dwordx4): lane t's float4 at
+// base + voff lands at LDS byte lds + 16 t.  Inline asm, so the compiler neither tracks it
+// nor drains it with vmcnt(0) at the next global-load use or barrier (cdna_hip_programming.md
+// "Pipelining across barriers"): the kernel retires it with a counted s_waitcnt itself.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16(const float* base, uint32_t voff, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :: "v"(voff), "s"(base), "s"(lds) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// Relation barrier: this wave's slab copies are retired (every VMEM op but the last four —
+// the next relation's first pair loads, always issued last — is complete) and its LDS ops
+// are done; then s_barrier.
+__device__ __forceinline__ void relation_barrier() {
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedArgs a) {
@@ -109,6 +117,8 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     const int n_cols = g.n_cols;
     const int k0 = c * g.out_chunk;
     const int nk = min(g.out_chunk, g.n_rels - k0);  // relations of this chunk
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     // LDS: xs[2] (columns 0..n_cols-1, then the zero column) | meta | acc
     float4* xs0 = lds;  // buffer 0 at offset 0
@@ -122,32 +132,24 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     if (tid < 8) xs0[(tid >> 2) * a.xs_f4 + n_cols * 5 + (tid & 3)] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
 
-    // relation i's slab slice into registers (T >= n_cols: 4 slots per thread)
-    float4 xr0, xr1, xr2, xr3;
-    auto prefetch = [&](int i) {
+    // relation i's slab slice -> buffer i & 1 by glds: slot q of the buffer (column v = q / 5,
+    // float4 j = q mod 5, j = 4 the pad slot: any valid source) — columns 80 B apart, so the
+    // 16-byte bank slot of float4 j of column v is (5v + j) mod 16, a bijection of v & 15 for
+    // every j.  Wave w copies slots 64(w + 16r) .. +63; the zero column is never written.
+    const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xs0));
+    auto slab_copy = [&](int i) {
         const float* xk = g.x + (int64_t)__builtin_amdgcn_readfirstlane(slb[i]) * n_cols * g.x_ld + col0;
-        xr0 = *reinterpret_cast<const float4*>(xk + slab_off(tid, n_cols, g.x_ld, col0, d));
-        xr1 = *reinterpret_cast<const float4*>(xk + slab_off(tid + T, n_cols, g.x_ld, col0, d));
-        xr2 = *reinterpret_cast<const float4*>(xk + slab_off(tid + 2 * T, n_cols, g.x_ld, col0, d));
-        xr3 = *reinterpret_cast<const float4*>(xk + slab_off(tid + 3 * T, n_cols, g.x_ld, col0, d));
+        const uint32_t dst = lds0 + (i & 1) * a.xs_f4 * 16;
+        const int n5 = n_cols * 5;
+#pragma unroll 1
+        for (int q0 = 64 * wave; q0 < n5; q0 += 64 * 16) {
+            const int q = q0 + lane;
+            const int v = (q * 52429) >> 18;  // q / 5 (q < 5120)
+            const int j = min(q - 5 * v, 3);
+            const int off = __umul24(v, g.x_ld) + min(col0 + 4 * j, d - 4) - col0;
+            if (q < n5) glds16(xk, off * 4, dst + q0 * 16);
+        }
     };
-    auto put = [&](int i) {  // registers of relation i -> slab buffer i & 1
-        float4* xs = xs0 + (i & 1) * a.xs_f4;
-        const int n4 = n_cols * 4;
-        auto put4 = [&](int q, float4 v) {
-            if (q < n4) xs[(q >> 2) * 5 + (q & 3)] = v;
-        };
-        put4(tid, xr0);
-        put4(tid + T, xr1);
-        put4(tid + 2 * T, xr2);
-        put4(tid + 3 * T, xr3);
-    };
-    prefetch(0);
-    put(0);
-    prefetch(min(1, nk - 1));
-
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // relation i's tables, straight from global memory (L2-resident, read a relation ahead):
     // this wave's pair block (woff, rlw diagonals), the largest group, this lane's vinfo
     // (read unconditionally — jm ends with 1024 spare ints; used only by waves with rlw > 0)
@@ -159,18 +161,49 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         vi = t[36 + tid];
     };
     // the pairs of diagonals m .. m+3 of this lane: one coalesced 512-byte load per diagonal
+    // (waves without pairs read block 0: a group has >= 256 pairs)
     auto pairs4 = [&](int base, int2 (&u)[4]) {
         const int2* p = g.pairs + base + lane;
 #pragma unroll
         for (int q = 0; q < 4; ++q) u[q] = p[64 * q];
     };
+    // a finished relation's sums into the accumulators: a group's segments (consecutive lanes
+    // of this wave) summed in lane order by shuffles, then its first lane adds the row
+    auto accumulate = [&](float4 (&part)[4], int vi, int big) {
+        const int seg = (vi >> 10) & 7, gsz = ((vi >> 13) & 7) + 1;
+#pragma unroll 1
+        for (int j = 1; j < big; ++j) {
+            float4 o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = dg::shfl4(part[q], min(lane + j, 63));
+            if (seg == 0 && j < gsz) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dg::add4(part[q], o[q]);
+            }
+        }
+        const int row = vi & 1023;
+        if (seg == 0 && row != kDummyRow) {
+            float4* ar = acc + row * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float4 o = ar[j];
+                dg::add4(o, part[j]);
+                ar[j] = o;
+            }
+        }
+    };
+
+    slab_copy(0);
     int woff, rlw, big, vi;
     tables(0, woff, rlw, big, vi);
     woff = __builtin_amdgcn_readfirstlane(woff);
     rlw = __builtin_amdgcn_readfirstlane(rlw);
     int2 un[4];
-    pairs4(woff, un);  // waves without pairs read block 0 (valid: a group has >= 256 pairs)
+    pairs4(woff, un);
+    relation_barrier();  // slab 0 complete
 
+    float4 part[4];
+    int pvi = 0, pbig = 1, prlw = 0;  // the previous relation's lane info (none yet)
 #ifdef DG_STAGED_PROF
     unsigned long long c_bar = 0, c_put = 0, c_start = 0, c_gather = 0, c_acc = 0,
                        c0 = __builtin_readcyclecounter(), c1;
@@ -180,17 +213,19 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
 #endif
 #pragma unroll 1
     for (int i = 0; i < nk; ++i) {
-        __syncthreads();  // relation i-1's gathers done; relation i's slab buffer complete
-        DG_TICK(c_bar);
-        if (i + 1 < nk) put(i + 1);       // the other buffer: last read by relation i-1
-        // unconditional (clamped) loads past the chunk's end: see slab_off
-        prefetch(min(i + 2, nk - 1));
+        // relation i-1's sums (deferred past the barrier: they cover un's latency)
+        if (prlw > 0) accumulate(part, pvi, __builtin_amdgcn_readfirstlane(pbig));
+        DG_TICK(c_acc);
+        // un (relation i's first diagonals) must arrive before the slab copy is queued behind
+        // it: vmcnt retires in order
+        asm volatile("" :: "v"(un[0].x), "v"(un[0].y), "v"(un[1].x), "v"(un[1].y), "v"(un[2].x),
+                     "v"(un[2].y), "v"(un[3].x), "v"(un[3].y));
+        if (i + 1 < nk) slab_copy(i + 1);  // the other buffer: last read by relation i-1
         DG_TICK(c_put);
         int nwoff, nrlw, nbig, nvi;
         tables(min(i + 1, nk - 1), nwoff, nrlw, nbig, nvi);
         const float4* xs = xs0 + (i & 1) * a.xs_f4;
         DG_TICK(c_start);
-        float4 part[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) part[j] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 1
@@ -213,43 +248,20 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
                 for (int j = 0; j < 4; ++j) dg::fma4(part[j], v, gx[q][j]);
             }
         }
-        // the next relation's first diagonals: their latency hides behind the accumulation,
-        // the barrier and the slab copy
-        nwoff = __builtin_amdgcn_readfirstlane(nwoff);
-        nrlw = __builtin_amdgcn_readfirstlane(nrlw);
-        pairs4(nwoff, un);
         DG_TICK(c_gather);
-        if (rlw > 0) {
-            // a group's segments (consecutive lanes of this wave) summed in lane order
-            const int seg = (vi >> 10) & 7, gsz = ((vi >> 13) & 7) + 1;
-            const int bg = __builtin_amdgcn_readfirstlane(big);
-#pragma unroll 1
-            for (int j = 1; j < bg; ++j) {
-                float4 o[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] = dg::shfl4(part[q], min(lane + j, 63));
-                if (seg == 0 && j < gsz) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) dg::add4(part[q], o[q]);
-                }
-            }
-            const int row = vi & 1023;
-            if (seg == 0 && row != kDummyRow) {
-                float4* ar = acc + row * 4;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float4 o = ar[j];
-                    dg::add4(o, part[j]);
-                    ar[j] = o;
-                }
-            }
-        }
-        woff = nwoff;
-        rlw = nrlw;
+        pvi = vi;
+        pbig = big;
+        prlw = rlw;
+        woff = __builtin_amdgcn_readfirstlane(nwoff);
+        rlw = __builtin_amdgcn_readfirstlane(nrlw);
         big = nbig;
         vi = nvi;
-        DG_TICK(c_acc);
+        // the next relation's first diagonals: the last VMEM ops before the barrier
+        pairs4(woff, un);
+        relation_barrier();  // relation i's gathers done; slab i+1 complete
+        DG_TICK(c_bar);
     }
+    if (prlw > 0) accumulate(part, pvi, __builtin_amdgcn_readfirstlane(pbig));
 #ifdef DG_STAGED_PROF
     if (lane == 0) {
         unsigned long long* pw = a.prof + ((int64_t)b * (kMaxThreads / 64) + (tid >> 6)) * kProfSlots;
