@@ -34,6 +34,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "GCN-layer edges/sec + achieved HBM GB/s, 5-relation synthetic, 1/2/4/8 GPU"
+JSON_OUT = sys.stdout
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md §Chip-level parameters)
 H1, H2, BATCH, MARGIN = 64, 32, 512, 0.1
 
@@ -54,6 +55,12 @@ def parse():
                     help="steps captured back to back in one hipGraph (must divide --steps and --warmup)")
     ap.add_argument("--target-waves", type=int, default=32768)
     ap.add_argument("--chunk", type=int, default=None)
+    ap.add_argument("--force-shard", action="store_true",
+                    help="run the relation-sharded (N > 1) plan and its collectives even at N = 1 "
+                         "(launch under torchrun: a rehearsal of the multi-GPU step on one GPU)")
+    ap.add_argument("--collectives", choices=["graph", "eager"], default="graph",
+                    help="N > 1 over RCCL: capture the whole step, all-reduces included, in one "
+                         "hipGraph (graph), or replay the compute phases between eager collectives")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                     "gloo only to exercise the multi-rank path on a single-GPU box)")
     return ap.parse_args()
@@ -64,24 +71,24 @@ def glorot_stack(rng, k, d_in, d_out):
     return rng.uniform(-r, r, size=(k, d_in, d_out)).astype(np.float32)
 
 
-def build_workload(args, rank, world):
+def build_workload(args, rank, world, sharded):
     import torch
 
     from decagon_amd import synthetic
     from decagon_amd.sharding import RelationShard, torch_allreduce
 
-    allreduce = torch_allreduce() if world > 1 else None
+    allreduce = torch_allreduce() if sharded else None
     if args.config == "S":
         base = synthetic.load_S()
         graph = synthetic.replicate_sets(base, world) if world > 1 else base
-        shard = RelationShard.blocks(base.edge_types, rank, world, allreduce) if world > 1 else None
+        shard = RelationShard.blocks(base.edge_types, rank, world, allreduce) if sharded else None
         scaling = "weak"
         workload = ("S: main.py 5-relation / 10-matrix synthetic (reference-normalised, 105,974 nnz "
                     "per relation set), 2 GCN layers d=64/32 + DEDICOM decoder B=512+512")
     else:
         graph = synthetic.make_P(seed=0)
         shard = None
-        if world > 1:
+        if sharded:
             nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
             shard = RelationShard.lpt(graph.edge_types, nnz, rank, world, allreduce)
         scaling = "strong"
@@ -308,11 +315,16 @@ def main_decoder(args):
                      "algorithmic_flops": 2 * n * flop_pair},
         "cpu_baseline": None,
     }
-    print(json.dumps(rec))
+    print(json.dumps(rec), file=JSON_OUT, flush=True)
 
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line: libraries that print to fd 1 (RCCL prints its
+    # version banner at communicator init) are sent to stderr instead
+    global JSON_OUT
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if args.config == "D":
         return main_decoder(args)
     import torch
@@ -327,13 +339,14 @@ def main():
     dev_index = local_rank % max(1, torch.cuda.device_count())  # ranks share a GPU only in a gloo rehearsal
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    if world > 1:
+    sharded = world > 1 or args.force_shard
+    if sharded:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.backend)
 
-    graph, shard, scaling, workload = build_workload(args, rank, world)
+    graph, shard, scaling, workload = build_workload(args, rank, world, sharded)
     plan, dg = make_plan(args, graph, shard, device)
     dec = Decoder(graph, plan, device, rank)
 
@@ -343,23 +356,38 @@ def main():
 
     stream = torch.cuda.Stream(device)
     use_graph = not args.no_graph
-    # N = 1: G complete steps per hipGraph replay (each replay runs exactly G steps, so the
-    # timed region still runs exactly --steps steps); G = 1 when it does not divide both counts.
-    # N > 1: the compute between the two per-layer all-reduces is captured (one hipGraph per
-    # phase); the RCCL collectives run eagerly between the replays.
-    G = args.graph_steps if use_graph and world == 1 else 1
+    # One GPU, or N > 1 over RCCL (--collectives graph): G complete steps per hipGraph replay,
+    # the per-layer all-reduces captured with the compute (each replay runs exactly G steps, so
+    # the timed region still runs exactly --steps steps; G = 1 when it does not divide both
+    # counts).  Otherwise (gloo, or --collectives eager): the compute between the two per-layer
+    # all-reduces is captured (one hipGraph per phase) and the collectives run eagerly between
+    # the replays.
+    full = use_graph and (not sharded or (args.backend == "nccl" and args.collectives == "graph"))
+    G = args.graph_steps if full else 1
     if G < 1 or args.steps % G or args.warmup % G:
         G = 1
+    mode = "eager"
     with torch.cuda.stream(stream):
         step()
         stream.synchronize()
-        if use_graph and world == 1:
-            cg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(cg, stream=stream):
-                for _ in range(G):
-                    step()
-            run = cg.replay
-        elif use_graph:
+        if sharded:
+            dist.barrier()
+        run = step
+        if full:
+            try:
+                cg = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(cg, stream=stream):
+                    for _ in range(G):
+                        step()
+                run = cg.replay
+                mode = "one hipGraph per %d steps%s" % (G, ", all-reduces captured" if sharded else "")
+            except RuntimeError as e:  # a collective that refuses capture: per-phase graphs
+                if not sharded:
+                    raise
+                print(f"bench: capturing the all-reduces failed ({e}); eager collectives", file=sys.stderr)
+                torch.cuda.synchronize()
+                full, G = False, 1
+        if not full and use_graph:
             phases = plan.phases()
             last = max(i for i, (kind, _) in enumerate(phases) if kind == "compute")
             seq = []
@@ -378,12 +406,11 @@ def main():
             def run():
                 for f in seq:
                     f()
-        else:
-            run = step
+            mode = "hipGraph per compute phase, eager collectives"
         for _ in range(args.warmup // G):
             run()
         stream.synchronize()
-        if world > 1:
+        if sharded:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -391,14 +418,14 @@ def main():
             run()
         stream.synchronize()
         torch.cuda.synchronize()
-        if world > 1:
+        if sharded:
             dist.barrier()
         el = time.perf_counter() - t0
 
     local_edges = 2 * dg.total_nnz
     el_max = el
     tot_edges = local_edges
-    if world > 1:
+    if sharded:
         t = torch.tensor([el, float(local_edges)], dtype=torch.float64, device=device)
         tm = t.clone()
         dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
@@ -438,8 +465,8 @@ def main():
             "config": {"workload": workload, "nnz_per_layer_total": int(tot_edges // 2),
                        "parallelism": (f"relation-sharded x{world}, "
                                        f"{'RCCL' if args.backend == 'nccl' else args.backend} all-reduce per layer"
-                                       if world > 1 else "1 GPU"),
-                       "hipgraph": use_graph, "steps_per_graph": G if world == 1 else None},
+                                       if sharded else "1 GPU"),
+                       "hipgraph": use_graph, "launch": mode, "steps_per_graph": G},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src, "traffic_profiled_kernel_ms": traffic_ms,
@@ -450,8 +477,8 @@ def main():
             "spmm_layer1_edges_per_s": dg.total_nnz / (k_ms * 1e-3),
             "cpu_baseline": cpu,
         }
-        print(json.dumps(rec))
-    if world > 1:
+        print(json.dumps(rec), file=JSON_OUT, flush=True)
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -264,8 +264,11 @@ class ForwardPlan:
         rels_from: Dict[int, int] = {}
         for et in self.edge_types:
             rels_from[et[1]] = rels_from.get(et[1], 0) + dgraph.groups[et].n_rels
+        # layer-1 rows finished by a fused launch (the SpMM one, or — sharded — the one that
+        # finishes the all-reduced sums) project themselves onto the layer-2 relations
+        finished = set(self.targets) if allreduce is not None else set(self.fused)
         proj_fused = [et for et in self.edge_types
-                      if dgraph.groups[et].n_rels and et[1] in self.fused
+                      if dgraph.groups[et].n_rels and et[1] in finished
                       and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS]
         if len(proj_fused) > DG_MAX_GROUPS:
             proj_fused = []
@@ -367,12 +370,39 @@ class ForwardPlan:
         launches += reduces
         need_zero = flat is not None and any(g.groups[et].n_rels == 0 for et in rest)
         epis = []
-        for i in self.targets:
-            if i in fused_t:
-                continue
-            src = [(views[et], 1) if flat is not None else partials[et] for et in self.targets[i]]
-            epis.append(kernels.PreparedEpilogue(src, outs[i], n[i], d, flags))
+        if flat is not None:
+            # sharded: the all-reduced group sums S_ij are finished by ONE fused launch over
+            # identity "adjacencies" (row r gathers S_ij[r] with weight 1.0f: exact), so the
+            # l2norm, Σ_j, relu and (layer 1) the layer-2 projections of every node type run in
+            # one kernel after the exchange
+            tl = [i for i in self.targets]
+            pspecs = []
+            for tgt_node, pj in projs:
+                pj.target = tl.index(tgt_node)
+                pspecs.append(pj)
+            epis.append(kernels.PreparedFused(
+                [(outs[i], n[i], [self._identity_spec(i, views[et], d) for et in self.targets[i]], relu)
+                 for i in tl], d, pspecs, 1))
+        else:
+            for i in self.targets:
+                if i in fused_t:
+                    continue
+                epis.append(kernels.PreparedEpilogue([partials[et] for et in self.targets[i]], outs[i], n[i], d, flags))
         return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t)
+
+    def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
+        """A group spec whose 'adjacency' is the identity of node type i (one nonzero 1.0f per
+        row): the fused kernel then reads the dense rows x[r] as the group sums."""
+        n_i = self.g.n_nodes[i]
+        if not hasattr(self, "_eye"):
+            self._eye = {}
+        if i not in self._eye:
+            dev = self.g.device
+            self._eye[i] = (torch.arange(n_i + 1, dtype=torch.int32, device=dev),
+                            torch.arange(n_i, dtype=torch.int32, device=dev),
+                            torch.ones(n_i, dtype=torch.float32, device=dev))
+        rp, vc, vv = self._eye[i]
+        return kernels.RelGroupSpec(rp, vc, vv, x, None, n_i, 1, d, n_i, vcol_max=n_i - 1)
 
     def run_layer1(self) -> None:
         for p in self._pre:
