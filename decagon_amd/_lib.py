@@ -21,7 +21,8 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 13
+ABI_VERSION = 14
+DG_MAX_ADAM_SEGS = 32
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -94,7 +95,17 @@ class DgGemmDesc(ctypes.Structure):
         ("n", c_int32),
         ("k", c_int32),
         ("batch", c_int32),
+        ("reduce", c_int32),
+        ("reserved", c_int32),
     ]
+
+
+class DgL2gGroup(ctypes.Structure):
+    _fields_ = [("s", c_void_p), ("ds", c_void_p)]
+
+
+class DgAdamSeg(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("m", c_void_p), ("v", c_void_p), ("n", c_int64)]
 
 
 # name -> (restype, argtypes); must match include/decagon_hip.h exactly.
@@ -133,6 +144,17 @@ SIGNATURES = {
     ),
     "dg_hinge_loss_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p]),
     "dg_xent_loss_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p]),
+    "dg_decoder_grad_workspace": (c_int64, [c_int32, c_int32]),
+    "dg_decoder_grad_f32": (
+        c_int32,
+        [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_int64, c_void_p],
+    ),
+    "dg_scatter_rows_f32": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
+    "dg_l2norm_grad_f32": (c_int32, [POINTER(DgL2gGroup), c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                     c_void_p]),
+    "dg_adam_f32": (c_int32, [POINTER(DgAdamSeg), c_int32, c_float, c_float, c_float, c_float, c_void_p]),
     "dg_unigram_sample": (
         c_int32,
         [c_void_p, c_int32, c_int32, c_uint64, c_uint64, c_void_p, c_void_p],

@@ -34,7 +34,7 @@ struct GemmOne {
     int32_t tiles_m, tiles_n, batch_per_wave;
     int32_t tile_blocks;   // blocks along the tile dimension (4 tiles each)
     int32_t block_begin;   // first block of this GEMM in the launch
-    int32_t pad;
+    int32_t reduce;        // batch-reduce mode: batches summed in runs of batch_per_wave
 };
 
 struct GemmArgs {
@@ -72,12 +72,13 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
     const bool col_ok = col < g.n;
     const int b0 = bblk * g.batch_per_wave;
     const int b1 = min(b0 + g.batch_per_wave, g.batch);
+    f32x16 acc = {};
 #pragma unroll 1
     for (int b = b0; b < b1; ++b) {
         const float* A = g.a + b * g.a_bs + (int64_t)row * g.a_sm;
         const int bb = g.b_map ? g.b_map[b] : b;
         const float* B = g.b + bb * g.b_bs + (int64_t)col * g.b_sn;
-        f32x16 acc = {};
+        if (!g.reduce) acc = f32x16{};
 #pragma unroll 4
         for (int k0 = 0; k0 < g.k; k0 += 2) {
             const int kk = k0 + h;
@@ -91,9 +92,10 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
             }
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
         }
+        if (g.reduce && b + 1 < b1) continue;  // batch-reduce: one store per run, at run index
         if (col_ok) {
             const float s = g.sc ? g.sc[col] : 1.0f;
-            float* C = g.c + bb * g.c_bs + (int64_t)col * g.c_sn;
+            float* C = g.c + (g.reduce ? bblk : bb) * g.c_bs + (int64_t)col * g.c_sn;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -308,11 +310,14 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
         // wave amortises its A fragment over up to 16 relations.
         int bpw = 1;
         while (bpw < 16 && (int64_t)g.tile_blocks * 4 * dg::ceil_div(d->batch, bpw * 2) >= 8192) bpw *= 2;
+        if (d->reduce < 0 || (d->reduce > 0 && d->b_map)) return DG_EINVAL;
+        g.reduce = d->reduce > 0 ? 1 : 0;
+        if (g.reduce) bpw = d->reduce;
         g.batch_per_wave = bpw;
         g.block_begin = static_cast<int32_t>(blocks);
         blocks += (int64_t)g.tile_blocks * dg::ceil_div(d->batch, bpw);
         if (blocks > 0x7fffffff) return DG_EINVAL;
-        const int kk = (d->k == 64 || d->k == 32) ? d->k : 0;
+        const int kk = (d->k == 64 || d->k == 32) && !g.reduce ? d->k : 0;  // reduce: generic path
         kd = (kd < 0 || kd == kk) ? kk : 0;
     }
     if (A.n == 0) return DG_OK;

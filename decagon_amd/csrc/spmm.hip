@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 13; }
+extern "C" int32_t dg_abi_version(void) { return 14; }
 
 namespace {
 

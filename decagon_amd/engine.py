@@ -113,6 +113,7 @@ class DeviceGroup:
     staged: bool = False           # runs through dg_spmm_staged_f32 (layout: chunk = 1)
     out_chunk: int = 1             # staged: snake-bin size (a layer's output chunk is a multiple)
     layout: Optional["kernels.StagedDevice"] = None  # staged: the diagonal-major layout
+    host: Optional[List[HostCSR]] = None  # the local relations (host CSR), device order
 
     @property
     def n_rels(self) -> int:
@@ -176,6 +177,7 @@ class DeviceGraph:
             if ids.size and not np.array_equal(ids, np.arange(K)):
                 g.rel_map = torch.from_numpy(ids).to(device)
             g.staged, g.out_chunk = staged, out_chunk
+            g.host = loc  # local relations in device order (the backward builds Âᵀ from them)
             if staged:
                 lay = staged_layout(loc, kernels.staged_order,
                                     split=os.environ.get("DG_STAGED_SPLIT", "1") != "0")
@@ -203,10 +205,14 @@ class ForwardPlan:
 
     def __init__(self, dgraph: DeviceGraph, features: Dict[int, Optional[HostCSR]],
                  w1: LayerWeights, w2: LayerWeights, h1: int, h2: int,
-                 allreduce: Optional[Callable[[torch.Tensor], None]] = None):
+                 allreduce: Optional[Callable[[torch.Tensor], None]] = None, keep_sums: bool = False):
         self.g = dgraph
         self.h1, self.h2 = h1, h2
         self.allreduce = allreduce
+        # flat mode: every group's pre-normalisation sum S_ij lands in one flat buffer per
+        # layer (all-reduced when sharded; kept for the backward when training), and one fused
+        # launch over identity "adjacencies" finishes every node type from it
+        self.flat_mode = allreduce is not None or keep_sums
         dev = dgraph.device
         f32 = dict(device=dev, dtype=torch.float32)
         self.edge_types = list(dgraph.edge_types)
@@ -266,7 +272,7 @@ class ForwardPlan:
             rels_from[et[1]] = rels_from.get(et[1], 0) + dgraph.groups[et].n_rels
         # layer-1 rows finished by a fused launch (the SpMM one, or — sharded — the one that
         # finishes the all-reduced sums) project themselves onto the layer-2 relations
-        finished = set(self.targets) if allreduce is not None else set(self.fused)
+        finished = set(self.targets) if self.flat_mode else set(self.fused)
         proj_fused = [et for et in self.edge_types
                       if dgraph.groups[et].n_rels and et[1] in finished
                       and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS]
@@ -298,7 +304,7 @@ class ForwardPlan:
 
     # ------------------------------------------------------------------ layer builder
     def _fused_targets(self) -> List[int]:
-        if self.allreduce is not None:
+        if self.flat_mode:
             return []
         return [i for i, ets in self.targets.items()
                 if all(self.g.groups[et].n_chunks == 1 and self.g.groups[et].n_rels > 0
@@ -337,7 +343,7 @@ class ForwardPlan:
         rest = [et for et in self.edge_types if et[0] not in fused_t]
         flags = DG_EPI_L2NORM | (DG_EPI_RELU if relu else 0)
         flat, views = None, {}
-        if self.allreduce is not None and rest:
+        if self.flat_mode and rest:
             sizes = [g.groups[et].n_rows * d for et in rest]
             flat = torch.zeros(int(sum(sizes)), **f32)
             off = 0
@@ -388,7 +394,7 @@ class ForwardPlan:
                 if i in fused_t:
                     continue
                 epis.append(kernels.PreparedEpilogue([partials[et] for et in self.targets[i]], outs[i], n[i], d, flags))
-        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t)
+        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views)
 
     def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
         """A group spec whose 'adjacency' is the identity of node type i (one nonzero 1.0f per
@@ -437,7 +443,7 @@ class ForwardPlan:
             if layer.need_zero:
                 cur.append(layer.flat.zero_)
             cur.extend(layer.launches)
-            if layer.flat is not None:
+            if layer.flat is not None and layer.allreduce is not None:
                 close()
                 flat, ar = layer.flat, layer.allreduce
                 out.append(("exchange", lambda flat=flat, ar=ar: ar(flat)))
@@ -485,9 +491,10 @@ class ForwardPlan:
 class _Layer:
     """The prepared launches of one layer and how to run them."""
 
-    def __init__(self, launches, flat, need_zero, allreduce, epilogues, fused_targets):
+    def __init__(self, launches, flat, need_zero, allreduce, epilogues, fused_targets, views=None):
         self.launches = launches
         self.flat = flat
+        self.views = views or {}  # flat mode: (i,j) -> that group's S_ij, [n_i * d]
         self.need_zero = need_zero
         self.allreduce = allreduce
         self.epilogues = epilogues
@@ -498,7 +505,7 @@ class _Layer:
             self.flat.zero_()  # groups without local relations contribute zeros
         for l in self.launches:
             l()
-        if self.flat is not None:
+        if self.flat is not None and self.allreduce is not None:
             self.allreduce(self.flat)
         for e in self.epilogues:
             e()

@@ -45,7 +45,13 @@ class Node:
 
 
 class Operation(Node):
-    """A node fetched for its side effect; fetching it yields None (like tf.Operation)."""
+    """A node fetched for its side effect; fetching it yields None (like tf.Operation).
+    `training` marks a training op: a run that fetches one evaluates the whole forward in
+    training mode (the plan that keeps what the backward needs)."""
+
+    def __init__(self, name: str, fn=None, training: bool = False):
+        super().__init__(name, fn)
+        self.training = training
 
 
 class Placeholder(Node):
@@ -105,10 +111,11 @@ class Variable(Node):
 
 
 class RunContext:
-    def __init__(self, session: "Session", feeds: Dict[Node, Any]):
+    def __init__(self, session: "Session", feeds: Dict[Node, Any], training: bool = False):
         self.session = session
         self.feeds = feeds
         self.cache: Dict[Any, Any] = {}
+        self.training = training
 
     def is_fed(self, node: Node) -> bool:
         return node in self.feeds
@@ -165,7 +172,17 @@ class Session:
         for k in feeds:
             if not isinstance(k, Node):
                 raise TypeError(f"feed_dict key {k!r} is not a graph node")
-        ctx = RunContext(self, feeds)
+
+        def any_training(f) -> bool:
+            if isinstance(f, Node):
+                return bool(getattr(f, "training", False))
+            if isinstance(f, dict):
+                return any(any_training(v) for v in f.values())
+            if isinstance(f, (list, tuple)):
+                return any(any_training(x) for x in f)
+            return False
+
+        ctx = RunContext(self, feeds, training=any_training(fetches))
 
         def ev(f):
             if f is None:

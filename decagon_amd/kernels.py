@@ -18,7 +18,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import DgEpiGroup, DgFusedTarget, DgGemmDesc, DgProj, DgRelGroup, DgStagedGroup, check
+from ._lib import (DgAdamSeg, DgEpiGroup, DgFusedTarget, DgGemmDesc, DgL2gGroup, DgProj, DgRelGroup,
+                   DgStagedGroup, check)
 
 
 def _stream_ptr(stream: Optional[torch.cuda.Stream] = None) -> int:
@@ -369,7 +370,7 @@ class PreparedGemm:
                  c_strides, m: int, n: int, k: int, batch: int = 1,
                  sa: Optional[torch.Tensor] = None, sc: Optional[torch.Tensor] = None,
                  b_map: Optional[torch.Tensor] = None, b_batches: Optional[int] = None,
-                 b_map_max: Optional[int] = None):
+                 b_map_max: Optional[int] = None, reduce: int = 0):
         for t, nm in ((a, "a"), (b, "b"), (c, "c")):
             if not (t.is_cuda and t.dtype == torch.float32):
                 raise ValueError(f"{nm}: float32 device tensor required")
@@ -387,7 +388,10 @@ class PreparedGemm:
         if m and n and k and batch:
             if a.numel() < span(a_strides, m, k) or b.numel() < span(b_strides, k, n, nb_b):
                 raise ValueError("gemm operand too small for its strides")
-        if m and n and batch and c.numel() < span(c_strides, m, n, nb_b):
+        if reduce < 0 or (reduce and b_map is not None):
+            raise ValueError("batch-reduce mode takes no b_map")
+        n_out = -(-batch // reduce) if reduce else nb_b
+        if m and n and batch and c.numel() < span(c_strides, m, n, n_out):
             raise ValueError("gemm output too small for its strides")
         if sa is not None and (sa.numel() < k or sa.dtype != torch.float32 or not sa.is_cuda):
             raise ValueError("sa must be a float32 device vector of length k")
@@ -402,6 +406,7 @@ class PreparedGemm:
         desc.b_bs, desc.b_sk, desc.b_sn = b_strides
         desc.c_bs, desc.c_sm, desc.c_sn = c_strides
         desc.m, desc.n, desc.k, desc.batch = m, n, k, batch
+        desc.reduce = reduce
         self._desc = desc
         self._keep = (a, b, c, sa, sc, b_map)
         self._fn = _lib.load().dg_gemm_f32
@@ -601,3 +606,121 @@ class PreparedDecoderHinge:
         a = list(self._args)
         a[9], a[10] = self.seed & (2**64 - 1), self.offset & (2**64 - 1)
         check(self._fn(*a, _stream_ptr(stream)), "dg_decoder_hinge_f32")
+
+
+# --------------------------------------------------------------------------------------
+# Training step (train.hip): decoder gradient, gather-gradient scatter, l2-norm backward, Adam
+# --------------------------------------------------------------------------------------
+class PreparedDecoderGrad:
+    """dg_decoder_grad_f32 for one batch: row / column gradient rows of the n positive and n
+    negative pairs, and the decoder parameter gradients dG = L·dM·L, dl, diag(dG) (each
+    written only if its output tensor is given)."""
+
+    def __init__(self, row_table, col_table, rows, cols, neg_rows, pos, neg, G, l, margin: float,
+                 dG: Optional[torch.Tensor] = None, dl: Optional[torch.Tensor] = None,
+                 dG_diag: Optional[torch.Tensor] = None):
+        for t, nm, dt in ((row_table, "row_table", torch.float32), (col_table, "col_table", torch.float32),
+                          (rows, "rows", torch.int32), (cols, "cols", torch.int32),
+                          (neg_rows, "neg_rows", torch.int32), (pos, "pos", torch.float32),
+                          (neg, "neg", torch.float32), (G, "G", torch.float32)):
+            _dev(t, dt, nm)
+        d = G.shape[0]
+        n = rows.numel()
+        if G.shape != (d, d) or row_table.shape[1] != d or col_table.shape[1] != d:
+            raise ValueError("decoder_grad: shape mismatch")
+        if cols.numel() != n or neg_rows.numel() != n or pos.numel() != n or neg.numel() != n:
+            raise ValueError("decoder_grad: batch sizes differ")
+        if l is not None:
+            _dev(l, torch.float32, "l")
+        if dl is not None and l is None:
+            raise ValueError("dl needs a diagonal L")
+        for t, nm, sz in ((dG, "dG", d * d), (dl, "dl", d), (dG_diag, "dG_diag", d)):
+            if t is not None:
+                _dev(t, torch.float32, nm)
+                if t.numel() != sz:
+                    raise ValueError(f"{nm} must have {sz} elements")
+        dev = G.device
+        self.grad_rows = torch.empty((2 * n, d), device=dev)
+        self.grad_cols = torch.empty((n, d), device=dev)
+        lib = _lib.load()
+        nbytes = int(lib.dg_decoder_grad_workspace(n, d))
+        self._ws = torch.empty(max(1, nbytes // 4), device=dev)
+        self.row_idx = torch.cat([rows, neg_rows])  # scatter order: positives, then negatives
+        self._keep = (row_table, col_table, rows, cols, neg_rows, pos, neg, G, l, dG, dl, dG_diag)
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        self._args = [row_table.data_ptr(), row_table.shape[1], col_table.data_ptr(), col_table.shape[1],
+                      rows.data_ptr(), cols.data_ptr(), neg_rows.data_ptr(), n, pos.data_ptr(), neg.data_ptr(),
+                      G.data_ptr(), ptr(l), d, float(margin), self.grad_rows.data_ptr(),
+                      self.grad_cols.data_ptr(), ptr(dG), ptr(dl), ptr(dG_diag), self._ws.data_ptr(), nbytes]
+        self._fn = lib.dg_decoder_grad_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(*self._args, _stream_ptr(stream)), "dg_decoder_grad_f32")
+
+
+def scatter_rows(idx: torch.Tensor, src: torch.Tensor, out: torch.Tensor, stream=None) -> None:
+    """out[idx[q]] += Σ src[q'] over the occurrences q' of idx[q] (fixed order)."""
+    _dev(idx, torch.int32, "idx")
+    _dev(src, torch.float32, "src")
+    _dev(out, torch.float32, "out")
+    n = idx.numel()
+    if src.dim() != 2 or src.shape[0] != n or out.dim() != 2 or out.shape[1] != src.shape[1]:
+        raise ValueError("scatter_rows: shapes")
+    if n and (int(idx.min()) < 0 or int(idx.max()) >= out.shape[0]):
+        raise ValueError("scatter_rows: index out of range")
+    check(_lib.load().dg_scatter_rows_f32(idx.data_ptr(), n, src.data_ptr(), src.shape[1], out.data_ptr(),
+                                          out.stride(0), _stream_ptr(stream)), "dg_scatter_rows_f32")
+
+
+class PreparedL2Grad:
+    """dg_l2norm_grad_f32: ds_g = backward of l2_normalize(s_g) at dy (∘ [mask > 0]) for the
+    groups (s_g, ds_g) of one node type."""
+
+    def __init__(self, groups: Sequence[Tuple[torch.Tensor, torch.Tensor]], dy: torch.Tensor,
+                 mask: Optional[torch.Tensor], n_rows: int, d: int):
+        if not 1 <= len(groups) <= _lib.DG_MAX_GROUPS:
+            raise ValueError("1..DG_MAX_GROUPS groups")
+        for t, nm in [(dy, "dy")] + ([(mask, "mask")] if mask is not None else []):
+            _dev(t, torch.float32, nm)
+            if t.numel() < n_rows * d:
+                raise ValueError(f"{nm} too small")
+        arr = (DgL2gGroup * len(groups))()
+        for i, (s_, ds) in enumerate(groups):
+            _dev(s_, torch.float32, "s")
+            _dev(ds, torch.float32, "ds")
+            if s_.numel() < n_rows * d or ds.numel() < n_rows * d:
+                raise ValueError("l2 grad group too small")
+            arr[i].s, arr[i].ds = s_.data_ptr(), ds.data_ptr()
+        self._arr, self._n = arr, len(groups)
+        self._keep = (list(groups), dy, mask)
+        self._args = (dy.data_ptr(), mask.data_ptr() if mask is not None else None, n_rows, d)
+        self._fn = _lib.load().dg_l2norm_grad_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(self._arr, self._n, *self._args, _stream_ptr(stream)), "dg_l2norm_grad_f32")
+
+
+class PreparedAdam:
+    """dg_adam_f32 over fixed (param, grad or None, m, v) segments (≤ DG_MAX_ADAM_SEGS per
+    launch; more segments → several launches)."""
+
+    def __init__(self, segs: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor], torch.Tensor, torch.Tensor]]):
+        self._arrs = []
+        for s0 in range(0, len(segs), _lib.DG_MAX_ADAM_SEGS):
+            chunk = segs[s0:s0 + _lib.DG_MAX_ADAM_SEGS]
+            arr = (DgAdamSeg * len(chunk))()
+            for i, (p, g, m, v) in enumerate(chunk):
+                for t, nm in ((p, "param"), (m, "m"), (v, "v")) + (((g, "grad"),) if g is not None else ()):
+                    _dev(t, torch.float32, nm)
+                    if t.numel() != p.numel():
+                        raise ValueError(f"adam {nm}: {t.numel()} elements, param has {p.numel()}")
+                arr[i].param, arr[i].m, arr[i].v = p.data_ptr(), m.data_ptr(), v.data_ptr()
+                arr[i].grad = g.data_ptr() if g is not None else None
+                arr[i].n = p.numel()
+            self._arrs.append((arr, len(chunk)))
+        self._keep = list(segs)
+        self._fn = _lib.load().dg_adam_f32
+
+    def __call__(self, alpha: float, beta1: float, beta2: float, eps: float, stream=None) -> None:
+        for arr, n in self._arrs:
+            check(self._fn(arr, n, alpha, beta1, beta2, eps, _stream_ptr(stream)), "dg_adam_f32")

@@ -193,11 +193,19 @@ class _DecoderBase(MultiLayer):
         self.act = act
         self.input_dim = input_dim
 
-    def _var(self, name: str, arr: np.ndarray) -> Variable:
-        t = torch.from_numpy(np.ascontiguousarray(arr, np.float32)).to(runtime.param_device())
-        v = Variable(t, f"{self._scope()}/{name}:0")
-        self.vars[name] = v
-        return v
+    def _make_vars(self, arrays: Dict[str, np.ndarray]) -> None:
+        """All of the decoder's variables as views of ONE flat device buffer (`self.flat`),
+        each starting 16-byte aligned — so the optimizer updates a decoder in one segment."""
+        offs, off = {}, 0
+        for name, a in arrays.items():
+            offs[name] = off
+            off += -(-int(np.asarray(a).size) // 4) * 4
+        self.flat = torch.zeros(off, dtype=torch.float32, device=runtime.param_device())
+        for name, a in arrays.items():
+            a = np.ascontiguousarray(a, np.float32)
+            view = self.flat[offs[name]:offs[name] + a.size].view(a.shape)
+            view.copy_(torch.from_numpy(a))
+            self.vars[name] = Variable(view, f"{self._scope()}/{name}:0")
 
     def latent(self, k: int):
         """(G kind, G variable or None, L kind, L variable or None) for relation k."""
@@ -228,9 +236,10 @@ class DEDICOMDecoder(_DecoderBase):
 
     def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
         super().__init__(input_dim, dropout, act, **kwargs)
-        self._var("global_interaction", inits.glorot_array(input_dim, input_dim))
+        arrays = {"global_interaction": inits.glorot_array(input_dim, input_dim)}
         for k in range(self.num_types):
-            self._var("local_variation_%d" % k, inits.glorot_array(input_dim, 1).reshape(-1))
+            arrays["local_variation_%d" % k] = inits.glorot_array(input_dim, 1).reshape(-1)
+        self._make_vars(arrays)
 
     def latent(self, k):
         return "dense", self.vars["global_interaction"], "diag", self.vars["local_variation_%d" % k]
@@ -241,8 +250,8 @@ class DistMultDecoder(_DecoderBase):
 
     def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
         super().__init__(input_dim, dropout, act, **kwargs)
-        for k in range(self.num_types):
-            self._var("relation_%d" % k, inits.glorot_array(input_dim, 1).reshape(-1))
+        self._make_vars({"relation_%d" % k: inits.glorot_array(input_dim, 1).reshape(-1)
+                         for k in range(self.num_types)})
 
     def latent(self, k):
         return "diag", self.vars["relation_%d" % k], "eye", None
@@ -253,8 +262,8 @@ class BilinearDecoder(_DecoderBase):
 
     def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
         super().__init__(input_dim, dropout, act, **kwargs)
-        for k in range(self.num_types):
-            self._var("relation_%d" % k, inits.glorot_array(input_dim, input_dim))
+        self._make_vars({"relation_%d" % k: inits.glorot_array(input_dim, input_dim)
+                         for k in range(self.num_types)})
 
     def latent(self, k):
         return "dense", self.vars["relation_%d" % k], "eye", None
@@ -262,6 +271,10 @@ class BilinearDecoder(_DecoderBase):
 
 class InnerProductDecoder(_DecoderBase):
     """layers.py:198-213: G = I, L = I (no parameters)."""
+
+    def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
+        super().__init__(input_dim, dropout, act, **kwargs)
+        self._make_vars({})
 
     def latent(self, k):
         return "eye", None, "eye", None

@@ -103,6 +103,7 @@ class DecagonModel(Model):
         for i in dict.fromkeys(i for i, _ in self.edge_types):
             self.hidden1[i] = Node(f"{self.name}/hidden1_{i}",
                                    lambda ctx, i=i: self._forward(ctx).hidden1[i])
+            self.hidden1[i].model = self
         for i, j in self.edge_types:
             self.layers2[i, j] = GraphConvolutionMulti(
                 input_dim=h1, output_dim=h2, edge_type=(i, j),
@@ -112,6 +113,7 @@ class DecagonModel(Model):
         for i in dict.fromkeys(i for i, _ in self.edge_types):
             self.embeddings[i] = Node(f"{self.name}/embeddings_{i}",
                                       lambda ctx, i=i: self._forward(ctx).embeddings[i])
+            self.embeddings[i].model = self  # the optimizer's training step finds the model here
 
         self.edge_type2decoder = {}
         for i, j in self.edge_types:
@@ -153,14 +155,15 @@ class DecagonModel(Model):
         return (LayerWeights({et: l.weights_stack for et, l in self.layers1.items()}),
                 LayerWeights({et: l.weights_stack for et, l in self.layers2.items()}))
 
-    def plan(self, ctx: RunContext, shard=None) -> ForwardPlan:
-        """The cached ForwardPlan for the adjacency/feature values fed in this run."""
+    def plan(self, ctx: RunContext, shard=None, training: bool = False) -> ForwardPlan:
+        """The cached ForwardPlan for the adjacency/feature values fed in this run (training:
+        the flat-mode plan that keeps every group's pre-normalisation sum for the backward)."""
         local = None if shard is None else shard.local
         dg = runtime.device_graph(ctx, self.edge_types, self.adj_mats, local)
         feats = {j: runtime.feature_csr(ctx, self.inputs[j]) if j in self.inputs else None
                  for j in dg.n_nodes}
         key = ("plan", id(self), id(dg), tuple((j, id(f)) for j, f in feats.items()),
-               None if shard is None else id(shard))
+               None if shard is None else id(shard), training)
         cache = ctx.session.caches.setdefault("plans", {})
         hit = cache.get(key)
         if hit is None:
@@ -170,7 +173,7 @@ class DecagonModel(Model):
                                        "(construct the model after a HIP device is visible)")
             w1, w2 = self.weight_stacks()
             p = ForwardPlan(dg, feats, w1, w2, self.h1, self.h2,
-                            allreduce=None if shard is None else shard.allreduce)
+                            allreduce=None if shard is None else shard.allreduce, keep_sums=training)
             hit = (dg, feats, p)
             cache[key] = hit
         return hit[2]
@@ -182,7 +185,7 @@ class DecagonModel(Model):
             if float(d) != 0.0:
                 raise NotImplementedError(
                     "dropout > 0 is the training path (SURVEY §8f); forward parity runs at 0")
-            p = self.plan(ctx, getattr(ctx.session, "shard", None))
+            p = self.plan(ctx, getattr(ctx.session, "shard", None), training=ctx.training)
             p.run()
             ctx.cache[key] = p
         return ctx.cache[key]

@@ -9,7 +9,9 @@ Negatives are drawn on the device from the same distortion-0.75 unigram distribu
 tf.nn.fixed_unigram_candidate_sampler (:37-49); feeding `opt.neg_samples` injects them
 (TF semantics: any tensor may be fed), which is how parity tests pin them.
 
-`opt_op` (backward + Adam, :108-114) is the next row of SURVEY §8f: fetching it raises.
+`opt_op` (:108-114) runs the training step on the device: the forward in training mode, the
+backward of the hinge cost (decagon_amd/train.py) and TF 1.8's Adam on every variable.
+`grads_vars` returns (gradient, value) pairs of every variable, like compute_gradients.
 """
 from __future__ import annotations
 
@@ -18,7 +20,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from . import kernels, runtime
+from . import kernels, runtime, train
 from .flags import FLAGS
 from .graph import InvalidArgumentError, Node, Operation, RunContext
 
@@ -183,14 +185,124 @@ class DecagonOptimizer:
 
     def _build(self):
         self.cost = self._hinge_loss(self.outputs, self.neg_outputs)
-        self.optimizer = None
+        self.optimizer = "adam"  # tf.train.AdamOptimizer(learning_rate=FLAGS.learning_rate)
+        self.opt_op = Operation("optimizer/opt_op", lambda ctx: self._train(ctx, apply=True), training=True)
+        self.grads_vars = Node("optimizer/grads_vars", lambda ctx: self._train(ctx, apply=False))
+        self.grads_vars.training = True
 
-        def _not_yet(ctx):
-            raise NotImplementedError(
-                "opt_op (backward + Adam, optimizer.py:108-114) is the next row of SURVEY §8f; "
-                "the HIP forward path serves cost / outputs / predictions")
-        self.opt_op = Operation("optimizer/opt_op", _not_yet)
-        self.grads_vars = Operation("optimizer/grads_vars", _not_yet)
+    # ------------------------------------------------------------------ training step
+    def _model(self):
+        for e in self.embeddings:
+            m = getattr(e, "model", None)
+            if m is not None:
+                return m
+        raise NotImplementedError("opt_op needs the embeddings of a DecagonModel")
+
+    def _train_plan(self, ctx: RunContext, model):
+        fwd = model._forward(ctx)
+        key = ("train", id(self), id(fwd))
+        cache = ctx.session.caches
+        if key not in cache:
+            feats = {j: runtime.feature_csr(ctx, model.inputs[j]) if j in model.inputs else None
+                     for j in fwd.g.n_nodes}
+            w1, w2 = model.weight_stacks()
+            cache[key] = train.TrainPlan(fwd, w1, w2, feats)
+        return fwd, cache[key]
+
+    def _decoder_grads(self, ctx: RunContext, model, e: int, rt: int, ct: int):
+        """Zeroed gradient buffers of every decoder, the batch relation's entries filled
+        (TF's gather over the stacked latent lists gives the others dense zeros)."""
+        key = ("dec_grads", id(self))
+        cache = ctx.session.caches
+        if key not in cache:
+            cache[key] = {et: torch.zeros_like(d.flat) for et, d in model.edge_type2decoder.items()}
+        grads = cache[key]
+        for t in grads.values():
+            t.zero_()
+        i, j, k = self._rel_of[e]
+        dec = model.edge_type2decoder[i, j]
+        gflat = grads[i, j]
+
+        def gview(var):
+            off = (var.tensor.data_ptr() - dec.flat.data_ptr()) // 4
+            return gflat[off:off + var.tensor.numel()]
+
+        gk, gv, lk, lv = model._latent_spec[e]
+        fed = ctx.is_fed(self.latent_inters[e]) or ctx.is_fed(self.latent_varies[e])
+        out = {"dG": None, "dl": None, "dG_diag": None}
+        if not fed:
+            if gk == "dense":
+                out["dG"] = gview(gv)
+            elif gk == "diag":
+                out["dG_diag"] = gview(gv)
+            if lk == "diag":
+                out["dl"] = gview(lv)
+        return grads, out
+
+    def _train(self, ctx: RunContext, apply: bool):
+        """One training step (apply) or the gradients only (compute_gradients)."""
+        if not ctx.training:
+            raise RuntimeError("training ops must be fetched through Session.run")
+        for nd in (self.outputs, self.neg_outputs, self.cost):
+            if ctx.is_fed(nd):
+                raise InvalidArgumentError(f"{nd.name} is fed: the cost's gradient does not reach the model")
+        model = self._model()
+        fwd, tp = self._train_plan(ctx, model)
+        pos, neg, _, negs_dev = ctx.value(self._decode)
+        e, rt, ct = self._edge(ctx)
+        row_t, col_t = self._tables(ctx, rt, ct)
+        rows = self._idx_dev(ctx, self.row_inputs, row_t.shape[0])
+        cols = self._idx_dev(ctx, self.col_inputs, col_t.shape[0])
+        negs = (self._idx_dev(ctx, self.neg_samples, row_t.shape[0]) if ctx.is_fed(self.neg_samples)
+                else negs_dev)
+        G, l = self._latent(ctx, e)
+        dec_grads, outs = self._decoder_grads(ctx, model, e, rt, ct)
+        if outs["dl"] is not None and l is None:
+            raise RuntimeError("DEDICOM decoder without its diagonal")
+        op = kernels.PreparedDecoderGrad(row_t, col_t, rows, cols, negs, pos, neg, G, l, self.margin, **outs)
+
+        def decoder_grad(dE):
+            op()
+            kernels.scatter_rows(op.row_idx, op.grad_rows, dE[rt])
+            kernels.scatter_rows(cols, op.grad_cols, dE[ct])
+
+        tp.backward(decoder_grad)
+        w1, w2 = model.weight_stacks()
+        ets = list(model.edge_types)
+        params = [w1.stacks[et] for et in ets] + [w2.stacks[et] for et in ets] + \
+                 [model.edge_type2decoder[et].flat for et in ets]
+        grads = [tp.gW1[et] for et in ets] + [tp.gW2[et] for et in ets] + [dec_grads[et] for et in ets]
+        if not apply:
+            return self._grads_vars(model, tp, dec_grads)
+        key = ("adam", id(self))
+        cache = ctx.session.caches
+        if key not in cache:
+            st = train.AdamState(params)
+            cache[key] = (st, {})
+        st, prepared = cache[key]
+        pk = tuple(g.data_ptr() for g in grads)
+        if pk not in prepared:
+            prepared[pk] = st.prepared(grads)
+        st.t += 1
+        alpha = train.adam_alpha(float(FLAGS.learning_rate), st.t)
+        prepared[pk](alpha, train.BETA1, train.BETA2, train.EPSILON)
+        return None
+
+    def _grads_vars(self, model, tp, dec_grads):
+        """[(gradient, variable value)] in model.vars order (layers 1, layers 2, decoders)."""
+        out = []
+        for et, lay in model.layers1.items():
+            for k in range(lay.num_types):
+                out.append((tp.gW1[et][k], lay.vars["weights_%d" % k].tensor))
+        for et, lay in model.layers2.items():
+            for k in range(lay.num_types):
+                out.append((tp.gW2[et][k], lay.vars["weights_%d" % k].tensor))
+        for et, dec in model.edge_type2decoder.items():
+            for var in dec.vars.values():
+                off = (var.tensor.data_ptr() - dec.flat.data_ptr()) // 4
+                out.append((dec_grads[et][off:off + var.tensor.numel()].view(var.tensor.shape).clone(),
+                            var.tensor.clone()))
+        return [(g.clone(), v.clone()) for g, v in out]
 
     def _hinge_loss(self, aff, neg_aff):
         """optimizer.py:116-120: sum(relu(neg - (pos - margin)))."""

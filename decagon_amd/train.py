@@ -1,0 +1,177 @@
+"""The training step: backward of the hinge cost through both GCN layers, and TF 1.8's Adam.
+
+Reference: `DecagonOptimizer._build` (decagon/deep/optimizer.py:108-114) —
+`tf.train.AdamOptimizer(FLAGS.learning_rate).minimize(self.cost)` — driven by
+`sess.run([opt.opt_op, opt.cost, ...])` (main.py:315, DecagonTrainer.py:90-102).  TF derives
+the backward graph automatically; here it is written out over the forward's saved state:
+
+  forward (ForwardPlan in flat mode)  S1_ij = Σ_k Â_k·W1_k,  H1_i = relu(Σ_j l2n(S1_ij))
+                                      S2_ij = Σ_k Â_k·(H1_j·W2_k),  E_i = Σ_j l2n(S2_ij)
+  decoder + gathers                   dE_i (dg_decoder_grad_f32 + dg_scatter_rows_f32)
+  layer 2                             dS2_ij = l2n'(S2_ij)·dE_i            dg_l2norm_grad_f32
+                                      dP_ijk = Â_kᵀ·dS2_ij                 dg_spmm_groups_f32 (Âᵀ)
+                                      dW2_ijk = H1_jᵀ·dP_ijk               dg_gemm_f32
+                                      dH1_j = Σ_ik dP_ijk·W2_ijkᵀ          dg_gemm_f32 (batch-reduce)
+                                                                           + dg_gcn_epilogue_f32
+  layer 1                             dS1_ij = l2n'(S1_ij)·(dH1_i∘[H1_i>0]) dg_l2norm_grad_f32
+                                      dW1_ijk = Â_kᵀ·dS1_ij                dg_spmm_groups_f32 (Âᵀ)
+  Adam (every variable, every step)   dg_adam_f32
+
+Âᵀ of every relation is built once on the host from the uploaded CSR and stored as a
+relation-chunked CSR whose virtual columns index the shared operand dS_ij directly, so the
+transposed SpMM writes dP / dW1 straight in the weight-stack layout [K][n_j][d].
+Scope: one GPU, identity features (sparse-feature and sharded training raise).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import kernels
+from ._lib import DG_MAX_GROUPS
+from .engine import ForwardPlan, LayerWeights
+from .sparse import HostCSR, merge_chunks
+
+EdgeType = Tuple[int, int]
+
+BETA1, BETA2, EPSILON = 0.9, 0.999, 1e-8  # tf.train.AdamOptimizer defaults
+
+
+def transpose_csr(c: HostCSR) -> HostCSR:
+    """Âᵀ in CSR (rows = Â's columns, each row's nonzeros in ascending Â-row order)."""
+    n_r, n_c = c.shape
+    lens = np.diff(c.rowptr.astype(np.int64))
+    rows = np.repeat(np.arange(n_r, dtype=np.int64), lens)
+    cols = c.col.astype(np.int64)
+    order = np.lexsort((rows, cols))
+    counts = np.bincount(cols, minlength=n_c)
+    rowptr = np.zeros(n_c + 1, np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    return HostCSR(rowptr.astype(np.int32), rows[order].astype(np.int32), c.val[order].astype(np.float32),
+                   (n_c, n_r))
+
+
+def adam_alpha(lr: float, t: int, beta1: float = BETA1, beta2: float = BETA2) -> float:
+    """lr·sqrt(1 − β2^t)/(1 − β1^t) in float32, with the beta powers kept as float32
+    variables multiplied once per step — as TF 1.8's Adam computes it."""
+    f = np.float32
+    b1p, b2p = f(beta1), f(beta2)
+    for _ in range(t - 1):
+        b1p, b2p = f(b1p * f(beta1)), f(b2p * f(beta2))
+    return float(f(f(lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p)))
+
+
+class AdamState:
+    """m / v slots of a list of parameters (zeros at creation, as TF's slots) and the step."""
+
+    def __init__(self, params: Sequence[torch.Tensor]):
+        self.params = list(params)
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.t = 0
+
+    def prepared(self, grads: Sequence[Optional[torch.Tensor]]) -> kernels.PreparedAdam:
+        return kernels.PreparedAdam([(p, g, m, v) for p, g, m, v in zip(self.params, grads, self.m, self.v)])
+
+
+class TrainPlan:
+    """Buffers and prepared launches of one backward over a flat-mode ForwardPlan."""
+
+    def __init__(self, fwd: ForwardPlan, w1: LayerWeights, w2: LayerWeights,
+                 features: Dict[int, Optional[HostCSR]]):
+        if not fwd.flat_mode or fwd.allreduce is not None:
+            raise NotImplementedError("training runs on one GPU over a ForwardPlan(keep_sums=True)")
+        if any(f is not None for f in features.values()):
+            raise NotImplementedError("the backward for sparse (non-identity) features is not on the HIP path")
+        g = fwd.g
+        self.fwd = fwd
+        dev = g.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        h1, h2 = fwd.h1, fwd.h2
+        n = g.n_nodes
+        self.h1, self.h2 = h1, h2
+        ets = fwd.edge_types
+        self.dE = {i: torch.zeros((n[i], h2), **f32) for i in fwd.targets}
+        srcs = sorted({et[1] for et in ets})
+        self.dH1 = {j: torch.zeros((n[j], h1), **f32) for j in srcs}
+        self.gW1: Dict[EdgeType, torch.Tensor] = {}
+        self.gW2: Dict[EdgeType, torch.Tensor] = {}
+        specs2, specs1, gemm_w2, gemm_h1 = [], [], [], []
+        runs: Dict[int, List[Tuple[torch.Tensor, int]]] = {j: [] for j in srcs}
+        self._dS1, self._dS2 = {}, {}
+        for et in ets:
+            i, j = et
+            grp = g.groups[et]
+            K = grp.K
+            if grp.n_rels != K or grp.host is None:
+                raise NotImplementedError("training needs every relation of a group on this device")
+            order = np.argsort(grp.rel_ids, kind="stable")
+            rels = [transpose_csr(grp.host[p]) for p in order]
+            m = merge_chunks(rels, [0] * K, 1, 1)  # chunk k = relation k; vcol = Â row (into dS)
+            rp, vc, vv = (torch.from_numpy(m.rowptr).to(dev), torch.from_numpy(m.vcol).to(dev),
+                          torch.from_numpy(m.val).to(dev))
+            vmax = int(m.vcol.max()) if m.nnz else -1
+            dS2 = torch.zeros((n[i], h2), **f32)
+            dS1 = torch.zeros((n[i], h1), **f32)
+            dP = torch.zeros((K, n[j], h2), **f32)
+            self._dS1[et], self._dS2[et] = dS1, dS2
+            self.gW2[et] = torch.zeros_like(w2.stacks[et])
+            self.gW1[et] = torch.zeros((K, n[j], h1), **f32)
+            if tuple(w1.stacks[et].shape) != (K, n[j], h1):
+                raise ValueError(f"layer-1 weights of {et} do not match identity features")
+            specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, n[i], vcol_max=vmax))
+            specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, self.gW1[et], n[j], K, h1, n[i], vcol_max=vmax))
+            H = fwd.hidden1[j]
+            # dW2_k = H1_jᵀ·dP_k: A(m, k) = H1_j[k][m]
+            gemm_w2.append(kernels.PreparedGemm(H, (0, 1, h1), dP, (n[j] * h2, h2, 1), self.gW2[et],
+                                                (h1 * h2, h2, 1), h1, h2, n[j], K))
+            # dH1_j partials = Σ_k dP_k·W2_kᵀ over runs of R relations: B(c, m) = W2_k[m][c]
+            R = K if K <= 64 else 32
+            n_runs = -(-K // R)
+            part = torch.zeros((n_runs, n[j], h1), **f32)
+            gemm_h1.append(kernels.PreparedGemm(dP, (n[j] * h2, h2, 1), w2.stacks[et], (h1 * h2, 1, h2), part,
+                                                (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R))
+            runs[j].append((part, n_runs))
+        chunked = lambda xs: [xs[s:s + DG_MAX_GROUPS] for s in range(0, len(xs), DG_MAX_GROUPS)]  # noqa: E731
+        self._spmm2 = [kernels.PreparedSpmm(c, h2) for c in chunked(specs2)]
+        self._spmm1 = [kernels.PreparedSpmm(c, h1) for c in chunked(specs1)]
+        self._gemm_w2 = [kernels.PreparedGemmMulti(c) for c in chunked(gemm_w2)]
+        self._gemm_h1 = [kernels.PreparedGemmMulti(c) for c in chunked(gemm_h1)]
+        self._epi_h1 = []
+        for j, lst in runs.items():
+            if len(lst) > DG_MAX_GROUPS:
+                raise ValueError(f"more than {DG_MAX_GROUPS} edge types out of node type {j}")
+            self._epi_h1.append(kernels.PreparedEpilogue(lst, self.dH1[j], n[j], h1, 0))
+        L1, L2 = fwd._layer1, fwd._layer2
+        self._l2g2, self._l2g1 = [], []
+        for i, tets in fwd.targets.items():
+            self._l2g2.append(kernels.PreparedL2Grad([(L2.views[et], self._dS2[et]) for et in tets],
+                                                     self.dE[i], None, n[i], h2))
+            dy = self.dH1.get(i)
+            if dy is None:  # no layer-2 relation reads H1_i: its gradient is zero
+                dy = self.dH1.setdefault(i, torch.zeros((n[i], h1), **f32))
+            self._l2g1.append(kernels.PreparedL2Grad([(L1.views[et], self._dS1[et]) for et in tets],
+                                                     dy, fwd.hidden1[i], n[i], h1))
+
+    def backward(self, decoder_grad) -> None:
+        """dE ← decoder_grad(dE) (it adds the decoder's row gradients into the zeroed dE),
+        then both layers' backward into gW2 / gW1."""
+        for t in self.dE.values():
+            t.zero_()
+        decoder_grad(self.dE)
+        for l in self._l2g2:
+            l()
+        for s in self._spmm2:
+            s()
+        for gm in self._gemm_w2:
+            gm()
+        for gm in self._gemm_h1:
+            gm()
+        for e in self._epi_h1:
+            e()
+        for l in self._l2g1:
+            l()
+        for s in self._spmm1:
+            s()

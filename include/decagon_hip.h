@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (11); bumped whenever a struct layout or a signature changes. */
+/* ABI version (14); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -221,11 +221,18 @@ typedef struct dg_gemm_desc {
     int64_t b_bs, b_sk, b_sn;
     int64_t c_bs, c_sm, c_sn;
     int32_t m, n, k, batch;
+    int32_t reduce;             /* 0, or R > 0: batch-reduce mode (below); b_map must be NULL */
+    int32_t reserved;
 } dg_gemm_desc;
 
 int dg_gemm_f32(const dg_gemm_desc* descs /* HOST array */, int32_t n_desc, void* stream);
 /* n_desc <= DG_MAX_GROUPS independent GEMMs in one launch (e.g. every (i,j) group's
- * layer-2 projection). */
+ * layer-2 projection).
+ * Batch-reduce mode (reduce = R > 0): the batches are summed in runs of R consecutive
+ * batches (in batch order) and run q's sum is written at c + q*c_bs, q < ceil(batch / R):
+ *     C_q = Σ_{b in [qR, min(qR+R, batch))} A_b·B_b
+ * — the backward's Σ_k dP_k·W_kᵀ (gradient of the per-relation projections, layers.py:113)
+ * as partial sums that dg_gcn_epilogue_f32 (no flags) adds up. */
 
 /* --------------------------------------------------------------------------------------
  * Edge decoder scores (T8 + T9):  for pair p,
@@ -278,6 +285,64 @@ int dg_hinge_loss_f32(const float* pos, const float* neg, int32_t n, float margi
  * (sigmoid_cross_entropy_with_logits with labels 1 / 0).  optimizer.py:122-127. */
 int dg_xent_loss_f32(const float* pos, const float* neg, int32_t n, float neg_weight,
                      float* loss, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Training step (backward of the hinge cost + TF Adam), optimizer.py:108-114.
+ * -------------------------------------------------------------------------------------- */
+/* Decoder gradient for the n positive pairs (rows[p], cols[p]) and negatives (neg_rows[p],
+ * cols[p]) whose scores pos / neg the forward produced (dg_decoder_hinge_f32): with
+ * a_p = [neg[p] - (pos[p] - margin) > 0] and M = L·G·L (L = diag(l), NULL = I),
+ *     grad_rows[p] = -a_p·M·v_p,  grad_rows[n + p] = a_p·M·v_p,  grad_cols[p] = a_p·Mᵀ·(un_p - u_p)
+ *     dM = Σ_p a_p·(un_p - u_p)·v_pᵀ;   dG = L·dM·L   (if dG != NULL)
+ *     dl[a] = Σ_b dM[a][b]G[a][b]l[b] + Σ_c dM[c][a]G[c][a]l[c]   (if dl != NULL; needs l)
+ *     dG_diag[a] = dG[a][a]                                      (if dG_diag != NULL)
+ * grad_rows is [2n][d], grad_cols [n][d] (dense rows; dg_scatter_rows_f32 adds them into the
+ * embedding gradients).  workspace: 16-byte aligned, dg_decoder_grad_workspace(n, d) bytes.
+ * d % 32 == 0, d <= 256.  Replaces the gradient of optimizer.py:51-57, :63-85, :116-120. */
+int64_t dg_decoder_grad_workspace(int32_t n, int32_t d);
+int dg_decoder_grad_f32(const float* row_table, int64_t ld_row, const float* col_table,
+                        int64_t ld_col, const int32_t* rows, const int32_t* cols,
+                        const int32_t* neg_rows, int32_t n, const float* pos, const float* neg,
+                        const float* G, const float* l, int32_t d, float margin,
+                        float* grad_rows, float* grad_cols, float* dG, float* dl, float* dG_diag,
+                        void* workspace, int64_t workspace_bytes, void* stream);
+
+/* out[idx[q]][:] += Σ_{q' : idx[q'] = idx[q]} src[q'][:]  (occurrences summed in q' order,
+ * each distinct row written once).  The gradient of tf.gather (optimizer.py:66-76).
+ * d <= 256; 0 <= idx[q] < rows of out (the caller's contract). */
+int dg_scatter_rows_f32(const int32_t* idx, int32_t n, const float* src, int32_t d, float* out,
+                        int64_t ld_out, void* stream);
+
+/* Backward of y_g = l2_normalize(s_g) for every group g of one node type (layers.py:93,
+ * :117; model.py:75): dy' = dy ∘ [mask > 0] (mask = the relu output, or NULL), then
+ *     ds_g = dy'·inv − s_g·inv³·(s_g·dy')·[Σs_g² >= 1e-12],   inv = rsqrt(max(Σs_g², 1e-12))
+ * (tf.maximum passes its gradient to Σs² where Σs² >= ε).  All rows [n_rows][d], 16-byte
+ * aligned; d % 4 == 0, d <= 256. */
+typedef struct dg_l2g_group {
+    const float* s;             /* [n_rows][d] the pre-normalisation sum (forward) */
+    float* ds;                  /* [n_rows][d] its gradient (output) */
+} dg_l2g_group;
+
+int dg_l2norm_grad_f32(const dg_l2g_group* groups /* HOST array */, int32_t n_groups,
+                       const float* dy, const float* mask, int32_t n_rows, int32_t d,
+                       void* stream);
+
+/* TF 1.8 ApplyAdam (use_nesterov = false) on up to DG_MAX_ADAM_SEGS segments in one launch:
+ *     m += (g − m)(1 − β1);  v += (g² − v)(1 − β2);  param −= alpha·m / (sqrt(v) + ε)
+ * with alpha = lr·sqrt(1 − β2^t)/(1 − β1^t) computed by the caller in fp32 (as TF does).
+ * grad NULL = a zero gradient (TF updates every variable each step).  16-byte aligned. */
+#define DG_MAX_ADAM_SEGS 32
+
+typedef struct dg_adam_seg {
+    float* param;
+    const float* grad;          /* or NULL */
+    float* m;
+    float* v;
+    int64_t n;
+} dg_adam_seg;
+
+int dg_adam_f32(const dg_adam_seg* segs /* HOST array */, int32_t n_segs, float alpha, float beta1,
+                float beta2, float eps, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, draw

@@ -148,3 +148,140 @@ def unigram_distribution(degrees: np.ndarray, distortion: float = 0.75) -> np.nd
     """Probabilities of tf.nn.fixed_unigram_candidate_sampler (optimizer.py:40-47)."""
     w = np.power(np.asarray(degrees, np.float64), distortion)
     return w / w.sum()
+
+
+# ----------------------------------------------------------------------------------------
+# Training step: gradients of the hinge cost and TF 1.8's Adam update
+# (DecagonOptimizer._build, decagon/deep/optimizer.py:108-114).  The reference delegates
+# both to TensorFlow (tf.train.AdamOptimizer(...).minimize(cost)); restated here by hand:
+# reverse-mode through model.py:64-88 and optimizer.py:51-57, 116-120.
+# ----------------------------------------------------------------------------------------
+def sparse_t_dense_matmul(coo, dense: np.ndarray, n_cols: int) -> np.ndarray:
+    """Aᵀ·G: the gradient of tf.sparse_tensor_dense_matmul(A, X) w.r.t. X."""
+    coords, values, _ = coo
+    coords = np.asarray(coords, dtype=np.int64).reshape(-1, 2)
+    values = np.asarray(values, dtype=np.float64)
+    out = np.zeros((n_cols, dense.shape[1]), dtype=np.float64)
+    if coords.shape[0]:
+        np.add.at(out, coords[:, 1], values[:, None] * dense[coords[:, 0]])
+    return out
+
+
+def l2_normalize_rows_grad(x: np.ndarray, dy: np.ndarray) -> np.ndarray:
+    """Gradient of tf.nn.l2_normalize(x, dim=1) = x·rsqrt(max(Σx², ε)): the max passes its
+    gradient to Σx² where Σx² >= ε (tf.maximum's gradient mask), so
+        dx = dy·inv − x·inv³·(x·dy)·[Σx² >= ε],  inv = rsqrt(max(Σx², ε))."""
+    ss = np.sum(x * x, axis=1, keepdims=True)
+    inv = 1.0 / np.sqrt(np.maximum(ss, EPS_L2))
+    dot = np.sum(x * dy, axis=1, keepdims=True)
+    return dy * inv - x * (inv ** 3) * dot * (ss >= EPS_L2)
+
+
+def train_grads(edge_types, adj, feats, w1, w2, decoders, dec_params, d2: int, batch, neg, e: int,
+                rt: int, ct: int, margin: float):
+    """Forward (model.py:64-88, optimizer.py:51-57) and the hinge cost's gradient w.r.t.
+    every variable, as TF's minimize() computes it (float64).
+
+    feats[j] is None for identity features.  batch [B, 2] local (row, col) ids of the edge
+    type; neg [B] the negative row ids; e the flat relation index (edge-type order).
+    Returns (cost, grads) with grads = {"w1": {et: [K arrays]}, "w2": {...},
+    "dec": {et: {var name: array}}} — every variable gets a gradient (zeros when the cost
+    does not reach it: TF's gather/concat gradients are dense zeros, not None)."""
+    ets = list(edge_types)
+    n_nodes = {}
+    for (i, j) in ets:
+        n_nodes[i] = int(adj[i, j][0][2][0])
+        n_nodes[j] = int(adj[i, j][0][2][1])
+    x1 = {}
+    for (i, j) in ets:
+        x1[i, j] = [w if feats.get(j) is None else _features_times(feats[j], w) for w in w1[i, j]]
+    S1 = {et: np.sum([sparse_dense_matmul(a, x) for a, x in zip(adj[et], x1[et])], axis=0) for et in ets}
+    pre1 = {}
+    for (i, j) in ets:
+        pre1[i] = pre1.get(i, 0.0) + l2_normalize_rows(S1[i, j])
+    H1 = {i: np.maximum(v, 0.0) for i, v in pre1.items()}
+    P = {(i, j): [H1[j] @ w for w in w2[i, j]] for (i, j) in ets}
+    S2 = {et: np.sum([sparse_dense_matmul(a, p) for a, p in zip(adj[et], P[et])], axis=0) for et in ets}
+    E = {}
+    for (i, j) in ets:
+        E[i] = E.get(i, 0.0) + l2_normalize_rows(S2[i, j])
+
+    inters, varies = latent_matrices(edge_types, decoders, dec_params, d2)
+    G, L = inters[e], varies[e]
+    M = L @ G @ L
+    rows, cols = np.asarray(batch)[:, 0], np.asarray(batch)[:, 1]
+    neg = np.asarray(neg)
+    u, v, un = E[rt][rows], E[ct][cols], E[rt][neg]
+    pos = np.sum((u @ M) * v, axis=1)
+    negs = np.sum((un @ M) * v, axis=1)
+    z = negs - (pos - margin)
+    cost = float(np.sum(np.maximum(z, 0.0)))
+    act = (z > 0).astype(np.float64)           # tf.nn.relu's gradient mask
+    dpos, dneg = -act, act
+    dM = u.T @ (dpos[:, None] * v) + un.T @ (dneg[:, None] * v)
+    dE = {i: np.zeros_like(E[i]) for i in E}
+    np.add.at(dE[rt], rows, dpos[:, None] * (v @ M.T))
+    np.add.at(dE[rt], neg, dneg[:, None] * (v @ M.T))
+    np.add.at(dE[ct], cols, dpos[:, None] * (u @ M) + dneg[:, None] * (un @ M))
+    dG = L.T @ dM @ L.T                          # M = L·G·L
+    dL = dM @ (G @ L).T + (L @ G).T @ dM
+
+    # decoder variables: only relation e's entries of latent_inters / latent_varies get a
+    # nonzero gradient; the rest are zeros of the variables' shapes
+    dec = {}
+    flat = 0
+    for et in ets:
+        kind = decoders[et]
+        p = dec_params.get(et, {})
+        g = {name: np.zeros_like(np.asarray(val, np.float64)) for name, val in p.items()}
+        for k in range(edge_types[et]):
+            if flat == e:
+                if kind == "distmult":
+                    g["relation_%d" % k] += np.diag(dG)
+                elif kind == "bilinear":
+                    g["relation_%d" % k] += dG
+                elif kind == "dedicom":
+                    g["global_interaction"] += dG
+                    g["local_variation_%d" % k] += np.diag(dL)
+            flat += 1
+        dec[et] = g
+
+    gw2, dH1 = {}, {j: np.zeros_like(H1[j]) for j in H1}
+    for (i, j) in ets:
+        dS2 = l2_normalize_rows_grad(S2[i, j], dE[i])
+        gw2[i, j] = []
+        for a, w in zip(adj[i, j], w2[i, j]):
+            dP = sparse_t_dense_matmul(a, dS2, n_nodes[j])
+            gw2[i, j].append(H1[j].T @ dP)
+            dH1[j] += dP @ w.T
+    dpre1 = {i: dH1[i] * (pre1[i] > 0) for i in dH1}   # tf.nn.relu's gradient mask (model.py:75)
+    gw1 = {}
+    for (i, j) in ets:
+        dS1 = l2_normalize_rows_grad(S1[i, j], dpre1[i])
+        gw1[i, j] = []
+        for a in adj[i, j]:
+            dX = sparse_t_dense_matmul(a, dS1, n_nodes[j])
+            if feats.get(j) is not None:
+                dX = sparse_t_dense_matmul(feats[j], dX, int(feats[j][2][1]))
+            gw1[i, j].append(dX)
+    return cost, {"w1": gw1, "w2": gw2, "dec": dec}
+
+
+def adam_tf(param: np.ndarray, grad: np.ndarray, m: np.ndarray, v: np.ndarray, t: int,
+            lr: float = 0.001, beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8):
+    """One tf.train.AdamOptimizer step (TF 1.8 ApplyAdam, use_nesterov=False) in float32,
+    as TF runs it on float32 variables; t is the 1-based step.  The beta powers are float32
+    variables multiplied by beta once per step, and
+        alpha = lr·sqrt(1 − β2^t)/(1 − β1^t);  m += (g − m)(1 − β1);  v += (g² − v)(1 − β2);
+        param −= alpha·m / (sqrt(v) + ε).
+    Returns new (param, m, v) as float32."""
+    f = np.float32
+    b1p, b2p = f(beta1), f(beta2)
+    for _ in range(t - 1):
+        b1p, b2p = f(b1p * f(beta1)), f(b2p * f(beta2))
+    alpha = f(f(lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p))
+    g = np.asarray(grad, np.float32)
+    m = (m + (g - m) * (f(1) - f(beta1))).astype(np.float32)
+    v = (v + (g * g - v) * (f(1) - f(beta2))).astype(np.float32)
+    p = (param - (m * alpha) / (np.sqrt(v) + f(eps))).astype(np.float32)
+    return p, m, v

@@ -1,0 +1,222 @@
+"""GPU: the training step (opt_op, grads_vars — decagon/deep/optimizer.py:108-114) against
+the oracle's float64 gradients (oracle/decagon_oracle.train_grads, itself checked against
+torch.autograd on the CPU in test_cpu_train_oracle.py) and TF 1.8's Adam restated in
+float32 (oracle.adam_tf); plus the backward kernels one by one.
+
+Tolerance: per gradient tensor max|g − g_ref| ≤ 1e-4·max|g_ref| (fp32 path).
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+from oracle import decagon_oracle as orc
+from test_gpu_model import _setup
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+TOL = 1e-4
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _oracle_inputs(z, model, edge_types):
+    w1 = {et: [model.layers1[et].vars["weights_%d" % k].eval().astype(np.float64) for k in range(K)]
+          for et, K in edge_types.items()}
+    w2 = {et: [model.layers2[et].vars["weights_%d" % k].eval().astype(np.float64) for k in range(K)]
+          for et, K in edge_types.items()}
+    dec = {et: {n: v.eval().astype(np.float64) for n, v in model.edge_type2decoder[et].vars.items()}
+           for et in edge_types}
+    adj = {et: [(z[f"adj_{et[0]}_{et[1]}_{k}_coords"], z[f"adj_{et[0]}_{et[1]}_{k}_values"],
+                 tuple(int(s) for s in z[f"adj_{et[0]}_{et[1]}_{k}_shape"])) for k in range(K)]
+           for et, K in edge_types.items()}
+    return w1, w2, dec, adj
+
+
+def _batch_feed(z, ph, opt, feed, b):
+    e, rt, ct = (int(v) for v in z[f"batch{b}_meta"])
+    f = dict(feed)
+    f.update({ph["batch"]: z[f"batch{b}_edges"], ph["batch_edge_type_idx"]: e, ph["batch_row_edge_type"]: rt,
+              ph["batch_col_edge_type"]: ct, opt.neg_samples: z[f"batch{b}_neg"]})
+    return f, e, rt, ct
+
+
+@pytest.mark.parametrize("b", [0, 1, 2, 3])
+def test_grads_vars_match_oracle(golden_S, b):
+    """Every variable's gradient (all four decoder kinds of config S appear across batches)."""
+    z = golden_S
+    dg, ph, model, opt, feed = _setup(z)
+    edge_types = model.edge_types
+    decoders = model.decoders
+    f, e, rt, ct = _batch_feed(z, ph, opt, feed, b)
+    sess = dg.Session()
+    gv = sess.run(opt.grads_vars, feed_dict=f)
+    w1, w2, dec, adj = _oracle_inputs(z, model, edge_types)
+    cost, ref = orc.train_grads(edge_types, adj, {0: None, 1: None}, w1, w2, decoders, dec, 32,
+                                z[f"batch{b}_edges"], z[f"batch{b}_neg"], e, rt, ct, 0.1)
+    want = []
+    for et, K in edge_types.items():
+        want += [ref["w1"][et][k] for k in range(K)]
+    for et, K in edge_types.items():
+        want += [ref["w2"][et][k] for k in range(K)]
+    for et in edge_types:
+        want += [ref["dec"][et][n] for n in model.edge_type2decoder[et].vars]
+    assert len(gv) == len(want)
+    nonzero = 0
+    for (g, v), w in zip(gv, want):
+        assert g.shape == w.shape
+        scale = np.max(np.abs(w))
+        if scale == 0:
+            assert np.max(np.abs(g)) == 0.0  # unreachable variables: exact zeros, as TF's
+        else:
+            nonzero += 1
+            assert np.max(np.abs(g - w)) <= TOL * scale, f"gradient off by {rel_err(g, w):.2e}"
+    assert nonzero > 0
+
+
+def test_opt_op_is_one_tf_adam_step(golden_S):
+    """opt_op = forward + backward + ApplyAdam: params after two steps equal adam_tf applied to
+    the device's own gradients (fetched by grads_vars on the same state), and the cost
+    fetched with opt_op is the pre-update cost."""
+    z = golden_S
+    dg, ph, model, opt, feed = _setup(z)
+    f, e, rt, ct = _batch_feed(z, ph, opt, feed, 3)
+    sess = dg.Session()
+    params = [v for v in model.vars.values()]
+    m = [np.zeros(p.shape, np.float32) for p in params]
+    v = [np.zeros(p.shape, np.float32) for p in params]
+    for t in (1, 2):
+        gv = sess.run(opt.grads_vars, feed_dict=f)
+        before = [p.eval() for p in params]
+        _, cost = sess.run([opt.opt_op, opt.cost], feed_dict=f)
+        after = [p.eval() for p in params]
+        for i, ((g, _), p0, p1) in enumerate(zip(gv, before, after)):
+            pw, m[i], v[i] = orc.adam_tf(p0, g, m[i], v[i], t)
+            assert np.max(np.abs(p1 - pw)) <= 1e-6 * max(1.0, np.max(np.abs(pw))), params[i].name
+        if t == 1:
+            assert abs(float(cost) - float(z["batch3_cost"])) <= TOL * abs(float(z["batch3_cost"]))
+    # training moves the cost down on the batch it fits
+    c_end = sess.run(opt.cost, feed_dict=f)
+    assert float(c_end) < float(z["batch3_cost"])
+
+
+def test_adam_kernel_matches_tf_restatement():
+    from decagon_amd import kernels, train
+
+    dev = _dev()
+    rng = np.random.default_rng(1)
+    sizes = [1, 3, 4, 4097, 5000]
+    p = [rng.standard_normal(n).astype(np.float32) for n in sizes]
+    g = [rng.standard_normal(n).astype(np.float32) for n in sizes]
+    dp = [torch.from_numpy(x.copy()).to(dev) for x in p]
+    dgr = [torch.from_numpy(x).to(dev) for x in g]
+    st = train.AdamState(dp)
+    grads = [dgr[0], None, dgr[2], dgr[3], dgr[4]]  # None: a zero gradient
+    op = st.prepared(grads)
+    m = [np.zeros(n, np.float32) for n in sizes]
+    v = [np.zeros(n, np.float32) for n in sizes]
+    for t in (1, 2, 3):
+        op(train.adam_alpha(0.01, t), train.BETA1, train.BETA2, train.EPSILON)
+        for i in range(len(sizes)):
+            gi = g[i] if grads[i] is not None else np.zeros_like(g[i])
+            p[i], m[i], v[i] = orc.adam_tf(p[i], gi, m[i], v[i], t, lr=0.01)
+    torch.cuda.synchronize()
+    for i in range(len(sizes)):
+        assert np.max(np.abs(dp[i].cpu().numpy() - p[i])) <= 1e-6
+        assert np.max(np.abs(st.m[i].cpu().numpy() - m[i])) <= 1e-6
+
+
+@pytest.mark.parametrize("kind", ["dedicom", "distmult", "bilinear", "innerproduct"])
+def test_decoder_grad_kernel(kind):
+    from decagon_amd import kernels
+
+    dev = _dev()
+    rng = np.random.default_rng(2)
+    d, n, nr, nc = 32, 300, 50, 40
+    U = rng.standard_normal((nr, d)).astype(np.float32)
+    V = rng.standard_normal((nc, d)).astype(np.float32)
+    rows, cols, negs = rng.integers(0, nr, n), rng.integers(0, nc, n), rng.integers(0, nr, n)
+    G = rng.standard_normal((d, d)).astype(np.float32) if kind in ("dedicom", "bilinear") else \
+        (np.diag(rng.standard_normal(d)).astype(np.float32) if kind == "distmult" else np.eye(d, dtype=np.float32))
+    l = rng.standard_normal(d).astype(np.float32) if kind == "dedicom" else None
+    L = np.diag(l) if l is not None else np.eye(d)
+    M = L @ G.astype(np.float64) @ L
+    pos = np.sum((U[rows] @ M) * V[cols], 1)
+    neg = np.sum((U[negs] @ M) * V[cols], 1)
+    a = ((neg - (pos - 0.1)) > 0).astype(np.float64)
+    T = lambda x, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(x)).to(dev, dt)  # noqa: E731
+    dG = torch.zeros(d * d, device=dev) if kind in ("dedicom", "bilinear") else None
+    dl = torch.zeros(d, device=dev) if kind == "dedicom" else None
+    dgd = torch.zeros(d, device=dev) if kind == "distmult" else None
+    op = kernels.PreparedDecoderGrad(T(U), T(V), T(rows, torch.int32), T(cols, torch.int32), T(negs, torch.int32),
+                                     T(pos), T(neg), T(G), T(l) if l is not None else None, 0.1,
+                                     dG=dG, dl=dl, dG_diag=dgd)
+    op()
+    torch.cuda.synchronize()
+    gr = op.grad_rows.cpu().numpy()
+    gc = op.grad_cols.cpu().numpy()
+    mv = V[cols] @ M.T
+    assert rel_err(gr[:n], -a[:, None] * mv) <= 1e-5
+    assert rel_err(gr[n:], a[:, None] * mv) <= 1e-5
+    assert rel_err(gc, a[:, None] * ((U[negs] - U[rows]) @ M)) <= 1e-5
+    dM = (a[:, None] * (U[negs] - U[rows])).T @ V[cols]
+    if dG is not None:
+        assert rel_err(dG.cpu().numpy().reshape(d, d), L.T @ dM @ L.T) <= 1e-5
+    if dl is not None:
+        ref = np.diag(dM @ (G @ L).T + (L @ G).T @ dM)
+        assert rel_err(dl.cpu().numpy(), ref) <= 1e-5
+    if dgd is not None:
+        assert rel_err(dgd.cpu().numpy(), np.diag(dM)) <= 1e-5
+
+
+def test_scatter_rows_and_l2norm_grad():
+    from decagon_amd import kernels
+
+    dev = _dev()
+    rng = np.random.default_rng(3)
+    n, d, nrow = 700, 32, 90
+    idx = rng.integers(0, nrow, n).astype(np.int32)
+    src = rng.standard_normal((n, d)).astype(np.float32)
+    out0 = rng.standard_normal((nrow, d)).astype(np.float32)
+    out = torch.from_numpy(out0.copy()).to(dev)
+    kernels.scatter_rows(torch.from_numpy(idx).to(dev), torch.from_numpy(src).to(dev), out)
+    ref = out0.astype(np.float64)
+    np.add.at(ref, idx, src)
+    assert rel_err(out.cpu().numpy(), ref) <= 1e-6
+    # l2 normalisation backward, with a relu mask and all-zero rows
+    for dd in (32, 64, 12):
+        S = rng.standard_normal((nrow, dd)).astype(np.float32)
+        S[::7] = 0.0
+        dy = rng.standard_normal((nrow, dd)).astype(np.float32)
+        mask = rng.standard_normal((nrow, dd)).astype(np.float32)
+        T = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
+        ds = torch.empty((nrow, dd), device=dev)
+        kernels.PreparedL2Grad([(T(S), ds)], T(dy), T(mask), nrow, dd)()
+        torch.cuda.synchronize()
+        want = orc.l2_normalize_rows_grad(S.astype(np.float64), dy * (mask > 0))
+        assert rel_err(ds.cpu().numpy(), want) <= 1e-5
+
+
+def test_gemm_batch_reduce():
+    """dg_gemm_f32's batch-reduce mode: Σ over runs of R batches, run partials in order."""
+    from decagon_amd import kernels
+
+    dev = _dev()
+    rng = np.random.default_rng(4)
+    K, n_j, c, h = 70, 45, 32, 64
+    dP = rng.standard_normal((K, n_j, c)).astype(np.float32)
+    W = rng.standard_normal((K, h, c)).astype(np.float32)
+    R = 32
+    runs = -(-K // R)
+    out = torch.zeros((runs, n_j, h), device=dev)
+    kernels.PreparedGemm(torch.from_numpy(dP).to(dev), (n_j * c, c, 1), torch.from_numpy(W).to(dev), (h * c, 1, c),
+                         out, (n_j * h, h, 1), n_j, h, c, K, reduce=R)()
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for q in range(runs):
+        ref = sum(dP[b].astype(np.float64) @ W[b].T.astype(np.float64) for b in range(q * R, min(K, q * R + R)))
+        assert rel_err(got[q], ref) <= 1e-5
