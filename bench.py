@@ -55,6 +55,9 @@ def parse():
                     help="steps captured back to back in one hipGraph (must divide --steps and --warmup)")
     ap.add_argument("--target-waves", type=int, default=32768)
     ap.add_argument("--chunk", type=int, default=None)
+    ap.add_argument("--train", action="store_true",
+                    help="S / P: time the TRAINING step (forward + hinge-cost backward + Adam on every "
+                         "variable, optimizer.py:108-114) instead of the forward step; one GPU")
     ap.add_argument("--force-shard", action="store_true",
                     help="run the relation-sharded (N > 1) plan and its collectives even at N = 1 "
                          "(launch under torchrun: a rehearsal of the multi-GPU step on one GPU)")
@@ -97,7 +100,7 @@ def build_workload(args, rank, world, sharded):
     return graph, shard, scaling, workload
 
 
-def make_plan(args, graph, shard, device):
+def make_plan(args, graph, shard, device, keep_sums=False):
     import torch
 
     from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
@@ -114,7 +117,8 @@ def make_plan(args, graph, shard, device):
     w2 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, H1, H2)).to(device)
                        for et, K in graph.edge_types.items()})
     plan = ForwardPlan(dg, {j: None for j in n}, w1, w2, H1, H2,
-                       allreduce=None if shard is None else shard.allreduce)
+                       allreduce=None if shard is None else shard.allreduce, keep_sums=keep_sums)
+    plan.w1, plan.w2 = w1, w2
     return plan, dg
 
 
@@ -318,6 +322,89 @@ def main_decoder(args):
     print(json.dumps(rec), file=JSON_OUT, flush=True)
 
 
+def main_train(args):
+    """The training step of DecagonOptimizer.opt_op (optimizer.py:108-114) on one GPU: the
+    forward in flat mode (pre-normalisation sums kept), the DEDICOM decoder + hinge on B
+    positives / B device-sampled negatives, the backward through the decoder, both GCN
+    layers (every relation's W1/W2 gradient) and ApplyAdam on every variable — one hipGraph
+    per step group, Adam's beta powers advanced on the device."""
+    import torch
+
+    from decagon_amd import kernels, train
+
+    torch.cuda.set_device(0)
+    device = torch.device("cuda", 0)
+    graph, shard, scaling, workload = build_workload(args, 0, 1, False)
+    plan, dg = make_plan(args, graph, None, device, keep_sums=True)
+    dec = Decoder(graph, plan, device, 0)
+    tp = train.TrainPlan(plan, plan.w1, plan.w2, {j: None for j in graph.n_nodes})
+    dR = torch.zeros_like(dec.R)
+    dl = torch.zeros_like(dec.l)
+    f = dec.fused
+    dgrad = kernels.PreparedDecoderGrad(dec.E, dec.E, dec.rows, dec.cols, f.neg_rows, f.pos, f.neg, dec.R, dec.l,
+                                        MARGIN, dG=dR.view(-1), dl=dl)
+
+    def decoder_grad(dE):
+        dgrad()
+        kernels.scatter_rows(dgrad.row_idx, dgrad.grad_rows, dE[1])
+        kernels.scatter_rows(dec.cols, dgrad.grad_cols, dE[1])
+
+    ets = list(graph.edge_types)
+    params = [plan.w1.stacks[et] for et in ets] + [plan.w2.stacks[et] for et in ets] + [dec.R, dec.l]
+    grads = [tp.gW1[et] for et in ets] + [tp.gW2[et] for et in ets] + [dR, dl]
+    adam = train.AdamState(params, lr=0.001)
+    prep = adam.prepared(grads)
+
+    def step():
+        plan.run()
+        dec()
+        tp.backward(decoder_grad)
+        adam.apply(prep)
+
+    stream = torch.cuda.Stream(device)
+    G = args.graph_steps if args.steps % max(1, args.graph_steps) == 0 and args.warmup % max(1, args.graph_steps) == 0 else 1
+    with torch.cuda.stream(stream):
+        step()
+        stream.synchronize()
+        loss0 = float(f.loss[0])
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg, stream=stream):
+            for _ in range(G):
+                step()
+        for _ in range(args.warmup // G):
+            cg.replay()
+        stream.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps // G):
+            cg.replay()
+        stream.synchronize()
+        el = time.perf_counter() - t0
+        loss1 = float(f.loss[0])
+    params_n = int(sum(p.numel() for p in params))
+    rec = {
+        "metric": "GCN training-step edges/sec (forward + backward + Adam), " + ("5-relation synthetic" if args.config == "S" else "polypharmacy-shaped"),
+        "value": 2 * dg.total_nnz * args.steps / el,
+        "unit": "edges/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (as the forward bench), random glorot weights, device-sampled negatives",
+        "config": {"workload": workload + "; training step: backward + TF-Adam on %d parameters" % params_n,
+                   "nnz_per_layer_total": dg.total_nnz, "parallelism": "1 GPU", "hipgraph": True,
+                   "steps_per_graph": G},
+        "loss_first_step": loss0,
+        "loss_last_step": loss1,
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    print(json.dumps(rec), file=JSON_OUT, flush=True)
+
+
 def main():
     args = parse()
     # stdout carries exactly one JSON line: libraries that print to fd 1 (RCCL prints its
@@ -327,6 +414,8 @@ def main():
     os.dup2(2, 1)
     if args.config == "D":
         return main_decoder(args)
+    if args.train:
+        return main_train(args)
     import torch
     import torch.distributed as dist
 

@@ -112,6 +112,7 @@ class DgAdamSeg(ctypes.Structure):
 SIGNATURES = {
     "dg_abi_version": (c_int32, []),
     "dg_spmm_groups_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
+    "dg_spmm_groups_lds_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_csr_f32": (
         c_int32,
         [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32,
@@ -127,6 +128,8 @@ SIGNATURES = {
         [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     ),
     "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_int32, c_void_p]),
+    "dg_gemm_tn_f32": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_int32,
+                                 c_int32, c_int32, c_int32, c_void_p, c_void_p]),
     "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
     "dg_staged_order": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
@@ -151,10 +154,13 @@ SIGNATURES = {
          c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_int64, c_void_p],
     ),
-    "dg_scatter_rows_f32": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
+    "dg_scatter_rows_f32": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int64, c_int32,
+                                      c_void_p]),
     "dg_l2norm_grad_f32": (c_int32, [POINTER(DgL2gGroup), c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                      c_void_p]),
-    "dg_adam_f32": (c_int32, [POINTER(DgAdamSeg), c_int32, c_float, c_float, c_float, c_float, c_void_p]),
+    "dg_adam_f32": (c_int32, [POINTER(DgAdamSeg), c_int32, c_float, c_float, c_float, c_float, c_void_p,
+                              c_void_p]),
+    "dg_adam_advance": (c_int32, [c_void_p, c_float, c_float, c_float, c_void_p]),
     "dg_unigram_sample": (
         c_int32,
         [c_void_p, c_int32, c_int32, c_uint64, c_uint64, c_void_p, c_void_p],

@@ -269,7 +269,104 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
     }
 }
 
+// C_b = Aᵀ·B_b with A shared ([rows][M], row stride lda) and B_b = b + b*b_bs ([rows][N],
+// row stride ldb): the weight gradient H_jᵀ·dP_k of the per-relation projections (the
+// backward of layers.py:113).  The reduction runs over `rows` (up to the node count), so a
+// workgroup takes one (batch, row split) and its 4 waves interleave the split's row pairs,
+// each on MT×NT accumulators of v_mfma_f32_32x32x2_f32 (both operand fragments are rows of
+// A / B read by 32 consecutive lanes: coalesced); the waves meet in LDS in wave order.
+struct TnArgs {
+    const float* a;
+    const float* b;
+    float* out;            // [batch][M][N], or the split partials [n_split][batch][M][N]
+    int64_t lda, ldb, b_bs;
+    int32_t rows, M, N, batch;
+    int32_t n_split, rows_per_split;
+};
+
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(const TnArgs a) {
+    __shared__ float red[4][MT * NT][16][64];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int i = lane & 31, h = lane >> 5;
+    const int b = blockIdx.x / a.n_split;
+    const int s = blockIdx.x - b * a.n_split;
+    const int r_begin = s * a.rows_per_split;
+    const int r_end = min(a.rows, r_begin + a.rows_per_split);
+    const float* A = a.a;
+    const float* B = a.b + (int64_t)b * a.b_bs;
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x16{};
+#pragma unroll 4
+    for (int r0 = r_begin + 2 * w; r0 < r_end; r0 += 8) {
+        const int r = r0 + h;
+        const bool ok = r < r_end;
+        float af[MT], bf[NT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) af[mt] = ok ? A[(int64_t)r * a.lda + mt * 32 + i] : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bf[nt] = ok ? B[(int64_t)r * a.ldb + nt * 32 + i] : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mt], bf[nt], acc[mt][nt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[w][mt * NT + nt][r][lane] = acc[mt][nt][r];
+    __syncthreads();
+    float* out = a.out + ((int64_t)s * a.batch + b) * a.M * a.N;
+    for (int e = threadIdx.x; e < MT * NT * 1024; e += 256) {
+        const int q = e >> 10, r = (e >> 6) & 15, l = e & 63;
+        const float v = red[0][q][r][l] + red[1][q][r][l] + red[2][q][r][l] + red[3][q][r][l];
+        const int mt = q / NT, nt = q - mt * NT;
+        const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+        out[(int64_t)row * a.N + nt * 32 + (l & 31)] = v;
+    }
+}
+
 }  // namespace
+
+extern "C" int dg_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t b_bs, float* c,
+                              int32_t rows, int32_t M, int32_t N, int32_t batch, int32_t n_split, float* partial,
+                              void* stream) {
+    if (rows < 0 || batch < 0 || n_split < 1) return DG_EINVAL;
+    if (M < 32 || N < 32 || (M & 31) || (N & 31) || (M / 32) * (N / 32) > 4) return DG_EINVAL;
+    if (lda < M || ldb < N) return DG_EINVAL;
+    if (batch == 0) return DG_OK;
+    if (!a || !b || !c || (n_split > 1 && !partial)) return DG_EINVAL;
+    if (n_split > 1 && !dg::aligned16(partial)) return DG_EALIGN;
+    TnArgs t{a, b, n_split > 1 ? partial : c, lda, ldb, b_bs, rows, M, N, batch, n_split,
+             2 * dg::ceil_div(dg::ceil_div(rows, n_split), 2)};
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t blocks = (int64_t)batch * n_split;
+    if (blocks > 0x7fffffff) return DG_EINVAL;
+    dim3 grid(static_cast<unsigned>(blocks)), block(256);
+    const int mt = M / 32, nt = N / 32;
+    if (mt == 1 && nt == 1) hipLaunchKernelGGL((gemm_tn_kernel<1, 1>), grid, block, 0, st, t);
+    else if (mt == 2 && nt == 1) hipLaunchKernelGGL((gemm_tn_kernel<2, 1>), grid, block, 0, st, t);
+    else if (mt == 1 && nt == 2) hipLaunchKernelGGL((gemm_tn_kernel<1, 2>), grid, block, 0, st, t);
+    else if (mt == 2 && nt == 2) hipLaunchKernelGGL((gemm_tn_kernel<2, 2>), grid, block, 0, st, t);
+    else if (mt == 4 && nt == 1) hipLaunchKernelGGL((gemm_tn_kernel<4, 1>), grid, block, 0, st, t);
+    else if (mt == 1 && nt == 4) hipLaunchKernelGGL((gemm_tn_kernel<1, 4>), grid, block, 0, st, t);
+    else if (mt == 3 && nt == 1) hipLaunchKernelGGL((gemm_tn_kernel<3, 1>), grid, block, 0, st, t);
+    else if (mt == 1 && nt == 3) hipLaunchKernelGGL((gemm_tn_kernel<1, 3>), grid, block, 0, st, t);
+    else return DG_EINVAL;
+    int rc = dg::launch_status();
+    if (rc != DG_OK || n_split == 1) return rc;
+    // the split partials, summed in split order (dg_gcn_epilogue_f32 without flags)
+    if (!dg::aligned16(c)) return DG_EALIGN;
+    dg_epi_group g{partial, n_split, 0};
+    return dg_gcn_epilogue_f32(&g, 1, c, batch * M, N, 0, stream);
+}
 
 extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stream) {
     if (!descs || n_desc < 1) return DG_EINVAL;

@@ -347,9 +347,89 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
     if (qok && cg == 0) *reinterpret_cast<float4*>(a.out + off) = tot;
 }
 
+// Partial mode over a SMALL shared operand (every nonzero of the launch gathers from one
+// dense X of at most kLdsRowsMax rows — the backward's Âᵀ·dS, whose operand dS_ij is the
+// same for all K relations of the group): a workgroup copies a 32-float column slice of X
+// into LDS once (rows 144 B apart: the 16-byte bank slot of float4 j of row v is
+// (9v + j) mod 16, a bijection of v mod 16), then each of its 1024 threads owns one
+// (chunk, row) item and walks that row's nonzeros — two (vcol, val) loads ahead — with 8
+// ds_read_b128 + 32 fmaf per nonzero.  No per-relation barrier, no operand re-read.
+constexpr int kLdsSlice = 32;                 // floats per column slice
+constexpr int kLdsRowF4 = 9;                  // float4 slots per staged row (8 + 1 pad)
+constexpr int kLdsRowsMax = 160 * 1024 / (16 * kLdsRowF4);
+
+struct LdsGroupK {
+    const int32_t* rowptr;
+    const int32_t* vcol;
+    const float* val;
+    const float* x;
+    float* out;
+    int32_t x_ld;
+    int32_t x_rows;
+    int32_t n_items;      // n_chunks * n_rows
+    int32_t item_blocks;  // ceil(n_items / 1024)
+    int32_t block_begin;
+    int32_t pad;
+};
+
+struct LdsArgs {
+    LdsGroupK g[DG_MAX_GROUPS];
+    int32_t n_groups;
+    int32_t d;
+    int32_t n_slices;
+    int32_t pad;
+};
+
+__global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
+    extern __shared__ float4 xs[];
+    const int b = blockIdx.x;
+    int gi = 0;
+#pragma unroll 1
+    while (gi + 1 < a.n_groups && b >= a.g[gi + 1].block_begin) ++gi;
+    const LdsGroupK& g = a.g[gi];
+    const int lb = b - g.block_begin;
+    const int s = lb / g.item_blocks;             // column slice
+    const int ib = lb - s * g.item_blocks;        // item block
+    const int d = a.d;
+    const int c0 = s * kLdsSlice;
+    const int cw = min(kLdsSlice, d - c0);        // columns of this slice (multiple of 4)
+    for (int q = threadIdx.x; q < g.x_rows * 8; q += blockDim.x) {
+        const int v = q >> 3, j = q & 7;
+        xs[v * kLdsRowF4 + j] = 4 * j < cw ? *reinterpret_cast<const float4*>(g.x + (int64_t)v * g.x_ld + c0 + 4 * j)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int item = ib * blockDim.x + threadIdx.x;
+    if (item >= g.n_items) return;  // no barrier below
+    float4 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int beg = g.rowptr[item], end = g.rowptr[item + 1];
+    int vc = 0, vc1 = 0;
+    float vv = 0.f, vv1 = 0.f;
+    if (beg < end) { vc = g.vcol[beg]; vv = g.val[beg]; }
+    if (beg + 1 < end) { vc1 = g.vcol[beg + 1]; vv1 = g.val[beg + 1]; }
+#pragma unroll 1
+    for (int p = beg; p < end; ++p) {
+        const int cv = vc;
+        const float w = vv;
+        vc = vc1;
+        vv = vv1;
+        if (p + 2 < end) { vc1 = g.vcol[p + 2]; vv1 = g.val[p + 2]; }
+        const float4* xr = xs + cv * kLdsRowF4;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dg::fma4(acc[j], w, xr[j]);
+    }
+    float* o = g.out + (int64_t)item * d + c0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (4 * j < cw) *reinterpret_cast<float4*>(o + 4 * j) = acc[j];
+}
+
 }  // namespace
 
 extern "C" int32_t dg_abi_version(void) { return 14; }
+
 
 namespace {
 
@@ -509,5 +589,51 @@ extern "C" int dg_gcn_epilogue_f32(const dg_epi_group* groups, int32_t n_groups,
 #define DG_LAUNCH_EPI(L) hipLaunchKernelGGL(epilogue_kernel<L>, grid, block, 0, st, a)
     DG_LP_SWITCH(lp, DG_LAUNCH_EPI)
 #undef DG_LAUNCH_EPI
+    return dg::launch_status();
+}
+
+extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_groups, int32_t d, void* stream) {
+    if (n_groups < 0 || (n_groups > 0 && groups == nullptr)) return DG_EINVAL;
+    if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
+    if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
+    LdsArgs a{};
+    a.d = d;
+    a.n_slices = dg::ceil_div(d, kLdsSlice);
+    int64_t blocks = 0;
+    int max_rows = 0;
+    for (int i = 0; i < n_groups; ++i) {
+        const dg_rel_group& s = groups[i];
+        if (s.n_rows == 0) continue;
+        SpmmGroupK k;
+        const int rc = convert_group(s, d, true, k);
+        if (rc != DG_OK) return rc;
+        if (s.x_rows > kLdsRowsMax || !dg::aligned16(s.out)) return s.x_rows > kLdsRowsMax ? DG_EINVAL : DG_EALIGN;
+        const int64_t items = (int64_t)s.n_chunks * s.n_rows;
+        if (items > 0x7fffffff) return DG_EINVAL;
+        LdsGroupK& g = a.g[a.n_groups++];
+        g.rowptr = k.rowptr;
+        g.vcol = k.vcol;
+        g.val = k.val;
+        g.x = k.x;
+        g.out = k.out;
+        g.x_ld = k.x_ld;
+        g.x_rows = s.x_rows;
+        g.n_items = static_cast<int32_t>(items);
+        g.item_blocks = dg::ceil_div(items, 1024);
+        g.block_begin = static_cast<int32_t>(blocks);
+        blocks += (int64_t)g.item_blocks * a.n_slices;
+        if (blocks > 0x7fffffff) return DG_EINVAL;
+        max_rows = s.x_rows > max_rows ? s.x_rows : max_rows;
+    }
+    if (blocks == 0) return DG_OK;
+    const int lds = max_rows * kLdsRowF4 * 16;
+    static bool configured = false;
+    if (!configured) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmm_lds_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        configured = true;
+    }
+    hipLaunchKernelGGL(spmm_lds_kernel, dim3(static_cast<unsigned>(blocks)), dim3(1024), lds,
+                       reinterpret_cast<hipStream_t>(stream), a);
     return dg::launch_status();
 }

@@ -160,11 +160,12 @@ __global__ __launch_bounds__(256) void decoder_grad_vec_kernel(const float* dM, 
 // (optimizer.py:75-76).  One wave per q; the wave of a row's first occurrence sums every
 // occurrence in order and owns the read-modify-write, so rows are updated once, race-free.
 __global__ __launch_bounds__(256) void scatter_rows_kernel(const int32_t* idx, int n, const float* src, int d,
-                                                           float* out, int64_t ld_out) {
+                                                           float* out, int64_t ld_out, int n_out) {
     const int lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= n) return;
     const int r = idx[q];
+    if (r < 0 || r >= n_out) return;  // outside the table: no row to update (wave-uniform)
     for (int q0 = 0; q0 < q; q0 += 64) {
         const int j = q0 + lane;
         if (__any(j < q && idx[j] == r)) return;  // an earlier occurrence owns the row
@@ -251,6 +252,7 @@ struct AdamSegK {
 
 struct AdamArgs {
     AdamSegK s[DG_MAX_ADAM_SEGS];
+    const float* state;  // device {β1^t, β2^t, alpha} or NULL (then `alpha`)
     int32_t n_segs;
     float alpha;
     float beta1;
@@ -264,10 +266,10 @@ constexpr int kAdamF4PerBlock = 256 * 4;  // float4s per block (4 per thread)
 // TF 1.8 ApplyAdam (use_nesterov = false), element-wise in fp32:
 //   m += (g − m)(1 − β1);  v += (g² − v)(1 − β2);  p −= alpha·m / (sqrt(v) + ε)
 // alpha = lr·sqrt(1 − β2^t)/(1 − β1^t) is computed by the caller as TF does (fp32).
-__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, const AdamArgs& a) {
+__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float alpha, const AdamArgs& a) {
     m += (g - m) * (1.0f - a.beta1);
     v += (g * g - v) * (1.0f - a.beta2);
-    p -= (m * a.alpha) / (sqrtf(v) + a.eps);
+    p -= (m * alpha) / (sqrtf(v) + a.eps);
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
@@ -276,6 +278,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
 #pragma unroll 1
     while (si + 1 < a.n_segs && b >= a.s[si + 1].block_begin) ++si;
     const AdamSegK& s = a.s[si];
+    const float alpha = a.state ? a.state[2] : a.alpha;
     const int64_t f0 = (int64_t)(b - s.block_begin) * kAdamF4PerBlock;
     const int64_t nf4 = s.n >> 2;
 #pragma unroll
@@ -286,10 +289,10 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
             float4 m = reinterpret_cast<float4*>(s.m)[f];
             float4 v = reinterpret_cast<float4*>(s.v)[f];
             const float4 g = s.g ? reinterpret_cast<const float4*>(s.g)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-            adam1(p.x, g.x, m.x, v.x, a);
-            adam1(p.y, g.y, m.y, v.y, a);
-            adam1(p.z, g.z, m.z, v.z, a);
-            adam1(p.w, g.w, m.w, v.w, a);
+            adam1(p.x, g.x, m.x, v.x, alpha, a);
+            adam1(p.y, g.y, m.y, v.y, alpha, a);
+            adam1(p.z, g.z, m.z, v.z, alpha, a);
+            adam1(p.w, g.w, m.w, v.w, alpha, a);
             reinterpret_cast<float4*>(s.p)[f] = p;
             reinterpret_cast<float4*>(s.m)[f] = m;
             reinterpret_cast<float4*>(s.v)[f] = v;
@@ -299,7 +302,18 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     const int64_t tail0 = nf4 << 2;
     if (tail0 < s.n && f0 <= nf4 && nf4 < f0 + kAdamF4PerBlock && threadIdx.x < s.n - tail0) {
         const int64_t e = tail0 + threadIdx.x;
-        adam1(s.p[e], s.g ? s.g[e] : 0.f, s.m[e], s.v[e], a);
+        adam1(s.p[e], s.g ? s.g[e] : 0.f, s.m[e], s.v[e], alpha, a);
+    }
+}
+
+// TF's _finish: β1^t, β2^t ← ·β1, ·β2 (float32 variables), then the next step's
+// alpha = lr·sqrt(1 − β2^t)/(1 − β1^t).
+__global__ void adam_advance_kernel(float* state, float lr, float beta1, float beta2) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const float b1p = state[0] * beta1, b2p = state[1] * beta2;
+        state[0] = b1p;
+        state[1] = b2p;
+        state[2] = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
     }
 }
 
@@ -346,12 +360,12 @@ extern "C" int dg_decoder_grad_f32(const float* row_table, int64_t ld_row, const
 }
 
 extern "C" int dg_scatter_rows_f32(const int32_t* idx, int32_t n, const float* src, int32_t d, float* out,
-                                   int64_t ld_out, void* stream) {
-    if (n < 0 || d < 1 || d > 256 || ld_out < d) return DG_EINVAL;
+                                   int64_t ld_out, int32_t n_out_rows, void* stream) {
+    if (n < 0 || d < 1 || d > 256 || ld_out < d || n_out_rows < 0) return DG_EINVAL;
     if (n == 0) return DG_OK;
     if (!idx || !src || !out) return DG_EINVAL;
     hipLaunchKernelGGL(scatter_rows_kernel, dim3(dg::ceil_div(n, 4)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), idx, n, src, d, out, ld_out);
+                       reinterpret_cast<hipStream_t>(stream), idx, n, src, d, out, ld_out, n_out_rows);
     return dg::launch_status();
 }
 
@@ -393,10 +407,11 @@ extern "C" int dg_l2norm_grad_f32(const dg_l2g_group* groups, int32_t n_groups, 
 }
 
 extern "C" int dg_adam_f32(const dg_adam_seg* segs, int32_t n_segs, float alpha, float beta1, float beta2,
-                           float eps, void* stream) {
+                           float eps, const float* state, void* stream) {
     if (n_segs < 0 || (n_segs > 0 && !segs)) return DG_EINVAL;
     if (n_segs > DG_MAX_ADAM_SEGS) return DG_ETOOMANY;
     AdamArgs a{};
+    a.state = state;
     a.alpha = alpha;
     a.beta1 = beta1;
     a.beta2 = beta2;
@@ -422,5 +437,12 @@ extern "C" int dg_adam_f32(const dg_adam_seg* segs, int32_t n_segs, float alpha,
     if (blocks == 0) return DG_OK;
     hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), a);
+    return dg::launch_status();
+}
+
+extern "C" int dg_adam_advance(float* state, float lr, float beta1, float beta2, void* stream) {
+    if (!state) return DG_EINVAL;
+    hipLaunchKernelGGL(adam_advance_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), state, lr,
+                       beta1, beta2);
     return dg::launch_status();
 }

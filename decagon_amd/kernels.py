@@ -96,10 +96,14 @@ def _fill_group(g, s: RelGroupSpec) -> None:
     g.x_rows = s.x_rows
 
 
-class PreparedSpmm:
-    """A fixed dg_spmm_groups_f32 launch (descriptor block built once)."""
+SPMM_LDS_MAX_ROWS = 160 * 1024 // 144  # dg_spmm_groups_lds_f32: operand rows staged in LDS
 
-    def __init__(self, specs: Sequence[RelGroupSpec], d: int):
+
+class PreparedSpmm:
+    """A fixed dg_spmm_groups_f32 launch (descriptor block built once); lds=True: the
+    dg_spmm_groups_lds_f32 form for small shared operands (x_rows <= SPMM_LDS_MAX_ROWS)."""
+
+    def __init__(self, specs: Sequence[RelGroupSpec], d: int, lds: bool = False):
         if len(specs) > _lib.DG_MAX_GROUPS:
             raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups per launch")
         for s in specs:
@@ -112,10 +116,13 @@ class PreparedSpmm:
             _fill_group(g, s)
         self._arr = arr
         self._n = len(specs)
-        self._fn = _lib.load().dg_spmm_groups_f32
+        if lds and any(s.x_rows > SPMM_LDS_MAX_ROWS for s in specs):
+            raise ValueError("dg_spmm_groups_lds_f32: operand too large for LDS")
+        self._name = "dg_spmm_groups_lds_f32" if lds else "dg_spmm_groups_f32"
+        self._fn = getattr(_lib.load(), self._name)
 
     def __call__(self, stream: Optional[torch.cuda.Stream] = None) -> None:
-        check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_groups_f32")
+        check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), self._name)
 
 
 @dataclass
@@ -432,6 +439,32 @@ class PreparedGemmMulti:
         check(self._fn(self._arr, self._n, _stream_ptr(stream)), "dg_gemm_f32")
 
 
+class PreparedGemmTN:
+    """dg_gemm_tn_f32: c[b] = aᵀ·b_stack[b] for a [rows][M] shared and b_stack [batch][rows][N]
+    (contiguous), c [batch][M][N]; the rows split into ranges of about `rows_per_split`."""
+
+    def __init__(self, a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, rows_per_split: int = 0):
+        _dev(a, torch.float32, "a")
+        _dev(b, torch.float32, "b")
+        _dev(c, torch.float32, "c")
+        rows, M = a.shape
+        batch, rb, N = b.shape
+        if rb != rows or tuple(c.shape) != (batch, M, N):
+            raise ValueError("gemm_tn: shapes")
+        if rows_per_split <= 0:  # enough workgroups to fill the chip, ranges of >= 64 rows
+            self.n_split = max(1, min(-(-2048 // max(1, batch)), -(-rows // 64)))
+        else:
+            self.n_split = max(1, -(-rows // max(2, rows_per_split)))
+        self.partial = (torch.empty((self.n_split, batch, M, N), device=a.device) if self.n_split > 1 else None)
+        self._keep = (a, b, c)
+        self._args = (a.data_ptr(), M, b.data_ptr(), N, rows * N, c.data_ptr(), rows, M, N, batch, self.n_split,
+                      self.partial.data_ptr() if self.partial is not None else None)
+        self._fn = _lib.load().dg_gemm_tn_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(*self._args, _stream_ptr(stream)), "dg_gemm_tn_f32")
+
+
 def matmul(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
            sa: Optional[torch.Tensor] = None, sc: Optional[torch.Tensor] = None, stream=None):
     """out = diag-scaled a @ b for 2-D fp32 device tensors (any strides)."""
@@ -645,7 +678,8 @@ class PreparedDecoderGrad:
         lib = _lib.load()
         nbytes = int(lib.dg_decoder_grad_workspace(n, d))
         self._ws = torch.empty(max(1, nbytes // 4), device=dev)
-        self.row_idx = torch.cat([rows, neg_rows])  # scatter order: positives, then negatives
+        self.row_idx = torch.empty(2 * n, device=dev, dtype=torch.int32)  # positives, then negatives
+        self._rows, self._negs = rows, neg_rows
         self._keep = (row_table, col_table, rows, cols, neg_rows, pos, neg, G, l, dG, dl, dG_diag)
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         self._args = [row_table.data_ptr(), row_table.shape[1], col_table.data_ptr(), col_table.shape[1],
@@ -656,20 +690,23 @@ class PreparedDecoderGrad:
 
     def __call__(self, stream=None) -> None:
         check(self._fn(*self._args, _stream_ptr(stream)), "dg_decoder_grad_f32")
+        n = self._rows.numel()  # the scatter's row index list (negatives may be resampled per step)
+        self.row_idx[:n].copy_(self._rows)
+        self.row_idx[n:].copy_(self._negs)
 
 
 def scatter_rows(idx: torch.Tensor, src: torch.Tensor, out: torch.Tensor, stream=None) -> None:
-    """out[idx[q]] += Σ src[q'] over the occurrences q' of idx[q] (fixed order)."""
+    """out[idx[q]] += Σ src[q'] over the occurrences q' of idx[q] (fixed order); indices
+    outside out's rows update nothing (checked on the device: no host synchronisation, so
+    the call is capturable)."""
     _dev(idx, torch.int32, "idx")
     _dev(src, torch.float32, "src")
     _dev(out, torch.float32, "out")
     n = idx.numel()
     if src.dim() != 2 or src.shape[0] != n or out.dim() != 2 or out.shape[1] != src.shape[1]:
         raise ValueError("scatter_rows: shapes")
-    if n and (int(idx.min()) < 0 or int(idx.max()) >= out.shape[0]):
-        raise ValueError("scatter_rows: index out of range")
     check(_lib.load().dg_scatter_rows_f32(idx.data_ptr(), n, src.data_ptr(), src.shape[1], out.data_ptr(),
-                                          out.stride(0), _stream_ptr(stream)), "dg_scatter_rows_f32")
+                                          out.stride(0), out.shape[0], _stream_ptr(stream)), "dg_scatter_rows_f32")
 
 
 class PreparedL2Grad:
@@ -721,6 +758,19 @@ class PreparedAdam:
         self._keep = list(segs)
         self._fn = _lib.load().dg_adam_f32
 
-    def __call__(self, alpha: float, beta1: float, beta2: float, eps: float, stream=None) -> None:
+    def __call__(self, alpha: float, beta1: float, beta2: float, eps: float,
+                 state: Optional[torch.Tensor] = None, stream=None) -> None:
+        """alpha from the argument, or (state given: device float[3] {β1^t, β2^t, alpha}) from
+        the device — the graph-capturable form."""
+        sp = None
+        if state is not None:
+            _dev(state, torch.float32, "adam state")
+            sp = state.data_ptr()
         for arr, n in self._arrs:
-            check(self._fn(arr, n, alpha, beta1, beta2, eps, _stream_ptr(stream)), "dg_adam_f32")
+            check(self._fn(arr, n, alpha, beta1, beta2, eps, sp, _stream_ptr(stream)), "dg_adam_f32")
+
+
+def adam_advance(state: torch.Tensor, lr: float, beta1: float, beta2: float, stream=None) -> None:
+    """β1^t, β2^t ← ·β1, ·β2 and the next alpha, on the device (TF's _finish)."""
+    _dev(state, torch.float32, "adam state")
+    check(_lib.load().dg_adam_advance(state.data_ptr(), lr, beta1, beta2, _stream_ptr(stream)), "dg_adam_advance")

@@ -277,15 +277,13 @@ class DecagonOptimizer:
         key = ("adam", id(self))
         cache = ctx.session.caches
         if key not in cache:
-            st = train.AdamState(params)
+            st = train.AdamState(params, lr=float(FLAGS.learning_rate))
             cache[key] = (st, {})
         st, prepared = cache[key]
         pk = tuple(g.data_ptr() for g in grads)
         if pk not in prepared:
             prepared[pk] = st.prepared(grads)
-        st.t += 1
-        alpha = train.adam_alpha(float(FLAGS.learning_rate), st.t)
-        prepared[pk](alpha, train.BETA1, train.BETA2, train.EPSILON)
+        st.apply(prepared[pk])
         return None
 
     def _grads_vars(self, model, tp, dec_grads):

@@ -10,7 +10,7 @@ the backward graph automatically; here it is written out over the forward's save
   decoder + gathers                   dE_i (dg_decoder_grad_f32 + dg_scatter_rows_f32)
   layer 2                             dS2_ij = l2n'(S2_ij)·dE_i            dg_l2norm_grad_f32
                                       dP_ijk = Â_kᵀ·dS2_ij                 dg_spmm_groups_f32 (Âᵀ)
-                                      dW2_ijk = H1_jᵀ·dP_ijk               dg_gemm_f32
+                                      dW2_ijk = H1_jᵀ·dP_ijk               dg_gemm_tn_f32
                                       dH1_j = Σ_ik dP_ijk·W2_ijkᵀ          dg_gemm_f32 (batch-reduce)
                                                                            + dg_gcn_epilogue_f32
   layer 1                             dS1_ij = l2n'(S1_ij)·(dH1_i∘[H1_i>0]) dg_l2norm_grad_f32
@@ -64,16 +64,25 @@ def adam_alpha(lr: float, t: int, beta1: float = BETA1, beta2: float = BETA2) ->
 
 
 class AdamState:
-    """m / v slots of a list of parameters (zeros at creation, as TF's slots) and the step."""
+    """m / v slots of a list of parameters (zeros at creation, as TF's slots) and the beta
+    powers + alpha on the device ({β1^t, β2^t, alpha}, advanced after every update), so a
+    whole training step is capturable into one hipGraph."""
 
-    def __init__(self, params: Sequence[torch.Tensor]):
+    def __init__(self, params: Sequence[torch.Tensor], lr: float = 0.001):
         self.params = list(params)
+        self.lr = float(lr)
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
-        self.t = 0
+        dev = self.params[0].device if self.params else torch.device("cuda")
+        self.state = torch.tensor([BETA1, BETA2, adam_alpha(self.lr, 1)], dtype=torch.float32, device=dev)
 
     def prepared(self, grads: Sequence[Optional[torch.Tensor]]) -> kernels.PreparedAdam:
         return kernels.PreparedAdam([(p, g, m, v) for p, g, m, v in zip(self.params, grads, self.m, self.v)])
+
+    def apply(self, prepared: kernels.PreparedAdam) -> None:
+        """One ApplyAdam over every segment, then the beta powers / alpha advance."""
+        prepared(0.0, BETA1, BETA2, EPSILON, state=self.state)
+        kernels.adam_advance(self.state, self.lr, BETA1, BETA2)
 
 
 class TrainPlan:
@@ -124,9 +133,8 @@ class TrainPlan:
             specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, n[i], vcol_max=vmax))
             specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, self.gW1[et], n[j], K, h1, n[i], vcol_max=vmax))
             H = fwd.hidden1[j]
-            # dW2_k = H1_jᵀ·dP_k: A(m, k) = H1_j[k][m]
-            gemm_w2.append(kernels.PreparedGemm(H, (0, 1, h1), dP, (n[j] * h2, h2, 1), self.gW2[et],
-                                                (h1 * h2, h2, 1), h1, h2, n[j], K))
+            # dW2_k = H1_jᵀ·dP_k (reduction over the n_j rows, split for long ones)
+            gemm_w2.append(kernels.PreparedGemmTN(H, dP, self.gW2[et]))
             # dH1_j partials = Σ_k dP_k·W2_kᵀ over runs of R relations: B(c, m) = W2_k[m][c]
             R = K if K <= 64 else 32
             n_runs = -(-K // R)
@@ -135,9 +143,14 @@ class TrainPlan:
                                                 (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R))
             runs[j].append((part, n_runs))
         chunked = lambda xs: [xs[s:s + DG_MAX_GROUPS] for s in range(0, len(xs), DG_MAX_GROUPS)]  # noqa: E731
-        self._spmm2 = [kernels.PreparedSpmm(c, h2) for c in chunked(specs2)]
-        self._spmm1 = [kernels.PreparedSpmm(c, h1) for c in chunked(specs1)]
-        self._gemm_w2 = [kernels.PreparedGemmMulti(c) for c in chunked(gemm_w2)]
+        # Âᵀ·dS: operands small enough for LDS (the drug side) take the LDS-staged form
+        small = lambda s: s.x_rows <= kernels.SPMM_LDS_MAX_ROWS  # noqa: E731
+        self._spmm2, self._spmm1 = [], []
+        for specs, d, out in ((specs2, h2, self._spmm2), (specs1, h1, self._spmm1)):
+            for lds in (True, False):
+                sel = [s for s in specs if small(s) == lds]
+                out += [kernels.PreparedSpmm(c, d, lds=lds) for c in chunked(sel)]
+        self._gemm_w2 = gemm_w2
         self._gemm_h1 = [kernels.PreparedGemmMulti(c) for c in chunked(gemm_h1)]
         self._epi_h1 = []
         for j, lst in runs.items():

@@ -75,6 +75,15 @@ int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_gr
 
 /* Single relation, plain CSR: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
  * Replaces one tf.sparse_tensor_dense_matmul (layers.py:90).  ldy must equal d. */
+/* The same partial-mode product (out[c][r][:] = Σ val·X[vcol][:]) for groups whose whole
+ * dense operand is small — x_rows <= 1137 rows (it is staged in LDS, 144 B per row per
+ * 32-column slice): the backward's Âᵀ·dS_ij, where every relation of the group reads the
+ * same dS_ij (decagon_amd/train.py).  out must be 16-byte aligned; other requirements as
+ * dg_spmm_groups_f32.  Replaces the gradient of tf.sparse_tensor_dense_matmul w.r.t. its
+ * dense operand (layers.py:90, :114). */
+int dg_spmm_groups_lds_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups, int32_t d,
+                           void* stream);
+
 int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                     int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx, float* y,
                     int64_t ldy, int32_t d, void* stream);
@@ -234,6 +243,15 @@ int dg_gemm_f32(const dg_gemm_desc* descs /* HOST array */, int32_t n_desc, void
  * — the backward's Σ_k dP_k·W_kᵀ (gradient of the per-relation projections, layers.py:113)
  * as partial sums that dg_gcn_epilogue_f32 (no flags) adds up. */
 
+/* Batched Aᵀ·B over a long reduction (the weight gradient H_jᵀ·dP_k, backward of
+ * layers.py:113):  C_b[m][n] = Σ_{r < rows} A[r*lda + m] · B[b*b_bs + r*ldb + n],  C
+ * contiguous [batch][M][N].  M, N multiples of 32 with (M/32)(N/32) <= 4.  With n_split > 1
+ * the rows are cut into n_split ranges whose partials ([n_split][batch][M][N], caller's
+ * 16-byte aligned `partial`) are then summed in range order. */
+int dg_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t b_bs, float* c,
+                   int32_t rows, int32_t M, int32_t N, int32_t batch, int32_t n_split, float* partial,
+                   void* stream);
+
 /* --------------------------------------------------------------------------------------
  * Edge decoder scores (T8 + T9):  for pair p,
  *     u = row_table[row_idx[p]],  v = col_table[col_idx[p]]       (rows of length d)
@@ -309,9 +327,10 @@ int dg_decoder_grad_f32(const float* row_table, int64_t ld_row, const float* col
 
 /* out[idx[q]][:] += Σ_{q' : idx[q'] = idx[q]} src[q'][:]  (occurrences summed in q' order,
  * each distinct row written once).  The gradient of tf.gather (optimizer.py:66-76).
- * d <= 256; 0 <= idx[q] < rows of out (the caller's contract). */
+ * d <= 256; indices outside [0, n_out_rows) update nothing (device-side guard: the
+ * indices may be sampled on the device, where the host cannot check them). */
 int dg_scatter_rows_f32(const int32_t* idx, int32_t n, const float* src, int32_t d, float* out,
-                        int64_t ld_out, void* stream);
+                        int64_t ld_out, int32_t n_out_rows, void* stream);
 
 /* Backward of y_g = l2_normalize(s_g) for every group g of one node type (layers.py:93,
  * :117; model.py:75): dy' = dy ∘ [mask > 0] (mask = the relu output, or NULL), then
@@ -329,8 +348,11 @@ int dg_l2norm_grad_f32(const dg_l2g_group* groups /* HOST array */, int32_t n_gr
 
 /* TF 1.8 ApplyAdam (use_nesterov = false) on up to DG_MAX_ADAM_SEGS segments in one launch:
  *     m += (g − m)(1 − β1);  v += (g² − v)(1 − β2);  param −= alpha·m / (sqrt(v) + ε)
- * with alpha = lr·sqrt(1 − β2^t)/(1 − β1^t) computed by the caller in fp32 (as TF does).
- * grad NULL = a zero gradient (TF updates every variable each step).  16-byte aligned. */
+ * alpha = lr·sqrt(1 − β2^t)/(1 − β1^t): read from state[2] when `state` (device, float[3] =
+ * {β1^t, β2^t, alpha}) is non-NULL — graph-capturable, advanced on the device by
+ * dg_adam_advance after the update, as TF's _finish advances its beta-power variables —
+ * else the `alpha` argument.  grad NULL = a zero gradient (TF updates every variable each
+ * step).  16-byte aligned.  Initial state: {β1, β2, lr·sqrt(1 − β2)/(1 − β1)}. */
 #define DG_MAX_ADAM_SEGS 32
 
 typedef struct dg_adam_seg {
@@ -342,7 +364,8 @@ typedef struct dg_adam_seg {
 } dg_adam_seg;
 
 int dg_adam_f32(const dg_adam_seg* segs /* HOST array */, int32_t n_segs, float alpha, float beta1,
-                float beta2, float eps, void* stream);
+                float beta2, float eps, const float* state, void* stream);
+int dg_adam_advance(float* state, float lr, float beta1, float beta2, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, draw

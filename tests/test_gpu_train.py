@@ -114,13 +114,17 @@ def test_adam_kernel_matches_tf_restatement():
     g = [rng.standard_normal(n).astype(np.float32) for n in sizes]
     dp = [torch.from_numpy(x.copy()).to(dev) for x in p]
     dgr = [torch.from_numpy(x).to(dev) for x in g]
-    st = train.AdamState(dp)
+    st = train.AdamState(dp, lr=0.01)
     grads = [dgr[0], None, dgr[2], dgr[3], dgr[4]]  # None: a zero gradient
     op = st.prepared(grads)
     m = [np.zeros(n, np.float32) for n in sizes]
     v = [np.zeros(n, np.float32) for n in sizes]
     for t in (1, 2, 3):
-        op(train.adam_alpha(0.01, t), train.BETA1, train.BETA2, train.EPSILON)
+        if t == 2:  # the host-alpha form of the same step
+            op(train.adam_alpha(0.01, t), train.BETA1, train.BETA2, train.EPSILON)
+            kernels.adam_advance(st.state, 0.01, train.BETA1, train.BETA2)
+        else:  # device beta powers (graph-capturable)
+            st.apply(op)
         for i in range(len(sizes)):
             gi = g[i] if grads[i] is not None else np.zeros_like(g[i])
             p[i], m[i], v[i] = orc.adam_tf(p[i], gi, m[i], v[i], t, lr=0.01)
@@ -128,6 +132,7 @@ def test_adam_kernel_matches_tf_restatement():
     for i in range(len(sizes)):
         assert np.max(np.abs(dp[i].cpu().numpy() - p[i])) <= 1e-6
         assert np.max(np.abs(st.m[i].cpu().numpy() - m[i])) <= 1e-6
+    assert abs(float(st.state[2]) - train.adam_alpha(0.01, 4)) <= 1e-7
 
 
 @pytest.mark.parametrize("kind", ["dedicom", "distmult", "bilinear", "innerproduct"])
@@ -220,3 +225,61 @@ def test_gemm_batch_reduce():
     for q in range(runs):
         ref = sum(dP[b].astype(np.float64) @ W[b].T.astype(np.float64) for b in range(q * R, min(K, q * R + R)))
         assert rel_err(got[q], ref) <= 1e-5
+
+
+@pytest.mark.parametrize("rows,split", [(645, 1024), (3001, 700), (1, 64)])
+def test_gemm_tn_split(rows, split):
+    """dg_gemm_tn_f32: c[b] = aᵀ·b[b] over a long row reduction, with split partials."""
+    from decagon_amd import kernels
+
+    dev = _dev()
+    rng = np.random.default_rng(5)
+    M, N, batch = 64, 32, 7
+    A = rng.standard_normal((rows, M)).astype(np.float32)
+    B = rng.standard_normal((batch, rows, N)).astype(np.float32)
+    C = torch.empty((batch, M, N), device=dev)
+    kernels.PreparedGemmTN(torch.from_numpy(A).to(dev), torch.from_numpy(B).to(dev), C, rows_per_split=split)()
+    torch.cuda.synchronize()
+    ref = np.einsum("rm,brn->bmn", A.astype(np.float64), B.astype(np.float64))
+    assert rel_err(C.cpu().numpy(), ref) <= 1e-5
+
+
+@pytest.mark.parametrize("d", [64, 32, 12])
+def test_spmm_lds_shared_operand(d):
+    """dg_spmm_groups_lds_f32 = dg_spmm_groups_f32 (partial mode) for a small shared operand:
+    out[k] = Âᵀ_k·X with empty rows and a long row."""
+    from decagon_amd import kernels
+    from decagon_amd.sparse import coo_to_csr, merge_chunks
+    from decagon_amd.train import transpose_csr
+
+    dev = _dev()
+    rng = np.random.default_rng(6)
+    n_i, n_j, K = 300, 200, 5
+    rels = []
+    for k in range(K):
+        nnz = 900
+        r, c = rng.integers(0, n_i, nnz), rng.integers(0, n_j, nnz)
+        c[:60] = 3  # a long column → a long row of Âᵀ
+        c[c == 7] = 8  # an empty row of Âᵀ
+        keys = np.unique(r * n_j + c)
+        co = np.stack([keys // n_j, keys % n_j], 1)
+        rels.append(coo_to_csr(co, rng.standard_normal(len(keys)), (n_i, n_j)))
+    tr = [transpose_csr(x) for x in rels]
+    m = merge_chunks(tr, [0] * K, 1, 1)
+    X = rng.standard_normal((n_i, d)).astype(np.float32)
+    T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    outs = []
+    for lds in (True, False):
+        out = torch.zeros((K, n_j, d), device=dev)
+        spec = kernels.RelGroupSpec(T(m.rowptr), T(m.vcol), T(m.val), T(X), out, n_j, K, d, n_i,
+                                    vcol_max=int(m.vcol.max()))
+        kernels.PreparedSpmm([spec], d, lds=lds)()
+        outs.append(out)
+    torch.cuda.synchronize()
+    for k, rel in enumerate(rels):
+        dense = np.zeros((n_i, n_j))
+        lens = np.diff(rel.rowptr)
+        dense[np.repeat(np.arange(n_i), lens), rel.col] = rel.val
+        ref = dense.T @ X.astype(np.float64)
+        assert rel_err(outs[0][k].cpu().numpy(), ref) <= 1e-5
+    assert rel_err(outs[0].cpu().numpy(), outs[1].cpu().numpy()) <= 1e-6
