@@ -351,12 +351,15 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 // dense X of at most kLdsRowsMax rows — the backward's Âᵀ·dS, whose operand dS_ij is the
 // same for all K relations of the group): a workgroup copies a 32-float column slice of X
 // into LDS once (rows 144 B apart: the 16-byte bank slot of float4 j of row v is
-// (9v + j) mod 16, a bijection of v mod 16), then each of its 1024 threads owns one
-// (chunk, row) item and walks that row's nonzeros — two (vcol, val) loads ahead — with 8
-// ds_read_b128 + 32 fmaf per nonzero.  No per-relation barrier, no operand re-read.
+// (9v + j) mod 16, a bijection of v mod 16), then its 16 waves walk kLdsItems (chunk, row)
+// items, 8 rows at a time per wave: 8 lanes per row, one float4 column piece each.  A row's
+// (vcol, val) pairs come in 8 at a time with one coalesced load per lane group (the next 8
+// prefetched), are handed out by shuffles, and each gathers one ds_read_b128 per lane.
+// No per-relation barrier, no operand re-read from L2.
 constexpr int kLdsSlice = 32;                 // floats per column slice
 constexpr int kLdsRowF4 = 9;                  // float4 slots per staged row (8 + 1 pad)
 constexpr int kLdsRowsMax = 160 * 1024 / (16 * kLdsRowF4);
+constexpr int kLdsItems = 2048;               // (chunk, row) items per workgroup
 
 struct LdsGroupK {
     const int32_t* rowptr;
@@ -367,7 +370,7 @@ struct LdsGroupK {
     int32_t x_ld;
     int32_t x_rows;
     int32_t n_items;      // n_chunks * n_rows
-    int32_t item_blocks;  // ceil(n_items / 1024)
+    int32_t item_blocks;  // ceil(n_items / kLdsItems)
     int32_t block_begin;
     int32_t pad;
 };
@@ -398,32 +401,58 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
         xs[v * kLdsRowF4 + j] = 4 * j < cw ? *reinterpret_cast<const float4*>(g.x + (int64_t)v * g.x_ld + c0 + 4 * j)
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    __syncthreads();
-    const int item = ib * blockDim.x + threadIdx.x;
-    if (item >= g.n_items) return;  // no barrier below
-    float4 acc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int beg = g.rowptr[item], end = g.rowptr[item + 1];
-    int vc = 0, vc1 = 0;
-    float vv = 0.f, vv1 = 0.f;
-    if (beg < end) { vc = g.vcol[beg]; vv = g.val[beg]; }
-    if (beg + 1 < end) { vc1 = g.vcol[beg + 1]; vv1 = g.val[beg + 1]; }
+    __syncthreads();  // the only barrier
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int rg = lane >> 3;                     // row of the wave's 8
+    const int q = lane & 7;                       // float4 piece of the slice
+    const bool qok = 4 * q < cw;
+    // this wave's 128 consecutive items: their 129 row pointers in three registers (one
+    // coalesced load), so a row's range never waits on memory
+    const int wbase = ib * kLdsItems + wave * 128;
+    const int item_end = min(g.n_items, (ib + 1) * kLdsItems);
+    if (wbase >= item_end) return;
+    const int rp0 = g.rowptr[min(wbase + lane, g.n_items)];
+    const int rp1 = g.rowptr[min(wbase + 64 + lane, g.n_items)];
+    const int rp2 = g.rowptr[min(wbase + 128, g.n_items)];
+    auto rp = [&](int idx) {  // row pointer wbase + idx, idx in [0, 128]
+        const int v0 = __shfl(rp0, idx & 63), v1 = __shfl(rp1, idx & 63);
+        return idx < 64 ? v0 : (idx < 128 ? v1 : rp2);
+    };
+    int nb = rp(rg), ne = rp(rg + 1);
+    int npc = nb + q < ne ? g.vcol[nb + q] : 0;
+    float npv = nb + q < ne ? g.val[nb + q] : 0.f;
 #pragma unroll 1
-    for (int p = beg; p < end; ++p) {
-        const int cv = vc;
-        const float w = vv;
-        vc = vc1;
-        vv = vv1;
-        if (p + 2 < end) { vc1 = g.vcol[p + 2]; vv1 = g.val[p + 2]; }
-        const float4* xr = xs + cv * kLdsRowF4;
+    for (int t = 0; t < 16 && wbase + 8 * t < item_end; ++t) {
+        const int item = wbase + 8 * t + rg;
+        const int beg = nb, end = ne;
+        int vc = npc;
+        float vv = npv;
+        if (t < 15) {  // the next 8 rows' ranges and first pairs
+            nb = rp(8 * t + 8 + rg);
+            ne = rp(8 * t + 9 + rg);
+            npc = nb + q < ne ? g.vcol[nb + q] : 0;
+            npv = nb + q < ne ? g.val[nb + q] : 0.f;
+        }
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+        for (int cb = beg; __any(cb < end); cb += 8) {
+            const int cv = vc;
+            const float w = vv;
+            const int p = cb + 8 + q;  // the next 8 pairs of this row
+            vc = p < end ? g.vcol[p] : 0;
+            vv = p < end ? g.val[p] : 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dg::fma4(acc[j], w, xr[j]);
+            for (int u = 0; u < 8; ++u) {
+                const int src = (lane & ~7) + u;
+                const int xv = __shfl(cv, src);
+                const float wv = __shfl(w, src);  // 0 past the row's end
+                const float4 xr = xs[xv * kLdsRowF4 + q];
+                dg::fma4(acc, wv, xr);
+            }
+        }
+        if (item < item_end && qok) *reinterpret_cast<float4*>(g.out + (int64_t)item * d + c0 + 4 * q) = acc;
     }
-    float* o = g.out + (int64_t)item * d + c0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (4 * j < cw) *reinterpret_cast<float4*>(o + 4 * j) = acc[j];
 }
 
 }  // namespace
@@ -619,7 +648,7 @@ extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_grou
         g.x_ld = k.x_ld;
         g.x_rows = s.x_rows;
         g.n_items = static_cast<int32_t>(items);
-        g.item_blocks = dg::ceil_div(items, 1024);
+        g.item_blocks = dg::ceil_div(items, kLdsItems);
         g.block_begin = static_cast<int32_t>(blocks);
         blocks += (int64_t)g.item_blocks * a.n_slices;
         if (blocks > 0x7fffffff) return DG_EINVAL;
