@@ -151,13 +151,14 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         }
     };
     // relation i's tables, straight from global memory (L2-resident, read a relation ahead):
-    // this wave's pair block (woff, rlw diagonals), the largest group, this lane's vinfo
+    // this wave's pair block (woff, rlw diagonals), its largest group, this lane's vinfo
     // (read unconditionally — jm ends with 1024 spare ints; used only by waves with rlw > 0)
     auto tables = [&](int i, int& woff, int& rlw, int& big, int& vi) {
         const int32_t* t = g.jm + __builtin_amdgcn_readfirstlane(jof[i]);
-        big = t[1];
         woff = t[4 + wave];
-        rlw = t[20 + wave];
+        const int rw = t[20 + wave];
+        rlw = rw & 0xFFFF;  // this wave's diagonals
+        big = rw >> 16;     // its largest group (1: no split row, no segment combine)
         vi = t[36 + tid];
     };
     // the pairs of diagonals m .. m+3 of this lane: one coalesced 512-byte load per diagonal

@@ -30,7 +30,7 @@ import torch
 
 from . import kernels
 from ._lib import DG_EPI_L2NORM, DG_EPI_RELU, DG_MAX_GROUPS
-from .sparse import HostCSR, MergedCSR, merge_chunks, staged_layout
+from .sparse import HostCSR, MergedCSR, merge_chunks, merge_windows, staged_layout
 
 EdgeType = Tuple[int, int]
 
@@ -50,6 +50,16 @@ def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
 
 
 STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "512"))  # ~2 rounds on 256 CUs
+
+# Large groups whose relations fit one chunk (PPI: 2 x 19,085^2) are laid out in column
+# windows (sparse.merge_windows): each window's gathers stay in its XCDs' L2.  Measured on
+# config P's PPI (scripts/exp_window.py): d=64 63.6 us merged -> 40.0 us with 2 windows
+# (+5.6 us epilogue); 4 windows 40.8, 8 windows 53.7 (the window partials start to cost).
+WINDOW_MIN_ROWS = int(os.environ.get("DG_WINDOW_MIN_ROWS", "4096"))
+N_WINDOWS = int(os.environ.get("DG_WINDOWS", "2"))
+# node types with at most this many rows finish in the fused row-per-workgroup kernel; larger
+# ones run partial mode + epilogue (one wave per row keeps more gathers in flight)
+FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
 
 
 def staged_out_chunk(grp, d: int) -> int:
@@ -164,7 +174,11 @@ class DeviceGraph:
                 ch = 1
             if ch is None:
                 ch = choose_chunk(len(loc), n_r, nnz, d_policy, target_waves)
-            if loc:
+            windows = (not staged and loc and ch >= len(loc) and n_r >= WINDOW_MIN_ROWS
+                       and N_WINDOWS > 1 and (chunk is None))
+            if windows:
+                m = merge_windows(loc, ids, N_WINDOWS, K)
+            elif loc:
                 m = merge_chunks(loc, ids, ch, K)
             else:
                 m = MergedCSR(np.zeros(n_r + 1, np.int32), np.zeros(0, np.int32), np.zeros(0, np.float32),
@@ -307,8 +321,9 @@ class ForwardPlan:
         if self.flat_mode:
             return []
         return [i for i, ets in self.targets.items()
-                if all(self.g.groups[et].n_chunks == 1 and self.g.groups[et].n_rels > 0
-                       and not self.g.groups[et].staged for et in ets)]
+                if self.g.n_nodes[i] <= FUSED_MAX_ROWS
+                and all(self.g.groups[et].n_chunks == 1 and self.g.groups[et].n_rels > 0
+                        and not self.g.groups[et].staged for et in ets)]
 
     def _spec(self, et, x: torch.Tensor, out, d) -> kernels.RelGroupSpec:
         grp = self.g.groups[et]
@@ -460,22 +475,22 @@ class ForwardPlan:
 
     # ---- accounting (bench / DESIGN.md roofline) ----
     def layer_bytes(self, layer: int) -> int:
-        """Algorithmic (compulsory) HBM bytes of one layer's SpMM launches: the merged CSR
-        once (row pointers 4 B per (chunk,row), vcol+val 8 B per nonzero), every distinct
-        dense operand X_k once (4·d B per row of X_k), the output once — 4·d B per row per
-        chunk partial in partial mode, per output row in fused mode — and, for layer 1, the
-        fused projections' W2 reads and P writes."""
+        """Algorithmic (compulsory) HBM bytes of one layer's SpMM launches: the CSR once
+        (row pointers 4 B per row of each relation, vcol+val 8 B per nonzero), every distinct
+        dense operand X_k once (4·d B per row of X_k), the output once — 4·d B per row of each
+        group's sum S_ij in partial mode (chunk / window partials are the implementation's
+        choice, not counted), per output row in fused mode — and, for layer 1, the fused
+        projections' W2 reads and P writes."""
         L = self._layer1 if layer == 1 else self._layer2
         d = self.h1 if layer == 1 else self.h2
         tot = 0
         for et, grp in self.g.groups.items():
             if not grp.n_rels:
                 continue
-            tot += 4 * (grp.n_chunks * grp.n_rows + 1) + 8 * grp.nnz
+            tot += 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz
             tot += 4 * d * grp.n_cols * grp.n_rels
             if et[0] not in L.fused_targets:
-                n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
-                tot += 4 * d * grp.n_rows * n_out
+                tot += 4 * d * grp.n_rows
         for i in L.fused_targets:
             tot += 4 * d * self.g.n_nodes[i]
         if layer == 1:

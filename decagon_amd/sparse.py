@@ -228,6 +228,41 @@ def merge_chunks(csrs: Sequence[HostCSR], slabs: Sequence[int], chunk: int, n_sl
     return MergedCSR(rowptr.astype(np.int32), vcol, val, n_r, n_c, n_chunks, chunk, n_slabs * n_c)
 
 
+def merge_windows(csrs: Sequence[HostCSR], slabs: Sequence[int], n_windows: int, n_slabs: int) -> MergedCSR:
+    """The chunk-merged layout with COLUMN-WINDOW chunks: chunk w holds, for every row, the
+    nonzeros of every relation whose column lies in window w (columns split into n_windows
+    equal ranges), relation by relation, each relation's in-row order kept.  The partial
+    sums of a row over the windows add up to the row's full sum.  Launched in partial mode,
+    the XCD-contiguous item map puts each window on its own XCDs, so the operand rows a
+    window gathers stay in those XCDs' L2 (large square groups such as PPI)."""
+    if not csrs:
+        raise ValueError("empty relation group")
+    n_r, n_c = csrs[0].shape
+    n_windows = max(1, int(n_windows))
+    edges = np.linspace(0, n_c, n_windows + 1).astype(np.int64)
+    keys, vcols, vals = [], [], []
+    for k, c in enumerate(csrs):
+        if c.shape != (n_r, n_c):
+            raise ValueError("all relations of a group must share one shape")
+        lens = np.diff(c.rowptr.astype(np.int64))
+        rows = np.repeat(np.arange(n_r, dtype=np.int64), lens)
+        win = np.searchsorted(edges, c.col.astype(np.int64), side="right") - 1
+        keys.append(win * n_r + rows)
+        vcols.append(int(slabs[k]) * n_c + c.col.astype(np.int64))
+        vals.append(c.val)
+    key = np.concatenate(keys) if keys else np.zeros(0, np.int64)
+    total = key.shape[0]
+    if total >= 2**31 or n_slabs * n_c >= 2**31:
+        raise ValueError("group exceeds int32 indexing")
+    order = np.argsort(key, kind="stable")  # stable: relation order, then in-row order
+    counts = np.bincount(key, minlength=n_windows * n_r)
+    rowptr = np.zeros(n_windows * n_r + 1, np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    vcol = np.concatenate(vcols)[order].astype(np.int32) if total else np.zeros(0, np.int32)
+    val = np.concatenate(vals)[order].astype(np.float32) if total else np.zeros(0, np.float32)
+    return MergedCSR(rowptr.astype(np.int32), vcol, val, n_r, n_c, n_windows, len(csrs), n_slabs * n_c)
+
+
 @dataclass
 class StagedLayout:
     """Device layout of a group for dg_spmm_staged_f32 (include/decagon_hip.h).
@@ -388,8 +423,11 @@ def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
             rel_pairs[dst, 1] = vval.view(np.int32)
         pairs_parts.append(rel_pairs)
         big = int(max(lgs)) if n_v else 1
+        # per wave: diagonals (low 16 bits) and its largest group (bits 16+): a wave whose
+        # rows are all unsplit skips the segment combine
+        gs_w = np.asarray(lgs, np.int64).reshape(n_w, 64).max(axis=1) if n_w else np.zeros(0, np.int64)
         rl16 = np.zeros(16, np.int64)
-        rl16[:n_w] = rlw
+        rl16[:n_w] = rlw | (gs_w << 16)
         vinfo = (np.asarray(lrow, np.int64) | (np.asarray(lseg, np.int64) << 10)
                  | ((np.asarray(lgs, np.int64) - 1) << 13) | (llen << 16))
         seg = np.concatenate([[n_w, big, 0, 0], woff, rl16, vinfo]).astype(np.int64)

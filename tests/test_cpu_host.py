@@ -218,13 +218,16 @@ def test_staged_layout_reproduces_every_relation():
     for k, m in enumerate(mats):
         jm = lay.jm[lay.jmoff[k]:lay.jmoff[k + 1]]
         n_w, big = int(jm[0]), int(jm[1])
-        woff, rlw = jm[4:20].astype(np.int64), jm[20:36].astype(np.int64)
+        woff, rw = jm[4:20].astype(np.int64), jm[20:36].astype(np.int64)
+        rlw, wbig = rw & 0xFFFF, rw >> 16                                 # per wave: diagonals, largest group
         vinfo = jm[36:].astype(np.int64)
         assert len(vinfo) == 64 * n_w and 64 * n_w <= lanes
         assert np.all(rlw[n_w:] == 0) and np.all(rlw % 4 == 0)
         row, seg, gsz, vlen = vinfo & 1023, (vinfo >> 10) & 7, ((vinfo >> 13) & 7) + 1, vinfo >> 16
         assert np.all(np.diff(vlen) <= 0)                                 # sorted by length
         assert big == (gsz.max() if n_w else 1)
+        for w in range(n_w):
+            assert wbig[w] == gsz[64 * w:64 * w + 64].max()
         for i in range(64 * n_w):                                         # groups inside a wave
             if row[i] != 1023 and seg[i] == 0:
                 assert i // 64 == (i + gsz[i] - 1) // 64
