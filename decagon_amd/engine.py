@@ -60,6 +60,7 @@ N_WINDOWS = int(os.environ.get("DG_WINDOWS", "2"))
 # node types with at most this many rows finish in the fused row-per-workgroup kernel; larger
 # ones run partial mode + epilogue (one wave per row keeps more gathers in flight)
 FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
+CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "1") != "0"
 
 
 def staged_out_chunk(grp, d: int) -> int:
@@ -227,6 +228,7 @@ class ForwardPlan:
         # layer (all-reduced when sharded; kept for the backward when training), and one fused
         # launch over identity "adjacencies" finishes every node type from it
         self.flat_mode = allreduce is not None or keep_sums
+        self.launch_groups: Dict[int, List[EdgeType]] = {}  # id(SpMM launch) -> its groups
         dev = dgraph.device
         f32 = dict(device=dev, dtype=torch.float32)
         self.edge_types = list(dgraph.edge_types)
@@ -278,6 +280,10 @@ class ForwardPlan:
             if et[1] not in self.hidden1:
                 raise ValueError(f"node type {et[1]} has no incoming edge type; layer 2 needs hidden1[{et[1]}]")
             self.proj[et] = torch.empty((K, n[et[1]], h2), **f32)
+
+        # a second stream: a layer's gather-bound launch (dg_spmm_groups_f32) runs beside its
+        # LDS-bound staged launch (dg_spmm_staged_f32) — different units, no data dependence
+        self.side_stream = (torch.cuda.Stream(dev) if dev.type == "cuda" and CONCURRENT_LAUNCHES else None)
 
         # ---- layer 1 (+ the layer-2 projections of rows it finishes) ----
         self.fused = self._fused_targets()
@@ -355,6 +361,7 @@ class ForwardPlan:
             launches.append(kernels.PreparedFused(
                 [(outs[i], n[i], [self._spec(et, xs[et], None, d) for et in self.targets[i]], relu)
                  for i in fused_t], d, pspecs, wpg))
+            self.launch_groups[id(launches[-1])] = [et for i in fused_t for et in self.targets[i]]
         rest = [et for et in self.edge_types if et[0] not in fused_t]
         flags = DG_EPI_L2NORM | (DG_EPI_RELU if relu else 0)
         flat, views = None, {}
@@ -384,10 +391,14 @@ class ForwardPlan:
                     slab_max=int(grp.rel_ids.max())))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
-        launches += [kernels.PreparedStaged(staged[s:s + DG_MAX_GROUPS], d)
-                     for s in range(0, len(staged), DG_MAX_GROUPS)]
-        launches += [kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d)
-                     for s in range(0, len(specs), DG_MAX_GROUPS)]
+        staged_ets = [et for et in rest if g.groups[et].n_rels and g.groups[et].staged]
+        spmm_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged]
+        for s in range(0, len(staged), DG_MAX_GROUPS):
+            launches.append(kernels.PreparedStaged(staged[s:s + DG_MAX_GROUPS], d))
+            self.launch_groups[id(launches[-1])] = staged_ets[s:s + DG_MAX_GROUPS]
+        for s in range(0, len(specs), DG_MAX_GROUPS):
+            launches.append(kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d))
+            self.launch_groups[id(launches[-1])] = spmm_ets[s:s + DG_MAX_GROUPS]
         launches += reduces
         need_zero = flat is not None and any(g.groups[et].n_rels == 0 for et in rest)
         epis = []
@@ -409,7 +420,7 @@ class ForwardPlan:
                 if i in fused_t:
                     continue
                 epis.append(kernels.PreparedEpilogue([partials[et] for et in self.targets[i]], outs[i], n[i], d, flags))
-        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views)
+        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream)
 
     def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
         """A group spec whose 'adjacency' is the identity of node type i (one nonzero 1.0f per
@@ -474,6 +485,33 @@ class ForwardPlan:
         return pick(self._layer1), pick(self._layer2)
 
     # ---- accounting (bench / DESIGN.md roofline) ----
+    def group_bytes(self, et: EdgeType, d: int, fused: bool) -> int:
+        """Algorithmic bytes of one group's SpMM: its CSR once (4 B per row of each
+        relation + 8 B per nonzero), its dense operands once (4·d B per row of each X_k) and,
+        in partial mode, its sum S_ij once (4·d B per output row)."""
+        grp = self.g.groups[et]
+        if not grp.n_rels:
+            return 0
+        tot = 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz + 4 * d * grp.n_cols * grp.n_rels
+        return tot if fused else tot + 4 * d * grp.n_rows
+
+    def launch_bytes(self, launch, layer: int) -> int:
+        """Algorithmic bytes of one SpMM launch of a layer (its groups; a fused launch also
+        writes its targets' rows once, and in layer 1 reads W2 / writes P for its fused
+        projections)."""
+        L = self._layer1 if layer == 1 else self._layer2
+        d = self.h1 if layer == 1 else self.h2
+        ets = self.launch_groups.get(id(launch), [])
+        fused = isinstance(launch, kernels.PreparedFused)
+        tot = sum(self.group_bytes(et, d, fused) for et in ets)
+        if fused:
+            tot += sum(4 * d * self.g.n_nodes[i] for i in L.fused_targets)
+            if layer == 1:
+                for pj in launch._keep[2]:
+                    K, din, dout = pj.w.shape
+                    tot += 4 * pj.n_rels * (din * dout + pj.out.shape[1] * dout)
+        return tot
+
     def layer_bytes(self, layer: int) -> int:
         """Algorithmic (compulsory) HBM bytes of one layer's SpMM launches: the CSR once
         (row pointers 4 B per row of each relation, vcol+val 8 B per nonzero), every distinct
@@ -506,8 +544,10 @@ class ForwardPlan:
 class _Layer:
     """The prepared launches of one layer and how to run them."""
 
-    def __init__(self, launches, flat, need_zero, allreduce, epilogues, fused_targets, views=None):
+    def __init__(self, launches, flat, need_zero, allreduce, epilogues, fused_targets, views=None,
+                 side_stream=None):
         self.launches = launches
+        self.side_stream = side_stream
         self.flat = flat
         self.views = views or {}  # flat mode: (i,j) -> that group's S_ij, [n_i * d]
         self.need_zero = need_zero
@@ -518,9 +558,32 @@ class _Layer:
     def run(self) -> None:
         if self.need_zero:
             self.flat.zero_()  # groups without local relations contribute zeros
-        for l in self.launches:
-            l()
+        self.run_spmm()
         if self.flat is not None and self.allreduce is not None:
             self.allreduce(self.flat)
         for e in self.epilogues:
             e()
+
+    def run_spmm(self) -> None:
+        """The layer's SpMM launches (and chunk reduces), as the forward runs them."""
+        side = [l for l in self.launches if isinstance(l, kernels.PreparedSpmm)]
+        main = [l for l in self.launches if not isinstance(l, kernels.PreparedSpmm)]
+        if (self.side_stream is not None and side
+                and any(isinstance(l, kernels.PreparedStaged) for l in main)):
+            # fork: the gather-bound launches on the side stream, the LDS-bound staged ones
+            # here; join before the chunk reduces / epilogues (graph-capturable)
+            cur = torch.cuda.current_stream()
+            self.side_stream.wait_stream(cur)
+            with torch.cuda.stream(self.side_stream):
+                for l in side:
+                    l()
+            for l in main:
+                if not isinstance(l, kernels.PreparedEpilogue):
+                    l()
+            cur.wait_stream(self.side_stream)
+            for l in main:
+                if isinstance(l, kernels.PreparedEpilogue):
+                    l()
+        else:
+            for l in self.launches:
+                l()
