@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 // dense X of at most kLdsRowsMax rows — the backward's Âᵀ·dS, whose operand dS_ij is the
 // same for all K relations of the group): a workgroup copies a 32-float column slice of X
 // into LDS once (rows 144 B apart: the 16-byte bank slot of float4 j of row v is
-// (9v + j) mod 16, a bijection of v mod 16), then its 16 waves walk kLdsItems (chunk, row)
+// (9v + j) mod 16, a bijection of v mod 16), then its 16 waves walk up to 16 x 128 (chunk, row)
 // items, 8 rows at a time per wave: 8 lanes per row, one float4 column piece each.  A row's
 // (vcol, val) pairs come in 8 at a time with one coalesced load per lane group (the next 8
 // prefetched), are handed out by shuffles, and each gathers one ds_read_b128 per lane.
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 constexpr int kLdsSlice = 32;                 // floats per column slice
 constexpr int kLdsRowF4 = 9;                  // float4 slots per staged row (8 + 1 pad)
 constexpr int kLdsRowsMax = 160 * 1024 / (16 * kLdsRowF4);
-constexpr int kLdsItems = 2048;               // (chunk, row) items per workgroup
+constexpr int kLdsItemsMax = 128;            // (chunk, row) items per wave (at most)
 
 struct LdsGroupK {
     const int32_t* rowptr;
@@ -370,9 +370,9 @@ struct LdsGroupK {
     int32_t x_ld;
     int32_t x_rows;
     int32_t n_items;      // n_chunks * n_rows
-    int32_t item_blocks;  // ceil(n_items / kLdsItems)
+    int32_t item_blocks;  // ceil(n_items / (16 * per_wave))
     int32_t block_begin;
-    int32_t pad;
+    int32_t per_wave;     // items per wave: a multiple of 8, <= kLdsItemsMax
 };
 
 struct LdsArgs {
@@ -407,14 +407,15 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
     const int rg = lane >> 3;                     // row of the wave's 8
     const int q = lane & 7;                       // float4 piece of the slice
     const bool qok = 4 * q < cw;
-    // this wave's 128 consecutive items: their 129 row pointers in three registers (one
-    // coalesced load), so a row's range never waits on memory
-    const int wbase = ib * kLdsItems + wave * 128;
-    const int item_end = min(g.n_items, (ib + 1) * kLdsItems);
+    // this wave's per_wave (<= 128) consecutive items: their row pointers in three registers
+    // (one coalesced load), so a row's range never waits on memory
+    const int pw = g.per_wave;
+    const int wbase = (ib * 16 + wave) * pw;
+    const int item_end = min(g.n_items, wbase + pw);
     if (wbase >= item_end) return;
     const int rp0 = g.rowptr[min(wbase + lane, g.n_items)];
     const int rp1 = g.rowptr[min(wbase + 64 + lane, g.n_items)];
-    const int rp2 = g.rowptr[min(wbase + 128, g.n_items)];
+    const int rp2 = g.rowptr[min(wbase + 128, g.n_items)];  // (read only when pw == 128)
     auto rp = [&](int idx) {  // row pointer wbase + idx, idx in [0, 128]
         const int v0 = __shfl(rp0, idx & 63), v1 = __shfl(rp1, idx & 63);
         return idx < 64 ? v0 : (idx < 128 ? v1 : rp2);
@@ -423,12 +424,12 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
     int npc = nb + q < ne ? g.vcol[nb + q] : 0;
     float npv = nb + q < ne ? g.val[nb + q] : 0.f;
 #pragma unroll 1
-    for (int t = 0; t < 16 && wbase + 8 * t < item_end; ++t) {
+    for (int t = 0; wbase + 8 * t < item_end; ++t) {
         const int item = wbase + 8 * t + rg;
         const int beg = nb, end = ne;
         int vc = npc;
         float vv = npv;
-        if (t < 15) {  // the next 8 rows' ranges and first pairs
+        if (8 * t + 8 < pw) {  // the next 8 rows' ranges and first pairs
             nb = rp(8 * t + 8 + rg);
             ne = rp(8 * t + 9 + rg);
             npc = nb + q < ne ? g.vcol[nb + q] : 0;
@@ -648,7 +649,11 @@ extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_grou
         g.x_ld = k.x_ld;
         g.x_rows = s.x_rows;
         g.n_items = static_cast<int32_t>(items);
-        g.item_blocks = dg::ceil_div(items, kLdsItems);
+        // items per wave: enough workgroups (~512) to fill the chip, 8..128 items per wave
+        int pw = static_cast<int>((items + 512 * 16 - 1) / (512 * 16));
+        pw = pw < 8 ? 8 : (pw > kLdsItemsMax ? kLdsItemsMax : (pw + 7) / 8 * 8);
+        g.per_wave = pw;
+        g.item_blocks = dg::ceil_div(items, 16 * pw);
         g.block_begin = static_cast<int32_t>(blocks);
         blocks += (int64_t)g.item_blocks * a.n_slices;
         if (blocks > 0x7fffffff) return DG_EINVAL;

@@ -63,18 +63,41 @@ def main(root):
         traffic_json(root, sys.argv[3])
         return
     print(f"# rocprofv3 summary: {os.path.basename(root.rstrip('/'))}\n")
-    for cfg in ("S", "P"):
+    for cfg in ("S", "P", "trainS", "trainP"):
         st = stats(os.path.join(root, f"{cfg}_trace"))
         if not st:
+            continue
+        if cfg.startswith("train"):
+            bj = os.path.join(root, f"{cfg}_bench.json")
+            if os.path.exists(bj):
+                try:
+                    rec = json.loads(open(bj).read().strip().splitlines()[-1])
+                    print(f"## {cfg}: training step (bench.py --train) under the profiler\n")
+                    print(f"{rec['ms_per_step']*1e3:.1f} us/step, {rec['value']:.4g} edges/s\n")
+                except Exception:
+                    pass
+            print("| kernel | calls | avg us | total % |")
+            print("|---|---|---|---|")
+            for r in st[:16]:
+                print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | "
+                      f"{float(r['Percentage']):.1f} |")
+            print()
             continue
         bj = os.path.join(root, f"{cfg}_bench.json")
         if os.path.exists(bj):
             try:
                 rec = json.loads(open(bj).read().strip().splitlines()[-1])
                 print(f"## config {cfg}: bench line under the profiler\n")
+                ro = rec["roofline"]
                 print(f"value {rec['value']:.4g} edges/s, {rec['ms_per_step']*1e3:.1f} us/step; "
-                      f"layer-1 SpMM {rec['roofline']['kernel_ms']*1e3:.2f} us, "
-                      f"{rec['roofline']['algorithmic_bytes']} algorithmic B\n")
+                      f"dominant kernel {ro['kernel']} {ro['kernel_ms']*1e3:.2f} us, "
+                      f"{ro['algorithmic_bytes']} algorithmic B, {ro['achieved']:.0f} GB/s "
+                      f"({100 * ro['frac']:.1f} % of {ro['peak']:.0f})")
+                l1 = rec.get("spmm_layer1")
+                if l1:
+                    print(f"; whole layer-1 SpMM {l1['ms']*1e3:.2f} us, {l1['GB_s']:.0f} GB/s "
+                          f"({100 * l1['frac']:.1f} %)")
+                print()
             except Exception:
                 pass
         counters = {}

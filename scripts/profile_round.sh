@@ -19,5 +19,12 @@ for cfg in S P; do
     echo "$cfg $ctr done"
   done
 done
+for cfg in S P; do
+  if [ $cfg = S ]; then steps="--steps 100 --warmup 10"; else steps="--steps 5 --warmup 1 --graph-steps 1"; fi
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/train${cfg}_trace -o run -- \
+    python3 bench.py --train --config $cfg $steps > $out/train${cfg}_bench.json 2> $out/train${cfg}_trace.log
+  echo "train $cfg trace done"
+done
 python3 scripts/prof_summary.py $out > $out/summary.md
+python3 scripts/prof_summary.py $out --json $out/traffic.json
 echo summary done
