@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="S / P: time the TRAINING step (forward + hinge-cost backward + Adam on every "
                          "variable, optimizer.py:108-114) instead of the forward step; one GPU")
+    ap.add_argument("--dropout", type=float, default=0.0,
+                    help="--train: dropout rate of both GCN layers (main.py trains at FLAGS.dropout = 0.1)")
     ap.add_argument("--force-shard", action="store_true",
                     help="run the relation-sharded (N > 1) plan and its collectives even at N = 1 "
                          "(launch under torchrun: a rehearsal of the multi-GPU step on one GPU)")
@@ -100,7 +102,7 @@ def build_workload(args, rank, world, sharded):
     return graph, shard, scaling, workload
 
 
-def make_plan(args, graph, shard, device, keep_sums=False):
+def make_plan(args, graph, shard, device, keep_sums=False, dropout=None):
     import torch
 
     from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
@@ -117,7 +119,8 @@ def make_plan(args, graph, shard, device, keep_sums=False):
     w2 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, H1, H2)).to(device)
                        for et, K in graph.edge_types.items()})
     plan = ForwardPlan(dg, {j: None for j in n}, w1, w2, H1, H2,
-                       allreduce=None if shard is None else shard.allreduce, keep_sums=keep_sums)
+                       allreduce=None if shard is None else shard.allreduce, keep_sums=keep_sums,
+                       dropout=dropout)
     plan.w1, plan.w2 = w1, w2
     return plan, dg
 
@@ -335,7 +338,11 @@ def main_train(args):
     torch.cuda.set_device(0)
     device = torch.device("cuda", 0)
     graph, shard, scaling, workload = build_workload(args, 0, 1, False)
-    plan, dg = make_plan(args, graph, None, device, keep_sums=True)
+    drop = None
+    if args.dropout > 0:
+        drop = (1.0 - args.dropout, torch.tensor([20180701, 0], dtype=torch.int64, device=device))
+        workload += f"; dropout {args.dropout}"
+    plan, dg = make_plan(args, graph, None, device, keep_sums=True, dropout=drop)
     dec = Decoder(graph, plan, device, 0)
     tp = train.TrainPlan(plan, plan.w1, plan.w2, {j: None for j in graph.n_nodes})
     dR = torch.zeros_like(dec.R)

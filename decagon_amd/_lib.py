@@ -21,7 +21,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 14
+ABI_VERSION = 15
 DG_MAX_ADAM_SEGS = 32
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
@@ -96,6 +96,9 @@ class DgGemmDesc(ctypes.Structure):
         ("k", c_int32),
         ("batch", c_int32),
         ("reduce", c_int32),
+        ("drop_tag", ctypes.c_uint32),
+        ("drop_state", c_void_p),
+        ("drop_keep", c_float),
         ("reserved", c_int32),
     ]
 
@@ -128,8 +131,13 @@ SIGNATURES = {
         [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     ),
     "dg_gemm_f32": (c_int32, [POINTER(DgGemmDesc), c_int32, c_void_p]),
-    "dg_gemm_tn_f32": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_int32,
-                                 c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "dg_gemm_tn_f32": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int32,
+                                 c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "dg_dropout_rows_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, ctypes.c_uint32, c_float,
+                                      c_void_p]),
+    "dg_dropout_elems_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
+                                       ctypes.c_uint32, c_float, c_void_p]),
+    "dg_dropout_advance": (c_int32, [c_void_p, c_void_p]),
     "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
     "dg_staged_order": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,

@@ -15,6 +15,7 @@
 // relations of the batch, so H_j is read once per KB relations; the B fragments (W_k, 8 KB)
 // and the C stores (two 128-byte row segments per register) are coalesced.
 #include "common.h"
+#include "dropout.h"
 
 namespace {
 
@@ -35,6 +36,9 @@ struct GemmOne {
     int32_t tile_blocks;   // blocks along the tile dimension (4 tiles each)
     int32_t block_begin;   // first block of this GEMM in the launch
     int32_t reduce;        // batch-reduce mode: batches summed in runs of batch_per_wave
+    const uint64_t* drop_state;  // batch-reduce only: batch products masked before the sum
+    uint32_t drop_tag;
+    float drop_keep;
 };
 
 struct GemmArgs {
@@ -73,12 +77,16 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
     const int b0 = bblk * g.batch_per_wave;
     const int b1 = min(b0 + g.batch_per_wave, g.batch);
     f32x16 acc = {};
+    const bool drop = g.reduce && g.drop_state;  // masked batch-reduce (dropout backward)
+    f32x16 dsum = {};
+    const uint32_t dkey = drop ? dg::drop_key(g.drop_state, g.drop_tag) : 0u;
 #pragma unroll 1
     for (int b = b0; b < b1; ++b) {
         const float* A = g.a + b * g.a_bs + (int64_t)row * g.a_sm;
         const int bb = g.b_map ? g.b_map[b] : b;
         const float* B = g.b + bb * g.b_bs + (int64_t)col * g.b_sn;
-        if (!g.reduce) acc = f32x16{};
+        if (!g.reduce || drop) acc = f32x16{};
+        f32x16& t = acc;
 #pragma unroll 4
         for (int k0 = 0; k0 < g.k; k0 += 2) {
             const int kk = k0 + h;
@@ -90,9 +98,19 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
                 }
                 if (col_ok) bv = B[kk * g.b_sk];
             }
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, t, 0, 0, 0);
+        }
+        if (drop) {
+            // Σ_b M_b∘(A_b·B_b): element (row, col) of batch b carries mask bit (b·m + row)·n + col
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const uint32_t idx = static_cast<uint32_t>(((int64_t)b * g.m + mrow) * g.n + col);
+                dsum[r] += t[r] * dg::keep_scale(dkey, idx, g.drop_keep);
+            }
         }
         if (g.reduce && b + 1 < b1) continue;  // batch-reduce: one store per run, at run index
+        if (drop) acc = dsum;
         if (col_ok) {
             const float s = g.sc ? g.sc[col] : 1.0f;
             float* C = g.c + (g.reduce ? bblk : bb) * g.c_bs + (int64_t)col * g.c_sn;
@@ -279,7 +297,7 @@ struct TnArgs {
     const float* a;
     const float* b;
     float* out;            // [batch][M][N], or the split partials [n_split][batch][M][N]
-    int64_t lda, ldb, b_bs;
+    int64_t lda, a_bs, ldb, b_bs;
     int32_t rows, M, N, batch;
     int32_t n_split, rows_per_split;
 };
@@ -294,7 +312,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const TnArgs a) {
     const int s = blockIdx.x - b * a.n_split;
     const int r_begin = s * a.rows_per_split;
     const int r_end = min(a.rows, r_begin + a.rows_per_split);
-    const float* A = a.a;
+    const float* A = a.a + (int64_t)b * a.a_bs;
     const float* B = a.b + (int64_t)b * a.b_bs;
     f32x16 acc[MT][NT];
 #pragma unroll
@@ -335,7 +353,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const TnArgs a) {
 
 }  // namespace
 
-extern "C" int dg_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t b_bs, float* c,
+extern "C" int dg_gemm_tn_f32(const float* a, int64_t lda, int64_t a_bs, const float* b, int64_t ldb, int64_t b_bs, float* c,
                               int32_t rows, int32_t M, int32_t N, int32_t batch, int32_t n_split, float* partial,
                               void* stream) {
     if (rows < 0 || batch < 0 || n_split < 1) return DG_EINVAL;
@@ -344,7 +362,7 @@ extern "C" int dg_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64
     if (batch == 0) return DG_OK;
     if (!a || !b || !c || (n_split > 1 && !partial)) return DG_EINVAL;
     if (n_split > 1 && !dg::aligned16(partial)) return DG_EALIGN;
-    TnArgs t{a, b, n_split > 1 ? partial : c, lda, ldb, b_bs, rows, M, N, batch, n_split,
+    TnArgs t{a, b, n_split > 1 ? partial : c, lda, a_bs, ldb, b_bs, rows, M, N, batch, n_split,
              2 * dg::ceil_div(dg::ceil_div(rows, n_split), 2)};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t blocks = (int64_t)batch * n_split;
@@ -408,7 +426,12 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
         int bpw = 1;
         while (bpw < 16 && (int64_t)g.tile_blocks * 4 * dg::ceil_div(d->batch, bpw * 2) >= 8192) bpw *= 2;
         if (d->reduce < 0 || (d->reduce > 0 && d->b_map)) return DG_EINVAL;
+        if (d->drop_state && (d->reduce <= 0 || !(d->drop_keep > 0.f && d->drop_keep <= 1.f))) return DG_EINVAL;
+        if (d->drop_state && (int64_t)d->batch * d->m * d->n >= 0xFFFFFFFFLL) return DG_EINVAL;
         g.reduce = d->reduce > 0 ? 1 : 0;
+        g.drop_state = d->drop_state;
+        g.drop_tag = d->drop_tag;
+        g.drop_keep = d->drop_keep;
         if (g.reduce) bpw = d->reduce;
         g.batch_per_wave = bpw;
         g.block_begin = static_cast<int32_t>(blocks);

@@ -43,6 +43,12 @@ STAGED_MAX_ROWS = 1022
 STAGED_BINS = int(os.environ.get("DG_STAGED_BINS", "128"))
 
 
+def drop_tag(layer: int, group: int) -> int:
+    """The dropout mask stream of (layer, edge-type index): layer 1 masks rows of the
+    relation-stacked W1 of the group, layer 2 masks elements of H1_j per relation."""
+    return (layer << 16) | group
+
+
 def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
     return (os.environ.get("DG_STAGED", "1") != "0" and n_rels >= STAGED_MIN_RELS
             and 0 < n_cols <= STAGED_MAX_COLS and 0 < n_rows <= STAGED_MAX_ROWS
@@ -220,10 +226,20 @@ class ForwardPlan:
 
     def __init__(self, dgraph: DeviceGraph, features: Dict[int, Optional[HostCSR]],
                  w1: LayerWeights, w2: LayerWeights, h1: int, h2: int,
-                 allreduce: Optional[Callable[[torch.Tensor], None]] = None, keep_sums: bool = False):
+                 allreduce: Optional[Callable[[torch.Tensor], None]] = None, keep_sums: bool = False,
+                 dropout: Optional[Tuple[float, torch.Tensor]] = None):
         self.g = dgraph
         self.h1, self.h2 = h1, h2
         self.allreduce = allreduce
+        # dropout (training): (keep probability, device state {seed, step}); every forward
+        # draws new masks (the step advances first), the backward reuses them
+        self.keep, self.drop_state = 1.0, None
+        if dropout is not None and float(dropout[0]) < 1.0:
+            if allreduce is not None:
+                raise NotImplementedError("dropout with a relation-sharded forward is not on the HIP path")
+            if any(f is not None for f in features.values()):
+                raise NotImplementedError("dropout with sparse (non-identity) features is not on the HIP path")
+            self.keep, self.drop_state = float(dropout[0]), dropout[1]
         # flat mode: every group's pre-normalisation sum S_ij lands in one flat buffer per
         # layer (all-reduced when sharded; kept for the backward when training), and one fused
         # launch over identity "adjacencies" finishes every node type from it
@@ -242,6 +258,9 @@ class ForwardPlan:
         # ---- layer-1 dense operand: W1 (identity features) or X_j·W1_k (sparse features) ----
         self._pre: List[Callable[[], None]] = []
         x1: Dict[EdgeType, torch.Tensor] = {}
+        self.et_index = {et: n for n, et in enumerate(self.edge_types)}
+        if self.drop_state is not None:
+            self._pre.append(lambda st=self.drop_state: kernels.dropout_advance(st))
         for et in self.edge_types:
             i, j = et
             grp = dgraph.groups[et]
@@ -254,6 +273,13 @@ class ForwardPlan:
                 if F != n[j]:
                     raise ValueError(f"identity features of type {j} need {n[j]} weight rows, got {F}")
                 x1[et] = W
+                if self.drop_state is not None:
+                    # dropout_sparse on the identity (layers.py:87-88): relation k's operand is W1_k
+                    # with rows kept / scaled by 1/keep — a masked copy of the stack per forward
+                    xd = torch.empty_like(W)
+                    self._pre.append(lambda W=W, xd=xd, t=drop_tag(1, self.et_index[et]):
+                                     kernels.dropout_rows(W, xd, self.drop_state, t, self.keep))
+                    x1[et] = xd
                 continue
             if fj.shape[0] != n[j] or fj.shape[1] != F:
                 raise ValueError(f"features of type {j} have shape {fj.shape}, weights expect (*, {F})")
@@ -295,7 +321,7 @@ class ForwardPlan:
         finished = set(self.targets) if self.flat_mode else set(self.fused)
         proj_fused = [et for et in self.edge_types
                       if dgraph.groups[et].n_rels and et[1] in finished
-                      and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS]
+                      and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS and self.drop_state is None]
         if len(proj_fused) > DG_MAX_GROUPS:
             proj_fused = []
         projs = []
@@ -307,19 +333,30 @@ class ForwardPlan:
         self._layer1 = self._build_layer(x1, h1, True, f32, projs)
 
         # ---- layer 2: remaining projections in one batched MFMA GEMM launch, then SpMM ----
-        gemms = []
+        gemms, drops = [], []
+        self.hdrop: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
             if not grp.n_rels or et in proj_fused:
                 continue
             j = et[1]
             W = w2.stacks[et]
+            if self.drop_state is not None:
+                # tf.nn.dropout(H1_j) drawn per relation (layers.py:111-113): H_k = M_k∘H1_j/keep
+                hd = torch.empty((grp.K, n[j], h1), **f32)
+                self.hdrop[et] = hd
+                drops.append(lambda j=j, hd=hd, t=drop_tag(2, self.et_index[et]):
+                             kernels.dropout_elems(self.hidden1[j], hd, self.drop_state, t, self.keep))
+                gemms.append(kernels.PreparedGemm(
+                    hd, (n[j] * h1, h1, 1), W, (h1 * h2, h2, 1), self.proj[et], (n[j] * h2, h2, 1),
+                    n[j], h2, h1, grp.n_rels))
+                continue
             gemms.append(kernels.PreparedGemm(
                 self.hidden1[j], (0, h1, 1), W, (h1 * h2, h2, 1), self.proj[et], (n[j] * h2, h2, 1),
                 n[j], h2, h1, grp.n_rels, b_map=grp.rel_map, b_batches=W.shape[0],
                 b_map_max=int(grp.rel_ids.max()) if grp.rel_map is not None else None))
-        self._gemm2 = [kernels.PreparedGemmMulti(gemms[s:s + DG_MAX_GROUPS])
-                       for s in range(0, len(gemms), DG_MAX_GROUPS)]
+        self._gemm2 = drops + [kernels.PreparedGemmMulti(gemms[s:s + DG_MAX_GROUPS])
+                               for s in range(0, len(gemms), DG_MAX_GROUPS)]
         self._layer2 = self._build_layer(self.proj, h2, False, f32)
 
     # ------------------------------------------------------------------ layer builder

@@ -377,7 +377,8 @@ class PreparedGemm:
                  c_strides, m: int, n: int, k: int, batch: int = 1,
                  sa: Optional[torch.Tensor] = None, sc: Optional[torch.Tensor] = None,
                  b_map: Optional[torch.Tensor] = None, b_batches: Optional[int] = None,
-                 b_map_max: Optional[int] = None, reduce: int = 0):
+                 b_map_max: Optional[int] = None, reduce: int = 0,
+                 drop: Optional[Tuple[torch.Tensor, int, float]] = None):
         for t, nm in ((a, "a"), (b, "b"), (c, "c")):
             if not (t.is_cuda and t.dtype == torch.float32):
                 raise ValueError(f"{nm}: float32 device tensor required")
@@ -414,8 +415,15 @@ class PreparedGemm:
         desc.c_bs, desc.c_sm, desc.c_sn = c_strides
         desc.m, desc.n, desc.k, desc.batch = m, n, k, batch
         desc.reduce = reduce
+        if drop is not None:  # (device state {seed, step}, stream tag, keep): masked batch-reduce
+            state, tag, keep_p = drop
+            if not reduce:
+                raise ValueError("the dropout mask applies in batch-reduce mode")
+            if state.dtype != torch.int64 or not state.is_cuda:
+                raise ValueError("dropout state: int64 device tensor {seed, step}")
+            desc.drop_state, desc.drop_tag, desc.drop_keep = state.data_ptr(), int(tag), float(keep_p)
         self._desc = desc
-        self._keep = (a, b, c, sa, sc, b_map)
+        self._keep = (a, b, c, sa, sc, b_map, drop)
         self._fn = _lib.load().dg_gemm_f32
 
     def __call__(self, stream=None) -> None:
@@ -440,15 +448,23 @@ class PreparedGemmMulti:
 
 
 class PreparedGemmTN:
-    """dg_gemm_tn_f32: c[b] = aᵀ·b_stack[b] for a [rows][M] shared and b_stack [batch][rows][N]
-    (contiguous), c [batch][M][N]; the rows split into ranges of about `rows_per_split`."""
+    """dg_gemm_tn_f32: c[b] = a[b]ᵀ·b_stack[b] for a [rows][M] shared (or [batch][rows][M]) and
+    b_stack [batch][rows][N] (contiguous), c [batch][M][N]; rows split into ranges of about
+    `rows_per_split` (0: enough to fill the chip)."""
 
     def __init__(self, a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, rows_per_split: int = 0):
         _dev(a, torch.float32, "a")
         _dev(b, torch.float32, "b")
         _dev(c, torch.float32, "c")
-        rows, M = a.shape
         batch, rb, N = b.shape
+        if a.dim() == 3:
+            if a.shape[0] != batch:
+                raise ValueError("gemm_tn: batched a must have one matrix per batch")
+            rows, M = a.shape[1], a.shape[2]
+            a_bs = rows * M
+        else:
+            rows, M = a.shape
+            a_bs = 0
         if rb != rows or tuple(c.shape) != (batch, M, N):
             raise ValueError("gemm_tn: shapes")
         if rows_per_split <= 0:  # enough workgroups to fill the chip, ranges of >= 64 rows
@@ -457,7 +473,7 @@ class PreparedGemmTN:
             self.n_split = max(1, -(-rows // max(2, rows_per_split)))
         self.partial = (torch.empty((self.n_split, batch, M, N), device=a.device) if self.n_split > 1 else None)
         self._keep = (a, b, c)
-        self._args = (a.data_ptr(), M, b.data_ptr(), N, rows * N, c.data_ptr(), rows, M, N, batch, self.n_split,
+        self._args = (a.data_ptr(), M, a_bs, b.data_ptr(), N, rows * N, c.data_ptr(), rows, M, N, batch, self.n_split,
                       self.partial.data_ptr() if self.partial is not None else None)
         self._fn = _lib.load().dg_gemm_tn_f32
 
@@ -774,3 +790,44 @@ def adam_advance(state: torch.Tensor, lr: float, beta1: float, beta2: float, str
     """β1^t, β2^t ← ·β1, ·β2 and the next alpha, on the device (TF's _finish)."""
     _dev(state, torch.float32, "adam state")
     check(_lib.load().dg_adam_advance(state.data_ptr(), lr, beta1, beta2, _stream_ptr(stream)), "dg_adam_advance")
+
+
+# --------------------------------------------------------------------------------------
+# Dropout (dropout.hip)
+# --------------------------------------------------------------------------------------
+def _drop_state(state: torch.Tensor) -> None:
+    if not (isinstance(state, torch.Tensor) and state.is_cuda and state.dtype == torch.int64
+            and state.numel() >= 2):
+        raise ValueError("dropout state must be an int64 device tensor {seed, step}")
+
+
+def dropout_rows(inp: torch.Tensor, out: torch.Tensor, state: torch.Tensor, tag: int, keep: float,
+                 stream=None) -> None:
+    """out[r] = inp[r] · s(r) over the rows of a 2-D view (in place allowed)."""
+    _dev(inp, torch.float32, "in")
+    _dev(out, torch.float32, "out")
+    _drop_state(state)
+    d = inp.shape[-1]
+    n = inp.numel() // d
+    if out.numel() != inp.numel():
+        raise ValueError("dropout_rows: shapes")
+    check(_lib.load().dg_dropout_rows_f32(inp.data_ptr(), out.data_ptr(), n, d, state.data_ptr(), tag, keep,
+                                          _stream_ptr(stream)), "dg_dropout_rows_f32")
+
+
+def dropout_elems(src: torch.Tensor, out: torch.Tensor, state: torch.Tensor, tag: int, keep: float,
+                  stream=None) -> None:
+    """out[k] = src ∘ M_k / keep for k < out.shape[0] (src [n][d], out [K][n][d])."""
+    _dev(src, torch.float32, "src")
+    _dev(out, torch.float32, "out")
+    _drop_state(state)
+    K, n, d = out.shape
+    if tuple(src.shape) != (n, d):
+        raise ValueError("dropout_elems: shapes")
+    check(_lib.load().dg_dropout_elems_f32(src.data_ptr(), out.data_ptr(), K, n, d, state.data_ptr(), tag, keep,
+                                           _stream_ptr(stream)), "dg_dropout_elems_f32")
+
+
+def dropout_advance(state: torch.Tensor, stream=None) -> None:
+    _drop_state(state)
+    check(_lib.load().dg_dropout_advance(state.data_ptr(), _stream_ptr(stream)), "dg_dropout_advance")

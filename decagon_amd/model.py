@@ -155,15 +155,28 @@ class DecagonModel(Model):
         return (LayerWeights({et: l.weights_stack for et, l in self.layers1.items()}),
                 LayerWeights({et: l.weights_stack for et, l in self.layers2.items()}))
 
-    def plan(self, ctx: RunContext, shard=None, training: bool = False) -> ForwardPlan:
+    # the counter-based dropout masks (dropout.hip) of this model start from this seed
+    dropout_seed = 20180701
+
+    def dropout_state(self, ctx: RunContext) -> torch.Tensor:
+        """The device dropout state {seed, step} of this model in the session (step = the
+        number of forwards run with dropout so far)."""
+        key = ("dropout_state", id(self))
+        cache = ctx.session.caches
+        if key not in cache:
+            cache[key] = torch.tensor([self.dropout_seed, 0], dtype=torch.int64, device=ctx.session.device)
+        return cache[key]
+
+    def plan(self, ctx: RunContext, shard=None, training: bool = False, keep: float = 1.0) -> ForwardPlan:
         """The cached ForwardPlan for the adjacency/feature values fed in this run (training:
-        the flat-mode plan that keeps every group's pre-normalisation sum for the backward)."""
+        the flat-mode plan that keeps every group's pre-normalisation sum for the backward;
+        keep < 1: dropout, layers.py:87-88 and :112)."""
         local = None if shard is None else shard.local
         dg = runtime.device_graph(ctx, self.edge_types, self.adj_mats, local)
         feats = {j: runtime.feature_csr(ctx, self.inputs[j]) if j in self.inputs else None
                  for j in dg.n_nodes}
         key = ("plan", id(self), id(dg), tuple((j, id(f)) for j, f in feats.items()),
-               None if shard is None else id(shard), training)
+               None if shard is None else id(shard), training, keep)
         cache = ctx.session.caches.setdefault("plans", {})
         hit = cache.get(key)
         if hit is None:
@@ -173,7 +186,8 @@ class DecagonModel(Model):
                                        "(construct the model after a HIP device is visible)")
             w1, w2 = self.weight_stacks()
             p = ForwardPlan(dg, feats, w1, w2, self.h1, self.h2,
-                            allreduce=None if shard is None else shard.allreduce, keep_sums=training)
+                            allreduce=None if shard is None else shard.allreduce, keep_sums=training,
+                            dropout=(keep, self.dropout_state(ctx)) if keep < 1.0 else None)
             hit = (dg, feats, p)
             cache[key] = hit
         return hit[2]
@@ -181,11 +195,10 @@ class DecagonModel(Model):
     def _forward(self, ctx: RunContext) -> ForwardPlan:
         key = ("forward", id(self))
         if key not in ctx.cache:
-            d = ctx.value(self.dropout)
-            if float(d) != 0.0:
-                raise NotImplementedError(
-                    "dropout > 0 is the training path (SURVEY §8f); forward parity runs at 0")
-            p = self.plan(ctx, getattr(ctx.session, "shard", None), training=ctx.training)
+            d = float(ctx.value(self.dropout))
+            if not 0.0 <= d < 1.0:
+                raise ValueError(f"dropout rate {d} outside [0, 1)")
+            p = self.plan(ctx, getattr(ctx.session, "shard", None), training=ctx.training, keep=1.0 - d)
             p.run()
             ctx.cache[key] = p
         return ctx.cache[key]

@@ -31,7 +31,7 @@ import torch
 
 from . import kernels
 from ._lib import DG_MAX_GROUPS
-from .engine import ForwardPlan, LayerWeights
+from .engine import ForwardPlan, LayerWeights, drop_tag
 from .sparse import HostCSR, merge_chunks
 
 EdgeType = Tuple[int, int]
@@ -92,6 +92,8 @@ class TrainPlan:
                  features: Dict[int, Optional[HostCSR]]):
         if not fwd.flat_mode or fwd.allreduce is not None:
             raise NotImplementedError("training runs on one GPU over a ForwardPlan(keep_sums=True)")
+        # with dropout (fwd.drop_state), the backward reuses the forward's masks: the draws of the
+        # forward's step, regenerated from the same counter-based hash (dropout.hip)
         if any(f is not None for f in features.values()):
             raise NotImplementedError("the backward for sparse (non-identity) features is not on the HIP path")
         g = fwd.g
@@ -108,6 +110,7 @@ class TrainPlan:
         self.gW1: Dict[EdgeType, torch.Tensor] = {}
         self.gW2: Dict[EdgeType, torch.Tensor] = {}
         specs2, specs1, gemm_w2, gemm_h1 = [], [], [], []
+        self._w1_drop = []
         runs: Dict[int, List[Tuple[torch.Tensor, int]]] = {j: [] for j in srcs}
         self._dS1, self._dS2 = {}, {}
         for et in ets:
@@ -132,15 +135,22 @@ class TrainPlan:
                 raise ValueError(f"layer-1 weights of {et} do not match identity features")
             specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, n[i], vcol_max=vmax))
             specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, self.gW1[et], n[j], K, h1, n[i], vcol_max=vmax))
-            H = fwd.hidden1[j]
-            # dW2_k = H1_jᵀ·dP_k (reduction over the n_j rows, split for long ones)
+            # dW2_k = H_kᵀ·dP_k with H_k = H1_j (or its per-relation dropout draw), the reduction
+            # over the n_j rows split for long ones
+            H = fwd.hdrop.get(et, fwd.hidden1[j])
             gemm_w2.append(kernels.PreparedGemmTN(H, dP, self.gW2[et]))
-            # dH1_j partials = Σ_k dP_k·W2_kᵀ over runs of R relations: B(c, m) = W2_k[m][c]
+            # dH1_j partials = Σ_k M_k∘(dP_k·W2_kᵀ) over runs of R relations: B(c, m) = W2_k[m][c]
+            # (M_k: layer 2's dropout mask of relation k, when dropout is on)
             R = K if K <= 64 else 32
             n_runs = -(-K // R)
             part = torch.zeros((n_runs, n[j], h1), **f32)
+            drop = ((fwd.drop_state, drop_tag(2, fwd.et_index[et]), fwd.keep) if fwd.drop_state is not None
+                    else None)
             gemm_h1.append(kernels.PreparedGemm(dP, (n[j] * h2, h2, 1), w2.stacks[et], (h1 * h2, 1, h2), part,
-                                                (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R))
+                                                (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R, drop=drop))
+            if fwd.drop_state is not None:  # dW1 rows through layer 1's row masks
+                self._w1_drop.append(lambda g=self.gW1[et], tg=drop_tag(1, fwd.et_index[et]):
+                                     kernels.dropout_rows(g, g, fwd.drop_state, tg, fwd.keep))
             runs[j].append((part, n_runs))
         chunked = lambda xs: [xs[s:s + DG_MAX_GROUPS] for s in range(0, len(xs), DG_MAX_GROUPS)]  # noqa: E731
         # Âᵀ·dS: operands small enough for LDS (the drug side) take the LDS-staged form
@@ -188,3 +198,5 @@ class TrainPlan:
             l()
         for s in self._spmm1:
             s()
+        for f in self._w1_drop:
+            f()

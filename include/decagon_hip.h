@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (14); bumped whenever a struct layout or a signature changes. */
+/* ABI version (15); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -231,6 +231,9 @@ typedef struct dg_gemm_desc {
     int64_t c_bs, c_sm, c_sn;
     int32_t m, n, k, batch;
     int32_t reduce;             /* 0, or R > 0: batch-reduce mode (below); b_map must be NULL */
+    uint32_t drop_tag;          /* batch-reduce with dropout: mask stream tag */
+    const uint64_t* drop_state; /* NULL, or the device dropout state {seed, step} (below) */
+    float drop_keep;            /* keep probability when drop_state != NULL */
     int32_t reserved;
 } dg_gemm_desc;
 
@@ -241,16 +244,19 @@ int dg_gemm_f32(const dg_gemm_desc* descs /* HOST array */, int32_t n_desc, void
  * batches (in batch order) and run q's sum is written at c + q*c_bs, q < ceil(batch / R):
  *     C_q = Σ_{b in [qR, min(qR+R, batch))} A_b·B_b
  * — the backward's Σ_k dP_k·W_kᵀ (gradient of the per-relation projections, layers.py:113)
- * as partial sums that dg_gcn_epilogue_f32 (no flags) adds up. */
+ * as partial sums that dg_gcn_epilogue_f32 (no flags) adds up.  With drop_state != NULL each
+ * batch product is first multiplied element-wise by its dropout mask (mask element
+ * (b·m + row)·n + col of stream drop_tag, scaled by 1/keep, as dg_dropout_elems_f32 draws it):
+ *     C_q = Σ_b M_b∘(A_b·B_b)   — the gradient through tf.nn.dropout (layers.py:112). */
 
 /* Batched Aᵀ·B over a long reduction (the weight gradient H_jᵀ·dP_k, backward of
- * layers.py:113):  C_b[m][n] = Σ_{r < rows} A[r*lda + m] · B[b*b_bs + r*ldb + n],  C
+ * layers.py:113):  C_b[m][n] = Σ_{r < rows} A[b*a_bs + r*lda + m] · B[b*b_bs + r*ldb + n],  C
  * contiguous [batch][M][N].  M, N multiples of 32 with (M/32)(N/32) <= 4.  With n_split > 1
  * the rows are cut into n_split ranges whose partials ([n_split][batch][M][N], caller's
  * 16-byte aligned `partial`) are then summed in range order. */
-int dg_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t b_bs, float* c,
-                   int32_t rows, int32_t M, int32_t N, int32_t batch, int32_t n_split, float* partial,
-                   void* stream);
+int dg_gemm_tn_f32(const float* a, int64_t lda, int64_t a_bs, const float* b, int64_t ldb, int64_t b_bs,
+                   float* c, int32_t rows, int32_t M, int32_t N, int32_t batch, int32_t n_split,
+                   float* partial, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Edge decoder scores (T8 + T9):  for pair p,
@@ -366,6 +372,26 @@ typedef struct dg_adam_seg {
 int dg_adam_f32(const dg_adam_seg* segs /* HOST array */, int32_t n_segs, float alpha, float beta1,
                 float beta2, float eps, const float* state, void* stream);
 int dg_adam_advance(float* state, float lr, float beta1, float beta2, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Dropout (training path): dropout_sparse (layers.py:23-31, :88) and tf.nn.dropout (:112).
+ * state: device uint64 {seed, step}.  Element idx of stream `tag` is kept iff
+ *   lowbias32(key ^ idx) >> 8 < (uint32)(keep·2^24),
+ *   key = lowbias32(lowbias32(seed_lo ^ tag·0x9E3779B9) ^ (seed_hi + step·0x85EBCA6B)),
+ *   lowbias32(x): x ^= x>>16; x *= 0x7feb352d; x ^= x>>15; x *= 0x846ca68b; x ^= x>>16,
+ * and a kept element is scaled by 1/keep (TF's distribution; its RNG stream is not
+ * reproducible).  dg_dropout_advance increments step (a new draw per training step, on the
+ * device: graph-capturable).
+ * -------------------------------------------------------------------------------------- */
+/* out[r][:] = in[r][:] · s(r)  (row masks: identity features' dropout_sparse, one relation's
+ * rows at a time in the relation-stacked W1; in place allowed).  n_rows·d < 2^32. */
+int dg_dropout_rows_f32(const float* in, float* out, int64_t n_rows, int32_t d, const uint64_t* state,
+                        uint32_t tag, float keep, void* stream);
+/* out[k][r][f] = src[r][f] · s(k·n_rows·d + r·d + f)  for k < K: tf.nn.dropout of H_j drawn
+ * independently for each of the K relations.  K·n_rows·d < 2^32. */
+int dg_dropout_elems_f32(const float* src, float* out, int32_t K, int32_t n_rows, int32_t d,
+                         const uint64_t* state, uint32_t tag, float keep, void* stream);
+int dg_dropout_advance(uint64_t* state, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, draw

@@ -177,8 +177,32 @@ def l2_normalize_rows_grad(x: np.ndarray, dy: np.ndarray) -> np.ndarray:
     return dy * inv - x * (inv ** 3) * dot * (ss >= EPS_L2)
 
 
+def _lowbias32(x):
+    x = np.asarray(x, np.uint32)
+    x = x ^ (x >> np.uint32(16))
+    x = (x * np.uint32(0x7FEB352D)).astype(np.uint32)
+    x = x ^ (x >> np.uint32(15))
+    x = (x * np.uint32(0x846CA68B)).astype(np.uint32)
+    return x ^ (x >> np.uint32(16))
+
+
+def dropout_scale(seed: int, step: int, tag: int, n: int, keep: float) -> np.ndarray:
+    """The dropout masks of stream `tag` at (seed, step), elements 0..n-1, as the device draws
+    them (decagon_amd/csrc/dropout.h): element idx kept iff lowbias32(key ^ idx) >> 8 <
+    (uint32)(keep·2^24), scaled by 1/keep (float32).  TF's own RNG stream cannot be reproduced;
+    this restates the device's draw so forward and backward are checked on identical masks."""
+    with np.errstate(over="ignore"):
+        lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32((seed >> 32) & 0xFFFFFFFF)
+        k1 = _lowbias32(lo ^ np.uint32((tag * 0x9E3779B9) & 0xFFFFFFFF))
+        key = _lowbias32(k1 ^ np.uint32((int(hi) + step * 0x85EBCA6B) & 0xFFFFFFFF))
+        h = _lowbias32(key ^ np.arange(n, dtype=np.uint32))
+    thr = np.uint32(np.float32(keep) * np.float32(16777216.0))
+    inv = np.float32(1.0) / np.float32(keep)
+    return np.where((h >> np.uint32(8)) < thr, inv, np.float32(0.0)).astype(np.float32)
+
+
 def train_grads(edge_types, adj, feats, w1, w2, decoders, dec_params, d2: int, batch, neg, e: int,
-                rt: int, ct: int, margin: float):
+                rt: int, ct: int, margin: float, drop1=None, drop2=None):
     """Forward (model.py:64-88, optimizer.py:51-57) and the hinge cost's gradient w.r.t.
     every variable, as TF's minimize() computes it (float64).
 
@@ -186,7 +210,10 @@ def train_grads(edge_types, adj, feats, w1, w2, decoders, dec_params, d2: int, b
     type; neg [B] the negative row ids; e the flat relation index (edge-type order).
     Returns (cost, grads) with grads = {"w1": {et: [K arrays]}, "w2": {...},
     "dec": {et: {var name: array}}} — every variable gets a gradient (zeros when the cost
-    does not reach it: TF's gather/concat gradients are dense zeros, not None)."""
+    does not reach it: TF's gather/concat gradients are dense zeros, not None).
+    Dropout (layers.py:87-88, :112): drop1[et] [K, n_j] scales rows of relation k's layer-1
+    operand (dropout_sparse on the identity features), drop2[et] [K, n_j, h1] the elements of
+    H1_j fed to relation k's projection (tf.nn.dropout); None = no dropout."""
     ets = list(edge_types)
     n_nodes = {}
     for (i, j) in ets:
@@ -195,12 +222,15 @@ def train_grads(edge_types, adj, feats, w1, w2, decoders, dec_params, d2: int, b
     x1 = {}
     for (i, j) in ets:
         x1[i, j] = [w if feats.get(j) is None else _features_times(feats[j], w) for w in w1[i, j]]
+        if drop1 is not None:
+            x1[i, j] = [x * drop1[i, j][k][:, None] for k, x in enumerate(x1[i, j])]
+    hin = (lambda et, k, h: h * drop2[et][k]) if drop2 is not None else (lambda et, k, h: h)
     S1 = {et: np.sum([sparse_dense_matmul(a, x) for a, x in zip(adj[et], x1[et])], axis=0) for et in ets}
     pre1 = {}
     for (i, j) in ets:
         pre1[i] = pre1.get(i, 0.0) + l2_normalize_rows(S1[i, j])
     H1 = {i: np.maximum(v, 0.0) for i, v in pre1.items()}
-    P = {(i, j): [H1[j] @ w for w in w2[i, j]] for (i, j) in ets}
+    P = {(i, j): [hin((i, j), k, H1[j]) @ w for k, w in enumerate(w2[i, j])] for (i, j) in ets}
     S2 = {et: np.sum([sparse_dense_matmul(a, p) for a, p in zip(adj[et], P[et])], axis=0) for et in ets}
     E = {}
     for (i, j) in ets:
@@ -250,17 +280,19 @@ def train_grads(edge_types, adj, feats, w1, w2, decoders, dec_params, d2: int, b
     for (i, j) in ets:
         dS2 = l2_normalize_rows_grad(S2[i, j], dE[i])
         gw2[i, j] = []
-        for a, w in zip(adj[i, j], w2[i, j]):
+        for k, (a, w) in enumerate(zip(adj[i, j], w2[i, j])):
             dP = sparse_t_dense_matmul(a, dS2, n_nodes[j])
-            gw2[i, j].append(H1[j].T @ dP)
-            dH1[j] += dP @ w.T
+            gw2[i, j].append(hin((i, j), k, H1[j]).T @ dP)
+            dH1[j] += hin((i, j), k, dP @ w.T)
     dpre1 = {i: dH1[i] * (pre1[i] > 0) for i in dH1}   # tf.nn.relu's gradient mask (model.py:75)
     gw1 = {}
     for (i, j) in ets:
         dS1 = l2_normalize_rows_grad(S1[i, j], dpre1[i])
         gw1[i, j] = []
-        for a in adj[i, j]:
+        for k, a in enumerate(adj[i, j]):
             dX = sparse_t_dense_matmul(a, dS1, n_nodes[j])
+            if drop1 is not None:
+                dX = dX * drop1[i, j][k][:, None]
             if feats.get(j) is not None:
                 dX = sparse_t_dense_matmul(feats[j], dX, int(feats[j][2][1]))
             gw1[i, j].append(dX)

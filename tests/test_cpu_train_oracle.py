@@ -30,8 +30,9 @@ def _inputs(z, b=3):
     return edge_types, decoders, adj, w1, w2, dec, z[f"batch{b}_edges"], z[f"batch{b}_neg"], e, rt, ct
 
 
-def _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, margin):
-    """The same cost with torch autograd (float64, dense adjacencies)."""
+def _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, margin, drop1=None, drop2=None):
+    """The same cost with torch autograd (float64, dense adjacencies; optional dropout masks
+    applied as layers.py:87-88 / :112 do)."""
     T = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, requires_grad=True)  # noqa: E731
     tw1 = {et: [T(w) for w in ws] for et, ws in w1.items()}
     tw2 = {et: [T(w) for w in ws] for et, ws in w2.items()}
@@ -49,14 +50,18 @@ def _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, m
     def l2n(x):  # tf.nn.l2_normalize
         return x * torch.rsqrt(torch.maximum((x * x).sum(1, keepdim=True), torch.tensor(1e-12, dtype=torch.float64)))
 
+    D1 = (lambda et, k: torch.as_tensor(drop1[et][k], dtype=torch.float64)[:, None]) if drop1 is not None \
+        else (lambda et, k: 1.0)
+    D2 = (lambda et, k: torch.as_tensor(drop2[et][k], dtype=torch.float64)) if drop2 is not None \
+        else (lambda et, k: 1.0)
     pre1 = {}
     for (i, j) in edge_types:
-        s = sum(a @ w for a, w in zip(A[i, j], tw1[i, j]))
+        s = sum(a @ (D1((i, j), k) * w) for k, (a, w) in enumerate(zip(A[i, j], tw1[i, j])))
         pre1[i] = pre1.get(i, 0) + l2n(s)
     h1 = {i: torch.relu(v) for i, v in pre1.items()}
     E = {}
     for (i, j) in edge_types:
-        s = sum(a @ (h1[j] @ w) for a, w in zip(A[i, j], tw2[i, j]))
+        s = sum(a @ ((D2((i, j), k) * h1[j]) @ w) for k, (a, w) in enumerate(zip(A[i, j], tw2[i, j])))
         E[i] = E.get(i, 0) + l2n(s)
     flat = 0
     G = L = None
@@ -84,15 +89,28 @@ def _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, m
     return cost, tw1, tw2, tdec
 
 
-@pytest.mark.parametrize("b", [0, 3])
-def test_oracle_grads_match_autograd(golden_S, b):
+def _masks(edge_types, adj, keep, step=1):
+    """Dropout masks of every group as the device draws them (tags: decagon_amd.engine.drop_tag)."""
+    drop1, drop2 = {}, {}
+    for g, (et, K) in enumerate(edge_types.items()):
+        n_j = int(adj[et][0][2][1])
+        drop1[et] = orc.dropout_scale(20180701, step, (1 << 16) | g, K * n_j, keep).reshape(K, n_j)
+        drop2[et] = orc.dropout_scale(20180701, step, (2 << 16) | g, K * n_j * 64, keep).reshape(K, n_j, 64)
+    return drop1, drop2
+
+
+@pytest.mark.parametrize("b,dropout", [(0, False), (3, False), (3, True)])
+def test_oracle_grads_match_autograd(golden_S, b, dropout):
     args = _inputs(golden_S, b)
     edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct = args
     feats = {0: None, 1: None}
-    cost, g = orc.train_grads(edge_types, adj, feats, w1, w2, decoders, dec, 32, batch, neg, e, rt, ct, 0.1)
-    tcost, tw1, tw2, tdec = _torch_cost(*args, 0.1)
+    drop1, drop2 = _masks(edge_types, adj, 0.9) if dropout else (None, None)
+    cost, g = orc.train_grads(edge_types, adj, feats, w1, w2, decoders, dec, 32, batch, neg, e, rt, ct, 0.1,
+                              drop1=drop1, drop2=drop2)
+    tcost, tw1, tw2, tdec = _torch_cost(*args, 0.1, drop1=drop1, drop2=drop2)
     assert abs(cost - float(tcost)) <= 1e-12 * max(1.0, abs(cost))
-    assert abs(cost - float(golden_S[f"batch{b}_cost"])) <= 1e-9 * max(1.0, abs(cost))
+    if not dropout:
+        assert abs(cost - float(golden_S[f"batch{b}_cost"])) <= 1e-9 * max(1.0, abs(cost))
     for et in edge_types:
         for k in range(edge_types[et]):
             for mine, t in ((g["w1"][et][k], tw1[et][k]), (g["w2"][et][k], tw2[et][k])):
@@ -121,3 +139,15 @@ def test_adam_first_step_closed_form():
     assert np.all(np.abs(p2 - p1) > 0)
     p3, _, _ = orc.adam_tf(p, z, z, z, 1)
     assert np.array_equal(p3, p)
+
+
+def test_dropout_masks_distribution():
+    """The restated draw keeps ~keep of the elements, independently per stream and step."""
+    a = orc.dropout_scale(7, 1, 3, 200000, 0.9)
+    b = orc.dropout_scale(7, 2, 3, 200000, 0.9)
+    c = orc.dropout_scale(7, 1, 4, 200000, 0.9)
+    for m in (a, b, c):
+        assert abs((m > 0).mean() - 0.9) < 0.005
+        assert set(np.unique(m)) <= {np.float32(0.0), np.float32(1 / np.float32(0.9))}
+    assert 0.79 < ((a > 0) == (b > 0)).mean() < 0.85  # independent draws agree on ~0.82
+    assert 0.79 < ((a > 0) == (c > 0)).mean() < 0.85

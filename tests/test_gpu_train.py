@@ -283,3 +283,89 @@ def test_spmm_lds_shared_operand(d):
         ref = dense.T @ X.astype(np.float64)
         assert rel_err(outs[0][k].cpu().numpy(), ref) <= 1e-5
     assert rel_err(outs[0].cpu().numpy(), outs[1].cpu().numpy()) <= 1e-6
+
+
+def test_dropout_masks_match_restatement():
+    """dg_dropout_rows_f32 / dg_dropout_elems_f32 draw exactly oracle.dropout_scale's masks."""
+    from decagon_amd import kernels
+
+    dev = _dev()
+    state = torch.tensor([123456789012, 5], dtype=torch.int64, device=dev)
+    rows = torch.ones((3000, 8), device=dev)
+    out = torch.empty_like(rows)
+    kernels.dropout_rows(rows, out, state, 77, 0.8)
+    src = torch.ones((50, 64), device=dev)
+    el = torch.empty((7, 50, 64), device=dev)
+    kernels.dropout_elems(src, el, state, 78, 0.8)
+    torch.cuda.synchronize()
+    want_r = orc.dropout_scale(123456789012, 5, 77, 3000, 0.8)
+    want_e = orc.dropout_scale(123456789012, 5, 78, 7 * 50 * 64, 0.8)
+    assert np.array_equal(out.cpu().numpy(), np.repeat(want_r[:, None], 8, 1))
+    assert np.array_equal(el.cpu().numpy().reshape(-1), want_e)
+    kernels.dropout_advance(state)
+    torch.cuda.synchronize()
+    assert int(state[1]) == 6
+
+
+def test_gemm_batch_reduce_with_dropout_mask():
+    from decagon_amd import kernels
+
+    dev = _dev()
+    rng = np.random.default_rng(8)
+    K, n_j, c, h = 40, 37, 32, 64
+    dP = rng.standard_normal((K, n_j, c)).astype(np.float32)
+    W = rng.standard_normal((K, h, c)).astype(np.float32)
+    state = torch.tensor([99, 3], dtype=torch.int64, device=dev)
+    R = 16
+    runs = -(-K // R)
+    out = torch.zeros((runs, n_j, h), device=dev)
+    kernels.PreparedGemm(torch.from_numpy(dP).to(dev), (n_j * c, c, 1), torch.from_numpy(W).to(dev), (h * c, 1, c),
+                         out, (n_j * h, h, 1), n_j, h, c, K, reduce=R, drop=(state, 5, 0.7))()
+    torch.cuda.synchronize()
+    m = orc.dropout_scale(99, 3, 5, K * n_j * h, 0.7).reshape(K, n_j, h).astype(np.float64)
+    got = out.cpu().numpy()
+    for q in range(runs):
+        ref = sum(m[b] * (dP[b].astype(np.float64) @ W[b].T.astype(np.float64)) for b in range(q * R, min(K, q * R + R)))
+        assert rel_err(got[q], ref) <= 1e-5
+
+
+def test_grads_vars_with_dropout_match_oracle(golden_S):
+    """The training step at FLAGS.dropout = 0.1 (main.py:235, :307): every gradient against the
+    oracle on the same masks (the device's draw for step 1, regenerated by the oracle)."""
+    from test_cpu_train_oracle import _masks
+
+    z = golden_S
+    dg, ph, model, opt, feed = _setup(z)
+    edge_types, decoders = model.edge_types, model.decoders
+    f, e, rt, ct = _batch_feed(z, ph, opt, feed, 3)
+    f[ph["dropout"]] = 0.1
+    sess = dg.Session()
+    gv = sess.run(opt.grads_vars, feed_dict=f)
+    w1, w2, dec, adj = _oracle_inputs(z, model, edge_types)
+    drop1, drop2 = _masks(edge_types, adj, 0.9, step=1)
+    cost, ref = orc.train_grads(edge_types, adj, {0: None, 1: None}, w1, w2, decoders, dec, 32,
+                                z["batch3_edges"], z["batch3_neg"], e, rt, ct, 0.1, drop1=drop1, drop2=drop2)
+    want = []
+    for et, K in edge_types.items():
+        want += [ref["w1"][et][k] for k in range(K)]
+    for et, K in edge_types.items():
+        want += [ref["w2"][et][k] for k in range(K)]
+    for et in edge_types:
+        want += [ref["dec"][et][n] for n in model.edge_type2decoder[et].vars]
+    for (g, v), w in zip(gv, want):
+        scale = np.max(np.abs(w))
+        if scale == 0:
+            assert np.max(np.abs(g)) == 0.0
+        else:
+            assert np.max(np.abs(g - w)) <= TOL * scale, f"gradient off by {rel_err(g, w):.2e}"
+    # the cost with dropout differs from the dropout-free one, and a second run draws new masks
+    c1 = sess.run(opt.cost, feed_dict=f)
+    assert abs(float(c1) - cost) > 1e-6 * abs(cost)
+    st = model.dropout_state(type("C", (), {"session": sess})())
+    assert int(st[1]) == 2
+    # opt_op with dropout trains (the reference's main.py loop)
+    for _ in range(5):
+        sess.run([opt.opt_op, opt.cost], feed_dict=f)
+    f0 = dict(f)
+    f0[ph["dropout"]] = 0.0
+    assert float(sess.run(opt.cost, feed_dict=f0)) < float(z["batch3_cost"])
