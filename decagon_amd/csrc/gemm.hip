@@ -123,6 +123,85 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
     }
 }
 
+// Batch-reduce with K == 32 and both operands contiguous along k (A(m,k) = a[m*a_sm + k],
+// B(k,n) = b[n*b_sn + k]): the backward's Σ_b dP_b·W2_bᵀ.  The 32 k-values are consumed in
+// the order c = 16h + s (s = MFMA step, h = lane half) — a permutation of the same sum — so
+// each lane reads 16 contiguous floats of its row (4 float4 loads) instead of 16 scattered
+// ones.  A wave computes a 32-row tile against all n (≤ 64: NT tiles) for its run of batches;
+// with a dropout descriptor each batch product is masked before it joins the run's sum.
+template <int NT>
+__global__ __launch_bounds__(256) void gemm_f32_reduce_k32(const GemmArgs args) {
+    int tb, bblk;
+    const GemmOne& g = pick(args, blockIdx.x, tb, bblk);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int tm = tb * 4 + wave;
+    if (tm >= g.tiles_m) return;
+    const int i = lane & 31;
+    const int h = lane >> 5;
+    const int row = tm * 32 + i;
+    const bool row_ok = row < g.m;
+    const int b0 = bblk * g.batch_per_wave;
+    const int b1 = min(b0 + g.batch_per_wave, g.batch);
+    const bool drop = g.drop_state != nullptr;
+    const uint32_t dkey = drop ? dg::drop_key(g.drop_state, g.drop_tag) : 0u;
+    f32x16 sum[NT], acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sum[t] = f32x16{};
+#pragma unroll 1
+    for (int b = b0; b < b1; ++b) {
+        float4 a4[4], b4[NT][4];
+        const float* A = g.a + b * g.a_bs + (int64_t)(row_ok ? row : 0) * g.a_sm + 16 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            a4[q] = row_ok ? *reinterpret_cast<const float4*>(A + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int col = t * 32 + i;
+            const float* B = g.b + b * g.b_bs + (int64_t)(col < g.n ? col : 0) * g.b_sn + 16 * h;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                b4[t][q] = col < g.n ? *reinterpret_cast<const float4*>(B + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = drop ? f32x16{} : sum[t];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float av[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w};
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float bv[4] = {b4[t][q].x, b4[t][q].y, b4[t][q].z, b4[t][q].w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc[t], 0, 0, 0);
+            }
+        }
+        if (drop) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const uint32_t idx = static_cast<uint32_t>(((int64_t)b * g.m + mrow) * g.n + t * 32 + i);
+                    sum[t][r] += acc[t][r] * dg::keep_scale(dkey, idx, g.drop_keep);
+                }
+        } else {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) sum[t] = acc[t];
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int col = t * 32 + i;
+        if (col >= g.n) continue;
+        float* C = g.c + bblk * g.c_bs + (int64_t)col * g.c_sn;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (mrow < g.m) C[(int64_t)mrow * g.c_sm] = sum[t][r];
+        }
+    }
+}
+
 // Projection path: K == KD (compile-time), the A fragment (KD/2 values per lane) lives in
 // registers for all relations the wave handles.
 template <int KD>
@@ -442,6 +521,32 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
     }
     if (A.n == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // batch-reduce, K = 32, both operands contiguous along k, n <= 64, no scaling / map
+    bool rk32 = true;
+    int nt_max = 1;
+    for (int i = 0; i < A.n && rk32; ++i) {
+        const GemmOne& g = A.g[i];
+        rk32 = g.reduce && g.k == 32 && g.a_sk == 1 && g.b_sk == 1 && g.n <= 64 && !g.sa && !g.sc &&
+               (g.a_sm & 3) == 0 && (g.a_bs & 3) == 0 && (g.b_sn & 3) == 0 && (g.b_bs & 3) == 0 &&
+               dg::aligned16(g.a) && dg::aligned16(g.b);
+        nt_max = g.tiles_n > nt_max ? g.tiles_n : nt_max;
+    }
+    if (rk32) {
+        int64_t rblocks = 0;
+        for (int i = 0; i < A.n; ++i) {
+            GemmOne& g = A.g[i];
+            g.tile_blocks = dg::ceil_div(g.tiles_m, 4);  // 4 waves = 4 row tiles per block
+            g.block_begin = static_cast<int32_t>(rblocks);
+            rblocks += (int64_t)g.tile_blocks * dg::ceil_div(g.batch, g.batch_per_wave);
+        }
+        if (rblocks > 0x7fffffff) return DG_EINVAL;
+        dim3 rgrid(static_cast<unsigned>(rblocks)), rblock(256);
+        if (nt_max == 1)
+            hipLaunchKernelGGL(gemm_f32_reduce_k32<1>, rgrid, rblock, 0, st, A);
+        else
+            hipLaunchKernelGGL(gemm_f32_reduce_k32<2>, rgrid, rblock, 0, st, A);
+        return dg::launch_status();
+    }
     // the projection shape (every descriptor): shared A, n <= 32 (a multiple of 4), K in
     // {32, 64}, unscaled, C rows 16-byte aligned and contiguous
     bool proj = kd > 0;
