@@ -169,6 +169,9 @@ SIGNATURES = {
     "dg_adam_f32": (c_int32, [POINTER(DgAdamSeg), c_int32, c_float, c_float, c_float, c_float, c_void_p,
                               c_void_p]),
     "dg_adam_advance": (c_int32, [c_void_p, c_float, c_float, c_float, c_void_p]),
+    "dg_rank_metrics_workspace": (c_int64, [c_int32]),
+    "dg_rank_metrics_f32": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int64,
+                                      c_void_p]),
     "dg_unigram_sample": (
         c_int32,
         [c_void_p, c_int32, c_int32, c_uint64, c_uint64, c_void_p, c_void_p],

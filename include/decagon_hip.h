@@ -394,6 +394,18 @@ int dg_dropout_elems_f32(const float* src, float* out, int32_t K, int32_t n_rows
 int dg_dropout_advance(uint64_t* state, void* stream);
 
 /* --------------------------------------------------------------------------------------
+ * Evaluation: AUROC, AUPRC and AP@k of n_pos positive vs n_neg negative edge
+ * scores, exactly as roc_auc_score (ties count ½), average_precision_score and
+ * rank_metrics.apk(actual = positives, predicted = all sorted by score, stable, descending)
+ * compute them in get_accuracy_scores (main.py:38-80): out[0..2] = {auroc, auprc, apk}
+ * (double).  Integer pair counts per positive, no sort; workspace 16-byte aligned,
+ * dg_rank_metrics_workspace(n_pos) bytes.
+ * -------------------------------------------------------------------------------------- */
+int64_t dg_rank_metrics_workspace(int32_t n_pos);
+int dg_rank_metrics_f32(const float* pos, int32_t n_pos, const float* neg, int32_t n_neg, int32_t k,
+                        double* out, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* --------------------------------------------------------------------------------------
  * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, draw
  * (offset + i) of a counter-based hash stream, through a Walker alias table of `range`
  * entries {acceptance probability as float bits, alias index} (uint32 pairs, built once on

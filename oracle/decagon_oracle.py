@@ -317,3 +317,40 @@ def adam_tf(param: np.ndarray, grad: np.ndarray, m: np.ndarray, v: np.ndarray, t
     v = (v + (g * g - v) * (f(1) - f(beta2))).astype(np.float32)
     p = (param - (m * alpha) / (np.sqrt(v) + f(eps))).astype(np.float32)
     return p, m, v
+
+
+# ----------------------------------------------------------------------------------------
+# Evaluation path: get_accuracy_scores (main.py:38-80)
+# ----------------------------------------------------------------------------------------
+def apk(actual, predicted, k: int = 10) -> float:
+    """rank_metrics.apk (decagon/utility/rank_metrics.py:4-40), restated."""
+    if len(predicted) > k:
+        predicted = predicted[:k]
+    score, num_hits = 0.0, 0.0
+    seen = set()
+    actual = set(actual)
+    for i, p in enumerate(predicted):
+        if p in actual and p not in seen:
+            num_hits += 1.0
+            score += num_hits / (i + 1.0)
+        seen.add(p)
+    if not actual:
+        return 0.0
+    return score / min(len(actual), k)
+
+
+def accuracy_scores(pos_scores: np.ndarray, neg_scores: np.ndarray, k: int = 50):
+    """(roc, auprc, apk@k) as get_accuracy_scores forms them from per-edge scores: labels 1
+    for the positives then 0 for the negatives; `predicted` = edge indices sorted by score,
+    descending, Python's stable sort (main.py:66-76)."""
+    from sklearn import metrics
+
+    pos = np.asarray(pos_scores, np.float64)
+    neg = np.asarray(neg_scores, np.float64)
+    preds_all = np.hstack([pos, neg])
+    labels_all = np.hstack([np.ones(len(pos)), np.zeros(len(neg))])
+    predicted = [i for _, i in sorted(zip(preds_all.tolist(), range(len(preds_all))), reverse=True,
+                                      key=lambda t: t[0])]
+    roc = metrics.roc_auc_score(labels_all, preds_all)
+    aupr = metrics.average_precision_score(labels_all, preds_all)
+    return roc, aupr, apk(list(range(len(pos))), predicted, k=k)

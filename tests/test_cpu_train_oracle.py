@@ -151,3 +151,26 @@ def test_dropout_masks_distribution():
         assert set(np.unique(m)) <= {np.float32(0.0), np.float32(1 / np.float32(0.9))}
     assert 0.79 < ((a > 0) == (b > 0)).mean() < 0.85  # independent draws agree on ~0.82
     assert 0.79 < ((a > 0) == (c > 0)).mean() < 0.85
+
+
+def test_apk_restatement_matches_reference():
+    """oracle.apk against the reference's own rank_metrics.apk (decagon/utility/rank_metrics.py,
+    numpy-only, imported from /root/reference when present — this container)."""
+    import importlib.util
+    import os
+
+    path = "/root/reference/decagon/utility/rank_metrics.py"
+    if not os.path.exists(path):
+        pytest.skip("reference tree not present (GPU box)")
+    os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+    spec = importlib.util.spec_from_file_location("ref_rank_metrics", path)
+    mod = importlib.util.module_from_spec(spec)
+    import sys
+    sys.dont_write_bytecode = True
+    spec.loader.exec_module(mod)
+    rng = np.random.default_rng(4)
+    for n, k in ((100, 50), (30, 50), (500, 10)):
+        scores = rng.integers(0, 15, n).astype(float)
+        actual = list(range(n // 3))
+        predicted = [i for _, i in sorted(zip(scores.tolist(), range(n)), reverse=True, key=lambda t: t[0])]
+        assert orc.apk(actual, predicted, k) == mod.apk(actual, predicted, k)

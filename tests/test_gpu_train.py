@@ -369,3 +369,52 @@ def test_grads_vars_with_dropout_match_oracle(golden_S):
     f0 = dict(f)
     f0[ph["dropout"]] = 0.0
     assert float(sess.run(opt.cost, feed_dict=f0)) < float(z["batch3_cost"])
+
+
+@pytest.mark.parametrize("P,N,k,ties", [(1000, 1000, 50, True), (700, 1500, 50, False), (10, 3, 50, True),
+                                        (60, 40, 50, True)])
+def test_rank_metrics_match_sklearn(P, N, k, ties):
+    """dg_rank_metrics_f32 = roc_auc_score / average_precision_score / rank_metrics.apk."""
+    from decagon_amd.evaluate import rank_metrics
+
+    dev = _dev()
+    rng = np.random.default_rng(P + N)
+    if ties:
+        pos = rng.integers(0, 20, P).astype(np.float32) + 2.0
+        neg = rng.integers(0, 20, N).astype(np.float32)
+    else:
+        pos = (rng.standard_normal(P) + 0.7).astype(np.float32)
+        neg = rng.standard_normal(N).astype(np.float32)
+    got = rank_metrics(torch.from_numpy(pos).to(dev), torch.from_numpy(neg).to(dev), k)
+    want = orc.accuracy_scores(pos, neg, k)
+    for g, w in zip(got, want):
+        assert abs(g - w) <= 1e-12, (got, want)
+
+
+def test_accuracy_scores_through_the_model(golden_S):
+    """evaluate.accuracy_scores (main.py:38-80 on the device) against sklearn on the oracle's
+    predictions of the same sampled edges."""
+    from decagon_amd import evaluate
+
+    z = golden_S
+    dg, ph, model, opt, feed = _setup(z)
+    edge_types = model.edge_types
+    sess = dg.Session()
+    rng = np.random.default_rng(11)
+    et = (1, 1, 2)
+    pos = z["adj_1_1_2_coords"][rng.choice(len(z["adj_1_1_2_coords"]), 300, replace=False)]
+    neg = rng.integers(0, 400, (300, 2))
+    edges_pos = {(1, 1): {2: pos}}
+    edges_neg = {(1, 1): {2: neg}}
+    flat = {}
+    for i, j in edge_types:
+        for k in range(edge_types[i, j]):
+            flat[i, j, k] = len(flat)
+    got = evaluate.accuracy_scores(sess, opt, ph, feed, edges_pos, edges_neg, et, flat, k=50)
+    emb = [z["emb_0"], z["emb_1"]]
+    R = z["dec_1_1_global_interaction"].astype(np.float64)
+    D = np.diag(z["dec_1_1_local_variation_2"].astype(np.float64))
+    pred = orc.predict(emb, 1, 1, R, D)
+    want = orc.accuracy_scores(pred[pos[:, 0], pos[:, 1]], pred[neg[:, 0], neg[:, 1]], 50)
+    for g, w in zip(got, want):
+        assert abs(g - w) <= 1e-3, (got, want)  # fp32 scores vs float64: near-ties may swap
