@@ -352,9 +352,10 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 // same for all K relations of the group): a workgroup copies a 32-float column slice of X
 // into LDS once (rows 144 B apart: the 16-byte bank slot of float4 j of row v is
 // (9v + j) mod 16, a bijection of v mod 16), then its 16 waves walk up to 16 x 128 (chunk, row)
-// items, 8 rows at a time per wave: 8 lanes per row, one float4 column piece each.  A row's
-// (vcol, val) pairs come in 8 at a time with one coalesced load per lane group (the next 8
-// prefetched), are handed out by shuffles, and each gathers one ds_read_b128 per lane.
+// items, 16 rows at a time per wave: 4 lanes per row, two float4 column pieces each.  A row's
+// (vcol, val) pairs come in 4 at a time with one coalesced load per lane group (the next 4
+// prefetched), are handed out by shuffles (two per nonzero and 16 rows), and each gathers two
+// ds_read_b128 per lane.
 // No per-relation barrier, no operand re-read from L2.
 constexpr int kLdsSlice = 32;                 // floats per column slice
 constexpr int kLdsRowF4 = 9;                  // float4 slots per staged row (8 + 1 pad)
@@ -372,7 +373,7 @@ struct LdsGroupK {
     int32_t n_items;      // n_chunks * n_rows
     int32_t item_blocks;  // ceil(n_items / (16 * per_wave))
     int32_t block_begin;
-    int32_t per_wave;     // items per wave: a multiple of 8, <= kLdsItemsMax
+    int32_t per_wave;     // items per wave: a multiple of 16, <= kLdsItemsMax
 };
 
 struct LdsArgs {
@@ -404,9 +405,9 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
     __syncthreads();  // the only barrier
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int rg = lane >> 3;                     // row of the wave's 8
-    const int q = lane & 7;                       // float4 piece of the slice
-    const bool qok = 4 * q < cw;
+    const int rg = lane >> 2;                     // row of the wave's 16
+    const int q = lane & 3;                       // float4 pieces q and q + 4 of the slice
+    const bool qok0 = 4 * q < cw, qok1 = 4 * (q + 4) < cw;
     // this wave's per_wave (<= 128) consecutive items: their row pointers in three registers
     // (one coalesced load), so a row's range never waits on memory
     const int pw = g.per_wave;
@@ -424,35 +425,38 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
     int npc = nb + q < ne ? g.vcol[nb + q] : 0;
     float npv = nb + q < ne ? g.val[nb + q] : 0.f;
 #pragma unroll 1
-    for (int t = 0; wbase + 8 * t < item_end; ++t) {
-        const int item = wbase + 8 * t + rg;
+    for (int t = 0; wbase + 16 * t < item_end; ++t) {
+        const int item = wbase + 16 * t + rg;
         const int beg = nb, end = ne;
         int vc = npc;
         float vv = npv;
-        if (8 * t + 8 < pw) {  // the next 8 rows' ranges and first pairs
-            nb = rp(8 * t + 8 + rg);
-            ne = rp(8 * t + 9 + rg);
+        if (16 * t + 16 < pw) {  // the next 16 rows' ranges and first pairs
+            nb = rp(16 * t + 16 + rg);
+            ne = rp(16 * t + 17 + rg);
             npc = nb + q < ne ? g.vcol[nb + q] : 0;
             npv = nb + q < ne ? g.val[nb + q] : 0.f;
         }
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
 #pragma unroll 1
-        for (int cb = beg; __any(cb < end); cb += 8) {
+        for (int cb = beg; __any(cb < end); cb += 4) {
             const int cv = vc;
             const float w = vv;
-            const int p = cb + 8 + q;  // the next 8 pairs of this row
+            const int p = cb + 4 + q;  // the next 4 pairs of this row
             vc = p < end ? g.vcol[p] : 0;
             vv = p < end ? g.val[p] : 0.f;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int src = (lane & ~7) + u;
+            for (int u = 0; u < 4; ++u) {
+                const int src = (lane & ~3) + u;
                 const int xv = __shfl(cv, src);
                 const float wv = __shfl(w, src);  // 0 past the row's end
-                const float4 xr = xs[xv * kLdsRowF4 + q];
-                dg::fma4(acc, wv, xr);
+                const float4* xr = xs + xv * kLdsRowF4;
+                dg::fma4(acc0, wv, xr[q]);
+                dg::fma4(acc1, wv, xr[q + 4]);
             }
         }
-        if (item < item_end && qok) *reinterpret_cast<float4*>(g.out + (int64_t)item * d + c0 + 4 * q) = acc;
+        float* o = g.out + (int64_t)item * d + c0;
+        if (item < item_end && qok0) *reinterpret_cast<float4*>(o + 4 * q) = acc0;
+        if (item < item_end && qok1) *reinterpret_cast<float4*>(o + 4 * (q + 4)) = acc1;
     }
 }
 
@@ -651,7 +655,7 @@ extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_grou
         g.n_items = static_cast<int32_t>(items);
         // items per wave: enough workgroups (~512) to fill the chip, 8..128 items per wave
         int pw = static_cast<int>((items + 512 * 16 - 1) / (512 * 16));
-        pw = pw < 8 ? 8 : (pw > kLdsItemsMax ? kLdsItemsMax : (pw + 7) / 8 * 8);
+        pw = pw < 16 ? 16 : (pw > kLdsItemsMax ? kLdsItemsMax : (pw + 15) / 16 * 16);
         g.per_wave = pw;
         g.item_blocks = dg::ceil_div(items, 16 * pw);
         g.block_begin = static_cast<int32_t>(blocks);
