@@ -148,9 +148,9 @@ __global__ __launch_bounds__(256) void gemm_f32_reduce_k32(const GemmArgs args) 
     f32x16 sum[NT], acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) sum[t] = f32x16{};
-#pragma unroll 1
-    for (int b = b0; b < b1; ++b) {
-        float4 a4[4], b4[NT][4];
+    // the next batch's fragments are loaded while the current batch's MFMAs run
+    float4 a4[4], b4[NT][4];
+    auto load = [&](int b) {
         const float* A = g.a + b * g.a_bs + (int64_t)(row_ok ? row : 0) * g.a_sm + 16 * h;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -163,14 +163,26 @@ __global__ __launch_bounds__(256) void gemm_f32_reduce_k32(const GemmArgs args) 
             for (int q = 0; q < 4; ++q)
                 b4[t][q] = col < g.n ? *reinterpret_cast<const float4*>(B + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+    };
+    if (b0 < b1) load(b0);
+#pragma unroll 1
+    for (int b = b0; b < b1; ++b) {
+        float4 ca[4], cb[NT][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ca[q] = a4[q];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cb[t][q] = b4[t][q];
+        if (b + 1 < b1) load(b + 1);
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] = drop ? f32x16{} : sum[t];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float av[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w};
+            const float av[4] = {ca[q].x, ca[q].y, ca[q].z, ca[q].w};
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const float bv[4] = {b4[t][q].x, b4[t][q].y, b4[t][q].z, b4[t][q].w};
+                const float bv[4] = {cb[t][q].x, cb[t][q].y, cb[t][q].z, cb[t][q].w};
 #pragma unroll
                 for (int u = 0; u < 4; ++u) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc[t], 0, 0, 0);
             }
@@ -371,7 +383,7 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
 // backward of layers.py:113).  The reduction runs over `rows` (up to the node count), so a
 // workgroup takes one (batch, row split) and its 4 waves interleave the split's row pairs,
 // each on MT×NT accumulators of v_mfma_f32_32x32x2_f32 (both operand fragments are rows of
-// A / B read by 32 consecutive lanes: coalesced); the waves meet in LDS in wave order.
+// A / B read by 32 consecutive lanes: coalesced); the waves meet in LDS in a fixed order.
 struct TnArgs {
     const float* a;
     const float* b;
@@ -383,7 +395,7 @@ struct TnArgs {
 
 template <int MT, int NT>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const TnArgs a) {
-    __shared__ float red[4][MT * NT][16][64];
+    __shared__ float red[2][MT * NT][16][64];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int i = lane & 31, h = lane >> 5;
@@ -398,7 +410,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const TnArgs a) {
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x16{};
-#pragma unroll 4
+#pragma unroll 8
     for (int r0 = r_begin + 2 * w; r0 < r_end; r0 += 8) {
         const int r = r0 + h;
         const bool ok = r < r_end;
@@ -413,17 +425,29 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const TnArgs a) {
             for (int nt = 0; nt < NT; ++nt)
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mt], bf[nt], acc[mt][nt], 0, 0, 0);
     }
+    // the 4 waves' sums meet in two LDS stages, (w0 + w2) + (w1 + w3): 16 KB per MT·NT pair
+    if (w >= 2) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+            for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) red[w][mt * NT + nt][r][lane] = acc[mt][nt][r];
+                for (int r = 0; r < 16; ++r) red[w - 2][mt * NT + nt][r][lane] = acc[mt][nt][r];
+    }
+    __syncthreads();
+    if (w < 2) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) red[w][mt * NT + nt][r][lane] += acc[mt][nt][r];
+    }
     __syncthreads();
     float* out = a.out + ((int64_t)s * a.batch + b) * a.M * a.N;
     for (int e = threadIdx.x; e < MT * NT * 1024; e += 256) {
         const int q = e >> 10, r = (e >> 6) & 15, l = e & 63;
-        const float v = red[0][q][r][l] + red[1][q][r][l] + red[2][q][r][l] + red[3][q][r][l];
+        const float v = red[0][q][r][l] + red[1][q][r][l];
         const int mt = q / NT, nt = q - mt * NT;
         const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
         out[(int64_t)row * a.N + nt * 32 + (l & 31)] = v;

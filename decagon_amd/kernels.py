@@ -468,7 +468,7 @@ class PreparedGemmTN:
         if rb != rows or tuple(c.shape) != (batch, M, N):
             raise ValueError("gemm_tn: shapes")
         if rows_per_split <= 0:  # enough workgroups to fill the chip, ranges of >= 64 rows
-            self.n_split = max(1, min(-(-2048 // max(1, batch)), -(-rows // 64)))
+            self.n_split = max(1, min(-(-1024 // max(1, batch)), -(-rows // 64)))
         else:
             self.n_split = max(1, -(-rows // max(2, rows_per_split)))
         self.partial = (torch.empty((self.n_split, batch, M, N), device=a.device) if self.n_split > 1 else None)
