@@ -374,6 +374,7 @@ struct LdsGroupK {
     int32_t item_blocks;  // ceil(n_items / (16 * per_wave))
     int32_t block_begin;
     int32_t per_wave;     // items per wave: a multiple of 16, <= kLdsItemsMax
+    int32_t persist;      // workgroups per column slice; workgroup p takes item blocks p, p + persist, ...
 };
 
 struct LdsArgs {
@@ -392,8 +393,8 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
     while (gi + 1 < a.n_groups && b >= a.g[gi + 1].block_begin) ++gi;
     const LdsGroupK& g = a.g[gi];
     const int lb = b - g.block_begin;
-    const int s = lb / g.item_blocks;             // column slice
-    const int ib = lb - s * g.item_blocks;        // item block
+    const int s = lb / g.persist;                 // column slice
+    const int p0 = lb - s * g.persist;            // first item block
     const int d = a.d;
     const int c0 = s * kLdsSlice;
     const int cw = min(kLdsSlice, d - c0);        // columns of this slice (multiple of 4)
@@ -408,55 +409,59 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
     const int rg = lane >> 2;                     // row of the wave's 16
     const int q = lane & 3;                       // float4 pieces q and q + 4 of the slice
     const bool qok0 = 4 * q < cw, qok1 = 4 * (q + 4) < cw;
-    // this wave's per_wave (<= 128) consecutive items: their row pointers in three registers
-    // (one coalesced load), so a row's range never waits on memory
-    const int pw = g.per_wave;
-    const int wbase = (ib * 16 + wave) * pw;
-    const int item_end = min(g.n_items, wbase + pw);
-    if (wbase >= item_end) return;
-    const int rp0 = g.rowptr[min(wbase + lane, g.n_items)];
-    const int rp1 = g.rowptr[min(wbase + 64 + lane, g.n_items)];
-    const int rp2 = g.rowptr[min(wbase + 128, g.n_items)];  // (read only when pw == 128)
-    auto rp = [&](int idx) {  // row pointer wbase + idx, idx in [0, 128]
-        const int v0 = __shfl(rp0, idx & 63), v1 = __shfl(rp1, idx & 63);
-        return idx < 64 ? v0 : (idx < 128 ? v1 : rp2);
-    };
-    int nb = rp(rg), ne = rp(rg + 1);
-    int npc = nb + q < ne ? g.vcol[nb + q] : 0;
-    float npv = nb + q < ne ? g.val[nb + q] : 0.f;
+    // the slice is staged once per workgroup; the workgroup then walks its item blocks
 #pragma unroll 1
-    for (int t = 0; wbase + 16 * t < item_end; ++t) {
-        const int item = wbase + 16 * t + rg;
-        const int beg = nb, end = ne;
-        int vc = npc;
-        float vv = npv;
-        if (16 * t + 16 < pw) {  // the next 16 rows' ranges and first pairs
-            nb = rp(16 * t + 16 + rg);
-            ne = rp(16 * t + 17 + rg);
-            npc = nb + q < ne ? g.vcol[nb + q] : 0;
-            npv = nb + q < ne ? g.val[nb + q] : 0.f;
-        }
-        float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
+    for (int ib = p0; ib < g.item_blocks; ib += g.persist) {
+        // this wave's per_wave (<= 128) consecutive items: their row pointers in three registers
+        // (one coalesced load), so a row's range never waits on memory
+        const int pw = g.per_wave;
+        const int wbase = (ib * 16 + wave) * pw;
+        const int item_end = min(g.n_items, wbase + pw);
+        if (wbase >= item_end) continue;
+        const int rp0 = g.rowptr[min(wbase + lane, g.n_items)];
+        const int rp1 = g.rowptr[min(wbase + 64 + lane, g.n_items)];
+        const int rp2 = g.rowptr[min(wbase + 128, g.n_items)];  // (read only when pw == 128)
+        auto rp = [&](int idx) {  // row pointer wbase + idx, idx in [0, 128]
+            const int v0 = __shfl(rp0, idx & 63), v1 = __shfl(rp1, idx & 63);
+            return idx < 64 ? v0 : (idx < 128 ? v1 : rp2);
+        };
+        int nb = rp(rg), ne = rp(rg + 1);
+        int npc = nb + q < ne ? g.vcol[nb + q] : 0;
+        float npv = nb + q < ne ? g.val[nb + q] : 0.f;
 #pragma unroll 1
-        for (int cb = beg; __any(cb < end); cb += 4) {
-            const int cv = vc;
-            const float w = vv;
-            const int p = cb + 4 + q;  // the next 4 pairs of this row
-            vc = p < end ? g.vcol[p] : 0;
-            vv = p < end ? g.val[p] : 0.f;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int src = (lane & ~3) + u;
-                const int xv = __shfl(cv, src);
-                const float wv = __shfl(w, src);  // 0 past the row's end
-                const float4* xr = xs + xv * kLdsRowF4;
-                dg::fma4(acc0, wv, xr[q]);
-                dg::fma4(acc1, wv, xr[q + 4]);
+        for (int t = 0; wbase + 16 * t < item_end; ++t) {
+            const int item = wbase + 16 * t + rg;
+            const int beg = nb, end = ne;
+            int vc = npc;
+            float vv = npv;
+            if (16 * t + 16 < pw) {  // the next 16 rows' ranges and first pairs
+                nb = rp(16 * t + 16 + rg);
+                ne = rp(16 * t + 17 + rg);
+                npc = nb + q < ne ? g.vcol[nb + q] : 0;
+                npv = nb + q < ne ? g.val[nb + q] : 0.f;
             }
+            float4 acc0 = make_float4(0.f, 0.f, 0.f, 0.f), acc1 = acc0;
+#pragma unroll 1
+            for (int cb = beg; __any(cb < end); cb += 4) {
+                const int cv = vc;
+                const float w = vv;
+                const int p = cb + 4 + q;  // the next 4 pairs of this row
+                vc = p < end ? g.vcol[p] : 0;
+                vv = p < end ? g.val[p] : 0.f;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int src = (lane & ~3) + u;
+                    const int xv = __shfl(cv, src);
+                    const float wv = __shfl(w, src);  // 0 past the row's end
+                    const float4* xr = xs + xv * kLdsRowF4;
+                    dg::fma4(acc0, wv, xr[q]);
+                    dg::fma4(acc1, wv, xr[q + 4]);
+                }
+            }
+            float* o = g.out + (int64_t)item * d + c0;
+            if (item < item_end && qok0) *reinterpret_cast<float4*>(o + 4 * q) = acc0;
+            if (item < item_end && qok1) *reinterpret_cast<float4*>(o + 4 * (q + 4)) = acc1;
         }
-        float* o = g.out + (int64_t)item * d + c0;
-        if (item < item_end && qok0) *reinterpret_cast<float4*>(o + 4 * q) = acc0;
-        if (item < item_end && qok1) *reinterpret_cast<float4*>(o + 4 * (q + 4)) = acc1;
     }
 }
 
@@ -633,7 +638,7 @@ extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_grou
     LdsArgs a{};
     a.d = d;
     a.n_slices = dg::ceil_div(d, kLdsSlice);
-    int64_t blocks = 0;
+    int64_t blocks = 0, total_items = 0;
     int max_rows = 0;
     for (int i = 0; i < n_groups; ++i) {
         const dg_rel_group& s = groups[i];
@@ -653,18 +658,32 @@ extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_grou
         g.x_ld = k.x_ld;
         g.x_rows = s.x_rows;
         g.n_items = static_cast<int32_t>(items);
-        // items per wave: enough workgroups (~512) to fill the chip, 8..128 items per wave
-        int pw = static_cast<int>((items + 512 * 16 - 1) / (512 * 16));
+        // items per wave: ~2048 item blocks of 16 waves for balance over the resident
+        // workgroups, 16..128 items per wave
+        int pw = static_cast<int>((items + 2048 * 16 - 1) / (2048 * 16));
         pw = pw < 16 ? 16 : (pw > kLdsItemsMax ? kLdsItemsMax : (pw + 15) / 16 * 16);
         g.per_wave = pw;
         g.item_blocks = dg::ceil_div(items, 16 * pw);
-        g.block_begin = static_cast<int32_t>(blocks);
-        blocks += (int64_t)g.item_blocks * a.n_slices;
-        if (blocks > 0x7fffffff) return DG_EINVAL;
+        total_items += items;
         max_rows = s.x_rows > max_rows ? s.x_rows : max_rows;
     }
-    if (blocks == 0) return DG_OK;
+    if (a.n_groups == 0) return DG_OK;
     const int lds = max_rows * kLdsRowF4 * 16;
+    // persistent workgroups: as many as are resident at once (two 1024-thread workgroups per CU
+    // at most, fewer when the staged slice is large), shared by the groups in proportion to
+    // their items, so each slice is staged once per resident workgroup instead of once per
+    // item block
+    const int per_cu = lds > 0 ? (160 * 1024 / lds < 2 ? 1 : 2) : 2;
+    const int64_t resident = 256LL * per_cu;
+    for (int i = 0; i < a.n_groups; ++i) {
+        LdsGroupK& g = a.g[i];
+        int64_t share = (resident * g.n_items + total_items - 1) / total_items;
+        share = (share + a.n_slices - 1) / a.n_slices;
+        g.persist = static_cast<int32_t>(share < 1 ? 1 : (share > g.item_blocks ? g.item_blocks : share));
+        g.block_begin = static_cast<int32_t>(blocks);
+        blocks += (int64_t)g.persist * a.n_slices;
+    }
+    if (blocks > 0x7fffffff) return DG_EINVAL;
     static bool configured = false;
     if (!configured) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmm_lds_kernel),
