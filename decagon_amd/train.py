@@ -95,8 +95,8 @@ class TrainPlan:
             raise NotImplementedError("training runs on one GPU over a ForwardPlan(keep_sums=True)")
         # with dropout (fwd.drop_state), the backward reuses the forward's masks: the draws of the
         # forward's step, regenerated from the same counter-based hash (dropout.hip)
-        if any(f is not None for f in features.values()):
-            raise NotImplementedError("the backward for sparse (non-identity) features is not on the HIP path")
+        # sparse features X_j (mono side effects): layer 1's weight gradient is X_jᵀ·(Â_kᵀ·dS1)
+        # per relation, a second transposed SpMM over the same K chunks the forward used
         g = fwd.g
         self.fwd = fwd
         dev = g.device
@@ -112,6 +112,7 @@ class TrainPlan:
         self.gW2: Dict[EdgeType, torch.Tensor] = {}
         specs2, specs1, gemm_w2, gemm_h1 = [], [], [], []
         self._w1_drop = []
+        self._feat_specs: List[kernels.RelGroupSpec] = []
         runs: Dict[int, List[Tuple[torch.Tensor, int]]] = {j: [] for j in srcs}
         self._dS1, self._dS2 = {}, {}
         for et in ets:
@@ -131,11 +132,22 @@ class TrainPlan:
             dP = torch.zeros((K, n[j], h2), **f32)
             self._dS1[et], self._dS2[et] = dS1, dS2
             self.gW2[et] = torch.zeros_like(w2.stacks[et])
-            self.gW1[et] = torch.zeros((K, n[j], h1), **f32)
-            if tuple(w1.stacks[et].shape) != (K, n[j], h1):
-                raise ValueError(f"layer-1 weights of {et} do not match identity features")
+            fj = features.get(j)
+            F = n[j] if fj is None else int(fj.shape[1])
+            self.gW1[et] = torch.zeros((K, F, h1), **f32)
+            if tuple(w1.stacks[et].shape) != (K, F, h1):
+                raise ValueError(f"layer-1 weights of {et} are {tuple(w1.stacks[et].shape)}, expected ({K}, {F}, {h1})")
+            # Âᵀ·dS1 per relation: the weight gradient itself (identity features), or the
+            # operand of X_jᵀ·(·) (sparse features)
+            g1 = self.gW1[et] if fj is None else torch.zeros((K, n[j], h1), **f32)
             specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, n[i], vcol_max=vmax))
-            specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, self.gW1[et], n[j], K, h1, n[i], vcol_max=vmax))
+            specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, g1, n[j], K, h1, n[i], vcol_max=vmax))
+            if fj is not None:
+                xt = merge_chunks([transpose_csr(fj)] * K, np.arange(K), 1, K)  # vcol = k·n_j + drug
+                self._feat_specs.append(kernels.RelGroupSpec(
+                    torch.from_numpy(xt.rowptr).to(dev), torch.from_numpy(xt.vcol).to(dev),
+                    torch.from_numpy(xt.val).to(dev), g1, self.gW1[et], F, K, h1, K * n[j],
+                    vcol_max=int(xt.vcol.max()) if xt.nnz else -1))
             # dW2_k = H_kᵀ·dP_k with H_k = H1_j (or its per-relation dropout draw), the reduction
             # over the n_j rows split for long ones
             H = fwd.hdrop.get(et, fwd.hidden1[j])
@@ -161,6 +173,7 @@ class TrainPlan:
             for lds in (True, False):
                 sel = [s for s in specs if small(s) == lds]
                 out += [kernels.PreparedSpmm(c, d, lds=lds) for c in chunked(sel)]
+        self._feat = [kernels.PreparedSpmm(c, h1) for c in chunked(self._feat_specs)]
         self._gemm_w2 = gemm_w2
         self._gemm_h1 = [kernels.PreparedGemmMulti(c) for c in chunked(gemm_h1)]
         self._epi_h1 = []
@@ -198,6 +211,8 @@ class TrainPlan:
         for l in self._l2g1:
             l()
         for s in self._spmm1:
+            s()
+        for s in self._feat:
             s()
         for f in self._w1_drop:
             f()
