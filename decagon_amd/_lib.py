@@ -21,7 +21,8 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 15
+ABI_VERSION = 16
+DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
 DG_MAX_ADAM_SEGS = 32
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
@@ -38,7 +39,8 @@ class DgRelGroup(ctypes.Structure):
         ("n_rows", c_int32),
         ("n_chunks", c_int32),
         ("x_rows", c_int32),
-        ("reserved", c_int32 * 3),
+        ("flags", c_int32),
+        ("reserved", c_int32 * 2),
     ]
 
 

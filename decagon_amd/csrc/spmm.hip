@@ -55,6 +55,7 @@ struct SpmmGroupK {
     int32_t row_blocks;
     int32_t block_begin;
     int32_t n_blocks;
+    int64_t chunk_x;  // shared pattern: elements between the chunks' X slabs (0: merged CSR)
 };
 
 struct SpmmArgs {
@@ -70,14 +71,14 @@ constexpr int kUnroll = 8;        // gathers in flight per lane
 // starting at batch wpart.  Returns the folded row in every lane (lane l holds columns
 // 4(l%LP) .. 4(l%LP)+3).
 template <int LP>
-__device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, int beg, int end, int d,
+__device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb, int beg, int end, int d,
                                             int wpart = 0, int wcount = 1) {
     constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const int q = lane % LP;
     const bool qact = q * 4 < d;
-    const float* __restrict__ xq = g.x + q * 4;
+    const float* __restrict__ xq = xb + q * 4;
     const int32_t* __restrict__ vcolp = g.vcol;
     const float* __restrict__ valp = g.val;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -148,7 +149,9 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
     if (r >= g.n_rows) return;  // wave-uniform; no barriers in this kernel
     const int d = args.d;
     const int64_t slot = (int64_t)c * g.n_rows + r;
-    const float4 acc = range_sum<LP>(g, g.rowptr[slot], g.rowptr[slot + 1], d);
+    // shared pattern: every chunk reads rowptr[r] over its own X slab
+    const int64_t ps = g.chunk_x ? r : slot;
+    const float4 acc = range_sum<LP>(g, g.x + c * g.chunk_x, g.rowptr[ps], g.rowptr[ps + 1], d);
     if (lane < LP && lane * 4 < d) *reinterpret_cast<float4*>(g.out + slot * d + lane * 4) = acc;
 }
 
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
     const int q = lane % LP;
     if (gl < t.g_count) {
         const SpmmGroupK& g = a.g[t.g_begin + gl];
-        const float4 s = range_sum<LP>(g, g.rowptr[r], g.rowptr[r + 1], d, part, W);
+        const float4 s = range_sum<LP>(g, g.x, g.rowptr[r], g.rowptr[r + 1], d, part, W);
         if (lane < LP) pbuf[wave][lane] = s;
     }
     __syncthreads();
@@ -467,14 +470,16 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 15; }
+extern "C" int32_t dg_abi_version(void) { return 16; }
 
 
 namespace {
 
 // Validate one descriptor and copy it into the kernel form.  Returns DG_OK or an error.
-int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k) {
+int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k, bool allow_shared = false) {
     if (s.n_rows < 0 || s.n_chunks < 1 || s.x_rows < 0) return DG_EINVAL;
+    if (s.flags & ~DG_GROUP_SHARED_PATTERN) return DG_EINVAL;
+    if ((s.flags & DG_GROUP_SHARED_PATTERN) && !allow_shared) return DG_EINVAL;
     // vcol/val may be NULL for a group without nonzeros (rowptr all zero: never read)
     if (!s.rowptr || !s.x || (need_out && !s.out)) return DG_EINVAL;
     if (!dg::aligned16(s.x) || (need_out && !dg::aligned16(s.out)) || (s.x_ld & 3)) return DG_EALIGN;
@@ -489,6 +494,7 @@ int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k) {
     k.n_rows = s.n_rows;
     k.n_chunks = s.n_chunks;
     k.row_blocks = dg::ceil_div(s.n_rows, kRowsPerBlock);
+    k.chunk_x = (s.flags & DG_GROUP_SHARED_PATTERN) ? (int64_t)s.x_rows * s.x_ld : 0;
     return DG_OK;
 }
 
@@ -507,7 +513,7 @@ extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, 
         const dg_rel_group& s = groups[i];
         if (s.n_rows == 0) continue;
         SpmmGroupK& k = args.g[ng];
-        const int rc = convert_group(s, d, true, k);
+        const int rc = convert_group(s, d, true, k, true);
         if (rc != DG_OK) return rc;
         ++ng;
         const int64_t items = (int64_t)k.n_chunks * k.row_blocks;

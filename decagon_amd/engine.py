@@ -284,12 +284,12 @@ class ForwardPlan:
             if fj.shape[0] != n[j] or fj.shape[1] != F:
                 raise ValueError(f"features of type {j} have shape {fj.shape}, weights expect (*, {F})")
             # X_j·W1_k for every relation k of the group (global slabs; sharded ranks compute
-            # all of them — sparse features are small next to the adjacency)
-            fm = merge_chunks([fj] * K, np.arange(K), 1, K)
+            # all of them — sparse features are small next to the adjacency): one copy of X_j's
+            # pattern shared by the K chunks, chunk k reading W1_k
             xw = torch.empty((K, n[j], h1), **f32)
-            spec = kernels.RelGroupSpec(torch.from_numpy(fm.rowptr).to(dev), torch.from_numpy(fm.vcol).to(dev),
-                                        torch.from_numpy(fm.val).to(dev), W, xw, n[j], K, h1, K * F,
-                                        vcol_max=int(fm.vcol.max()) if fm.nnz else -1)
+            spec = kernels.RelGroupSpec(torch.from_numpy(fj.rowptr).to(dev), torch.from_numpy(fj.col).to(dev),
+                                        torch.from_numpy(fj.val).to(dev), W, xw, n[j], K, h1, F,
+                                        vcol_max=int(fj.col.max()) if fj.nnz else -1, shared=True)
             self._pre.append(kernels.PreparedSpmm([spec], h1))
             x1[et] = xw
 

@@ -54,8 +54,10 @@ class RelGroupSpec:
     n_rows: int
     n_chunks: int
     x_ld: int
-    x_rows: int                   # rows of x the kernel may address
+    x_rows: int                   # rows of x the kernel may address (per chunk when shared)
     vcol_max: int = -1            # host-known max(vcol) (-1: no nonzeros)
+    shared: bool = False          # DG_GROUP_SHARED_PATTERN: one CSR [n_rows] for every chunk, chunk c
+                                  # reading x rows [c*x_rows, (c+1)*x_rows) (dg_spmm_groups_f32 only)
 
     def validate(self, d: int, need_out: bool = True) -> None:
         _dev(self.rowptr, torch.int32, "rowptr")
@@ -68,16 +70,18 @@ class RelGroupSpec:
             return
         if self.n_chunks < 1:
             raise ValueError("n_chunks must be >= 1")
-        if self.rowptr.numel() < self.n_chunks * self.n_rows + 1:
-            raise ValueError(f"rowptr has {self.rowptr.numel()} entries, kernel reads {self.n_chunks * self.n_rows + 1}")
+        n_ptr = (self.n_rows if self.shared else self.n_chunks * self.n_rows) + 1
+        if self.rowptr.numel() < n_ptr:
+            raise ValueError(f"rowptr has {self.rowptr.numel()} entries, kernel reads {n_ptr}")
         if self.vcol.numel() != self.val.numel():
             raise ValueError("vcol/val length mismatch")
         if self.x_ld < d or self.x_ld % 4:
             raise ValueError("x_ld must be >= d and a multiple of 4")
         if self.vcol_max >= self.x_rows:
             raise ValueError(f"vcol reaches row {self.vcol_max} of a {self.x_rows}-row operand")
-        if self.x_rows > 0 and self.x.numel() < (self.x_rows - 1) * self.x_ld + d:
-            raise ValueError(f"x has {self.x.numel()} elements, kernel may read {(self.x_rows - 1) * self.x_ld + d}")
+        slabs = self.n_chunks if self.shared else 1
+        if self.x_rows > 0 and self.x.numel() < (slabs * self.x_rows - 1) * self.x_ld + d:
+            raise ValueError(f"x has {self.x.numel()} elements, kernel may read {(slabs * self.x_rows - 1) * self.x_ld + d}")
         if self.x_rows * self.x_ld >= 2**31:
             raise ValueError("dense operand too large for 32-bit gather offsets")
         if need_out and self.out.numel() < self.n_chunks * self.n_rows * d:
@@ -94,6 +98,7 @@ def _fill_group(g, s: RelGroupSpec) -> None:
     g.n_rows = s.n_rows
     g.n_chunks = s.n_chunks
     g.x_rows = s.x_rows
+    g.flags = _lib.DG_GROUP_SHARED_PATTERN if s.shared else 0
 
 
 SPMM_LDS_MAX_ROWS = 160 * 1024 // 144  # dg_spmm_groups_lds_f32: operand rows staged in LDS

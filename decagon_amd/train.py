@@ -142,12 +142,12 @@ class TrainPlan:
             g1 = self.gW1[et] if fj is None else torch.zeros((K, n[j], h1), **f32)
             specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, n[i], vcol_max=vmax))
             specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, g1, n[j], K, h1, n[i], vcol_max=vmax))
-            if fj is not None:
-                xt = merge_chunks([transpose_csr(fj)] * K, np.arange(K), 1, K)  # vcol = k·n_j + drug
+            if fj is not None:  # X_jᵀ's pattern shared by the K chunks, chunk k reading G_k
+                xt = transpose_csr(fj)
                 self._feat_specs.append(kernels.RelGroupSpec(
-                    torch.from_numpy(xt.rowptr).to(dev), torch.from_numpy(xt.vcol).to(dev),
-                    torch.from_numpy(xt.val).to(dev), g1, self.gW1[et], F, K, h1, K * n[j],
-                    vcol_max=int(xt.vcol.max()) if xt.nnz else -1))
+                    torch.from_numpy(xt.rowptr).to(dev), torch.from_numpy(xt.col).to(dev),
+                    torch.from_numpy(xt.val).to(dev), g1, self.gW1[et], F, K, h1, n[j],
+                    vcol_max=int(xt.col.max()) if xt.nnz else -1, shared=True))
             # dW2_k = H_kᵀ·dP_k with H_k = H1_j (or its per-relation dropout draw), the reduction
             # over the n_j rows split for long ones
             H = fwd.hdrop.get(et, fwd.hidden1[j])

@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (15); bumped whenever a struct layout or a signature changes. */
+/* ABI version (16); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -66,9 +66,17 @@ typedef struct dg_rel_group {
     int64_t x_ld;               /* elements between consecutive rows of X                 */
     int32_t n_rows;
     int32_t n_chunks;
-    int32_t x_rows;             /* rows of X addressable (bound on vcol)                  */
-    int32_t reserved[3];        /* zero                                                   */
+    int32_t x_rows;             /* rows of X addressable (bound on vcol); per chunk when  */
+                                /* DG_GROUP_SHARED_PATTERN is set                         */
+    int32_t flags;              /* 0, or DG_GROUP_SHARED_PATTERN (dg_spmm_groups_f32 only) */
+    int32_t reserved[2];        /* zero                                                   */
 } dg_rel_group;
+
+/* Every chunk c uses the same CSR pattern (rowptr[0..n_rows], vcol, val) over its own slab of
+ * X: rows [c*x_rows, (c+1)*x_rows).  The relation-batched X_j·W_k of sparse features
+ * (layers.py:89, one X_j for every relation k) and its backward X_jᵀ·G_k, without K copies
+ * of the pattern. */
+#define DG_GROUP_SHARED_PATTERN 1
 
 int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
                        int32_t d, void* stream);

@@ -110,6 +110,42 @@ def test_spmm_groups_chunks_and_slabs(K, chunk, d):
         assert rel_err(s.out.cpu().numpy(), w) <= 1e-5
 
 
+@pytest.mark.parametrize("d", [12, 64])
+def test_spmm_shared_pattern(K, d):
+    """DG_GROUP_SHARED_PATTERN: one CSR (X_j's) for every chunk, chunk k over its own slab
+    (X_j·W_k for all k, layers.py:89) — bit-identical to the merged layout that repeats the
+    pattern K times, beside a merged group in the same launch; rejected by the fused and LDS
+    entry points."""
+    from decagon_amd import _lib
+    from decagon_amd.sparse import coo_to_csr, merge_chunks, sparse_to_tuple
+
+    rng = np.random.default_rng(d)
+    n_r, F, nrel = 77, 130, 5
+    m = _rand_csr(rng, n_r, F, 0.06, empty_rows=0.15)
+    h = coo_to_csr(*sparse_to_tuple(m))
+    W = torch.from_numpy(rng.standard_normal((nrel, F, d)).astype(np.float32)).cuda()
+    out_s = torch.zeros((nrel, n_r, d), device="cuda")
+    out_m = torch.zeros((nrel, n_r, d), device="cuda")
+    shared = K.RelGroupSpec(torch.from_numpy(h.rowptr).cuda(), torch.from_numpy(h.col).cuda(),
+                            torch.from_numpy(h.val).cuda(), W, out_s, n_r, nrel, d, F,
+                            vcol_max=int(h.col.max()), shared=True)
+    mm = merge_chunks([h] * nrel, np.arange(nrel), 1, nrel)
+    merged = K.RelGroupSpec(torch.from_numpy(mm.rowptr).cuda(), torch.from_numpy(mm.vcol).cuda(),
+                            torch.from_numpy(mm.val).cuda(), W, out_m, n_r, nrel, d, nrel * F,
+                            vcol_max=int(mm.vcol.max()))
+    K.spmm_groups([shared, merged], d)
+    assert torch.equal(out_s, out_m)
+    want = np.stack([m @ W[k].cpu().numpy().astype(np.float64) for k in range(nrel)])
+    assert rel_err(out_s.cpu().numpy(), want) <= 1e-5
+    with pytest.raises(_lib.KernelError):
+        K.PreparedSpmm([shared], d, lds=True)()
+    # an unknown flag bit is refused before launch
+    arr = (_lib.DgRelGroup * 1)()
+    K._fill_group(arr[0], shared)
+    arr[0].flags = 2
+    assert _lib.load().dg_spmm_groups_f32(arr, 1, d, None) != 0
+
+
 def test_fused_kernel_matches_oracle(K):
     """dg_gcn_fused_f32 with two targets, several groups each, waves_per_group 1..3 and a
     projection epilogue against the float64 restatement."""
