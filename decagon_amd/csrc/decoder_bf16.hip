@@ -48,7 +48,9 @@ struct Bf16DecArgs {
 template <int D>
 constexpr int threads_for() { return D == 256 ? 768 : 1024; }
 
-template <int D>
+// HAS_L: per-relation diagonals present (DEDICOM) — a template flag, so no load sits behind a
+// branch (a runtime `if (L)` split every load into its own basic block, each waited on alone)
+template <int D, bool HAS_L>
 __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf16DecArgs a) {
     constexpr int kThreads = threads_for<D>();
     constexpr int KS = D / 16;  // k-steps of 16
@@ -86,14 +88,14 @@ __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf
         const int pk = (valid && a.rel) ? a.rel[p] : 0;
         const uint16_t* u = a.row_table + (int64_t)pr * a.ld_row;
         const uint16_t* v = a.col_table + (int64_t)pc * a.ld_col;
-        const uint16_t* lk = a.L ? a.L + (int64_t)pk * D : nullptr;
+        const uint16_t* lk = HAS_L ? a.L + (int64_t)pk * D : nullptr;
         // B operand: (u ∘ D_k)[16s + 8h + j] in bf16, s < KS
         bf16x8 bf[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const uint4 uu = *reinterpret_cast<const uint4*>(u + 16 * s + 8 * h);
             uint4 ll = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
-            if (lk) ll = *reinterpret_cast<const uint4*>(lk + 16 * s + 8 * h);
+            if (HAS_L) ll = *reinterpret_cast<const uint4*>(lk + 16 * s + 8 * h);
             const uint32_t uw[4] = {uu.x, uu.y, uu.z, uu.w}, lw[4] = {ll.x, ll.y, ll.z, ll.w};
             bf16v8 x;  // round-to-nearest-even by the cast (v_cvt_pk_bf16_f32)
 #pragma unroll
@@ -105,10 +107,22 @@ __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf
         }
         float part = 0.f;
         // two column tiles at a time: two independent accumulator chains, so each MFMA's
-        // operand read and its predecessor's result are not on one serial path
+        // operand read and its predecessor's result are not on one serial path.  The tile
+        // pair's v runs are loaded before its MFMAs (their latency hides behind them).
+        // Row gathers, not MFMAs, bound this kernel: every pair reads its own u and v rows,
+        // 32 distinct cache lines per wave load, so loads are kept 16 bytes wide.
 #pragma unroll 1
         for (int t = 0; t < NT; t += 2) {
-            const int na = 32 * t + r, nb = na + 32;  // A-operand rows of this lane
+            // Column tiles t, t+1 = n in [32t, 32t + 64).  The A rows are permuted so that lane
+            // half h ends owning the 32 CONTIGUOUS n = 32t + 32h + [0, 32): acc0 register j holds
+            // n = 32t + 32h + j, acc1 register j holds n + 16 — the epilogue then reads 64-byte
+            // runs of v and D_k (4 × 16 B per lane) instead of eight 8-byte pieces each.
+            const int nb0 = 32 * t + 32 * h;
+            uint4 ev[4], el[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ev[i] = *reinterpret_cast<const uint4*>(v + nb0 + 8 * i);
+            // A row m = r holds C row m = (j&3) + 8(j>>2) + 4h' for register j of lane half h'
+            const int na = 32 * t + 32 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3), nb = na + 16;
             f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
@@ -118,20 +132,24 @@ __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa), bf[s], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wb), bf[s], acc1, 0, 0, 0);
             }
-            // lane owns pair r: acc[reg] = T[n = 32t' + (reg&3) + 8(reg>>2) + 4h][p]
+            // D_k's run after the MFMAs: the pairs of a tile mostly share a relation, so these
+            // loads hit one line (and registers stay within 3 waves per SIMD)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                el[i] = HAS_L ? *reinterpret_cast<const uint4*>(lk + nb0 + 8 * i)
+                              : make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
+                const f32x16& acc = u ? acc1 : acc0;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int n0 = 32 * (t + u) + 8 * g + 4 * h;
-                    const uint2 vv = *reinterpret_cast<const uint2*>(v + n0);
-                    uint2 ll = make_uint2(0x3f803f80u, 0x3f803f80u);
-                    if (lk) ll = *reinterpret_cast<const uint2*>(lk + n0);
-                    const f32x16& acc = u ? acc1 : acc0;
-                    part = fmaf(acc[4 * g + 0], bf_lo(ll.x) * bf_lo(vv.x), part);
-                    part = fmaf(acc[4 * g + 1], bf_hi(ll.x) * bf_hi(vv.x), part);
-                    part = fmaf(acc[4 * g + 2], bf_lo(ll.y) * bf_lo(vv.y), part);
-                    part = fmaf(acc[4 * g + 3], bf_hi(ll.y) * bf_hi(vv.y), part);
+                for (int i = 0; i < 2; ++i) {
+                    const uint4 vv = ev[2 * u + i], ll = el[2 * u + i];
+                    const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w}, lw[4] = {ll.x, ll.y, ll.z, ll.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        part = fmaf(acc[8 * i + 2 * j], bf_lo(lw[j]) * bf_lo(vw[j]), part);
+                        part = fmaf(acc[8 * i + 2 * j + 1], bf_hi(lw[j]) * bf_hi(vw[j]), part);
+                    }
                 }
             }
         }
@@ -161,15 +179,22 @@ extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, 
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&decoder_bf16_kernel<256>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&decoder_bf16_kernel<256, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&decoder_bf16_kernel<256, false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         configured = true;
     }
-    if (d == 256)
-        hipLaunchKernelGGL(decoder_bf16_kernel<256>, dim3(blocks), dim3(threads_for<256>()), lds, st, a);
-    else if (d == 128)
-        hipLaunchKernelGGL(decoder_bf16_kernel<128>, dim3(blocks), dim3(threads_for<128>()), lds, st, a);
-    else
-        hipLaunchKernelGGL(decoder_bf16_kernel<64>, dim3(blocks), dim3(threads_for<64>()), lds, st, a);
+#define DG_DEC_LAUNCH(DD, HL) \
+    hipLaunchKernelGGL((decoder_bf16_kernel<DD, HL>), dim3(blocks), dim3(threads_for<DD>()), lds, st, a)
+    const bool hl = l_table != nullptr;
+    if (d == 256) {
+        if (hl) DG_DEC_LAUNCH(256, true); else DG_DEC_LAUNCH(256, false);
+    } else if (d == 128) {
+        if (hl) DG_DEC_LAUNCH(128, true); else DG_DEC_LAUNCH(128, false);
+    } else {
+        if (hl) DG_DEC_LAUNCH(64, true); else DG_DEC_LAUNCH(64, false);
+    }
+#undef DG_DEC_LAUNCH
     return dg::launch_status();
 }
