@@ -124,13 +124,20 @@ __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf
             // A row m = r holds C row m = (j&3) + 8(j>>2) + 4h' for register j of lane half h'
             const int na = 32 * t + 32 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3), nb = na + 16;
             f32x16 acc0 = {}, acc1 = {};
+            uint4 wa = rt[na * SL + (h ^ (na % SL))];
+            uint4 wb = rt[nb * SL + (h ^ (nb % SL))];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
-                const int q = 2 * s + h;  // slot of k = 16s + 8h .. +7
-                const uint4 wa = rt[na * SL + (q ^ (na % SL))];
-                const uint4 wb = rt[nb * SL + (q ^ (nb % SL))];
+                uint4 xa = wa, xb = wb;
+                if (s + 1 < KS) {  // the next k-step's Rᵀ fragments, one MFMA pair ahead
+                    const int q = 2 * (s + 1) + h;
+                    xa = rt[na * SL + (q ^ (na % SL))];
+                    xb = rt[nb * SL + (q ^ (nb % SL))];
+                }
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa), bf[s], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wb), bf[s], acc1, 0, 0, 0);
+                wa = xa;
+                wb = xb;
             }
             // D_k's run after the MFMAs: the pairs of a tile mostly share a relation, so these
             // loads hit one line (and registers stay within 3 waves per SIMD)
