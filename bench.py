@@ -284,19 +284,29 @@ def main_decoder(args):
     with torch.cuda.stream(stream):
         step()
         stream.synchronize()
-        G = args.graph_steps if args.steps % max(1, args.graph_steps) == 0 and args.warmup % max(1, args.graph_steps) == 0 else 1
-        cg = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(cg, stream=stream):
-            for _ in range(G):
+        if args.no_graph:  # eager launches (PMC passes attribute counters per dispatch)
+            for _ in range(args.warmup):
                 step()
-        for _ in range(args.warmup // G):
-            cg.replay()
-        stream.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps // G):
-            cg.replay()
-        stream.synchronize()
-        el = time.perf_counter() - t0
+            stream.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            stream.synchronize()
+            el = time.perf_counter() - t0
+        else:
+            G = args.graph_steps if args.steps % max(1, args.graph_steps) == 0 and args.warmup % max(1, args.graph_steps) == 0 else 1
+            cg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(cg, stream=stream):
+                for _ in range(G):
+                    step()
+            for _ in range(args.warmup // G):
+                cg.replay()
+            stream.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps // G):
+                cg.replay()
+            stream.synchronize()
+            el = time.perf_counter() - t0
     k_ms = time_kernel(score, args.kernel_reps, stream)
     flop_pair = 2 * d * d + 4 * d
     tflops = 2 * n * flop_pair / (k_ms * 1e-3) / 1e12
@@ -315,10 +325,10 @@ def main_decoder(args):
         "data": "synthetic drug pairs (uniform ids, 645 drugs), device-sampled negatives, random bf16 R / D_k",
         "config": {"workload": f"config 5: {slots} relation slots x ({B} pos + {B} neg) pairs, d={d}, "
                                "DEDICOM uT.D_k.R.D_k.v on v_mfma_f32_32x32x16_bf16",
-                   "pairs_per_step": 2 * n, "hipgraph": True},
+                   "pairs_per_step": 2 * n, "hipgraph": not args.no_graph},
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / BF16_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "decoder_bf16_kernel<256>", "kernel_ms": k_ms,
+                     "kernel": "decoder_bf16_kernel<256, true>", "kernel_ms": k_ms,
                      "algorithmic_flops": 2 * n * flop_pair},
         "cpu_baseline": None,
     }

@@ -114,6 +114,36 @@ def main(root):
             ws = f"{sum(w)/len(w):.1f}" if w else "-"
             print(f"| `{k}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | {fs} | {ws} |")
         print()
+    config_d(root)
+
+
+def config_d(root):
+    """Config 5: bench line, kernel stats and MFMA utilisation of the scorer =
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs × 1024 SIMDs)."""
+    st = stats(os.path.join(root, "D_trace"))
+    if not st:
+        return
+    print("## config 5 (bench.py --config D): bf16 DEDICOM scorer\n")
+    bj = os.path.join(root, "D_bench.json")
+    if os.path.exists(bj):
+        try:
+            rec = json.loads(open(bj).read().strip().splitlines()[-1])
+            ro = rec["roofline"]
+            print(f"value {rec['value']:.4g} pairs/s, {rec['ms_per_step']*1e3:.1f} us/step; scorer "
+                  f"{ro['achieved']:.0f} {ro['unit']} ({100 * ro['frac']:.1f} % of {ro['peak']:.0f})\n")
+        except Exception:
+            pass
+    c = pmc(os.path.join(root, "D_MFMA"))
+    print("| kernel | calls | avg us | total % | MFMA busy / (GPU cycles × 1024 SIMDs) |")
+    print("|---|---|---|---|---|")
+    for r in st[:8]:
+        k = short(r["Name"])
+        busy, gui = c.get((k, "SQ_VALU_MFMA_BUSY_CYCLES"), []), c.get((k, "GRBM_GUI_ACTIVE"), [])
+        util = "-"
+        if busy and gui and sum(gui) > 0:
+            util = f"{100 * sum(busy) / (sum(gui) / 8 * 1024):.1f} %"
+        print(f"| `{k}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | {util} |")
+    print()
 
 
 if __name__ == "__main__":

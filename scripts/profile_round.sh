@@ -25,6 +25,14 @@ for cfg in S P; do
     python3 bench.py --train --config $cfg $steps > $out/train${cfg}_bench.json 2> $out/train${cfg}_trace.log
   echo "train $cfg trace done"
 done
+# config 5 (bf16 DEDICOM scorer): kernel trace, then MFMA busy cycles against the GPU clock
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/D_trace -o run -- \
+  python3 bench.py --config D --steps 50 --warmup 5 --no-cpu-baseline > $out/D_bench.json 2> $out/D_trace.log
+echo "D trace done"
+timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
+  --output-format csv -d $out/D_MFMA -o run -- \
+  python3 bench.py --config D --no-graph --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> $out/D_MFMA.log
+echo "D mfma done"
 python3 scripts/prof_summary.py $out > $out/summary.md
 python3 scripts/prof_summary.py $out --json $out/traffic.json
 echo summary done
