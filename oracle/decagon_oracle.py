@@ -87,6 +87,22 @@ def decagon_forward(edge_types: Dict[Tuple[int, int], int], adj: Dict[Tuple[int,
     return h1, embeddings
 
 
+def decagon_forward_csr(edge_types: Dict[Tuple[int, int], int], adj_csr: Dict[Tuple[int, int], List],
+                        w1: Dict[Tuple[int, int], np.ndarray], w2: Dict[Tuple[int, int], np.ndarray]):
+    """decagon_forward for identity features at full size: the same layers (layers.py:85-94,
+    109-118; model.py:64-88) with each Â_k a float64 scipy CSR and W stacks [K, F, d]
+    (float64), products by scipy (summation order is immaterial in float64)."""
+    def layer(x_of):
+        acc: Dict[int, np.ndarray] = {}
+        for (i, j) in edge_types:
+            s = sum(adj_csr[i, j][k] @ x_of(i, j, k) for k in range(edge_types[i, j]))
+            acc[i] = acc.get(i, 0) + l2_normalize_rows(np.asarray(s))
+        return acc
+    h1 = {i: np.maximum(v, 0.0) for i, v in layer(lambda i, j, k: w1[i, j][k]).items()}
+    emb = layer(lambda i, j, k: h1[j] @ w2[i, j][k])
+    return h1, emb
+
+
 def latent_matrices(edge_types, decoders, dec_params, d: int):
     """latent_inters / latent_varies in edge-type order (model.py:116-137).
 

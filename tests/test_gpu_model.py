@@ -238,3 +238,37 @@ def test_polypharmacy_shaped_plan_matches_oracle(monkeypatch, staged):
     assert rel_err(plan.hidden1[1].cpu().numpy(), h1[1]) <= TOL
     assert rel_err(plan.embeddings[0].cpu().numpy(), emb[0]) <= TOL
     assert rel_err(plan.embeddings[1].cpu().numpy(), emb[1]) <= TOL
+
+
+def test_full_size_config_P_matches_oracle():
+    """BASELINE configs[2] at full size — 19,085 proteins, 645 drugs, 1,932 matrices, ≈23 M
+    nnz per layer, the plan bench.py times (staged drug×drug SpMM, PPI windows, projection
+    GEMM) — against the float64 restatement with scipy products, every output row."""
+    import scipy.sparse as sp
+
+    from oracle import decagon_oracle as orc
+    from decagon_amd import engine, synthetic
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    g = synthetic.make_P(seed=0)
+    rng = np.random.default_rng(11)
+    n = g.n_nodes
+    w1 = {et: rng.uniform(-0.1, 0.1, (K, n[et[1]], 64)).astype(np.float32) for et, K in g.edge_types.items()}
+    w2 = {et: rng.uniform(-0.2, 0.2, (K, 64, 32)).astype(np.float32) for et, K in g.edge_types.items()}
+    dev = torch.device("cuda")
+    dg = engine.DeviceGraph(g.edge_types, g.csr(), dev)
+    assert dg.groups[(1, 1)].staged
+    plan = engine.ForwardPlan(dg, {0: None, 1: None},
+                              engine.LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
+                              engine.LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, 32)
+    plan.run()
+    torch.cuda.synchronize()
+    # the adjacency values as fed: float64 preprocess_graph output cast to float32 (SURVEY §8c)
+    csr = {et: [sp.csr_matrix((v.astype(np.float32).astype(np.float64), (c[:, 0], c[:, 1])), shape=s)
+                for c, v, s in mats] for et, mats in g.adj.items()}
+    h1, emb = orc.decagon_forward_csr(g.edge_types, csr, {et: w.astype(np.float64) for et, w in w1.items()},
+                                      {et: w.astype(np.float64) for et, w in w2.items()})
+    for t in (0, 1):
+        assert rel_err(plan.hidden1[t].cpu().numpy(), h1[t]) <= TOL
+        assert rel_err(plan.embeddings[t].cpu().numpy(), emb[t]) <= TOL
