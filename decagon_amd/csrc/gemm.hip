@@ -14,6 +14,8 @@
 // each lane keeps its A fragment (the H_j rows) in registers across KB consecutive
 // relations of the batch, so H_j is read once per KB relations; the B fragments (W_k, 8 KB)
 // and the C stores (two 128-byte row segments per register) are coalesced.
+#include <type_traits>
+
 #include "common.h"
 #include "dropout.h"
 
@@ -321,18 +323,22 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
     // inside the loop
     const int bm = b0 + lane < b1 ? (g.b_map ? g.b_map[b0 + lane] : b0 + lane) : 0;
     auto map_of = [&](int b) { return __builtin_amdgcn_readlane(bm, b - b0); };
-    // B_map(b) in float4s of [KD][32]: thread t holds float4s t and t + blockDim (blockDim >= 256)
+    // B_map(b) in float4s of [KD][32]: thread t holds float4s t and t + blockDim, taken modulo
+    // NF4 (a duplicate slot is written twice with the same value) and columns >= n read as
+    // column 0 (they only feed output columns that are not stored) — so loads and LDS writes
+    // are unconditional, and the compiler's waits stay counted: a branch around them made it
+    // wait for vmcnt(0), i.e. for the previous batch's HBM stores, every batch
     float4 wr0 = make_float4(0.f, 0.f, 0.f, 0.f), wr1 = wr0;
+    const int f0 = threadIdx.x & (NF4 - 1), f1 = (threadIdx.x + blockDim.x) & (NF4 - 1);
+    const int c0 = 4 * (f0 & 7) < g.n ? 4 * (f0 & 7) : 0, c1 = 4 * (f1 & 7) < g.n ? 4 * (f1 & 7) : 0;
     auto load_b = [&](int b) {
         const float* B = g.b + map_of(b) * g.b_bs;
-        const int f0 = threadIdx.x, f1 = threadIdx.x + blockDim.x;
-        if (f0 < NF4 && 4 * (f0 & 7) < g.n) wr0 = *reinterpret_cast<const float4*>(B + (f0 >> 3) * g.b_sk + 4 * (f0 & 7));
-        if (f1 < NF4 && 4 * (f1 & 7) < g.n) wr1 = *reinterpret_cast<const float4*>(B + (f1 >> 3) * g.b_sk + 4 * (f1 & 7));
+        wr0 = *reinterpret_cast<const float4*>(B + (f0 >> 3) * g.b_sk + c0);
+        wr1 = *reinterpret_cast<const float4*>(B + (f1 >> 3) * g.b_sk + c1);
     };
     auto put_b = [&](int u) {
         float* w = wl + u * WB;
         auto put4 = [&](int f, float4 v) {
-            if (f >= NF4) return;
             const int k = f >> 3, n = 4 * (f & 7);
             float* d = w + (n * 2 + (k & 1)) * LDW + (k >> 1);
             d[0] = v.x;
@@ -340,18 +346,25 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
             d[4 * LDW] = v.z;
             d[6 * LDW] = v.w;
         };
-        put4(threadIdx.x, wr0);
-        put4(threadIdx.x + blockDim.x, wr1);
+        put4(f0, wr0);
+        put4(f1, wr1);
     };
     if (b0 < b1) {
         load_b(b0);
         put_b(0);
-        if (b0 + 1 < b1) load_b(b0 + 1);
+        load_b(min(b0 + 1, b1 - 1));
     }
     // iteration b: barrier | MFMAs on buffer b | B(b+1) registers -> the other buffer (its loads
-    // were issued before batch b-1's stores) | loads of B(b+2) | stores of batch b
-#pragma unroll 1
-    for (int b = b0; b < b1; ++b) {
+    // were issued before batch b-1's stores) | loads of B(b+2) | stores of batch b.
+    // MODE 0: this wave stores nothing (no tile); 1: n == 32 — every lane stores all four
+    // pieces unconditionally (a lane past the last row stores row m-1's values, shuffled in
+    // from the lane that owns it: the same bytes) so the wave's VMEM count per iteration is
+    // fixed and the waits before the LDS writes stay counted (vmcnt(4), not vmcnt(0): the
+    // previous batch's stores keep draining under this batch's MFMAs); 2: general n.
+    const bool last_tile = tm == g.tiles_m - 1;
+    const int src = row_ok ? lane : (g.m - 1 - tm * 32) + 32 * h;
+    auto body = [&](int b, auto mode_tag) {
+        constexpr int MODE = decltype(mode_tag)::value;
         __syncthreads();  // buffer (b - b0) & 1 staged; the other one is free
         const float* w = wl + ((b - b0) & 1) * WB + (i * 2 + h) * LDW;
         f32x16 acc = {};
@@ -363,18 +376,43 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.z, hf[s4 + 2], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, hf[s4 + 3], acc, 0, 0, 0);
         }
-        if (b + 1 < b1) put_b((b + 1 - b0) & 1);
-        if (b + 2 < b1) load_b(b + 2);
-        if (row_ok) {
-            float* C = g.c + map_of(b) * g.c_bs + (int64_t)row * g.c_sm;
+        put_b((b + 1 - b0) & 1);          // past the run's end: a harmless rewrite of the free buffer
+        load_b(min(b + 2, b1 - 1));
+        if constexpr (MODE == 1) {
+            if (last_tile) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int n = 8 * q + 4 * h;
-                if (n < g.n)
-                    *reinterpret_cast<float4*>(C + n) =
-                        make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                for (int r = 0; r < 16; ++r) acc[r] = __shfl(acc[r], src);
+            }
+            float* C = g.c + map_of(b) * g.c_bs + (int64_t)(row_ok ? row : g.m - 1) * g.c_sm;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<float4*>(C + 8 * q + 4 * h) =
+                    make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+        } else if constexpr (MODE == 2) {
+            if (row_ok) {
+                float* C = g.c + map_of(b) * g.c_bs + (int64_t)row * g.c_sm;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int n = 8 * q + 4 * h;
+                    if (n < g.n)
+                        *reinterpret_cast<float4*>(C + n) =
+                            make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+                }
             }
         }
+    };
+    using M0 = std::integral_constant<int, 0>;
+    using M1 = std::integral_constant<int, 1>;
+    using M2 = std::integral_constant<int, 2>;
+    if (tm >= g.tiles_m) {
+#pragma unroll 1
+        for (int b = b0; b < b1; ++b) body(b, M0{});
+    } else if (g.n == 32) {
+#pragma unroll 1
+        for (int b = b0; b < b1; ++b) body(b, M1{});
+    } else {
+#pragma unroll 1
+        for (int b = b0; b < b1; ++b) body(b, M2{});
     }
 }
 
