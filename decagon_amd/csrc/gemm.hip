@@ -283,10 +283,9 @@ __global__ __launch_bounds__(256) void gemm_f32_resident_a(const GemmArgs args) 
 // so lane l ends with row m0 + (l&31) and columns 8q + 4(l>>5) .. +3 of it for q < 4: four
 // 16-byte stores per lane.  One wave per 32-row tile of A (its fragment in registers for the
 // block's run of batches); B_map(b) (KD×32 floats) is staged through LDS once per block and
-// batch, double-buffered, in the fragment order [n][k&1][k>>1] (rows padded by 4 floats),
+// batch, double-buffered, in the fragment order [n][k / S][k % S] (rows padded by 4 floats),
 // its float4 loads issued two batches ahead and before the previous batch's stores (vmcnt
-// counts stores too: a wait for a load issued after a store would drain the store).  The
-// k-steps run in order on one accumulator: the result is bitwise a k-ordered fmaf chain.
+// counts stores too: a wait for a load issued after a store would drain the store).
 template <int KD>
 __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
     constexpr int S = KD / 2;
@@ -307,15 +306,19 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
     const int row = tm * 32 + i;
     const bool row_ok = tm < g.tiles_m && row < g.m;
 
-    float hf[S];  // B operand of the transposed product: A[row][2s + h]
+    // k order: MFMA step s contracts k = s (lane half 0) and k = S + s (half 1), so each lane's
+    // B operand is one contiguous half row of A — S/4 float4 loads (a permutation of the
+    // k-sum; A contiguous along k, rows 16-byte aligned)
+    float hf[S];  // B operand of the transposed product: A[row][S·h + s]
     {
-        const int64_t a_sk = g.a_sk;  // one kernel-argument read, not one per element
-        const float* A = g.a + (int64_t)(row_ok ? row : 0) * g.a_sm + h * a_sk;
+        const float4* A = reinterpret_cast<const float4*>(g.a + (int64_t)(row_ok ? row : 0) * g.a_sm + S * h);
 #pragma unroll
-        for (int s = 0; s < S; ++s) hf[s] = A[2 * s * a_sk];
-        if (!row_ok) {
-#pragma unroll
-            for (int s = 0; s < S; ++s) hf[s] = 0.f;
+        for (int q = 0; q < S / 4; ++q) {
+            const float4 v = row_ok ? A[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            hf[4 * q] = v.x;
+            hf[4 * q + 1] = v.y;
+            hf[4 * q + 2] = v.z;
+            hf[4 * q + 3] = v.w;
         }
     }
     // the block's batch map in one register (<= 64 batches): lane j holds map(b0 + j), read
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(512) void gemm_f32_proj(const GemmArgs args) {
         float* w = wl + u * WB;
         auto put4 = [&](int f, float4 v) {
             const int k = f >> 3, n = 4 * (f & 7);
-            float* d = w + (n * 2 + (k & 1)) * LDW + (k >> 1);
+            float* d = w + (n * 2 + k / S) * LDW + (k % S);
             d[0] = v.x;
             d[2 * LDW] = v.y;
             d[4 * LDW] = v.z;
@@ -614,7 +617,8 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
     bool proj = kd > 0;
     for (int i = 0; i < A.n && proj; ++i) {
         const GemmOne& g = A.g[i];
-        proj = g.a_bs == 0 && g.n <= 32 && (g.n & 3) == 0 && !g.sa && !g.sc && g.c_sn == 1 && (g.c_sm & 3) == 0 &&
+        proj = g.a_bs == 0 && g.a_sk == 1 && (g.a_sm & 3) == 0 && dg::aligned16(g.a) &&
+               g.n <= 32 && (g.n & 3) == 0 && !g.sa && !g.sc && g.c_sn == 1 && (g.c_sm & 3) == 0 &&
                (g.c_bs & 3) == 0 && dg::aligned16(g.c) && g.b_sn == 1 && (g.b_sk & 3) == 0 && (g.b_bs & 3) == 0 &&
                dg::aligned16(g.b);
     }
