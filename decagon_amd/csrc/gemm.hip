@@ -622,6 +622,7 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
                (g.c_bs & 3) == 0 && dg::aligned16(g.c) && g.b_sn == 1 && (g.b_sk & 3) == 0 && (g.b_bs & 3) == 0 &&
                dg::aligned16(g.b);
     }
+    static const int proj_blocks = [] { const char* e = getenv("DG_PROJ_BLOCKS"); return e ? atoi(e) : 512; }();
     if (proj) {
         // waves per block: the m tiles split evenly over ceil(tiles/8) blocks (>= 4 waves)
         int tiles_m_max = 0;
@@ -634,7 +635,7 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
             g.tile_blocks = dg::ceil_div(g.tiles_m, wpb);
             // batches per block: about 2 blocks per CU of 256, amortising each wave's A fragment
             int bpb = 1;
-            while (bpb < 64 && (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb * 2) >= 512) bpb *= 2;  // <= 64: one map register
+            while (bpb < 64 && (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb * 2) >= proj_blocks) bpb *= 2;  // <= 64: one map register
             g.batch_per_wave = bpb;
             g.block_begin = static_cast<int32_t>(pblocks);
             pblocks += (int64_t)g.tile_blocks * dg::ceil_div(g.batch, bpb);
