@@ -598,6 +598,16 @@ class _Layer:
         self.run_spmm()
         if self.flat is not None and self.allreduce is not None:
             self.allreduce(self.flat)
+        if self.side_stream is not None and len(self.epilogues) > 1:
+            # node types finish independently: their (latency-bound) epilogues run side by side
+            cur = torch.cuda.current_stream()
+            self.side_stream.wait_stream(cur)
+            with torch.cuda.stream(self.side_stream):
+                for e in self.epilogues[:-1]:
+                    e()
+            self.epilogues[-1]()
+            cur.wait_stream(self.side_stream)
+            return
         for e in self.epilogues:
             e()
 
