@@ -21,7 +21,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 16
+ABI_VERSION = 17
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
 DG_MAX_ADAM_SEGS = 32
 
@@ -76,6 +76,17 @@ class DgEpiGroup(ctypes.Structure):
     _fields_ = [("partial", c_void_p), ("n_chunks", c_int32), ("reserved", c_int32)]
 
 
+class DgEpiTarget(ctypes.Structure):
+    _fields_ = [
+        ("groups", POINTER(DgEpiGroup)),
+        ("n_groups", c_int32),
+        ("reserved0", c_int32),
+        ("out", c_void_p),
+        ("n_rows", c_int32),
+        ("reserved", c_int32 * 3),
+    ]
+
+
 class DgGemmDesc(ctypes.Structure):
     _fields_ = [
         ("a", c_void_p),
@@ -128,6 +139,7 @@ SIGNATURES = {
         [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, POINTER(DgProj), c_int32, c_int32,
          c_int32, c_void_p],
     ),
+    "dg_gcn_epilogue_multi_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, c_void_p]),
     "dg_gcn_epilogue_f32": (
         c_int32,
         [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],

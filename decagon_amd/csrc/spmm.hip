@@ -278,13 +278,21 @@ struct EpiGroupK {
     int32_t pad;
 };
 
+struct EpiTargetK {
+    float* out;
+    int32_t n_rows;
+    int32_t g_begin;      // its groups: g[g_begin .. g_begin + g_count)
+    int32_t g_count;
+    int32_t block_begin;  // its first workgroup
+};
+
 struct EpiArgs {
     EpiGroupK g[DG_MAX_GROUPS];
-    float* out;
-    int32_t n_groups;
-    int32_t n_rows;
+    EpiTargetK t[DG_EPI_MAX_TARGETS];
+    int32_t n_targets;
     int32_t d;
     int32_t flags;
+    int32_t pad;
 };
 
 // One wave per output row: LP lanes cover the row's d floats (a float4 each) and the
@@ -298,11 +306,15 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
     const int wave = threadIdx.x >> 6;
     const int cg = lane / LP;
     const int q = lane % LP;
-    const int r = blockIdx.x * 4 + wave;
-    if (r >= a.n_rows) return;  // wave-uniform; no barriers
+    int ti = 0;  // node type of this workgroup (several finish in one launch)
+#pragma unroll 1
+    while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
+    const EpiTargetK& t = a.t[ti];
+    const int r = ((int)blockIdx.x - t.block_begin) * 4 + wave;
+    if (r >= t.n_rows) return;  // wave-uniform; no barriers
     const int d = a.d;
     const bool qok = q * 4 < d;
-    const int64_t plane = (int64_t)a.n_rows * d;
+    const int64_t plane = (int64_t)t.n_rows * d;
     const int64_t off = (int64_t)r * d + q * 4;
     const bool crelu = a.flags & DG_EPI_CHUNK_RELU;
     auto relu4 = [](float4 v) {
@@ -311,7 +323,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
 
     float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 1
-    for (int gi = 0; gi < a.n_groups; ++gi) {
+    for (int gi = t.g_begin; gi < t.g_begin + t.g_count; ++gi) {
         const float* __restrict__ p = a.g[gi].partial + off;
         const int nc = a.g[gi].n_chunks;
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -347,7 +359,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
         dg::add4(tot, s);
     }
     if (a.flags & DG_EPI_RELU) tot = relu4(tot);
-    if (qok && cg == 0) *reinterpret_cast<float4*>(a.out + off) = tot;
+    if (qok && cg == 0) *reinterpret_cast<float4*>(t.out + off) = tot;
 }
 
 // Partial mode over a SMALL shared operand (every nonzero of the launch gathers from one
@@ -470,7 +482,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 16; }
+extern "C" int32_t dg_abi_version(void) { return 17; }
 
 
 namespace {
@@ -608,6 +620,49 @@ extern "C" int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const 
     return dg_spmm_groups_f32(&g, 1, d, stream);
 }
 
+extern "C" int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets, int32_t n_targets, int32_t d,
+                                         int32_t flags, void* stream) {
+    if (n_targets < 1 || targets == nullptr) return DG_EINVAL;
+    if (n_targets > DG_EPI_MAX_TARGETS) return DG_ETOOMANY;
+    if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
+    if (flags & ~(DG_EPI_L2NORM | DG_EPI_RELU | DG_EPI_CHUNK_RELU)) return DG_EINVAL;
+    EpiArgs a{};
+    int ng = 0;
+    int64_t blocks = 0;
+    for (int ti = 0; ti < n_targets; ++ti) {
+        const dg_epi_target& T = targets[ti];
+        if (T.n_groups < 1 || !T.groups || T.n_rows < 0) return DG_EINVAL;
+        if (ng + T.n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
+        if (T.n_rows == 0) continue;
+        if (!T.out || !dg::aligned16(T.out)) return T.out ? DG_EALIGN : DG_EINVAL;
+        EpiTargetK& k = a.t[a.n_targets++];
+        k.out = T.out;
+        k.n_rows = T.n_rows;
+        k.g_begin = ng;
+        k.g_count = T.n_groups;
+        k.block_begin = static_cast<int32_t>(blocks);
+        for (int i = 0; i < T.n_groups; ++i) {
+            if (!T.groups[i].partial || T.groups[i].n_chunks < 1) return DG_EINVAL;
+            if (!dg::aligned16(T.groups[i].partial)) return DG_EALIGN;
+            a.g[ng].partial = T.groups[i].partial;
+            a.g[ng].n_chunks = T.groups[i].n_chunks;
+            ++ng;
+        }
+        blocks += dg::ceil_div(T.n_rows, 4);  // one wave per row
+    }
+    if (blocks == 0) return DG_OK;
+    if (blocks > 0x7fffffff) return DG_EINVAL;
+    a.d = d;
+    a.flags = flags;
+    const int lp = dg::lanes_per_row(d);
+    dim3 grid(static_cast<unsigned>(blocks)), block(256);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define DG_LAUNCH_EPI(L) hipLaunchKernelGGL(epilogue_kernel<L>, grid, block, 0, st, a)
+    DG_LP_SWITCH(lp, DG_LAUNCH_EPI)
+#undef DG_LAUNCH_EPI
+    return dg::launch_status();
+}
+
 extern "C" int dg_gcn_epilogue_f32(const dg_epi_group* groups, int32_t n_groups, float* out,
                                    int32_t n_rows, int32_t d, int32_t flags, void* stream) {
     if (n_groups < 1 || groups == nullptr) return DG_EINVAL;
@@ -616,25 +671,8 @@ extern "C" int dg_gcn_epilogue_f32(const dg_epi_group* groups, int32_t n_groups,
     if (flags & ~(DG_EPI_L2NORM | DG_EPI_RELU | DG_EPI_CHUNK_RELU)) return DG_EINVAL;
     if (n_rows == 0) return DG_OK;
     if (!out || !dg::aligned16(out)) return out ? DG_EALIGN : DG_EINVAL;
-    EpiArgs a{};
-    for (int i = 0; i < n_groups; ++i) {
-        if (!groups[i].partial || groups[i].n_chunks < 1) return DG_EINVAL;
-        if (!dg::aligned16(groups[i].partial)) return DG_EALIGN;
-        a.g[i].partial = groups[i].partial;
-        a.g[i].n_chunks = groups[i].n_chunks;
-    }
-    a.out = out;
-    a.n_groups = n_groups;
-    a.n_rows = n_rows;
-    a.d = d;
-    a.flags = flags;
-    const int lp = dg::lanes_per_row(d);
-    dim3 grid(dg::ceil_div(n_rows, 4)), block(256);  // one wave per row
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define DG_LAUNCH_EPI(L) hipLaunchKernelGGL(epilogue_kernel<L>, grid, block, 0, st, a)
-    DG_LP_SWITCH(lp, DG_LAUNCH_EPI)
-#undef DG_LAUNCH_EPI
-    return dg::launch_status();
+    const dg_epi_target t{groups, n_groups, 0, out, n_rows, {0, 0, 0}};
+    return dg_gcn_epilogue_multi_f32(&t, 1, d, flags, stream);
 }
 
 extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_groups, int32_t d, void* stream) {

@@ -453,10 +453,13 @@ class ForwardPlan:
                 [(outs[i], n[i], [self._identity_spec(i, views[et], d) for et in self.targets[i]], relu)
                  for i in tl], d, pspecs, 1))
         else:
-            for i in self.targets:
-                if i in fused_t:
-                    continue
-                epis.append(kernels.PreparedEpilogue([partials[et] for et in self.targets[i]], outs[i], n[i], d, flags))
+            # every partial-mode node type finishes in ONE launch (side by side, no stream fork)
+            tl = [i for i in self.targets if i not in fused_t]
+            # node types with the most chunk partials per row first: their long rows start early
+            tl.sort(key=lambda i: -sum(partials[et][1] for et in self.targets[i]))
+            if tl:
+                epis.append(kernels.PreparedEpilogueMulti(
+                    [([partials[et] for et in self.targets[i]], outs[i], n[i]) for i in tl], d, flags))
         return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream)
 
     def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
@@ -598,16 +601,6 @@ class _Layer:
         self.run_spmm()
         if self.flat is not None and self.allreduce is not None:
             self.allreduce(self.flat)
-        if self.side_stream is not None and len(self.epilogues) > 1:
-            # node types finish independently: their (latency-bound) epilogues run side by side
-            cur = torch.cuda.current_stream()
-            self.side_stream.wait_stream(cur)
-            with torch.cuda.stream(self.side_stream):
-                for e in self.epilogues[:-1]:
-                    e()
-            self.epilogues[-1]()
-            cur.wait_stream(self.side_stream)
-            return
         for e in self.epilogues:
             e()
 

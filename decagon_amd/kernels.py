@@ -365,6 +365,47 @@ class PreparedEpilogue:
         check(self._fn(self._arr, n, o, r, d, f, _stream_ptr(stream)), "dg_gcn_epilogue_f32")
 
 
+class PreparedEpilogueMulti:
+    """dg_gcn_epilogue_multi_f32: several node types' epilogues in one launch —
+    targets = [(partials [(tensor, n_chunks)], out, n_rows)], one flag set."""
+
+    def __init__(self, targets: Sequence[Tuple[Sequence[Tuple[torch.Tensor, int]], torch.Tensor, int]], d: int,
+                 flags: int):
+        if not targets or len(targets) > 8:
+            raise ValueError("1..8 targets per launch")
+        if sum(len(p) for p, _, _ in targets) > _lib.DG_MAX_GROUPS:
+            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups over all targets")
+        self._keep, self._garrs = [], []
+        tarr = (_lib.DgEpiTarget * len(targets))()
+        for t, (partials, out, n_rows) in enumerate(targets):
+            if not partials:
+                raise ValueError("at least one group per target")
+            _dev(out, torch.float32, "out")
+            if out.numel() < n_rows * d:
+                raise ValueError("out too small")
+            garr = (DgEpiGroup * len(partials))()
+            for i, (p, nc) in enumerate(partials):
+                _dev(p, torch.float32, "partial")
+                if p.numel() < nc * n_rows * d:
+                    raise ValueError("partial too small for [n_chunks, n_rows, d]")
+                garr[i].partial = p.data_ptr()
+                garr[i].n_chunks = nc
+                self._keep.append(p)
+            self._keep.append(out)
+            self._garrs.append(garr)
+            tarr[t].groups = ctypes.cast(garr, ctypes.POINTER(DgEpiGroup))
+            tarr[t].n_groups = len(partials)
+            tarr[t].out = out.data_ptr()
+            tarr[t].n_rows = n_rows
+        self._tarr = tarr
+        self._args = (len(targets), d, flags)
+        self._fn = _lib.load().dg_gcn_epilogue_multi_f32
+
+    def __call__(self, stream=None) -> None:
+        n, d, f = self._args
+        check(self._fn(self._tarr, n, d, f, _stream_ptr(stream)), "dg_gcn_epilogue_multi_f32")
+
+
 def gcn_epilogue(partials, out, n_rows, d, flags, stream=None) -> None:
     PreparedEpilogue(partials, out, n_rows, d, flags)(stream)
 

@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (16); bumped whenever a struct layout or a signature changes. */
+/* ABI version (17); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -214,6 +214,21 @@ typedef struct dg_epi_group {
 
 int dg_gcn_epilogue_f32(const dg_epi_group* groups /* HOST array */, int32_t n_groups,
                         float* out, int32_t n_rows, int32_t d, int32_t flags, void* stream);
+
+/* Several node types' epilogues in one launch (every target's rows finish side by side; the
+ * groups of all targets together at most DG_MAX_GROUPS).  Same flags for all targets. */
+#define DG_EPI_MAX_TARGETS 8
+typedef struct dg_epi_target {
+    const dg_epi_group* groups; /* HOST array of n_groups                                   */
+    int32_t n_groups;
+    int32_t reserved0;
+    float* out;                 /* device, [n_rows][d], 16-byte aligned                     */
+    int32_t n_rows;
+    int32_t reserved[3];
+} dg_epi_target;
+
+int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets /* HOST array */, int32_t n_targets,
+                              int32_t d, int32_t flags, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Batched strided fp32 GEMM on the f32-input MFMA (v_mfma_f32_32x32x2_f32, exact fp32):

@@ -210,6 +210,27 @@ def test_epilogue(K, flags):
     assert np.all(out.cpu().numpy()[::7] == 0)
 
 
+@pytest.mark.parametrize("d", [32, 64])
+def test_epilogue_multi_target(K, d):
+    """dg_gcn_epilogue_multi_f32: three node types (one of them empty) in one launch, bit for
+    bit what one dg_gcn_epilogue_f32 per node type writes."""
+    from decagon_amd._lib import DG_EPI_L2NORM, DG_EPI_RELU
+
+    rng = np.random.default_rng(d)
+    flags = DG_EPI_L2NORM | DG_EPI_RELU
+    targets, singles = [], []
+    for n, chunks in ((1001, (2, 1)), (0, (1,)), (645, (3, 1, 1))):
+        parts = [(torch.from_numpy(rng.standard_normal((c, n, d)).astype(np.float32)).cuda(), c) for c in chunks]
+        out, ref = torch.zeros((n, d), device="cuda"), torch.zeros((n, d), device="cuda")
+        targets.append((parts, out, n))
+        singles.append((parts, ref, n))
+    K.PreparedEpilogueMulti(targets, d, flags)()
+    for parts, ref, n in singles:
+        K.gcn_epilogue(parts, ref, n, d, flags)
+    for (_, out, _), (_, ref, _) in zip(targets, singles):
+        assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("m,n,k,batch", [(645, 32, 64, 5), (37, 70, 19, 3), (1, 1, 1, 1), (500, 32, 32, 2),
                                          (64, 96, 0, 1)])
 def test_gemm(K, m, n, k, batch):
