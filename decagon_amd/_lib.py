@@ -21,7 +21,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 17
+ABI_VERSION = 18
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
 DG_MAX_ADAM_SEGS = 32
 
@@ -73,7 +73,7 @@ class DgFusedTarget(ctypes.Structure):
 
 
 class DgEpiGroup(ctypes.Structure):
-    _fields_ = [("partial", c_void_p), ("n_chunks", c_int32), ("reserved", c_int32)]
+    _fields_ = [("partial", c_void_p), ("sum_out", c_void_p), ("n_chunks", c_int32), ("reserved", c_int32)]
 
 
 class DgEpiTarget(ctypes.Structure):

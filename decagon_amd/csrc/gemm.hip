@@ -526,7 +526,7 @@ extern "C" int dg_gemm_tn_f32(const float* a, int64_t lda, int64_t a_bs, const f
     if (rc != DG_OK || n_split == 1) return rc;
     // the split partials, summed in split order (dg_gcn_epilogue_f32 without flags)
     if (!dg::aligned16(c)) return DG_EALIGN;
-    dg_epi_group g{partial, n_split, 0};
+    dg_epi_group g{partial, nullptr, n_split, 0};
     return dg_gcn_epilogue_f32(&g, 1, c, batch * M, N, 0, stream);
 }
 

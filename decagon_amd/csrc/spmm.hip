@@ -274,6 +274,7 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
 
 struct EpiGroupK {
     const float* partial;
+    float* sum;  // the group's pre-normalisation sum, or nullptr
     int32_t n_chunks;
     int32_t pad;
 };
@@ -345,6 +346,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
         }
 #pragma unroll
         for (int m = LP; m < dg::kWave; m <<= 1) dg::add4(s, dg::shfl_xor4(s, m));
+        if (a.g[gi].sum && qok && cg == 0) *reinterpret_cast<float4*>(a.g[gi].sum + off) = s;
         if (a.flags & DG_EPI_L2NORM) {
             // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); all-zero rows stay zero.
             float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
@@ -482,7 +484,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 17; }
+extern "C" int32_t dg_abi_version(void) { return 18; }
 
 
 namespace {
@@ -643,8 +645,9 @@ extern "C" int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets, int32_t n
         k.block_begin = static_cast<int32_t>(blocks);
         for (int i = 0; i < T.n_groups; ++i) {
             if (!T.groups[i].partial || T.groups[i].n_chunks < 1) return DG_EINVAL;
-            if (!dg::aligned16(T.groups[i].partial)) return DG_EALIGN;
+            if (!dg::aligned16(T.groups[i].partial) || !dg::aligned16(T.groups[i].sum_out)) return DG_EALIGN;
             a.g[ng].partial = T.groups[i].partial;
+            a.g[ng].sum = T.groups[i].sum_out;
             a.g[ng].n_chunks = T.groups[i].n_chunks;
             ++ng;
         }

@@ -244,6 +244,8 @@ class ForwardPlan:
         # layer (all-reduced when sharded; kept for the backward when training), and one fused
         # launch over identity "adjacencies" finishes every node type from it
         self.flat_mode = allreduce is not None or keep_sums
+        self.keep_sums = keep_sums
+        self.sums_mode = False  # set below: partial mode whose epilogue also writes each S_ij
         self.launch_groups: Dict[int, List[EdgeType]] = {}  # id(SpMM launch) -> its groups
         dev = dgraph.device
         f32 = dict(device=dev, dtype=torch.float32)
@@ -253,6 +255,15 @@ class ForwardPlan:
             self.targets.setdefault(et[0], []).append(et)
         if any(len(v) > DG_MAX_GROUPS for v in self.targets.values()):
             raise ValueError(f"more than {DG_MAX_GROUPS} edge types into one node type")
+        if keep_sums and allreduce is None:
+            # one GPU, training: when no node type would take the fused path anyway (config P),
+            # keep the partial-mode layers and let their one epilogue launch also write every
+            # group's pre-normalisation sum S_ij — no flat reduces, no finishing launch
+            self.flat_mode = False
+            if not self._fused_targets():
+                self.sums_mode = True
+            else:
+                self.flat_mode = True
         n = dgraph.n_nodes
 
         # ---- layer-1 dense operand: W1 (identity features) or X_j·W1_k (sparse features) ----
@@ -453,6 +464,10 @@ class ForwardPlan:
                 [(outs[i], n[i], [self._identity_spec(i, views[et], d) for et in self.targets[i]], relu)
                  for i in tl], d, pspecs, 1))
         else:
+            if self.sums_mode:  # training: the epilogue also writes each group's S_ij
+                for et in rest:
+                    views[et] = torch.empty(g.groups[et].n_rows * d, **f32)
+                    partials[et] = partials[et] + (views[et],)
             # every partial-mode node type finishes in ONE launch (side by side, no stream fork)
             tl = [i for i in self.targets if i not in fused_t]
             # node types with the most chunk partials per row first: their long rows start early

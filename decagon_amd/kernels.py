@@ -349,13 +349,13 @@ class PreparedEpilogue:
         if out.numel() < n_rows * d:
             raise ValueError("out too small")
         arr = (DgEpiGroup * len(partials))()
-        for i, (p, nc) in enumerate(partials):
+        for i, (p, nc, *rest) in enumerate(partials):
             _dev(p, torch.float32, "partial")
             if p.numel() < nc * n_rows * d:
                 raise ValueError("partial too small for [n_chunks, n_rows, d]")
             arr[i].partial = p.data_ptr()
             arr[i].n_chunks = nc
-        self._keep = [p for p, _ in partials] + [out]
+        self._keep = [p for p, *_ in partials] + [out]
         self._arr = arr
         self._args = (len(partials), out.data_ptr(), n_rows, d, flags)
         self._fn = _lib.load().dg_gcn_epilogue_f32
@@ -367,7 +367,8 @@ class PreparedEpilogue:
 
 class PreparedEpilogueMulti:
     """dg_gcn_epilogue_multi_f32: several node types' epilogues in one launch —
-    targets = [(partials [(tensor, n_chunks)], out, n_rows)], one flag set."""
+    targets = [(partials [(tensor, n_chunks[, sum_out])], out, n_rows)], one flag set; a
+    group's optional sum_out [n_rows, d] receives its pre-normalisation sum S_ij."""
 
     def __init__(self, targets: Sequence[Tuple[Sequence[Tuple[torch.Tensor, int]], torch.Tensor, int]], d: int,
                  flags: int):
@@ -384,12 +385,18 @@ class PreparedEpilogueMulti:
             if out.numel() < n_rows * d:
                 raise ValueError("out too small")
             garr = (DgEpiGroup * len(partials))()
-            for i, (p, nc) in enumerate(partials):
+            for i, (p, nc, *so) in enumerate(partials):
                 _dev(p, torch.float32, "partial")
                 if p.numel() < nc * n_rows * d:
                     raise ValueError("partial too small for [n_chunks, n_rows, d]")
                 garr[i].partial = p.data_ptr()
                 garr[i].n_chunks = nc
+                if so and so[0] is not None:  # the group's pre-normalisation sum S_ij
+                    _dev(so[0], torch.float32, "sum_out")
+                    if so[0].numel() < n_rows * d:
+                        raise ValueError("sum_out too small for [n_rows, d]")
+                    garr[i].sum_out = so[0].data_ptr()
+                    self._keep.append(so[0])
                 self._keep.append(p)
             self._keep.append(out)
             self._garrs.append(garr)

@@ -91,7 +91,7 @@ class TrainPlan:
 
     def __init__(self, fwd: ForwardPlan, w1: LayerWeights, w2: LayerWeights,
                  features: Dict[int, Optional[HostCSR]]):
-        if not fwd.flat_mode or fwd.allreduce is not None:
+        if not fwd.keep_sums or fwd.allreduce is not None:
             raise NotImplementedError("training runs on one GPU over a ForwardPlan(keep_sums=True)")
         # with dropout (fwd.drop_state), the backward reuses the forward's masks: the draws of the
         # forward's step, regenerated from the same counter-based hash (dropout.hip)

@@ -34,7 +34,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (17); bumped whenever a struct layout or a signature changes. */
+/* ABI version (18); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -208,6 +208,8 @@ int dg_staged_order(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
 
 typedef struct dg_epi_group {
     const float* partial;       /* device, [n_chunks][n_rows][d] */
+    float* sum_out;             /* device, [n_rows][d]: the group's pre-normalisation sum
+                                   S_ij (what the backward of l2_normalize needs), or NULL */
     int32_t n_chunks;
     int32_t reserved;
 } dg_epi_group;

@@ -272,3 +272,44 @@ def test_full_size_config_P_matches_oracle():
     for t in (0, 1):
         assert rel_err(plan.hidden1[t].cpu().numpy(), h1[t]) <= TOL
         assert rel_err(plan.embeddings[t].cpu().numpy(), emb[t]) <= TOL
+
+
+def test_training_sums_mode_matches_oracle(monkeypatch):
+    """ForwardPlan(keep_sums=True) on one GPU with no fused node type (config P's shape): the
+    partial-mode layers' single epilogue launch also writes every group's pre-normalisation
+    sum S_ij (the backward's input) — checked group by group against the float64 sums, with
+    H1 and the embeddings."""
+    from oracle import decagon_oracle as orc
+    from decagon_amd import engine, synthetic
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    monkeypatch.setattr(engine, "FUSED_MAX_ROWS", 0)  # every node type in partial mode
+    g = synthetic.make_P(seed=5, n_proteins=700, n_drugs=110, n_side_effects=30, ppi_edges=4000,
+                         target_edges=500)
+    rng = np.random.default_rng(2)
+    n = g.n_nodes
+    w1 = {et: rng.uniform(-0.2, 0.2, (K, n[et[1]], 64)).astype(np.float32) for et, K in g.edge_types.items()}
+    w2 = {et: rng.uniform(-0.3, 0.3, (K, 64, 32)).astype(np.float32) for et, K in g.edge_types.items()}
+    dev = torch.device("cuda")
+    dg = engine.DeviceGraph(g.edge_types, g.csr(), dev)
+    plan = engine.ForwardPlan(dg, {0: None, 1: None},
+                              engine.LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
+                              engine.LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}),
+                              64, 32, keep_sums=True)
+    assert plan.sums_mode and not plan.flat_mode
+    plan.run()
+    torch.cuda.synchronize()
+    feats = {t: (np.stack([np.arange(n[t])] * 2, 1), np.ones(n[t]), (n[t], n[t])) for t in n}
+    h1, emb = orc.decagon_forward(g.edge_types, g.adj, feats,
+                                  {et: [x.astype(np.float64) for x in w] for et, w in w1.items()},
+                                  {et: [x.astype(np.float64) for x in w] for et, w in w2.items()})
+    for t in (0, 1):
+        assert rel_err(plan.hidden1[t].cpu().numpy(), h1[t]) <= TOL
+        assert rel_err(plan.embeddings[t].cpu().numpy(), emb[t]) <= TOL
+    for et, K in g.edge_types.items():
+        i, j = et
+        s1 = sum(orc.sparse_dense_matmul(g.adj[et][k], w1[et][k].astype(np.float64)) for k in range(K))
+        s2 = sum(orc.sparse_dense_matmul(g.adj[et][k], h1[j] @ w2[et][k].astype(np.float64)) for k in range(K))
+        assert rel_err(plan._layer1.views[et].view(n[i], 64).cpu().numpy(), s1) <= TOL
+        assert rel_err(plan._layer2.views[et].view(n[i], 32).cpu().numpy(), s2) <= TOL
