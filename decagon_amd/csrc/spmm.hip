@@ -465,12 +465,21 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
                 const int p = cb + 4 + q;  // the next 4 pairs of this row
                 vc = p < end ? g.vcol[p] : 0;
                 vv = p < end ? g.val[p] : 0.f;
+                // pair u of the row's four goes to the row's 4 lanes by a DPP quad broadcast
+                // (quad_perm [u,u,u,u]: a VALU move, no LDS instruction beside the gathers)
+                const int xv4[4] = {__builtin_amdgcn_mov_dpp(cv, 0x00, 0xF, 0xF, false),
+                                    __builtin_amdgcn_mov_dpp(cv, 0x55, 0xF, 0xF, false),
+                                    __builtin_amdgcn_mov_dpp(cv, 0xAA, 0xF, 0xF, false),
+                                    __builtin_amdgcn_mov_dpp(cv, 0xFF, 0xF, 0xF, false)};
+                const int wi = __float_as_int(w);
+                const int wv4[4] = {__builtin_amdgcn_mov_dpp(wi, 0x00, 0xF, 0xF, false),
+                                    __builtin_amdgcn_mov_dpp(wi, 0x55, 0xF, 0xF, false),
+                                    __builtin_amdgcn_mov_dpp(wi, 0xAA, 0xF, 0xF, false),
+                                    __builtin_amdgcn_mov_dpp(wi, 0xFF, 0xF, 0xF, false)};
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int src = (lane & ~3) + u;
-                    const int xv = __shfl(cv, src);
-                    const float wv = __shfl(w, src);  // 0 past the row's end
-                    const float4* xr = xs + xv * kLdsRowF4;
+                    const float wv = __int_as_float(wv4[u]);  // 0 past the row's end
+                    const float4* xr = xs + xv4[u] * kLdsRowF4;
                     dg::fma4(acc0, wv, xr[q]);
                     dg::fma4(acc1, wv, xr[q + 4]);
                 }
