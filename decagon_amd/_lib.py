@@ -21,7 +21,9 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 18
+ABI_VERSION = 19
+DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
+DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
 DG_MAX_ADAM_SEGS = 32
 
@@ -168,6 +170,7 @@ SIGNATURES = {
          c_int32, c_void_p, c_void_p],
     ),
     "dg_hinge_loss_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p]),
+    "dg_hinge_loss_ws_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p, c_void_p]),
     "dg_xent_loss_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_float, c_void_p, c_void_p]),
     "dg_decoder_grad_workspace": (c_int64, [c_int32, c_int32]),
     "dg_decoder_grad_f32": (
@@ -184,6 +187,9 @@ SIGNATURES = {
                               c_void_p]),
     "dg_adam_advance": (c_int32, [c_void_p, c_float, c_float, c_float, c_void_p]),
     "dg_rank_metrics_workspace": (c_int64, [c_int32]),
+    "dg_rank_metrics_ex_workspace": (c_int64, [c_int32, c_int32]),
+    "dg_rank_metrics_ex_f32": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                         c_int64, c_void_p]),
     "dg_rank_metrics_f32": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int64,
                                       c_void_p]),
     "dg_unigram_sample": (

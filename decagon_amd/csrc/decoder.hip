@@ -270,6 +270,37 @@ __global__ __launch_bounds__(256) void hinge_kernel(const float* pos, const floa
     if (threadIdx.x == 0) loss[0] = s;
 }
 
+// Many-block hinge (config 5: 10^6 pairs): block b sums its contiguous chunk in a fixed
+// order, publishes the partial and takes a ticket; the last block adds the partials in block
+// order and resets the ticket (the decoder_hinge_kernel pattern) — deterministic for a given n.
+__global__ __launch_bounds__(256) void hinge_multi_kernel(const float* pos, const float* neg, int n,
+                                                          float margin, float* loss, float* partial,
+                                                          uint32_t* ticket) {
+    __shared__ int last;
+    const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int p0 = blockIdx.x * chunk;
+    const int cnt = max(0, min(n, p0 + chunk) - p0);
+    const float s = block_sum_256(cnt, [&](int q) {
+        return fmaxf(neg[p0 + q] - (pos[p0 + q] - margin), 0.f);
+    });
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;  // block-uniform
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+    const float t = block_sum_256((int)gridDim.x, [&](int b) {
+        return __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    });
+    if (threadIdx.x == 0) {
+        loss[0] = t;
+        atomicExch(ticket, 0u);
+    }
+}
+
 __device__ __forceinline__ float softplus_neg_abs(float x) { return log1pf(expf(-fabsf(x))); }
 
 __global__ __launch_bounds__(256) void xent_kernel(const float* pos, const float* neg, int n,
@@ -320,6 +351,17 @@ extern "C" int dg_hinge_loss_f32(const float* pos, const float* neg, int32_t n, 
     if (n < 0 || !loss || (n > 0 && (!pos || !neg))) return DG_EINVAL;
     hipLaunchKernelGGL(hinge_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        pos, neg, n, margin, loss);
+    return dg::launch_status();
+}
+
+extern "C" int dg_hinge_loss_ws_f32(const float* pos, const float* neg, int32_t n, float margin,
+                                    float* loss, void* workspace, void* stream) {
+    if (n < 0 || !loss || !workspace || (n > 0 && (!pos || !neg))) return DG_EINVAL;
+    if (!dg::aligned16(workspace)) return DG_EALIGN;
+    const int blocks = max(1, min(DG_HINGE_WS_BLOCKS, dg::ceil_div(n, 4096)));
+    hipLaunchKernelGGL(hinge_multi_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       pos, neg, n, margin, loss, reinterpret_cast<float*>(workspace) + 4,
+                       reinterpret_cast<uint32_t*>(workspace));
     return dg::launch_status();
 }
 

@@ -110,6 +110,12 @@ def choose_chunk(n_rels: int, n_rows: int, nnz: int, d: int, target_waves: int =
     return int(min(max(1, chunk), n_rels))
 
 
+def row_slice(c: HostCSR, a: int, b: int) -> HostCSR:
+    """Rows [a, b) of a CSR relation (a row-split rank's block), columns unchanged."""
+    p0, p1 = int(c.rowptr[a]), int(c.rowptr[b])
+    return HostCSR((c.rowptr[a:b + 1] - p0).astype(np.int32), c.col[p0:p1], c.val[p0:p1], (b - a, c.shape[1]))
+
+
 @dataclass
 class DeviceGroup:
     """One (i,j) group's (local) relations on the device, chunk-merged."""
@@ -146,12 +152,16 @@ class DeviceGraph:
 
     def __init__(self, edge_types: Dict[EdgeType, int], adj: Dict[EdgeType, Sequence[Optional[HostCSR]]],
                  device: torch.device, local: Optional[Dict[EdgeType, Sequence[int]]] = None,
-                 chunk=None, target_waves: int = 32768, d_policy: int = 64):
+                 chunk=None, target_waves: int = 32768, d_policy: int = 64,
+                 row_block: Optional[Dict[int, Tuple[int, int, int]]] = None):
         self.edge_types = dict(edge_types)
         self.device = device
         self.groups: Dict[EdgeType, DeviceGroup] = {}
         self.n_nodes: Dict[int, int] = {}
         self.sharded = local is not None
+        # row-split node types (sharding.py): this rank holds rows [a, b) of every relation
+        # into them; their groups' output rows are local row indices
+        self.row_block = dict(row_block or {})
         for et, K in self.edge_types.items():
             rels = list(adj[et])
             if len(rels) != K:
@@ -167,6 +177,10 @@ class DeviceGraph:
             if any(rels[k] is None for k in ids):
                 raise ValueError(f"edge type {et}: a local relation was not given")
             loc = [rels[k] for k in ids]
+            if et[0] in self.row_block:
+                a, b, _ = self.row_block[et[0]]
+                loc = [row_slice(c, a, b) for c in loc]
+                n_r = b - a
             nnz = int(sum(c.nnz for c in loc))
             ch = chunk.get(et) if isinstance(chunk, dict) else chunk
             staged = ch is None and stageable(len(loc), n_r, n_c)
@@ -227,16 +241,31 @@ class ForwardPlan:
     def __init__(self, dgraph: DeviceGraph, features: Dict[int, Optional[HostCSR]],
                  w1: LayerWeights, w2: LayerWeights, h1: int, h2: int,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None, keep_sums: bool = False,
-                 dropout: Optional[Tuple[float, torch.Tensor]] = None):
+                 dropout: Optional[Tuple[float, torch.Tensor]] = None, shard=None):
         self.g = dgraph
         self.h1, self.h2 = h1, h2
+        # multi-GPU (sharding.RelationShard): the collectives joining the ranks' shares —
+        # all-reduce of the relation-sharded node types' sums, all-gather of the row-split
+        # node types' finished row blocks
+        self.shard = shard
+        if shard is not None:
+            allreduce = shard.allreduce
         self.allreduce = allreduce
+        self.row_block = dict(dgraph.row_block)
+        self.world = shard.world_size if shard is not None else 1
+        self.allgather = shard.allgather if shard is not None else None
+        if self.row_block and (shard is None or self.allgather is None or shard.row_block != self.row_block):
+            raise ValueError("a row-split device graph needs its RelationShard (with an all-gather)")
+        if shard is not None and allreduce is None:
+            raise ValueError("a RelationShard needs its all-reduce")
+        if self.row_block and keep_sums:
+            raise NotImplementedError("training with row-split node types is not on the HIP path")
         # dropout (training): (keep probability, device state {seed, step}); every forward
         # draws new masks (the step advances first), the backward reuses them
         self.keep, self.drop_state = 1.0, None
         if dropout is not None and float(dropout[0]) < 1.0:
-            if allreduce is not None:
-                raise NotImplementedError("dropout with a relation-sharded forward is not on the HIP path")
+            if allreduce is not None or self.row_block:
+                raise NotImplementedError("dropout with a sharded forward is not on the HIP path")
             if any(f is not None for f in features.values()):
                 raise NotImplementedError("dropout with sparse (non-identity) features is not on the HIP path")
             self.keep, self.drop_state = float(dropout[0]), dropout[1]
@@ -304,8 +333,19 @@ class ForwardPlan:
             self._pre.append(kernels.PreparedSpmm([spec], h1))
             x1[et] = xw
 
-        self.hidden1 = {i: torch.empty((n[i], h1), **f32) for i in self.targets}
-        self.embeddings = {i: torch.empty((n[i], h2), **f32) for i in self.targets}
+        # row-split node types: the full output rows live in a buffer padded to world × block
+        # rows (this rank finishes its block in place, the all-gather fills the rest)
+        self._pad: Dict[Tuple[int, int], torch.Tensor] = {}
+
+        def out_buf(i, d):
+            if i not in self.row_block:
+                return torch.empty((n[i], d), **f32)
+            pad = torch.empty((self.world * self.row_block[i][2], d), **f32)
+            self._pad[i, d] = pad
+            return pad[:n[i]]
+
+        self.hidden1 = {i: out_buf(i, h1) for i in self.targets}
+        self.embeddings = {i: out_buf(i, h2) for i in self.targets}
 
         # ---- layer-2 projection buffers P_k = H1_j·W2_k (global slabs) ----
         self.proj: Dict[EdgeType, torch.Tensor] = {}
@@ -329,7 +369,7 @@ class ForwardPlan:
             rels_from[et[1]] = rels_from.get(et[1], 0) + dgraph.groups[et].n_rels
         # layer-1 rows finished by a fused launch (the SpMM one, or — sharded — the one that
         # finishes the all-reduced sums) project themselves onto the layer-2 relations
-        finished = set(self.targets) if self.flat_mode else set(self.fused)
+        finished = (set(self.targets) - set(self.row_block)) if self.flat_mode else set(self.fused)
         proj_fused = [et for et in self.edge_types
                       if dgraph.groups[et].n_rels and et[1] in finished
                       and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS and self.drop_state is None]
@@ -412,23 +452,27 @@ class ForwardPlan:
             self.launch_groups[id(launches[-1])] = [et for i in fused_t for et in self.targets[i]]
         rest = [et for et in self.edge_types if et[0] not in fused_t]
         flags = DG_EPI_L2NORM | (DG_EPI_RELU if relu else 0)
+        # row-split node types (sharded): their groups run in partial mode over this rank's
+        # row block and one epilogue finishes the block before the exchange
+        split_t = [i for i in self.targets if i in self.row_block]
+        red = [et for et in rest if et[0] not in self.row_block]
         flat, views = None, {}
-        if self.flat_mode and rest:
-            sizes = [g.groups[et].n_rows * d for et in rest]
+        if self.flat_mode and red:
+            sizes = [g.groups[et].n_rows * d for et in red]
             flat = torch.zeros(int(sum(sizes)), **f32)
             off = 0
-            for et, sz in zip(rest, sizes):
+            for et, sz in zip(red, sizes):
                 views[et] = flat[off:off + sz]
                 off += sz
         partials, specs, staged, reduces = {}, [], [], []
         for et in rest:
             grp = g.groups[et]
             n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
-            if flat is not None and n_out == 1:
+            if flat is not None and et in views and n_out == 1:
                 part = views[et]  # single chunk: the SpMM writes the group sum in place
             else:
                 part = torch.zeros((max(1, n_out), grp.n_rows, d), **f32)
-                if flat is not None and grp.n_rels:
+                if flat is not None and et in views and grp.n_rels:
                     reduces.append(kernels.PreparedEpilogue([(part, n_out)], views[et], grp.n_rows, d, 0))
             partials[et] = (part, max(1, n_out))
             if not grp.n_rels:
@@ -448,14 +492,23 @@ class ForwardPlan:
             launches.append(kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d))
             self.launch_groups[id(launches[-1])] = spmm_ets[s:s + DG_MAX_GROUPS]
         launches += reduces
-        need_zero = flat is not None and any(g.groups[et].n_rels == 0 for et in rest)
-        epis = []
+        need_zero = flat is not None and any(g.groups[et].n_rels == 0 for et in red)
+        epis, local_epis, gathers = [], [], []
+        if split_t:
+            blocks = []
+            for i in split_t:
+                a, b, blk = self.row_block[i]
+                pad = self._pad[i, d]
+                r0 = self.shard.rank * blk
+                blocks.append(([partials[et] for et in self.targets[i]], pad[r0:r0 + (b - a)], b - a))
+                gathers.append((pad, pad[r0:r0 + blk]))
+            local_epis.append(kernels.PreparedEpilogueMulti(blocks, d, flags))
         if flat is not None:
             # sharded: the all-reduced group sums S_ij are finished by ONE fused launch over
             # identity "adjacencies" (row r gathers S_ij[r] with weight 1.0f: exact), so the
             # l2norm, Σ_j, relu and (layer 1) the layer-2 projections of every node type run in
             # one kernel after the exchange
-            tl = [i for i in self.targets]
+            tl = [i for i in self.targets if i not in self.row_block]
             pspecs = []
             for tgt_node, pj in projs:
                 pj.target = tl.index(tgt_node)
@@ -463,7 +516,7 @@ class ForwardPlan:
             epis.append(kernels.PreparedFused(
                 [(outs[i], n[i], [self._identity_spec(i, views[et], d) for et in self.targets[i]], relu)
                  for i in tl], d, pspecs, 1))
-        else:
+        elif not split_t:
             if self.sums_mode:  # training: the epilogue also writes each group's S_ij
                 for et in rest:
                     views[et] = torch.empty(g.groups[et].n_rows * d, **f32)
@@ -475,7 +528,8 @@ class ForwardPlan:
             if tl:
                 epis.append(kernels.PreparedEpilogueMulti(
                     [([partials[et] for et in self.targets[i]], outs[i], n[i]) for i in tl], d, flags))
-        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream)
+        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream,
+                      local_epis, gathers, self.allgather)
 
     def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
         """A group spec whose 'adjacency' is the identity of node type i (one nonzero 1.0f per
@@ -523,14 +577,17 @@ class ForwardPlan:
             cur.extend(before)
             if layer.need_zero:
                 cur.append(layer.flat.zero_)
-            cur.extend(layer.launches)
-            if layer.flat is not None and layer.allreduce is not None:
+            cur.append(layer.run_spmm)
+            cur.extend(layer.local_epilogues)
+            if layer.has_exchange:
                 close()
-                flat, ar = layer.flat, layer.allreduce
-                out.append(("exchange", lambda flat=flat, ar=ar: ar(flat)))
+                out.append(("exchange", layer.exchange))
             cur.extend(layer.epilogues)
         close()
         return out
+
+    def parallelism(self, backend: str = "nccl") -> str:
+        return "1 GPU" if self.shard is None else self.shard.describe(backend)
 
     @property
     def spmm_launches(self):
@@ -600,7 +657,7 @@ class _Layer:
     """The prepared launches of one layer and how to run them."""
 
     def __init__(self, launches, flat, need_zero, allreduce, epilogues, fused_targets, views=None,
-                 side_stream=None):
+                 side_stream=None, local_epilogues=(), gathers=(), allgather=None):
         self.launches = launches
         self.side_stream = side_stream
         self.flat = flat
@@ -609,13 +666,30 @@ class _Layer:
         self.allreduce = allreduce
         self.epilogues = epilogues
         self.fused_targets = fused_targets
+        self.local_epilogues = list(local_epilogues)  # row-split blocks, finished before the exchange
+        self.gathers = list(gathers)                  # (padded out, this rank's block) per node type
+        self.allgather = allgather
+
+    @property
+    def has_exchange(self) -> bool:
+        return (self.flat is not None and self.allreduce is not None) or bool(self.gathers)
+
+    def exchange(self) -> None:
+        """The layer's collectives: all-reduce of the relation-sharded sums, then the
+        all-gather of the row-split blocks."""
+        if self.flat is not None and self.allreduce is not None:
+            self.allreduce(self.flat)
+        for out, blk in self.gathers:
+            self.allgather(out, blk)
 
     def run(self) -> None:
         if self.need_zero:
             self.flat.zero_()  # groups without local relations contribute zeros
         self.run_spmm()
-        if self.flat is not None and self.allreduce is not None:
-            self.allreduce(self.flat)
+        for e in self.local_epilogues:
+            e()
+        if self.has_exchange:
+            self.exchange()
         for e in self.epilogues:
             e()
 

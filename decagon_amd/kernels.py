@@ -613,16 +613,30 @@ def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: t
 
 
 def hinge_loss(pos: torch.Tensor, neg: torch.Tensor, margin: float,
-               out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+               out: Optional[torch.Tensor] = None, stream=None,
+               workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Σ relu(neg − pos + margin) (optimizer.py:116-120): one workgroup, or — with a
+    workspace of DG_HINGE_WS_BYTES (first word zero; hinge_workspace()) — up to 256."""
     _dev(pos, torch.float32, "pos")
     _dev(neg, torch.float32, "neg")
     if pos.numel() != neg.numel():
         raise ValueError("pos/neg length mismatch")
     if out is None:
         out = torch.empty(1, device=pos.device, dtype=torch.float32)
+    if workspace is not None:
+        if workspace.numel() * workspace.element_size() < _lib.DG_HINGE_WS_BYTES or not workspace.is_cuda:
+            raise ValueError("hinge workspace too small")
+        check(_lib.load().dg_hinge_loss_ws_f32(pos.data_ptr(), neg.data_ptr(), pos.numel(), float(margin),
+                                                out.data_ptr(), workspace.data_ptr(), _stream_ptr(stream)),
+              "dg_hinge_loss_ws_f32")
+        return out
     check(_lib.load().dg_hinge_loss_f32(pos.data_ptr(), neg.data_ptr(), pos.numel(), float(margin),
                                          out.data_ptr(), _stream_ptr(stream)), "dg_hinge_loss_f32")
     return out
+
+
+def hinge_workspace(device) -> torch.Tensor:
+    return torch.zeros(_lib.DG_HINGE_WS_BYTES // 4, dtype=torch.int32, device=device)
 
 
 def xent_loss(pos: torch.Tensor, neg: torch.Tensor, neg_weight: float,

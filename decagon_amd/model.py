@@ -172,7 +172,8 @@ class DecagonModel(Model):
         the flat-mode plan that keeps every group's pre-normalisation sum for the backward;
         keep < 1: dropout, layers.py:87-88 and :112)."""
         local = None if shard is None else shard.local
-        dg = runtime.device_graph(ctx, self.edge_types, self.adj_mats, local)
+        dg = runtime.device_graph(ctx, self.edge_types, self.adj_mats, local,
+                                  row_block=None if shard is None else shard.row_block)
         feats = {j: runtime.feature_csr(ctx, self.inputs[j]) if j in self.inputs else None
                  for j in dg.n_nodes}
         key = ("plan", id(self), id(dg), tuple((j, id(f)) for j, f in feats.items()),
@@ -186,7 +187,7 @@ class DecagonModel(Model):
                                        "(construct the model after a HIP device is visible)")
             w1, w2 = self.weight_stacks()
             p = ForwardPlan(dg, feats, w1, w2, self.h1, self.h2,
-                            allreduce=None if shard is None else shard.allreduce, keep_sums=training,
+                            shard=shard, keep_sums=training,
                             dropout=(keep, self.dropout_state(ctx)) if keep < 1.0 else None)
             hit = (dg, feats, p)
             cache[key] = hit

@@ -86,14 +86,15 @@ def feature_csr(ctx: RunContext, node: Node):
 
 def device_graph(ctx: RunContext, edge_types: Dict[Tuple[int, int], int],
                  adj_nodes: Dict[Tuple[int, int], Sequence[Node]],
-                 local: Optional[Dict] = None, chunk=None) -> DeviceGraph:
+                 local: Optional[Dict] = None, chunk=None, row_block: Optional[Dict] = None) -> DeviceGraph:
     csrs = {et: [host_csr(ctx, n) for n in adj_nodes[et]] for et in edge_types}
     key = ("dgraph", tuple((et, tuple(id(c) for c in csrs[et])) for et in edge_types),
-           None if local is None else tuple((et, tuple(v)) for et, v in local.items()), chunk)
+           None if local is None else tuple((et, tuple(v)) for et, v in local.items()), chunk,
+           None if not row_block else tuple(sorted(row_block.items())))
     cache = ctx.session.caches.setdefault("dgraph", {})
     hit = cache.get(key)
     if hit is None:
-        hit = (csrs, DeviceGraph(edge_types, csrs, ctx.session.device, local, chunk=chunk))
+        hit = (csrs, DeviceGraph(edge_types, csrs, ctx.session.device, local, chunk=chunk, row_block=row_block))
         cache[key] = hit
     return hit[1]
 

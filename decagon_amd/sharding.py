@@ -1,17 +1,26 @@
-"""Relation sharding across GPUs (one process per GPU, torch.distributed over RCCL/xGMI).
+"""Sharding the GCN forward across GPUs (one process per GPU, torch.distributed over
+RCCL/xGMI).
 
-The reference has no parallelism.  The GCN forward shards naturally: every
-relation's Â_k·X_k is independent until the per-(i,j) sum Σ_k, which must be complete
-before the row L2 normalisation (decagon/deep/layers.py:92-93).  So each rank
+The reference has no parallelism.  Every relation's Â_k·X_k is independent
+until the per-(i,j) sum Σ_k, which must be complete before the row L2 normalisation
+(decagon/deep/layers.py:92-93); after it, the layer's rows are independent.  Two ways to
+split a node type's work follow from that, and a plan uses both:
 
-  1. owns a subset of the relations of every group (LPT over nonzero counts, or whole
-     relation sets — one set per GPU in the weak-scaling bench),
-  2. runs the SpMM of its relations and reduces its chunk partials to one
-     pre-normalisation sum S_ij per group,
-  3. all-reduces the flat buffer of every S_ij (one RCCL all-reduce per layer: 2 per
-     forward; the only collective on the data path),
-  4. runs the epilogue (normalise, Σ_j, relu) redundantly — every rank ends with the full
-     hidden1 / embeddings, which layer 2 and the decoder need.
+  relation-sharded  (small node types: the 645 drugs, config S's genes and drugs)
+      each rank owns a subset of the relations of every group into the node type (LPT over
+      nonzero counts, or whole relation sets — one per GPU in the weak-scaling bench), writes
+      its partial pre-normalisation sums S_ij into one flat buffer and the ranks all-reduce
+      it (one RCCL all-reduce per layer); every rank then finishes those rows redundantly.
+  row-split         (node types of >= ROW_SPLIT_MIN rows: the 19,085 proteins)
+      each rank owns a contiguous block of the node type's rows for EVERY relation into it,
+      so its S_ij rows are complete locally: it normalises and finishes its block, and the
+      blocks are all-gathered (padded to equal size) into the full hidden1 / embeddings that
+      the next layer's gathers and the decoder read.
+
+Per layer the exchange is therefore one all-reduce of the relation-sharded node types' sums
+(config P: 2 × 645 × d floats) plus one all-gather of the row-split node types' finished
+rows (19,085 × d floats in total) — not an all-reduce of the proteins' 2 × 19,085 × d sums,
+which bounded round 1's relation-only sharding at ≈3× on 8 GPUs.
 
 Weights are replicated (the largest stack, polypharmacy W1 of (1,1), is 318 MB — small
 against 288 GB of HBM); kernels pick a rank's relations out of the full stack through the
@@ -28,12 +37,17 @@ import torch
 
 EdgeType = Tuple[int, int]
 
+# node types with at least this many rows are row-split across ranks (the others are
+# relation-sharded); config P's proteins (19,085) are, its drugs (645) and config S are not
+ROW_SPLIT_MIN = 4096
 
-def lpt_assign(costs: Sequence[float], world_size: int) -> List[int]:
+
+def lpt_assign(costs: Sequence[float], world_size: int, start: Optional[Sequence[float]] = None) -> List[int]:
     """Longest-processing-time-first assignment of items to ranks (deterministic: ties by
-    item index, then rank)."""
+    item index, then rank); `start` = each rank's load before the items."""
     order = sorted(range(len(costs)), key=lambda i: (-float(costs[i]), i))
-    heap = [(0.0, r) for r in range(world_size)]
+    heap = [(0.0 if start is None else float(start[r]), r) for r in range(world_size)]
+    heapq.heapify(heap)
     owner = [0] * len(costs)
     for i in order:
         load, r = heapq.heappop(heap)
@@ -42,19 +56,41 @@ def lpt_assign(costs: Sequence[float], world_size: int) -> List[int]:
     return owner
 
 
+def row_block(n_rows: int, rank: int, world_size: int) -> Tuple[int, int, int]:
+    """(first row, end row, padded block size) of `rank`'s block of a row-split node type:
+    equal blocks of ceil(n / world) rows (the last one short), so the all-gather moves
+    equal-sized pieces."""
+    blk = -(-n_rows // world_size)
+    a = min(n_rows, rank * blk)
+    return a, min(n_rows, a + blk), blk
+
+
+def slot_range(n_slots: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous, balanced block of relation slots of `rank` (config 5's scorer)."""
+    base, extra = divmod(n_slots, world_size)
+    a = rank * base + min(rank, extra)
+    return a, a + base + (1 if rank < extra else 0)
+
+
 @dataclass
 class RelationShard:
-    """This rank's relations per group and the collective that sums group partials."""
+    """This rank's share of the forward: the local relations of every group, the row blocks
+    of the row-split node types, and the collectives that join the shares."""
 
     rank: int
     world_size: int
     local: Dict[EdgeType, List[int]]
     allreduce: Optional[Callable[[torch.Tensor], None]] = None
     loads: List[float] = field(default_factory=list)
+    # node type -> (first row, end row, padded block) of this rank (row-split node types)
+    row_block: Dict[int, Tuple[int, int, int]] = field(default_factory=dict)
+    # allgather(out [world * blk, d], inp = out[rank * blk:(rank + 1) * blk]) — in place
+    allgather: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None
 
     @staticmethod
     def lpt(edge_types: Dict[EdgeType, int], rel_cost: Dict[EdgeType, Sequence[float]], rank: int,
             world_size: int, allreduce=None) -> "RelationShard":
+        """Every relation whole to one rank, LPT over its cost (no row split)."""
         items = [(et, k) for et in edge_types for k in range(edge_types[et])]
         costs = [float(rel_cost[et][k]) for et, k in items]
         owner = lpt_assign(costs, world_size)
@@ -67,12 +103,76 @@ class RelationShard:
         return RelationShard(rank, world_size, local, allreduce, loads)
 
     @staticmethod
+    def split(edge_types: Dict[EdgeType, int], n_nodes: Dict[int, int], rel_cost: Dict[EdgeType, Sequence[float]],
+              rank: int, world_size: int, allreduce=None, allgather=None,
+              row_split_min: int = ROW_SPLIT_MIN) -> "RelationShard":
+        """Row-split the node types of >= row_split_min rows (every rank keeps all relations
+        of the groups into them, on its row block); LPT the relations of the groups into the
+        other node types, starting from the row-split work each rank already holds."""
+        # (every rank must own at least one row of a row-split node type)
+        rows = {t for t, n in n_nodes.items()
+                if n >= row_split_min and (world_size - 1) * -(-n // world_size) < n}
+        blocks = {t: row_block(n_nodes[t], rank, world_size) for t in rows}
+        local: Dict[EdgeType, List[int]] = {}
+        items, costs = [], []
+        base = [0.0] * world_size
+        for et, K in edge_types.items():
+            if et[0] in rows:
+                local[et] = list(range(K))
+                share = sum(float(c) for c in rel_cost[et]) / world_size
+                base = [b + share for b in base]
+            else:
+                local[et] = []
+                for k in range(K):
+                    items.append((et, k))
+                    costs.append(float(rel_cost[et][k]))
+        owner = lpt_assign(costs, world_size, base)
+        loads = list(base)
+        for (et, k), r, c in zip(items, owner, costs):
+            loads[r] += c
+            if r == rank:
+                local[et].append(k)
+        return RelationShard(rank, world_size, local, allreduce, loads, blocks, allgather)
+
+    @staticmethod
+    def polypharmacy(graph, rank: int, world_size: int, comm: bool = True) -> "RelationShard":
+        """Config P's shard: proteins row-split, drug-target relations LPT on nonzeros.
+        comm=False: no collectives (a one-GPU timing rehearsal of one rank's share)."""
+        nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
+        ar, ag = (torch_allreduce(), torch_allgather()) if comm else (_no_op, _no_op)
+        return RelationShard.split(graph.edge_types, graph.n_nodes, nnz, rank, world_size, ar, ag)
+
+    @staticmethod
     def blocks(edge_types_per_rank: Dict[EdgeType, int], rank: int, world_size: int,
                allreduce=None) -> "RelationShard":
         """Weak scaling: the graph holds world_size relation sets; rank r owns set r, i.e.
         relations [r*K_ij, (r+1)*K_ij) of every group."""
         local = {et: list(range(rank * k, (rank + 1) * k)) for et, k in edge_types_per_rank.items()}
         return RelationShard(rank, world_size, local, allreduce)
+
+    def local_csr(self, csr: Dict[EdgeType, Sequence]) -> Dict[EdgeType, list]:
+        """The graph's per-group relation lists with the relations of other ranks replaced by
+        empty stand-ins of the same shape (never uploaded; they only carry the group's shape
+        when this rank owns none of its relations)."""
+        from .sparse import HostCSR
+
+        def empty(c):
+            return HostCSR(np.zeros(c.shape[0] + 1, np.int32), np.zeros(0, np.int32), np.zeros(0, np.float32),
+                           tuple(c.shape))
+
+        return {et: [c if k in set(self.local[et]) else empty(c) for k, c in enumerate(v)]
+                for et, v in csr.items()}
+
+    def describe(self, backend: str = "nccl") -> str:
+        lib = "RCCL" if backend == "nccl" else backend
+        rs = ", ".join(f"node type {t} row-split" for t in sorted(self.row_block))
+        return (f"x{self.world_size}: relations LPT-sharded" + (f", {rs}" if rs else "")
+                + f"; {lib} all-reduce of the relation-sharded sums"
+                + (" + all-gather of the row-split rows" if rs else "") + " per layer")
+
+
+def _no_op(*_a) -> None:
+    return None
 
 
 def torch_allreduce(group=None) -> Callable[[torch.Tensor], None]:
@@ -84,3 +184,20 @@ def torch_allreduce(group=None) -> Callable[[torch.Tensor], None]:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
     return _ar
+
+
+def torch_allgather(group=None) -> Callable[[torch.Tensor, torch.Tensor], None]:
+    """In-place all-gather of equal row blocks: `inp` is this rank's block of `out`."""
+    import torch.distributed as dist
+
+    def _ag(out: torch.Tensor, inp: torch.Tensor) -> None:
+        if out.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo (CPU tests, one-GPU multi-rank rehearsals): staged through host memory
+            off = (inp.data_ptr() - out.data_ptr()) // out.element_size()
+            flat = out.reshape(-1).cpu()
+            dist.all_gather_into_tensor(flat, flat[off:off + inp.numel()].clone(), group=group)
+            out.copy_(flat.view_as(out))
+            return
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+    return _ag

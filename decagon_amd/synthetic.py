@@ -1,8 +1,9 @@
 """Synthetic graphs of the benchmark configurations (BASELINE.json `configs`).
 
 S  — main.py's 5-relation / 10-matrix toy graph (main.py:137-217).  Its exact
-     reference-normalised train adjacencies are committed as tests/golden/synthetic_S.npz
-     (generated with the reference's own iterator); `load_S` reads them.
+     reference-normalised train adjacencies (generated with the reference's own iterator by
+     tests/golden/make_golden.py) are committed as package data, decagon_amd/data/
+     synthetic_S_adj.npz (inputs only: scripts/extract_S_inputs.py); `load_S` reads them.
 P  — polypharmacy-shaped: 19,085 proteins, 645 drugs; PPI with 715,612
      undirected edges; 18,596 drug–target edges as (0,1) and its transpose (1,0); 964
      drug–drug relations of Zipf sizes s_r = max(500, ⌊28,568·r^-0.31⌋), each symmetric,
@@ -22,7 +23,7 @@ from .sparse import HostCSR, coo_to_csr, preprocess_graph
 
 EdgeType = Tuple[int, int]
 ROOT = Path(__file__).resolve().parents[1]
-GOLDEN_S = ROOT / "tests" / "golden" / "synthetic_S.npz"
+GOLDEN_S = Path(__file__).resolve().parent / "data" / "synthetic_S_adj.npz"
 
 
 @dataclass
@@ -134,3 +135,32 @@ def replicate_sets(g: SyntheticGraph, copies: int) -> SyntheticGraph:
     deg = {t: list(v) * copies for t, v in g.degrees.items()}
     return SyntheticGraph(f"{g.name}x{copies}", dict(g.n_nodes), {et: len(v) for et, v in adj.items()},
                           dict(g.decoders), adj, deg)
+
+
+@dataclass
+class Config5:
+    """BASELINE configs[4]'s scorer inputs (float32 here; the bench and tests round them to
+    bf16): d = 256 drug embeddings, the global R, one D_k per drug-drug relation slot, B
+    positive pairs per slot (slot-major) and the drug degrees the sampler follows."""
+
+    E: np.ndarray
+    R: np.ndarray
+    D: np.ndarray
+    pos_rows: np.ndarray
+    pos_cols: np.ndarray
+    degrees: np.ndarray
+    batch: int
+
+
+def make_config5(seed: int = 5, n_drugs: int = 645, n_slots: int = 1928, d: int = 256, batch: int = 512) -> Config5:
+    rng = np.random.default_rng(seed)
+    E = (rng.standard_normal((n_drugs, d)) / 4).astype(np.float32)
+    r = np.sqrt(6.0 / (2 * d))
+    R = rng.uniform(-r, r, (d, d)).astype(np.float32)
+    r = np.sqrt(6.0 / (d + 1))
+    D = rng.uniform(-r, r, (n_slots, d)).astype(np.float32)
+    n = n_slots * batch
+    pos_rows = rng.integers(0, n_drugs, n).astype(np.int32)
+    pos_cols = rng.integers(0, n_drugs, n).astype(np.int32)
+    degrees = rng.integers(1, 200, n_drugs).astype(np.float64)
+    return Config5(E, R, D, pos_rows, pos_cols, degrees, batch)

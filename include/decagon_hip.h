@@ -330,6 +330,15 @@ int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* co
 int dg_hinge_loss_f32(const float* pos, const float* neg, int32_t n, float margin,
                       float* loss, void* stream);
 
+/* The same hinge sum over many pairs (config 5: every slot's batch, 10^6 pairs) on up to
+ * DG_HINGE_WS_BLOCKS workgroups, partials added in block order (deterministic for a given n).
+ * workspace: device, 16-byte aligned, DG_HINGE_WS_BYTES bytes, its first word zero before the
+ * first call (the kernel leaves it zero again).  optimizer.py:116-120. */
+#define DG_HINGE_WS_BLOCKS 256
+#define DG_HINGE_WS_BYTES (16 + 4 * DG_HINGE_WS_BLOCKS)
+int dg_hinge_loss_ws_f32(const float* pos, const float* neg, int32_t n, float margin, float* loss,
+                         void* workspace, void* stream);
+
 /* Cross-entropy loss:  loss[0] = sum_p softplus(-pos[p]) + w * sum_p softplus(neg[p])
  * (sigmoid_cross_entropy_with_logits with labels 1 / 0).  optimizer.py:122-127. */
 int dg_xent_loss_f32(const float* pos, const float* neg, int32_t n, float neg_weight,
@@ -429,6 +438,20 @@ int dg_dropout_advance(uint64_t* state, void* stream);
 int64_t dg_rank_metrics_workspace(int32_t n_pos);
 int dg_rank_metrics_f32(const float* pos, int32_t n_pos, const float* neg, int32_t n_neg, int32_t k,
                         double* out, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* The same metrics of the scores the reference actually ranks: mode DG_RANK_SIGMOID64 =
+ * main.py:51-52,60,70,81 under numpy 1.14 (requirements.txt:14) — float32 exp of TF's float32
+ * logit (correctly rounded, as glibc expf), float64 `1. / (1 + e)`, np.nan_to_num — so logits
+ * above ≈36.7 / below ≈-88.7 tie at 1.0 / 0.0; DG_RANK_SIGMOID32 = MathUtils.sigmoid on the
+ * float32 decoder output (DecagonAccuracyEvaluator.py:123, all float32); DG_RANK_LOGIT = the
+ * logits (as dg_rank_metrics_f32).  pos / neg are the LOGITS.  Workspace 16-byte aligned,
+ * dg_rank_metrics_ex_workspace(n_pos, n_neg) bytes. */
+#define DG_RANK_LOGIT 0
+#define DG_RANK_SIGMOID64 1
+#define DG_RANK_SIGMOID32 2
+int64_t dg_rank_metrics_ex_workspace(int32_t n_pos, int32_t n_neg);
+int dg_rank_metrics_ex_f32(const float* pos, int32_t n_pos, const float* neg, int32_t n_neg, int32_t k,
+                           int32_t mode, double* out, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Unigram negative sampler (T11):  out[i] ~ Categorical(p), p_c ∝ degree_c^0.75, draw

@@ -355,12 +355,38 @@ def apk(actual, predicted, k: int = 10) -> float:
     return score / min(len(actual), k)
 
 
-def accuracy_scores(pos_scores: np.ndarray, neg_scores: np.ndarray, k: int = 50):
-    """(roc, auprc, apk@k) as get_accuracy_scores forms them from per-edge scores: labels 1
-    for the positives then 0 for the negatives; `predicted` = edge indices sorted by score,
-    descending, Python's stable sort (main.py:66-76)."""
+def sigmoid_np114(logits, form: str = "main") -> np.ndarray:
+    """The scores the reference ranks, from TF's float32 logits, under numpy 1.14
+    (requirements.txt:14; value-based casting, pre-NEP 50):
+
+      "main"       main.py:51-52 `1. / (1 + np.exp(-x))` on a float32 scalar rec[u, v]:
+                   np.exp runs in float32 (libm expf — correctly rounded, restated as the
+                   float64 exp rounded to float32), `1 + e` and `1. / …` promote to float64;
+                   then np.nan_to_num (main.py:81)
+      "evaluator"  MathUtils.sigmoid (main/Utils/MathUtils.py:3-4) on the float32 decoder
+                   output ARRAY (DecagonAccuracyEvaluator.py:123): every step stays float32
+    """
+    x = np.asarray(logits, np.float32)
+    with np.errstate(over="ignore", invalid="ignore"):
+        e = np.exp(-x.astype(np.float64)).astype(np.float32)
+    if form == "main":
+        with np.errstate(over="ignore"):
+            return np.nan_to_num(1.0 / (1.0 + e.astype(np.float64)))
+    if form == "evaluator":
+        with np.errstate(over="ignore"):
+            return (np.float32(1.0) / (np.float32(1.0) + e)).astype(np.float32)
+    raise ValueError(form)
+
+
+def accuracy_scores(pos_scores: np.ndarray, neg_scores: np.ndarray, k: int = 50, sigmoid="main"):
+    """(roc, auprc, apk@k) as get_accuracy_scores forms them (main.py:38-90): the LOGITS of the
+    positive and negative edges go through the reference's sigmoid (`sigmoid_np114`; None:
+    ranked as given), labels 1 for the positives then 0 for the negatives; `predicted` = edge
+    indices sorted by score, descending, Python's stable sort (main.py:84)."""
     from sklearn import metrics
 
+    if sigmoid is not None:
+        pos_scores, neg_scores = sigmoid_np114(pos_scores, sigmoid), sigmoid_np114(neg_scores, sigmoid)
     pos = np.asarray(pos_scores, np.float64)
     neg = np.asarray(neg_scores, np.float64)
     preds_all = np.hstack([pos, neg])

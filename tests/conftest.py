@@ -40,3 +40,69 @@ def rel_err(got, want) -> float:
     if den == 0:
         return float(np.max(np.abs(got)))
     return float(np.max(np.abs(got - want)) / den)
+
+
+# ---------------------------------------------------------------- multi-rank tests (gloo)
+def _rank_entry(fn, rank, world, port, q, args):
+    """Child process of run_ranks: gloo group, fn(rank, world, *args) -> payload, reported
+    as (rank, "ok", payload) or (rank, "err", traceback) — a failing rank is seen at once."""
+    import datetime
+    import traceback
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=180))
+        q.put((rank, "ok", fn(rank, world, *args)))
+        dist.barrier()
+    except BaseException:
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def run_ranks(fn, world, args=(), timeout=400):
+    """Run fn(rank, world, *args) in `world` spawned processes over gloo (127.0.0.1) and return
+    {rank: payload}.  Polls every few seconds (printing a heartbeat), fails as soon as a rank
+    reports an error or dies, kills the others."""
+    import socket
+    import sys
+    import time
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_rank_entry, args=(fn, r, world, port, q, args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, t0 = {}, time.time()
+    try:
+        while len(got) < world:
+            try:
+                r, status, payload = q.get(timeout=5)
+            except Exception:
+                dead = [p for p in procs if p.exitcode not in (None, 0)]
+                if dead:
+                    raise AssertionError(f"rank process died with exit code {dead[0].exitcode}")
+                if time.time() - t0 > timeout:
+                    raise AssertionError(f"ranks did not finish within {timeout} s")
+                print(f"[run_ranks] waiting: {len(got)}/{world} ranks done, {time.time() - t0:.0f} s",
+                      file=sys.stderr, flush=True)
+                continue
+            if status != "ok":
+                raise AssertionError(f"rank {r} failed:\n{payload}")
+            got[r] = payload
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    return got

@@ -125,3 +125,16 @@ def test_transposed_relations_are_flipped_copies(golden_S):
 def test_unigram_distribution():
     p = orc.unigram_distribution(np.array([0.0, 1.0, 16.0]))
     assert p[0] == 0 and abs(p[2] / p[1] - 8.0) < 1e-12
+
+
+def test_sigmoid_np114_saturation():
+    """The reference's sigmoid forms saturate where numpy 1.14 + float32 logits put them:
+    main.py (float32 exp, float64 1/(1+e)) at 1.0 above ≈36.7 and 0.0 below ≈-88.7 (float32
+    exp overflow); MathUtils.sigmoid on the float32 array at 1.0 above ≈16.6."""
+    from oracle.decagon_oracle import sigmoid_np114
+
+    m = sigmoid_np114(np.array([37.0, 36.0, -88.0, -89.0, np.nan], np.float32), "main")
+    assert m[0] == 1.0 and m[1] < 1.0 and m[2] > 0.0 and m[3] == 0.0 and m[4] == 0.0
+    assert m.dtype == np.float64
+    e = sigmoid_np114(np.array([17.0, 16.0, 0.0], np.float32), "evaluator")
+    assert e.dtype == np.float32 and e[0] == 1.0 and e[1] < 1.0 and e[2] == np.float32(0.5)

@@ -1,0 +1,109 @@
+"""GPU: config 5 (BASELINE configs[4]) on the benched workload — every one of the 1,928
+drug-drug relation slots scoring 512 positives and 512 device-sampled negatives with the
+d = 256 bf16 DEDICOM decoder, then the hinge loss (decagon_amd.scorer.SlotScorer, as
+bench.py runs it) — against a float64 restatement of the reference's scores
+(decagon/deep/optimizer.py:51-57, 63-85 with G = R, L = D_k: model.py:130-134) and hinge
+(optimizer.py:116-120) over EVERY pair, with the same bf16 operand rounding as the kernel
+(inputs rounded to bf16; u∘D_k rounded to bf16 as the MFMA's operand; fp32 accumulation).
+
+The negatives are read back from the device: in range, distributed as degree^0.75
+(fixed_unigram_candidate_sampler, optimizer.py:40-47), and independent of how the slots are
+sharded: the 2-rank slot-sharded run (gloo on the one GPU, loss all-reduced) reproduces the
+one-rank draws and scores bit for bit.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_err, run_ranks
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _scorer(device, slots=None, allreduce=None):
+    from decagon_amd import kernels, synthetic
+    from decagon_amd.scorer import SlotScorer
+
+    c5 = synthetic.make_config5()
+    bf = torch.bfloat16
+    E = torch.from_numpy(c5.E).to(bf).to(device)
+    sc = SlotScorer(E, E, torch.from_numpy(c5.R).to(bf).to(device), torch.from_numpy(c5.D).to(bf).to(device),
+                    torch.from_numpy(c5.pos_rows).to(device), torch.from_numpy(c5.pos_cols).to(device),
+                    kernels.upload_alias(c5.degrees, device), c5.batch, 0.1, seed=11, slots=slots,
+                    allreduce=allreduce)
+    return c5, sc
+
+
+def _restated_scores(c5, rows, cols, rel):
+    """float64 uᵀ·D_k·R·D_k·v on the bf16-rounded inputs, u∘D_k rounded to bf16."""
+    bf = torch.bfloat16
+    E = torch.from_numpy(c5.E).to(bf).float().numpy()
+    R = torch.from_numpy(c5.R).to(bf).double().numpy()
+    D = torch.from_numpy(c5.D).to(bf).float().numpy()
+    out = np.empty(len(rows))
+    step = 1 << 16
+    for s in range(0, len(rows), step):
+        r, c, k = rows[s:s + step], cols[s:s + step], rel[s:s + step]
+        a = torch.from_numpy(E[r] * D[k]).to(bf).double().numpy()          # the MFMA operand
+        b = D[k].astype(np.float64) * E[c].astype(np.float64)
+        out[s:s + step] = np.einsum("pn,pn->p", a @ R, b)
+    return out
+
+
+def test_config5_full_workload_matches_restatement():
+    from oracle import decagon_oracle as orc
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    c5, sc = _scorer(torch.device("cuda"))
+    sc()
+    torch.cuda.synchronize()
+    n = sc.n
+    slots = c5.D.shape[0]
+    assert n == slots * c5.batch == 1928 * 512
+    neg_rows = sc.neg_rows.cpu().numpy()
+    pos, neg, loss = sc.pos.cpu().numpy(), sc.neg.cpu().numpy(), float(sc.loss[0])
+    # device-sampled negatives: in range, distributed as degree^0.75
+    assert neg_rows.min() >= 0 and neg_rows.max() < c5.E.shape[0]
+    p = orc.unigram_distribution(c5.degrees)
+    obs = np.bincount(neg_rows, minlength=len(p))
+    exp = p * n
+    assert np.all(np.abs(obs - exp) <= 6 * np.sqrt(exp) + 1)
+    rel = np.repeat(np.arange(slots), c5.batch)
+    want_pos = _restated_scores(c5, c5.pos_rows, c5.pos_cols, rel)
+    want_neg = _restated_scores(c5, neg_rows, c5.pos_cols, rel)
+    assert rel_err(pos, want_pos) <= 1e-4
+    assert rel_err(neg, want_neg) <= 1e-4
+    want_loss = orc.hinge_loss(want_pos, want_neg, 0.1)
+    assert abs(loss - want_loss) <= 1e-4 * abs(want_loss)
+    # the loss kernel itself, on the device's own scores (float64 sum): fp32-accumulation tight
+    own = orc.hinge_loss(pos.astype(np.float64), neg.astype(np.float64), 0.1)
+    assert abs(loss - own) <= 1e-5 * abs(own)
+
+
+def _rank(rank, world):
+    from decagon_amd.sharding import slot_range, torch_allreduce
+
+    s0, s1 = slot_range(1928, rank, world)
+    _, sc = _scorer(torch.device("cuda", 0), (s0, s1), torch_allreduce())
+    sc()
+    torch.cuda.synchronize()
+    return s0, s1, sc.neg_rows.cpu().numpy(), sc.out.cpu().numpy(), float(sc.loss[0])
+
+
+def test_config5_slot_sharded_two_ranks_equal_one_rank():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    c5, sc = _scorer(torch.device("cuda"))
+    sc()
+    torch.cuda.synchronize()
+    B = c5.batch
+    full_neg, full_pos, full_negs = sc.neg_rows.cpu().numpy(), sc.pos.cpu().numpy(), sc.neg.cpu().numpy()
+    full_loss = float(sc.loss[0])
+    got = run_ranks(_rank, 2).values()
+    for s0, s1, negr, out, loss in got:
+        m = (s1 - s0) * B
+        assert np.array_equal(negr, full_neg[s0 * B:s1 * B])
+        assert np.array_equal(out[:m], full_pos[s0 * B:s1 * B])
+        assert np.array_equal(out[m:], full_negs[s0 * B:s1 * B])
+        assert abs(loss - full_loss) <= 1e-5 * abs(full_loss)  # all-reduced per-rank sums

@@ -391,6 +391,30 @@ def test_rank_metrics_match_sklearn(P, N, k, ties):
         assert abs(g - w) <= 1e-12, (got, want)
 
 
+@pytest.mark.parametrize("mode", ["main", "evaluator", None])
+def test_rank_metrics_saturating_logits(mode):
+    """Logits spanning [-120, 120]: the reference ranks sigmoid scores that saturate (main.py
+    under numpy 1.14: float32 exp, float64 1/(1+e) — ties at exactly 1.0 above ≈36.7 and 0.0
+    below ≈-88.7; DecagonAccuracyEvaluator: all float32, ties above ≈16.6).  The device ranks
+    the same scores: AUROC / AUPRC / AP@50 equal the restated sklearn / rank_metrics values
+    within 1e-12, and (main, evaluator) differ from the logit ranking — the ties matter."""
+    from decagon_amd.evaluate import rank_metrics
+
+    dev = _dev()
+    rng = np.random.default_rng(120)
+    pos = rng.uniform(-60, 100, 1500).astype(np.float32)
+    neg = rng.uniform(-120, 110, 1300).astype(np.float32)
+    if mode == "main":
+        neg[:7] = np.nan  # nan_to_num (main.py:81) scores a NaN logit 0.0
+    got = rank_metrics(torch.from_numpy(pos).to(dev), torch.from_numpy(neg).to(dev), 50, sigmoid=mode)
+    want = orc.accuracy_scores(pos, neg, 50, sigmoid=mode)
+    for g, w in zip(got, want):
+        assert abs(g - w) <= 1e-12, (mode, got, want)
+    if mode is not None:
+        raw = orc.accuracy_scores(pos, np.nan_to_num(neg, nan=-200.0), 50, sigmoid=None)
+        assert abs(raw[0] - want[0]) > 1e-4 and abs(raw[2] - want[2]) > 1e-3, (raw, want)
+
+
 def test_accuracy_scores_through_the_model(golden_S):
     """evaluate.accuracy_scores (main.py:38-80 on the device) against sklearn on the oracle's
     predictions of the same sampled edges."""
