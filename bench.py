@@ -79,6 +79,10 @@ def parse(argv=None):
     ap.add_argument("--collectives", choices=["graph", "eager"], default="graph",
                     help="N > 1 over RCCL: capture the whole step, collectives included, in one "
                          "hipGraph (graph), or replay the compute phases between eager collectives")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="config P: time each rank's share of an N-GPU sharded step on this one GPU, "
+                         "collectives replaced by no-ops (prints per-rank step times and the bytes each "
+                         "collective would move)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                     "gloo only to exercise the multi-rank path on a single-GPU box)")
     return ap.parse_args(argv)
@@ -534,6 +538,53 @@ def main_train(args):
     print(json.dumps(rec), file=JSON_OUT, flush=True)
 
 
+# ----------------------------------------------------------------------------- rehearsal
+def main_simulate(args):
+    """One GPU standing in for each rank of an N-GPU config-P step in turn: the rank's shard
+    (proteins row-split, drug×drug relations LPT-sharded) with the collectives replaced by
+    no-ops, timed as the bench times a step.  max over ranks + the collectives' time is the
+    N-GPU step; the bytes each collective moves are printed beside it."""
+    import torch
+
+    from decagon_amd import synthetic
+    from decagon_amd.sharding import RelationShard
+
+    torch.cuda.set_device(0)
+    device = torch.device("cuda", 0)
+    N = args.simulate_world
+    graph = synthetic.make_P(seed=0)
+    stream = torch.cuda.Stream(device)
+    G = steps_per_graph(args.steps, args.graph_steps)
+    ranks = []
+    for r in range(N):
+        shard = RelationShard.polypharmacy(graph, r, N, comm=False)
+        plan, dg = make_plan(args, graph, shard, device)
+        dec = Decoder(graph, plan, device, r)
+
+        def step():
+            plan.run()
+            dec()
+        el = timed_steps(step, args.steps, args.warmup, G, stream)
+        l1, _ = plan.spmm_launches
+        phases = {"layer1_spmm_ms": time_kernel(plan._layer1.run_spmm, 20, stream),
+                  "layer2_spmm_ms": time_kernel(plan._layer2.run_spmm, 20, stream)}
+        coll = []
+        for L in (plan._layer1, plan._layer2):
+            coll.append({"allreduce_bytes": 0 if L.flat is None else 4 * L.flat.numel(),
+                         "allgather_bytes": sum(4 * o.numel() for o, _ in L.gathers)})
+        ranks.append({"rank": r, "ms_per_step": el * 1e3 / args.steps, "nnz_per_layer": dg.total_nnz,
+                      "collectives_per_layer": coll, **phases})
+        print(f"rank {r}/{N}: {ranks[-1]['ms_per_step'] * 1e3:.1f} us/step, {dg.total_nnz} nnz", file=sys.stderr,
+              flush=True)
+        del plan, dec, dg
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    rec = {"metric": "config P sharded-step rehearsal on one GPU (collectives not run)", "world": N,
+           "steps": args.steps, "warmup": args.warmup, "steps_per_graph": G,
+           "max_rank_ms_per_step": max(x["ms_per_step"] for x in ranks), "ranks": ranks}
+    print(json.dumps(rec), file=JSON_OUT, flush=True)
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -546,6 +597,8 @@ def main():
         return main_decoder(args)
     if args.train:
         return main_train(args)
+    if args.simulate_world:
+        return main_simulate(args)
     import torch
     import torch.distributed as dist
 

@@ -11,7 +11,7 @@ __version__ = "0.1.0"
 from . import flags  # noqa: F401
 from .flags import FLAGS  # noqa: F401
 from .graph import (InvalidArgumentError, Node, Operation, Placeholder, Session, Variable,  # noqa: F401
-                    float32, global_variables_initializer, int32, name_scope, placeholder,
+                    float32, global_variables, global_variables_initializer, int32, name_scope, placeholder,
                     placeholder_with_default, sparse_placeholder)
 from .inits import set_random_seed  # noqa: F401
 from .layers import (BilinearDecoder, DEDICOMDecoder, DistMultDecoder,  # noqa: F401

@@ -21,10 +21,11 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 19
+ABI_VERSION = 20
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
+DG_GROUP_DROPOUT = 2
 DG_MAX_ADAM_SEGS = 32
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
@@ -42,7 +43,11 @@ class DgRelGroup(ctypes.Structure):
         ("n_chunks", c_int32),
         ("x_rows", c_int32),
         ("flags", c_int32),
-        ("reserved", c_int32 * 2),
+        ("drop_tag", ctypes.c_uint32),
+        ("drop_keep", c_float),
+        ("drop_stride", c_int32),
+        ("drop_state", c_void_p),
+        ("drop_index", c_void_p),
     ]
 
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "decagon_hip.h"
 
 namespace dg {
@@ -18,6 +20,19 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 inline int launch_status() {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DG_OK : static_cast<int>(e);
+}
+
+// The one piece of process state the library keeps: per kernel, the set of devices on which
+// its dynamic-LDS opt-in (hipFuncSetAttribute, idempotent) has been applied — one bit per
+// device id, so every device a process launches on is configured, and concurrent callers at
+// worst set the attribute twice.
+inline void lds_optin(const void* fn, int bytes, std::atomic<uint64_t>& done) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return;
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    done.fetch_or(bit, std::memory_order_acq_rel);
 }
 
 // Lanes that cooperate on one dense row of width d (d/4 float4 lanes, rounded up to a

@@ -184,14 +184,9 @@ extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, 
     if (blocks > 256) blocks = 256;  // persistent: one Rᵀ-holding workgroup per CU
     const int lds = d * d * 2;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&decoder_bf16_kernel<256, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&decoder_bf16_kernel<256, false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        configured = true;
-    }
+    static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
+    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_kernel<256, true>), 160 * 1024, configured_l);
+    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_kernel<256, false>), 160 * 1024, configured_nl);
 #define DG_DEC_LAUNCH(DD, HL) \
     hipLaunchKernelGGL((decoder_bf16_kernel<DD, HL>), dim3(blocks), dim3(threads_for<DD>()), lds, st, a)
     const bool hl = l_table != nullptr;

@@ -24,6 +24,7 @@
 // the same workgroup: L2 norm per group, Σ over the node type's groups, relu, and optionally
 // the next layer's projection of the finished row.
 #include "common.h"
+#include "dropout.h"
 
 #ifndef DG_PROJ_UNROLL
 #define DG_PROJ_UNROLL 16  // W loads per batch of the projection chain (measured: 8 → 16 −0.4 µs at S)
@@ -56,7 +57,20 @@ struct SpmmGroupK {
     int32_t block_begin;
     int32_t n_blocks;
     int64_t chunk_x;  // shared pattern: elements between the chunks' X slabs (0: merged CSR)
+    // DG_GROUP_DROPOUT (shared pattern only): per-chunk masks on the pattern's values
+    const uint64_t* drop_state;  // NULL: no dropout
+    const int32_t* drop_index;
+    uint32_t drop_tag;
+    float drop_keep;
+    int32_t drop_stride;
+    int32_t pad;
 };
+
+// The dropout scale of nonzero p in chunk c (DG_GROUP_DROPOUT, dropout.h's stream).
+__device__ __forceinline__ float drop_mul(const SpmmGroupK& g, uint32_t key, uint32_t base, int p) {
+    const uint32_t e = g.drop_index ? (uint32_t)g.drop_index[p] : (uint32_t)p;
+    return dg::keep_scale(key, base + e, g.drop_keep);
+}
 
 struct SpmmArgs {
     SpmmGroupK g[DG_MAX_GROUPS];
@@ -72,7 +86,8 @@ constexpr int kUnroll = 8;        // gathers in flight per lane
 // 4(l%LP) .. 4(l%LP)+3).
 template <int LP>
 __device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb, int beg, int end, int d,
-                                            int wpart = 0, int wcount = 1) {
+                                            int wpart = 0, int wcount = 1, uint32_t dkey = 0,
+                                            uint32_t dbase = 0) {
     constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
@@ -89,6 +104,7 @@ __device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb
     if (base + lane < end) {
         vc = vcolp[base + lane];
         vv = valp[base + lane];
+        if (g.drop_state) vv *= drop_mul(g, dkey, dbase, base + lane);
     }
 #pragma unroll 1
     for (; base < end; base += stride) {
@@ -101,6 +117,7 @@ __device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb
         if (nb + lane < end) {
             vc = vcolp[nb + lane];
             vv = valp[nb + lane];
+            if (g.drop_state) vv *= drop_mul(g, dkey, dbase, nb + lane);
         }
 #pragma unroll 1
         for (int s0 = 0; s0 < n; s0 += kUnroll * G) {
@@ -151,7 +168,9 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
     const int64_t slot = (int64_t)c * g.n_rows + r;
     // shared pattern: every chunk reads rowptr[r] over its own X slab
     const int64_t ps = g.chunk_x ? r : slot;
-    const float4 acc = range_sum<LP>(g, g.x + c * g.chunk_x, g.rowptr[ps], g.rowptr[ps + 1], d);
+    const uint32_t dkey = g.drop_state ? dg::drop_key(g.drop_state, g.drop_tag) : 0u;
+    const float4 acc = range_sum<LP>(g, g.x + c * g.chunk_x, g.rowptr[ps], g.rowptr[ps + 1], d, 0, 1, dkey,
+                                     (uint32_t)c * (uint32_t)g.drop_stride);
     if (lane < LP && lane * 4 < d) *reinterpret_cast<float4*>(g.out + slot * d + lane * 4) = acc;
 }
 
@@ -493,7 +512,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 19; }
+extern "C" int32_t dg_abi_version(void) { return 20; }
 
 
 namespace {
@@ -501,8 +520,13 @@ namespace {
 // Validate one descriptor and copy it into the kernel form.  Returns DG_OK or an error.
 int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k, bool allow_shared = false) {
     if (s.n_rows < 0 || s.n_chunks < 1 || s.x_rows < 0) return DG_EINVAL;
-    if (s.flags & ~DG_GROUP_SHARED_PATTERN) return DG_EINVAL;
+    if (s.flags & ~(DG_GROUP_SHARED_PATTERN | DG_GROUP_DROPOUT)) return DG_EINVAL;
     if ((s.flags & DG_GROUP_SHARED_PATTERN) && !allow_shared) return DG_EINVAL;
+    if (s.flags & DG_GROUP_DROPOUT) {  // per-chunk masks of a shared pattern only
+        if (!(s.flags & DG_GROUP_SHARED_PATTERN) || !s.drop_state || s.drop_stride < 0) return DG_EINVAL;
+        if (!(s.drop_keep > 0.f && s.drop_keep <= 1.f)) return DG_EINVAL;
+        if ((int64_t)s.n_chunks * s.drop_stride > 0xffffffffLL) return DG_EINVAL;  // 32-bit mask counter
+    }
     // vcol/val may be NULL for a group without nonzeros (rowptr all zero: never read)
     if (!s.rowptr || !s.x || (need_out && !s.out)) return DG_EINVAL;
     if (!dg::aligned16(s.x) || (need_out && !dg::aligned16(s.out)) || (s.x_ld & 3)) return DG_EALIGN;
@@ -518,6 +542,12 @@ int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k, bo
     k.n_chunks = s.n_chunks;
     k.row_blocks = dg::ceil_div(s.n_rows, kRowsPerBlock);
     k.chunk_x = (s.flags & DG_GROUP_SHARED_PATTERN) ? (int64_t)s.x_rows * s.x_ld : 0;
+    const bool drop = (s.flags & DG_GROUP_DROPOUT) != 0;
+    k.drop_state = drop ? s.drop_state : nullptr;
+    k.drop_index = drop ? s.drop_index : nullptr;
+    k.drop_tag = s.drop_tag;
+    k.drop_keep = drop ? s.drop_keep : 1.f;
+    k.drop_stride = drop ? s.drop_stride : 0;
     return DG_OK;
 }
 
@@ -740,12 +770,8 @@ extern "C" int dg_spmm_groups_lds_f32(const dg_rel_group* groups, int32_t n_grou
         blocks += (int64_t)g.persist * a.n_slices;
     }
     if (blocks > 0x7fffffff) return DG_EINVAL;
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmm_lds_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        configured = true;
-    }
+    static std::atomic<uint64_t> configured{0};
+    dg::lds_optin(reinterpret_cast<const void*>(&spmm_lds_kernel), 160 * 1024, configured);
     hipLaunchKernelGGL(spmm_lds_kernel, dim3(static_cast<unsigned>(blocks)), dim3(1024), lds,
                        reinterpret_cast<hipStream_t>(stream), a);
     return dg::launch_status();

@@ -360,12 +360,8 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
     }
 #endif
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmm_staged_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        configured = true;
-    }
+    static std::atomic<uint64_t> configured{0};
+    dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel), kLdsBytes, configured);
     hipLaunchKernelGGL(spmm_staged_kernel, dim3(static_cast<unsigned>(blocks)), dim3(threads),
                        static_cast<int>(lds), st, a);
     return dg::launch_status();

@@ -266,8 +266,6 @@ class ForwardPlan:
         if dropout is not None and float(dropout[0]) < 1.0:
             if allreduce is not None or self.row_block:
                 raise NotImplementedError("dropout with a sharded forward is not on the HIP path")
-            if any(f is not None for f in features.values()):
-                raise NotImplementedError("dropout with sparse (non-identity) features is not on the HIP path")
             self.keep, self.drop_state = float(dropout[0]), dropout[1]
         # flat mode: every group's pre-normalisation sum S_ij lands in one flat buffer per
         # layer (all-reduced when sharded; kept for the backward when training), and one fused
@@ -325,11 +323,14 @@ class ForwardPlan:
                 raise ValueError(f"features of type {j} have shape {fj.shape}, weights expect (*, {F})")
             # X_j·W1_k for every relation k of the group (global slabs; sharded ranks compute
             # all of them — sparse features are small next to the adjacency): one copy of X_j's
-            # pattern shared by the K chunks, chunk k reading W1_k
+            # pattern shared by the K chunks, chunk k reading W1_k; with dropout, chunk k masks
+            # X_j's values with its own draw (dropout_sparse per relation, layers.py:23-31, :88)
             xw = torch.empty((K, n[j], h1), **f32)
+            drop = (None if self.drop_state is None
+                    else (self.drop_state, drop_tag(1, self.et_index[et]), self.keep))
             spec = kernels.RelGroupSpec(torch.from_numpy(fj.rowptr).to(dev), torch.from_numpy(fj.col).to(dev),
                                         torch.from_numpy(fj.val).to(dev), W, xw, n[j], K, h1, F,
-                                        vcol_max=int(fj.col.max()) if fj.nnz else -1, shared=True)
+                                        vcol_max=int(fj.col.max()) if fj.nnz else -1, shared=True, drop=drop)
             self._pre.append(kernels.PreparedSpmm([spec], h1))
             x1[et] = xw
 

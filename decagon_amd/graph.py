@@ -13,8 +13,8 @@ any node — not only a placeholder — may be fed, which overrides its computat
 from __future__ import annotations
 
 import contextlib
-
 import itertools
+import weakref
 from typing import Any, Callable, Dict, Optional
 
 import numpy as np
@@ -83,13 +83,19 @@ def placeholder_with_default(value, shape=None, name=None) -> Placeholder:
     return Placeholder(None, shape, name, default=value, has_default=True)
 
 
+_VARIABLES: list = []  # weak references to every Variable, in creation order (TF's GLOBAL_VARIABLES)
+
+
 class Variable(Node):
     """A device-resident parameter.  `value` is a view into a weight stack owned by the
-    model, so loading a new value never moves the buffer the kernels were prepared with."""
+    model, so loading a new value never moves the buffer the kernels were prepared with.
+    `initializer` draws a fresh value (host numpy) — what global_variables_initializer runs."""
 
-    def __init__(self, tensor: torch.Tensor, name: str):
+    def __init__(self, tensor: torch.Tensor, name: str, initializer: Optional[Callable[[], Any]] = None):
         super().__init__(name)
         self.tensor = tensor
+        self.initializer = initializer
+        _VARIABLES.append(weakref.ref(self))
 
     @property
     def shape(self):
@@ -165,6 +171,18 @@ class Session:
         self.caches.clear()
         self._closed = True
 
+    def invalidate_feeds(self) -> None:
+        """Forget every cached feed conversion, device graph and plan (after changing a fed
+        array's contents in place — which the read-only marking otherwise refuses)."""
+        for name in ("host_csr", "features", "dgraph", "plans"):
+            self.caches.pop(name, None)
+
+    def reset_optimizer_slots(self) -> None:
+        """Drop the optimizer state this session holds (Adam m / v / beta powers): the next
+        opt_op starts from step 1, as after TF's variable initializer."""
+        for key in [k for k in self.caches if isinstance(k, tuple) and k and k[0] == "adam"]:
+            del self.caches[key]
+
     def run(self, fetches, feed_dict: Optional[Dict] = None):
         if self._closed:
             raise RuntimeError("Attempted to use a closed Session.")
@@ -225,6 +243,23 @@ def name_scope(name: str):
     yield name
 
 
+def global_variables() -> list:
+    """Every live Variable, in creation order (tf.global_variables)."""
+    live = [r() for r in _VARIABLES]
+    _VARIABLES[:] = [r for r, v in zip(list(_VARIABLES), live) if v is not None]
+    return [v for v in live if v is not None]
+
+
 def global_variables_initializer() -> Operation:
-    """Variables are initialised at construction (glorot, inits.py); this is a no-op op."""
-    return Operation("init", lambda ctx: None)
+    """tf.global_variables_initializer (main.py:286, DecagonTrainer.py:49): running it
+    re-draws every variable from its initializer (glorot, inits.py:5-12 — in place, so the
+    prepared kernels keep their buffers) and resets the optimizer slots the session holds
+    (Adam's m, v and beta powers are TF variables too).  Variables are also initialised at
+    construction, so a model is usable without running it."""
+    def fn(ctx):
+        for v in global_variables():
+            if v.initializer is not None:
+                v.load(v.initializer())
+        ctx.session.reset_optimizer_slots()
+        return None
+    return Operation("init", fn)

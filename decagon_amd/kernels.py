@@ -58,6 +58,10 @@ class RelGroupSpec:
     vcol_max: int = -1            # host-known max(vcol) (-1: no nonzeros)
     shared: bool = False          # DG_GROUP_SHARED_PATTERN: one CSR [n_rows] for every chunk, chunk c
                                   # reading x rows [c*x_rows, (c+1)*x_rows) (dg_spmm_groups_f32 only)
+    drop: Optional[Tuple[torch.Tensor, int, float]] = None  # DG_GROUP_DROPOUT (shared only):
+                                  # (device state {seed, step}, stream tag, keep) — chunk c scales
+                                  # nonzero p by mask element c·nnz + (drop_index[p] or p)
+    drop_index: Optional[torch.Tensor] = None
 
     def validate(self, d: int, need_out: bool = True) -> None:
         _dev(self.rowptr, torch.int32, "rowptr")
@@ -86,6 +90,21 @@ class RelGroupSpec:
             raise ValueError("dense operand too large for 32-bit gather offsets")
         if need_out and self.out.numel() < self.n_chunks * self.n_rows * d:
             raise ValueError("out too small for [n_chunks, n_rows, d]")
+        if self.drop is not None:
+            state, _, keep = self.drop
+            if not self.shared:
+                raise ValueError("dropout masks apply to a shared pattern only")
+            if not (isinstance(state, torch.Tensor) and state.is_cuda and state.dtype == torch.int64
+                    and state.numel() >= 2):
+                raise ValueError("dropout state: int64 device tensor {seed, step}")
+            if not 0.0 < float(keep) <= 1.0:
+                raise ValueError("keep must be in (0, 1]")
+            if self.n_chunks * self.vcol.numel() >= 2**32:
+                raise ValueError("dropout mask counter exceeds 32 bits")
+            if self.drop_index is not None:
+                _dev(self.drop_index, torch.int32, "drop_index")
+                if self.drop_index.numel() != self.vcol.numel():
+                    raise ValueError("drop_index must have one entry per nonzero")
 
 
 def _fill_group(g, s: RelGroupSpec) -> None:
@@ -99,6 +118,16 @@ def _fill_group(g, s: RelGroupSpec) -> None:
     g.n_chunks = s.n_chunks
     g.x_rows = s.x_rows
     g.flags = _lib.DG_GROUP_SHARED_PATTERN if s.shared else 0
+    g.drop_state = None
+    g.drop_index = None
+    if s.drop is not None:
+        state, tag, keep = s.drop
+        g.flags |= _lib.DG_GROUP_DROPOUT
+        g.drop_state = state.data_ptr()
+        g.drop_tag = int(tag)
+        g.drop_keep = float(keep)
+        g.drop_stride = int(s.vcol.numel())
+        g.drop_index = s.drop_index.data_ptr() if s.drop_index is not None else None
 
 
 SPMM_LDS_MAX_ROWS = 160 * 1024 // 144  # dg_spmm_groups_lds_f32: operand rows staged in LDS

@@ -62,12 +62,42 @@ def act_kind(act) -> str:
     raise ValueError(f"unsupported activation {act!r} (identity, relu or sigmoid)")
 
 
-def dropout_sparse(x, keep_prob, num_nonzero_elems):
-    """layers.py:23-31.  keep_prob == 1 (dropout 0, the only forward with defined parity)
-    is the identity; stochastic dropout belongs to the training path."""
-    if float(keep_prob) != 1.0:
-        raise NotImplementedError("sparse dropout with keep_prob < 1 is not on the HIP path yet")
-    return x
+def dropout_sparse(x, keep_prob, num_nonzero_elems, seed: int = 0, step: int = 0, tag: int = 0):
+    """layers.py:23-31 on a host COO tuple (coords, values, shape): each of the
+    num_nonzero_elems values kept with probability keep_prob and scaled by 1/keep_prob,
+    dropped ones removed (tf.sparse_retain).  The draw is the device's counter-based stream
+    (dropout.h: element e of stream `tag` at (seed, step)) — TF's RNG is not reproducible.
+    Inside a model, the per-relation masks are drawn on the device by the SpMM that computes
+    X_j·W_k (DG_GROUP_DROPOUT); this standalone form is for callers of the layer API."""
+    kp = float(keep_prob)
+    if kp == 1.0:
+        return x
+    from .sparse import as_coo_tuple
+
+    coords, vals, shape = as_coo_tuple(x)
+    n = int(num_nonzero_elems)
+    if n != len(vals):
+        raise ValueError(f"num_nonzero_elems {n} != {len(vals)} values")
+    scale = _drop_scale_host(seed, step, tag, n, kp)
+    keep = scale != 0
+    return coords[keep], (np.asarray(vals, np.float32)[keep] * scale[keep]).astype(np.float32), shape
+
+
+def _drop_scale_host(seed: int, step: int, tag: int, n: int, keep: float) -> np.ndarray:
+    """dropout.h's mask stream on the host (the same bits the kernels draw)."""
+    def lowbias32(x):
+        x = np.asarray(x, np.uint32)
+        x = x ^ (x >> np.uint32(16))
+        x = (x * np.uint32(0x7FEB352D)).astype(np.uint32)
+        x = x ^ (x >> np.uint32(15))
+        x = (x * np.uint32(0x846CA68B)).astype(np.uint32)
+        return x ^ (x >> np.uint32(16))
+    with np.errstate(over="ignore"):
+        k1 = lowbias32(np.uint32(seed & 0xFFFFFFFF) ^ np.uint32((tag * 0x9E3779B9) & 0xFFFFFFFF))
+        key = lowbias32(k1 ^ np.uint32((((seed >> 32) & 0xFFFFFFFF) + step * 0x85EBCA6B) & 0xFFFFFFFF))
+        h = lowbias32(key ^ np.arange(n, dtype=np.uint32))
+    thr = np.uint32(np.float32(keep) * np.float32(16777216.0))
+    return np.where((h >> np.uint32(8)) < thr, np.float32(1.0) / np.float32(keep), np.float32(0)).astype(np.float32)
 
 
 class MultiLayer:
@@ -116,7 +146,8 @@ class _GraphConvBase(MultiLayer):
         self.weights_stack = _glorot_stack(self.num_types, d_in, d_out)
         scope = self._scope()
         for k in range(self.num_types):
-            self.vars["weights_%d" % k] = Variable(self.weights_stack[k], f"{scope}/weights_{k}:0")
+            self.vars["weights_%d" % k] = Variable(self.weights_stack[k], f"{scope}/weights_{k}:0",
+                                                   initializer=lambda: inits.glorot_array(d_in, d_out))
 
     def _adj_group(self, ctx, per_rel: bool):
         """Upload (cached) this layer's adjacency feeds as one device group: one chunk for
@@ -193,9 +224,11 @@ class _DecoderBase(MultiLayer):
         self.act = act
         self.input_dim = input_dim
 
-    def _make_vars(self, arrays: Dict[str, np.ndarray]) -> None:
+    def _make_vars(self, init_fns) -> None:
         """All of the decoder's variables as views of ONE flat device buffer (`self.flat`),
-        each starting 16-byte aligned — so the optimizer updates a decoder in one segment."""
+        each starting 16-byte aligned — so the optimizer updates a decoder in one segment.
+        init_fns: name -> initializer (drawn once here, again by global_variables_initializer)."""
+        arrays = {name: fn() for name, fn in init_fns.items()}
         offs, off = {}, 0
         for name, a in arrays.items():
             offs[name] = off
@@ -205,7 +238,7 @@ class _DecoderBase(MultiLayer):
             a = np.ascontiguousarray(a, np.float32)
             view = self.flat[offs[name]:offs[name] + a.size].view(a.shape)
             view.copy_(torch.from_numpy(a))
-            self.vars[name] = Variable(view, f"{self._scope()}/{name}:0")
+            self.vars[name] = Variable(view, f"{self._scope()}/{name}:0", initializer=init_fns[name])
 
     def latent(self, k: int):
         """(G kind, G variable or None, L kind, L variable or None) for relation k."""
@@ -236,10 +269,11 @@ class DEDICOMDecoder(_DecoderBase):
 
     def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
         super().__init__(input_dim, dropout, act, **kwargs)
-        arrays = {"global_interaction": inits.glorot_array(input_dim, input_dim)}
+        d = input_dim
+        fns = {"global_interaction": lambda: inits.glorot_array(d, d)}
         for k in range(self.num_types):
-            arrays["local_variation_%d" % k] = inits.glorot_array(input_dim, 1).reshape(-1)
-        self._make_vars(arrays)
+            fns["local_variation_%d" % k] = lambda: inits.glorot_array(d, 1).reshape(-1)
+        self._make_vars(fns)
 
     def latent(self, k):
         return "dense", self.vars["global_interaction"], "diag", self.vars["local_variation_%d" % k]
@@ -250,7 +284,8 @@ class DistMultDecoder(_DecoderBase):
 
     def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
         super().__init__(input_dim, dropout, act, **kwargs)
-        self._make_vars({"relation_%d" % k: inits.glorot_array(input_dim, 1).reshape(-1)
+        d = input_dim
+        self._make_vars({"relation_%d" % k: (lambda: inits.glorot_array(d, 1).reshape(-1))
                          for k in range(self.num_types)})
 
     def latent(self, k):
@@ -262,7 +297,8 @@ class BilinearDecoder(_DecoderBase):
 
     def __init__(self, input_dim, dropout=0., act=sigmoid, **kwargs):
         super().__init__(input_dim, dropout, act, **kwargs)
-        self._make_vars({"relation_%d" % k: inits.glorot_array(input_dim, input_dim)
+        d = input_dim
+        self._make_vars({"relation_%d" % k: (lambda: inits.glorot_array(d, d))
                          for k in range(self.num_types)})
 
     def latent(self, k):

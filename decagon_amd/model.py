@@ -178,7 +178,7 @@ class DecagonModel(Model):
                  for j in dg.n_nodes}
         key = ("plan", id(self), id(dg), tuple((j, id(f)) for j, f in feats.items()),
                None if shard is None else id(shard), training, keep)
-        cache = ctx.session.caches.setdefault("plans", {})
+        cache = runtime.plan_cache(ctx)
         hit = cache.get(key)
         if hit is None:
             for et in self.edge_types:
@@ -186,11 +186,12 @@ class DecagonModel(Model):
                     raise RuntimeError("model parameters are not on the session's device "
                                        "(construct the model after a HIP device is visible)")
             w1, w2 = self.weight_stacks()
+            before = torch.cuda.memory_allocated(ctx.session.device)
             p = ForwardPlan(dg, feats, w1, w2, self.h1, self.h2,
                             shard=shard, keep_sums=training,
                             dropout=(keep, self.dropout_state(ctx)) if keep < 1.0 else None)
             hit = (dg, feats, p)
-            cache[key] = hit
+            cache.put(key, hit, torch.cuda.memory_allocated(ctx.session.device) - before)
         return hit[2]
 
     def _forward(self, ctx: RunContext) -> ForwardPlan:

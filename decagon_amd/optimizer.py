@@ -200,14 +200,14 @@ class DecagonOptimizer:
 
     def _train_plan(self, ctx: RunContext, model):
         fwd = model._forward(ctx)
-        key = ("train", id(self), id(fwd))
-        cache = ctx.session.caches
-        if key not in cache:
+        # the backward plan lives on its forward plan: evicting the plan (runtime's LRU) drops both
+        plans = fwd.__dict__.setdefault("_train_plans", {})
+        if id(self) not in plans:
             feats = {j: runtime.feature_csr(ctx, model.inputs[j]) if j in model.inputs else None
                      for j in fwd.g.n_nodes}
             w1, w2 = model.weight_stacks()
-            cache[key] = train.TrainPlan(fwd, w1, w2, feats)
-        return fwd, cache[key]
+            plans[id(self)] = train.TrainPlan(fwd, w1, w2, feats)
+        return fwd, plans[id(self)]
 
     def _decoder_grads(self, ctx: RunContext, model, e: int, rt: int, ct: int):
         """Zeroed gradient buffers of every decoder, the batch relation's entries filled

@@ -3,25 +3,33 @@ variable scopes, feed → device conversion with caching, and the standalone (si
 type) layer forward.
 
 Feed caching.  The reference re-feeds every adjacency tuple on every step
-(minibatch.py:259-267).  A session caches the device copy of a fed sparse value keyed by the
-identity of its numpy arrays (and keeps those arrays referenced, so the key cannot be
-recycled); re-feeding the same tuples — what every reference driver does — costs nothing.
-Feeds are treated as immutable: mutate a fed array in place and the cached device copy is
-stale (call `Session.invalidate_feeds()`, or feed a new array).
+(minibatch.py:259-267).  A session caches the host CSR and the device copy of a fed sparse
+value keyed by the identity of the objects fed — the arrays of a (coords, values, shape)
+tuple, or the scipy matrix / SparseTensorValue itself — and keeps those objects referenced,
+so a key cannot be recycled; re-feeding the same values — what every reference driver does —
+costs nothing.  Fed numpy arrays are marked read-only when cached, so mutating one in place
+fails loudly instead of leaving a stale device copy (feed a new array instead, or call
+`Session.invalidate_feeds()`).  The caches are LRU-bounded by bytes (host: DG_FEED_CACHE_HOST_MB,
+default 8 GiB; device graphs + plans: DG_FEED_CACHE_DEVICE_MB, default 64 GiB of the 288 GB),
+so a driver that re-masks graphs every step (the active learners) cannot grow them without
+bound.
 """
 from __future__ import annotations
 
 import contextlib
-from typing import Dict, List, Optional, Sequence, Tuple
+import os
+from collections import OrderedDict
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
+import scipy.sparse as sp
 import torch
 
 from . import kernels
 from ._lib import DG_EPI_CHUNK_RELU, DG_EPI_L2NORM
 from .engine import DeviceGraph, DeviceGroup
 from .graph import InvalidArgumentError, Node, RunContext
-from .sparse import HostCSR, as_coo_tuple, coo_to_csr, is_identity
+from .sparse import HostCSR, SparseTensorValue, as_coo_tuple, coo_to_csr, is_identity
 
 _scope: List[str] = []
 
@@ -55,33 +63,138 @@ def as_device_f32(x) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------- sparse feeds → device
+class ByteLRU:
+    """An LRU map bounded by the bytes of its entries.  Inserting past the cap evicts the
+    least recently used entries (never the one just inserted); `on_evict(key, value)` runs
+    for each evicted entry."""
+
+    def __init__(self, cap_bytes: int, on_evict=None):
+        self.cap = int(cap_bytes)
+        self.on_evict = on_evict
+        self._d: "OrderedDict[Any, Tuple[Any, int]]" = OrderedDict()
+        self.bytes = 0
+
+    def __len__(self) -> int:
+        return len(self._d)
+
+    def __contains__(self, key) -> bool:
+        return key in self._d
+
+    def get(self, key):
+        hit = self._d.get(key)
+        if hit is None:
+            return None
+        self._d.move_to_end(key)
+        return hit[0]
+
+    def put(self, key, value, nbytes: int) -> None:
+        if key in self._d:
+            self.bytes -= self._d.pop(key)[1]
+        self._d[key] = (value, int(nbytes))
+        self.bytes += int(nbytes)
+        while self.bytes > self.cap and len(self._d) > 1:
+            k, (v, nb) = self._d.popitem(last=False)
+            self.bytes -= nb
+            if self.on_evict is not None:
+                self.on_evict(k, v)
+
+    def pop(self, key) -> None:
+        hit = self._d.pop(key, None)
+        if hit is not None:
+            self.bytes -= hit[1]
+
+    def keys(self):
+        return list(self._d.keys())
+
+
+HOST_CACHE_BYTES = int(os.environ.get("DG_FEED_CACHE_HOST_MB", "8192")) << 20
+DEVICE_CACHE_BYTES = int(os.environ.get("DG_FEED_CACHE_DEVICE_MB", "65536")) << 20
+
+
+def _lru(ctx: RunContext, name: str) -> ByteLRU:
+    caches = ctx.session.caches
+    if name not in caches:
+        if name == "dgraph":  # evicting a device graph also evicts the plans built on it
+            def drop_plans(key, hit):
+                plans = caches.get("plans")
+                if plans is not None:
+                    for pk in plans.keys():
+                        if pk[2] == id(hit[1]):
+                            plans.pop(pk)
+            caches[name] = ByteLRU(DEVICE_CACHE_BYTES, drop_plans)
+        else:
+            caches[name] = ByteLRU(DEVICE_CACHE_BYTES if name == "plans" else HOST_CACHE_BYTES)
+    return caches[name]
+
+
+def _freeze(*objs) -> None:
+    """Mark fed numpy arrays (and a scipy matrix's arrays) read-only: they are cached by
+    identity, so an in-place change must fail instead of silently going stale."""
+    for o in objs:
+        if sp.issparse(o):
+            for a in (getattr(o, "data", None), getattr(o, "indices", None), getattr(o, "indptr", None),
+                      getattr(o, "row", None), getattr(o, "col", None)):
+                if isinstance(a, np.ndarray):
+                    a.flags.writeable = False
+        elif isinstance(o, np.ndarray):
+            o.flags.writeable = False
+
+
 def _feed_key(value) -> Tuple:
-    c, v, s = as_coo_tuple(value)
-    return (id(c), id(v), tuple(s)), (c, v, s)
+    """Identity key of a fed sparse value: its (coords, values) objects — a tuple re-built
+    each step around the same arrays still hits — or the scipy matrix / SparseTensorValue."""
+    if sp.issparse(value):
+        return ("sp", id(value)), (value,)
+    if isinstance(value, SparseTensorValue):
+        return (id(value.indices), id(value.values), tuple(int(x) for x in value.dense_shape)), \
+            (value.indices, value.values)
+    if isinstance(value, (tuple, list)) and len(value) == 3:
+        return (id(value[0]), id(value[1]), tuple(int(x) for x in value[2])), (value[0], value[1])
+    raise TypeError(f"cannot feed {type(value).__name__} to a sparse placeholder")
+
+
+def _csr_bytes(c: Optional[HostCSR]) -> int:
+    return 0 if c is None else int(c.rowptr.nbytes + c.col.nbytes + c.val.nbytes)
 
 
 def host_csr(ctx: RunContext, node: Node) -> HostCSR:
-    """CSR of a fed sparse value, cached per session by array identity."""
+    """CSR of a fed sparse value, cached per session by the identity of what was fed."""
     value = ctx.value(node)
-    key, coo = _feed_key(value)
-    cache = ctx.session.caches.setdefault("host_csr", {})
+    key, keep = _feed_key(value)
+    cache = _lru(ctx, "host_csr")
     hit = cache.get(key)
     if hit is None:
-        hit = (coo, coo_to_csr(*coo))  # keep coo referenced: ids stay valid
-        cache[key] = hit
+        csr = coo_to_csr(*as_coo_tuple(value))
+        _freeze(*keep)
+        hit = (keep, csr)  # keep the fed objects referenced: ids stay valid
+        cache.put(key, hit, _csr_bytes(csr))
     return hit[1]
 
 
 def feature_csr(ctx: RunContext, node: Node):
     """None for identity features (X·W ≡ W), else a HostCSR."""
     value = ctx.value(node)
-    key, coo = _feed_key(value)
-    cache = ctx.session.caches.setdefault("features", {})
+    key, keep = _feed_key(value)
+    cache = _lru(ctx, "features")
     hit = cache.get(key)
     if hit is None:
-        hit = (coo, None if is_identity(*coo) else coo_to_csr(*coo))
-        cache[key] = hit
+        coo = as_coo_tuple(value)
+        csr = None if is_identity(*coo) else coo_to_csr(*coo)
+        _freeze(*keep)
+        hit = (keep, csr)
+        cache.put(key, hit, _csr_bytes(csr))
     return hit[1]
+
+
+def _device_bytes(dg: DeviceGraph) -> int:
+    tot = 0
+    for g in dg.groups.values():
+        for t in (g.rowptr, g.vcol, g.val, g.rel_map):
+            if t is not None:
+                tot += t.numel() * t.element_size()
+        if g.layout is not None:
+            tot += sum(t.numel() * t.element_size() for t in (g.layout.pairs, g.layout.jm, g.layout.jmoff))
+    return tot
 
 
 def device_graph(ctx: RunContext, edge_types: Dict[Tuple[int, int], int],
@@ -91,12 +204,18 @@ def device_graph(ctx: RunContext, edge_types: Dict[Tuple[int, int], int],
     key = ("dgraph", tuple((et, tuple(id(c) for c in csrs[et])) for et in edge_types),
            None if local is None else tuple((et, tuple(v)) for et, v in local.items()), chunk,
            None if not row_block else tuple(sorted(row_block.items())))
-    cache = ctx.session.caches.setdefault("dgraph", {})
+    cache = _lru(ctx, "dgraph")
     hit = cache.get(key)
     if hit is None:
-        hit = (csrs, DeviceGraph(edge_types, csrs, ctx.session.device, local, chunk=chunk, row_block=row_block))
-        cache[key] = hit
+        dg = DeviceGraph(edge_types, csrs, ctx.session.device, local, chunk=chunk, row_block=row_block)
+        hit = (csrs, dg)  # keep the host CSRs referenced: the key's ids stay valid
+        cache.put(key, hit, _device_bytes(dg))
     return hit[1]
+
+
+def plan_cache(ctx: RunContext) -> ByteLRU:
+    """The session's ForwardPlan cache (keys: ("plan", model id, device-graph id, ...))."""
+    return _lru(ctx, "plans")
 
 
 def device_group(ctx: RunContext, nodes: Sequence[Node], chunk: Optional[int] = None) -> DeviceGroup:

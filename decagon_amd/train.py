@@ -40,8 +40,9 @@ EdgeType = Tuple[int, int]
 BETA1, BETA2, EPSILON = 0.9, 0.999, 1e-8  # tf.train.AdamOptimizer defaults
 
 
-def transpose_csr(c: HostCSR) -> HostCSR:
-    """Âᵀ in CSR (rows = Â's columns, each row's nonzeros in ascending Â-row order)."""
+def transpose_csr(c: HostCSR, with_perm: bool = False):
+    """Âᵀ in CSR (rows = Â's columns, each row's nonzeros in ascending Â-row order);
+    with_perm: also each transposed nonzero's position in Â (int32)."""
     n_r, n_c = c.shape
     lens = np.diff(c.rowptr.astype(np.int64))
     rows = np.repeat(np.arange(n_r, dtype=np.int64), lens)
@@ -50,8 +51,9 @@ def transpose_csr(c: HostCSR) -> HostCSR:
     counts = np.bincount(cols, minlength=n_c)
     rowptr = np.zeros(n_c + 1, np.int64)
     np.cumsum(counts, out=rowptr[1:])
-    return HostCSR(rowptr.astype(np.int32), rows[order].astype(np.int32), c.val[order].astype(np.float32),
-                   (n_c, n_r))
+    t = HostCSR(rowptr.astype(np.int32), rows[order].astype(np.int32), c.val[order].astype(np.float32),
+                (n_c, n_r))
+    return (t, order.astype(np.int32)) if with_perm else t
 
 
 def adam_alpha(lr: float, t: int, beta1: float = BETA1, beta2: float = BETA2) -> float:
@@ -143,11 +145,15 @@ class TrainPlan:
             specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, n[i], vcol_max=vmax))
             specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, g1, n[j], K, h1, n[i], vcol_max=vmax))
             if fj is not None:  # X_jᵀ's pattern shared by the K chunks, chunk k reading G_k
-                xt = transpose_csr(fj)
+                xt, perm = transpose_csr(fj, with_perm=True)
+                drop = None
+                if fwd.drop_state is not None:  # the forward's per-relation masks of X_j's values
+                    drop = (fwd.drop_state, drop_tag(1, fwd.et_index[et]), fwd.keep)
                 self._feat_specs.append(kernels.RelGroupSpec(
                     torch.from_numpy(xt.rowptr).to(dev), torch.from_numpy(xt.col).to(dev),
                     torch.from_numpy(xt.val).to(dev), g1, self.gW1[et], F, K, h1, n[j],
-                    vcol_max=int(xt.col.max()) if xt.nnz else -1, shared=True))
+                    vcol_max=int(xt.col.max()) if xt.nnz else -1, shared=True, drop=drop,
+                    drop_index=torch.from_numpy(perm).to(dev) if drop is not None else None))
             # dW2_k = H_kᵀ·dP_k with H_k = H1_j (or its per-relation dropout draw), the reduction
             # over the n_j rows split for long ones
             H = fwd.hdrop.get(et, fwd.hidden1[j])
@@ -161,7 +167,7 @@ class TrainPlan:
                     else None)
             gemm_h1.append(kernels.PreparedGemm(dP, (n[j] * h2, h2, 1), w2.stacks[et], (h1 * h2, 1, h2), part,
                                                 (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R, drop=drop))
-            if fwd.drop_state is not None:  # dW1 rows through layer 1's row masks
+            if fwd.drop_state is not None and fj is None:  # dW1 rows through layer 1's row masks
                 self._w1_drop.append(lambda g=self.gW1[et], tg=drop_tag(1, fwd.et_index[et]):
                                      kernels.dropout_rows(g, g, fwd.drop_state, tg, fwd.keep))
             runs[j].append((part, n_runs))

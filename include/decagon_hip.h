@@ -10,7 +10,9 @@
  *
  * Conventions (all entry points):
  *   - every pointer argument is a caller-owned DEVICE pointer unless documented as host;
- *     the library never allocates or frees caller memory and keeps no state between calls;
+ *     the library never allocates or frees caller memory; the only state it keeps between
+ *     calls is, per kernel that opts into more than 64 KB of dynamic LDS, the set of devices
+ *     on which that (idempotent) hipFuncSetAttribute has been applied — thread-safe;
  *   - launches are asynchronous on `stream` (a hipStream_t passed as void*; NULL = the
  *     null stream) and are safe to capture into a hipGraph;
  *   - the return value is DG_OK (0), a negative DG_E* code for an argument error detected
@@ -34,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (18); bumped whenever a struct layout or a signature changes. */
+/* ABI version (19); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -68,8 +70,15 @@ typedef struct dg_rel_group {
     int32_t n_chunks;
     int32_t x_rows;             /* rows of X addressable (bound on vcol); per chunk when  */
                                 /* DG_GROUP_SHARED_PATTERN is set                         */
-    int32_t flags;              /* 0, or DG_GROUP_SHARED_PATTERN (dg_spmm_groups_f32 only) */
-    int32_t reserved[2];        /* zero                                                   */
+    int32_t flags;              /* 0, or DG_GROUP_SHARED_PATTERN [| DG_GROUP_DROPOUT]      */
+                                /* (dg_spmm_groups_f32 only)                              */
+    uint32_t drop_tag;          /* DG_GROUP_DROPOUT: mask stream of the group             */
+    float drop_keep;            /* DG_GROUP_DROPOUT: keep probability in (0, 1]           */
+    int32_t drop_stride;        /* DG_GROUP_DROPOUT: mask elements per chunk (the nnz of  */
+                                /* the pattern)                                           */
+    const uint64_t* drop_state; /* DG_GROUP_DROPOUT: device {seed, step}, else NULL       */
+    const int32_t* drop_index;  /* DG_GROUP_DROPOUT: device [nnz] mask element of each    */
+                                /* nonzero, or NULL (its position)                        */
 } dg_rel_group;
 
 /* Every chunk c uses the same CSR pattern (rowptr[0..n_rows], vcol, val) over its own slab of
@@ -77,6 +86,13 @@ typedef struct dg_rel_group {
  * (layers.py:89, one X_j for every relation k) and its backward X_jᵀ·G_k, without K copies
  * of the pattern. */
 #define DG_GROUP_SHARED_PATTERN 1
+
+/* With DG_GROUP_SHARED_PATTERN: chunk c multiplies nonzero p's value by the dropout scale of
+ * mask element c*drop_stride + (drop_index ? drop_index[p] : p) of stream drop_tag (dropout.h:
+ * kept with probability drop_keep, scaled by 1/drop_keep) — dropout_sparse on the features
+ * of every relation (layers.py:23-31, :88), each relation its own draw, the backward X_jᵀ·G_k
+ * (drop_index: the transposed pattern's nonzeros mapped to the forward's) on the same masks. */
+#define DG_GROUP_DROPOUT 2
 
 int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
                        int32_t d, void* stream);

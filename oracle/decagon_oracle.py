@@ -228,18 +228,29 @@ def train_grads(edge_types, adj, feats, w1, w2, decoders, dec_params, d2: int, b
     "dec": {et: {var name: array}}} — every variable gets a gradient (zeros when the cost
     does not reach it: TF's gather/concat gradients are dense zeros, not None).
     Dropout (layers.py:87-88, :112): drop1[et] [K, n_j] scales rows of relation k's layer-1
-    operand (dropout_sparse on the identity features), drop2[et] [K, n_j, h1] the elements of
-    H1_j fed to relation k's projection (tf.nn.dropout); None = no dropout."""
+    operand (dropout_sparse on the identity features) — or, for sparse features, drop1[et]
+    [K, nnz_j] scales relation k's copy of X_j's values (dropout_sparse on the feature tuple,
+    in its nonzero order); drop2[et] [K, n_j, h1] the elements of H1_j fed to relation k's
+    projection (tf.nn.dropout); None = no dropout."""
     ets = list(edge_types)
     n_nodes = {}
     for (i, j) in ets:
         n_nodes[i] = int(adj[i, j][0][2][0])
         n_nodes[j] = int(adj[i, j][0][2][1])
+    def feat_k(j, et, k):  # relation k's (dropped-out) copy of X_j
+        c, v, sh = feats[j]
+        if drop1 is None:
+            return feats[j]
+        return c, np.asarray(v, np.float64) * np.asarray(drop1[et][k], np.float64), sh
+
     x1 = {}
     for (i, j) in ets:
-        x1[i, j] = [w if feats.get(j) is None else _features_times(feats[j], w) for w in w1[i, j]]
-        if drop1 is not None:
-            x1[i, j] = [x * drop1[i, j][k][:, None] for k, x in enumerate(x1[i, j])]
+        if feats.get(j) is None:
+            x1[i, j] = list(w1[i, j])
+            if drop1 is not None:
+                x1[i, j] = [x * drop1[i, j][k][:, None] for k, x in enumerate(x1[i, j])]
+        else:
+            x1[i, j] = [_features_times(feat_k(j, (i, j), k), w) for k, w in enumerate(w1[i, j])]
     hin = (lambda et, k, h: h * drop2[et][k]) if drop2 is not None else (lambda et, k, h: h)
     S1 = {et: np.sum([sparse_dense_matmul(a, x) for a, x in zip(adj[et], x1[et])], axis=0) for et in ets}
     pre1 = {}
@@ -307,10 +318,11 @@ def train_grads(edge_types, adj, feats, w1, w2, decoders, dec_params, d2: int, b
         gw1[i, j] = []
         for k, a in enumerate(adj[i, j]):
             dX = sparse_t_dense_matmul(a, dS1, n_nodes[j])
-            if drop1 is not None:
-                dX = dX * drop1[i, j][k][:, None]
             if feats.get(j) is not None:
-                dX = sparse_t_dense_matmul(feats[j], dX, int(feats[j][2][1]))
+                fk = feat_k(j, (i, j), k)
+                dX = sparse_t_dense_matmul(fk, dX, int(fk[2][1]))
+            elif drop1 is not None:
+                dX = dX * drop1[i, j][k][:, None]
             gw1[i, j].append(dX)
     return cost, {"w1": gw1, "w2": gw2, "dec": dec}
 

@@ -261,3 +261,65 @@ def test_stageable_respects_the_lds_budget():
     assert not engine.stageable(64, 64, 1024)                 # slabs alone overflow
     assert not engine.stageable(64, 1023, 16)                 # rows beyond the 10-bit row id
     assert not engine.stageable(8, 645, 645)                  # too few relations to pay off
+
+
+# ---------------------------------------------------------------- session state (no GPU needed)
+def test_byte_lru_evicts_oldest_by_bytes():
+    from decagon_amd.runtime import ByteLRU
+
+    gone = []
+    c = ByteLRU(100, on_evict=lambda k, v: gone.append(k))
+    c.put("a", 1, 40)
+    c.put("b", 2, 40)
+    assert c.get("a") == 1          # a is now the most recent
+    c.put("c", 3, 40)               # over the cap: b (least recent) goes
+    assert gone == ["b"] and "a" in c and "c" in c and c.bytes == 80
+    c.put("huge", 4, 500)           # the entry just inserted is never evicted
+    assert "huge" in c and len(c) == 1 and gone == ["b", "a", "c"]
+
+
+def test_feed_keys_follow_the_fed_objects_and_freeze_them():
+    from decagon_amd.runtime import _feed_key, _freeze
+
+    coords = np.array([[0, 1], [1, 0]])
+    vals = np.array([1.0, 2.0])
+    k1, keep = _feed_key((coords, vals, (2, 2)))
+    k2, _ = _feed_key([coords, vals, [2, 2]])      # a tuple re-built around the same arrays
+    assert k1 == k2
+    m = sp.csr_matrix(np.eye(3))
+    assert _feed_key(m)[0] == _feed_key(m)[0] != _feed_key(sp.csr_matrix(np.eye(3)))[0]
+    _freeze(*keep, m)
+    with pytest.raises(ValueError):
+        vals[0] = 5.0                               # cached by identity: must not change silently
+    with pytest.raises(ValueError):
+        m.data[0] = 2.0
+
+
+def test_global_variables_initializer_redraws_in_place():
+    """tf.global_variables_initializer (main.py:286): every variable re-drawn from its
+    initializer into the same buffer; with the same seed the draws repeat construction's."""
+    import decagon_amd as dg
+    from decagon_amd import graph
+
+    et = {(0, 0): 2, (0, 1): 1, (1, 0): 1, (1, 1): 3}
+    dec = {(0, 0): "bilinear", (0, 1): "bilinear", (1, 0): "bilinear", (1, 1): "dedicom"}
+    dg.set_random_seed(42)
+    model = dg.DecagonModel(dg.construct_placeholders(et), {0: 30, 1: 20}, {0: 30, 1: 20}, et, dec)
+    vs = graph.global_variables()
+    mine = [v for v in vs if any(v is x for lay in list(model.layers1.values()) + list(model.layers2.values())
+                                 + list(model.edge_type2decoder.values()) for x in lay.vars.values())]
+    before = {id(v): (v.tensor.data_ptr(), v.eval().copy()) for v in mine}
+    reset = []
+
+    class _S:
+        def reset_optimizer_slots(self):
+            reset.append(1)
+
+    class _Ctx:
+        session = _S()
+
+    dg.set_random_seed(7)
+    dg.global_variables_initializer()._fn(_Ctx())
+    changed = [not np.array_equal(before[id(v)][1], v.eval()) for v in mine]
+    assert all(v.tensor.data_ptr() == before[id(v)][0] for v in mine)   # in place
+    assert sum(changed) == len(mine) and reset == [1]

@@ -30,9 +30,12 @@ def _inputs(z, b=3):
     return edge_types, decoders, adj, w1, w2, dec, z[f"batch{b}_edges"], z[f"batch{b}_neg"], e, rt, ct
 
 
-def _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, margin, drop1=None, drop2=None):
+def _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, margin, drop1=None, drop2=None,
+                feats=None):
     """The same cost with torch autograd (float64, dense adjacencies; optional dropout masks
-    applied as layers.py:87-88 / :112 do)."""
+    applied as layers.py:87-88 / :112 do; feats[j]: sparse features, whose values drop1
+    masks per relation)."""
+    feats = feats or {}
     T = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, requires_grad=True)  # noqa: E731
     tw1 = {et: [T(w) for w in ws] for et, ws in w1.items()}
     tw2 = {et: [T(w) for w in ws] for et, ws in w2.items()}
@@ -54,9 +57,17 @@ def _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, m
         else (lambda et, k: 1.0)
     D2 = (lambda et, k: torch.as_tensor(drop2[et][k], dtype=torch.float64)) if drop2 is not None \
         else (lambda et, k: 1.0)
+    def x1(et, k, w):
+        f = feats.get(et[1])
+        if f is None:
+            return D1(et, k) * w
+        c, v, sh = f
+        v = np.asarray(v, np.float64) * (1.0 if drop1 is None else np.asarray(drop1[et][k], np.float64))
+        return dense((c, v, sh)) @ w
+
     pre1 = {}
     for (i, j) in edge_types:
-        s = sum(a @ (D1((i, j), k) * w) for k, (a, w) in enumerate(zip(A[i, j], tw1[i, j])))
+        s = sum(a @ x1((i, j), k, w) for k, (a, w) in enumerate(zip(A[i, j], tw1[i, j])))
         pre1[i] = pre1.get(i, 0) + l2n(s)
     h1 = {i: torch.relu(v) for i, v in pre1.items()}
     E = {}
@@ -174,3 +185,36 @@ def test_apk_restatement_matches_reference():
         actual = list(range(n // 3))
         predicted = [i for _, i in sorted(zip(scores.tolist(), range(n)), reverse=True, key=lambda t: t[0])]
         assert orc.apk(actual, predicted, k) == mod.apk(actual, predicted, k)
+
+
+@pytest.mark.parametrize("dropout", [False, True])
+def test_oracle_grads_with_sparse_feature_dropout_match_autograd(golden_S, dropout):
+    """dropout_sparse on sparse drug features (layers.py:23-31, :88): relation k's own mask
+    over X_j's values (oracle drop1[et] [K, nnz]) — forward and every gradient against
+    autograd of the masked dense product."""
+    edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct = _inputs(golden_S, 3)
+    rng = np.random.default_rng(9)
+    F = 37
+    m = (rng.random((400, F)) < 0.15) * rng.uniform(0.2, 1.0, (400, F))
+    r, c = np.nonzero(m)
+    feat = (np.stack([r, c], 1), m[r, c], (400, F))
+    feats = {0: None, 1: feat}
+    for et in edge_types:
+        if et[1] == 1:
+            w1[et] = [rng.uniform(-0.2, 0.2, (F, 64)) for _ in range(edge_types[et])]
+    drop1 = None
+    if dropout:
+        drop1, _ = _masks(edge_types, adj, 0.9)
+        for g, (et, K) in enumerate(edge_types.items()):
+            if et[1] == 1:
+                drop1[et] = orc.dropout_scale(20180701, 1, (1 << 16) | g, K * len(r), 0.9).reshape(K, len(r))
+    cost, g = orc.train_grads(edge_types, adj, feats, w1, w2, decoders, dec, 32, batch, neg, e, rt, ct, 0.1,
+                              drop1=drop1)
+    tcost, tw1, tw2, tdec = _torch_cost(edge_types, decoders, adj, w1, w2, dec, batch, neg, e, rt, ct, 0.1,
+                                        drop1=drop1, feats=feats)
+    assert abs(cost - float(tcost)) <= 1e-12 * max(1.0, abs(cost))
+    for et in edge_types:
+        for k in range(edge_types[et]):
+            for mine, t in ((g["w1"][et][k], tw1[et][k]), (g["w2"][et][k], tw2[et][k])):
+                want = t.grad.numpy() if t.grad is not None else np.zeros_like(mine)
+                assert np.max(np.abs(mine - want)) <= 1e-10 * max(1.0, np.max(np.abs(want)))

@@ -104,6 +104,55 @@ def test_opt_op_is_one_tf_adam_step(golden_S):
     assert float(c_end) < float(z["batch3_cost"])
 
 
+def test_initializer_in_a_second_session_redraws_and_restarts_adam(golden_S):
+    """A second Session running global_variables_initializer (GreedyActiveLearner.py:18,
+    main.py:286): every variable re-drawn (not the trained values), and the next opt_op is
+    TF-Adam step t = 1 (fresh m / v / beta powers) on the device's own gradients."""
+    z = golden_S
+    dg, ph, model, opt, feed = _setup(z)
+    f, e, rt, ct = _batch_feed(z, ph, opt, feed, 3)
+    sess = dg.Session()
+    for _ in range(3):
+        sess.run(opt.opt_op, feed_dict=f)
+    params = [v for v in model.vars.values()]
+    trained = [p.eval() for p in params]
+    sess2 = dg.Session()
+    sess2.run(dg.global_variables_initializer())
+    fresh = [p.eval() for p in params]
+    assert all(not np.array_equal(a, b) for a, b in zip(trained, fresh) if a.size > 1)
+    for q in (sess, sess2):  # the same in the first session: its Adam restarts as well
+        if q is sess:
+            sess.run(dg.global_variables_initializer())
+        gv = q.run(opt.grads_vars, feed_dict=f)
+        before = [p.eval() for p in params]
+        q.run(opt.opt_op, feed_dict=f)
+        for (g, _), p0, prm in zip(gv, before, params):
+            pw, _, _ = orc.adam_tf(p0, g, np.zeros_like(p0), np.zeros_like(p0), 1)
+            assert np.max(np.abs(prm.eval() - pw)) <= 1e-6 * max(1.0, np.max(np.abs(pw))), prm.name
+
+
+def test_feed_cache_is_bounded_and_fed_arrays_read_only(golden_S, monkeypatch):
+    """Re-masked graphs fed every run (new arrays each time) stay within the device cache
+    cap (LRU by bytes; plans built on an evicted graph go with it), and a cached fed array
+    refuses in-place changes."""
+    from decagon_amd import runtime
+
+    z = golden_S
+    dg, ph, model, opt, feed = _setup(z)
+    monkeypatch.setattr(runtime, "DEVICE_CACHE_BYTES", 3 << 20)  # ~2 graphs of config S
+    sess = dg.Session()
+    key = ph["adj_mats_1,1,0"]
+    c, v, s = feed[key]
+    for it in range(6):
+        f = dict(feed)
+        f[key] = (c.copy(), v.copy() * (1.0 + 0.01 * it), s)   # a new graph each run
+        sess.run(model.embeddings[1], feed_dict=f)
+        assert len(sess.caches["dgraph"]) <= 3 and sess.caches["dgraph"].bytes <= (3 << 20) + (2 << 20)
+        assert len(sess.caches["plans"]) <= len(sess.caches["dgraph"])
+    with pytest.raises(ValueError):
+        f[key][1][0] = 0.5
+
+
 def test_adam_kernel_matches_tf_restatement():
     from decagon_amd import kernels, train
 
@@ -283,6 +332,67 @@ def test_spmm_lds_shared_operand(d):
         ref = dense.T @ X.astype(np.float64)
         assert rel_err(outs[0][k].cpu().numpy(), ref) <= 1e-5
     assert rel_err(outs[0].cpu().numpy(), outs[1].cpu().numpy()) <= 1e-6
+
+
+def _lds_case(rng, K, n_rows, n_x, per_row=2, long_row=True):
+    """K relations' transposed CSR (n_rows × n_x) merged one chunk per relation over a
+    shared operand of n_x rows (the Âᵀ·dS form), with an empty row and a long row."""
+    from decagon_amd.sparse import coo_to_csr, merge_chunks
+
+    rels = []
+    for k in range(K):
+        nnz = per_row * n_rows
+        r, c = rng.integers(0, n_rows, nnz), rng.integers(0, n_x, nnz)
+        r[r == 5] = 6  # an empty row
+        if long_row:
+            r[:300] = 11  # a long row (> 4 batches of 64 for its lanes)
+        keys = np.unique(r.astype(np.int64) * n_x + c)
+        co = np.stack([keys // n_x, keys % n_x], 1)
+        rels.append(coo_to_csr(co, rng.standard_normal(len(keys)), (n_rows, n_x)))
+    return rels, merge_chunks(rels, [0] * K, 1, 1)
+
+
+@pytest.mark.parametrize("cases,d", [
+    ([(64, 30000)], 32),                 # ≈1.9 M items: 64 items per wave
+    ([(64, 60000)], 36),                 # ≈3.8 M items: 128 per wave (rp2 at 128), partial d slice
+    ([(4, 500), (64, 30000)], 64),       # two groups in one launch: block_begin dispatch, persist > 1
+])
+def test_spmm_lds_per_wave_and_groups(cases, d):
+    """dg_spmm_groups_lds_f32 at the items-per-wave settings config P's training hits (64 /
+    128, the 64-item boundary), several groups per launch and a partial column slice (d = 36)
+    — against float64 Âᵀ·X per relation and the gather kernel (dg_spmm_groups_f32)."""
+    import scipy.sparse as sps
+
+    from decagon_amd import kernels
+
+    dev = _dev()
+    rng = np.random.default_rng(sum(k * n for k, n in cases) + d)
+    n_x = 1000
+    T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    groups = []
+    for K, n_rows in cases:
+        rels, m = _lds_case(rng, K, n_rows, n_x)
+        X = rng.standard_normal((n_x, d)).astype(np.float32)
+        groups.append((rels, m, X, K, n_rows))
+    outs = {}
+    for lds in (True, False):
+        specs, bufs = [], []
+        for rels, m, X, K, n_rows in groups:
+            out = torch.full((K, n_rows, d), float("nan"), device=dev)
+            specs.append(kernels.RelGroupSpec(T(m.rowptr), T(m.vcol), T(m.val), T(X), out, n_rows, K, d, n_x,
+                                              vcol_max=int(m.vcol.max())))
+            bufs.append(out)
+        kernels.PreparedSpmm(specs, d, lds=lds)()
+        torch.cuda.synchronize()
+        outs[lds] = [b.cpu().numpy() for b in bufs]
+    for gi, (rels, m, X, K, n_rows) in enumerate(groups):
+        got = outs[True][gi]
+        assert np.array_equal(got, outs[False][gi]) or rel_err(got, outs[False][gi]) <= 1e-6
+        for k in (0, K // 2, K - 1):
+            rel = rels[k]
+            a = sps.csr_matrix((rel.val.astype(np.float64), rel.col, rel.rowptr), shape=rel.shape)
+            assert rel_err(got[k], a @ X.astype(np.float64)) <= 1e-5, (gi, k)
+        assert not np.isnan(got).any()
 
 
 def test_dropout_masks_match_restatement():
