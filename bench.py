@@ -83,6 +83,8 @@ def parse(argv=None):
                     help="config P: time each rank's share of an N-GPU sharded step on this one GPU, "
                          "collectives replaced by no-ops (prints per-rank step times and the bytes each "
                          "collective would move)")
+    ap.add_argument("--simulate-rank", type=int, default=-1,
+                    help="--simulate-world: time only this rank (default: every rank)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                     "gloo only to exercise the multi-rank path on a single-GPU box)")
     return ap.parse_args(argv)
@@ -556,7 +558,7 @@ def main_simulate(args):
     stream = torch.cuda.Stream(device)
     G = steps_per_graph(args.steps, args.graph_steps)
     ranks = []
-    for r in range(N):
+    for r in (range(N) if args.simulate_rank < 0 else [args.simulate_rank]):
         shard = RelationShard.polypharmacy(graph, r, N, comm=False)
         plan, dg = make_plan(args, graph, shard, device)
         dec = Decoder(graph, plan, device, r)

@@ -330,8 +330,11 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
         k.out_chunk = s.out_chunk < s.n_rels ? s.out_chunk : s.n_rels;
         k.n_out_chunks = dg::ceil_div(s.n_rels, k.out_chunk);
         k.n_slices = dg::ceil_div(d, 16);
-        const int64_t items = (int64_t)k.n_out_chunks * k.n_slices;
-        k.n_blocks = static_cast<int32_t>(8 * ((items + 7) / 8));
+        // XCD-aligned at chunk granularity: XCD x takes chunks [x·cpx, (x+1)·cpx) with all their
+        // slices, so a chunk's pairs are read into one L2 (the kernel's item map is
+        // (lb & 7)·per + (lb >> 3), per = n_blocks / 8 = cpx·n_slices)
+        const int64_t cpx = (k.n_out_chunks + 7) / 8;
+        k.n_blocks = static_cast<int32_t>(8 * cpx * k.n_slices);
         k.block_begin = static_cast<int32_t>(blocks);
         blocks += k.n_blocks;
         max_cols = s.n_cols > max_cols ? s.n_cols : max_cols;

@@ -55,7 +55,7 @@ def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
             and kernels.staged_lds_bytes(n_rows, n_cols) <= kernels.STAGED_LDS_BYTES)
 
 
-STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "512"))  # ~2 rounds on 256 CUs
+STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "256"))  # one round: a workgroup per CU
 
 # Large groups whose relations fit one chunk (PPI: 2 x 19,085^2) are laid out in column
 # windows (sparse.merge_windows): each window's gathers stay in its XCDs' L2.  Measured on
@@ -67,6 +67,7 @@ N_WINDOWS = int(os.environ.get("DG_WINDOWS", "2"))
 # ones run partial mode + epilogue (one wave per row keeps more gathers in flight)
 FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
 CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "1") != "0"
+STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 
 
 def staged_out_chunk(grp, d: int) -> int:
@@ -80,20 +81,66 @@ def staged_out_chunk(grp, d: int) -> int:
     return min(oc, 64)
 
 
-def snake_bins(costs: Sequence[float], bin_size: int) -> np.ndarray:
+# a staged relation's cost in "nonzeros": its nonzeros plus the per-relation overhead (slab
+# copy, tables, barrier) of the staged kernel
+STAGED_REL_OVERHEAD = 1500
+
+
+def snake_bins(costs: Sequence[float], bin_size: int, max_swaps: int = 4000) -> np.ndarray:
     """An order of the items in which every run of `bin_size` consecutive items has about
-    the same total cost: sort by cost, deal in snake order to ceil(n/bin_size) bins."""
+    the same total cost (a staged launch's output chunk is one or more such runs).  The
+    relation sizes are Zipf-skewed (P: 7.5 k - 58 k nonzeros), so dealing in snake order
+    leaves the bin with the largest relation 10-50 % over the mean, and that bin's workgroup
+    sets the launch time.  Here: rounds of n_bins items (largest first), each round's items
+    to the bins in increasing load order; then pairwise swaps between the heaviest bin and
+    any other that lower the heaviest load, until none does (deterministic).  Bins are
+    emitted heaviest-with-lightest so that runs of two bins balance as well."""
     n = len(costs)
     n_bins = max(1, -(-n // bin_size))
-    order = np.argsort(-np.asarray(costs, np.float64), kind="stable")
-    bins: List[List[int]] = [[] for _ in range(n_bins)]
-    for pos, item in enumerate(order):
-        rnd, k = divmod(pos, n_bins)
-        b = k if rnd % 2 == 0 else n_bins - 1 - k
-        if len(bins[b]) >= bin_size:  # last round is partial: fill the first free bin
-            b = next(i for i in range(n_bins) if len(bins[i]) < bin_size)
-        bins[b].append(int(item))
-    return np.asarray([i for b in bins for i in b], np.int64)
+    c = np.asarray(costs, np.float64)
+    order = np.argsort(-c, kind="stable")
+    B = np.full((n_bins, bin_size), -1, np.int64)     # item ids per bin (-1: empty slot)
+    cap = np.full(n_bins, bin_size, np.int64)
+    cap[-1] = n - (n_bins - 1) * bin_size               # only the last bin may be short
+    fill = np.zeros(n_bins, np.int64)
+    load = np.zeros(n_bins)
+    r0 = 0
+    while r0 < n:
+        open_ = np.nonzero(fill < cap)[0]
+        items = order[r0:r0 + len(open_)]
+        tgt = open_[np.argsort(load[open_], kind="stable")[:len(items)]]
+        B[tgt, fill[tgt]] = items
+        fill[tgt] += 1
+        load[tgt] += c[items]
+        r0 += len(items)
+    cost = np.where(B >= 0, c[np.maximum(B, 0)], np.nan)
+    for _ in range(max_swaps):
+        h = int(np.argmax(load))
+        ch = cost[h]                                    # [bs]
+        d = ch[None, :, None] - cost[:, None, :]        # [bins, bs_h, bs_l]: swap h's i with l's j
+        with np.errstate(invalid="ignore"):
+            new_max = np.maximum(load[h] - d, load[:, None, None] + d)
+            gain = np.where((d > 0) & np.isfinite(d), load[h] - new_max, -np.inf)
+        gain[h] = -np.inf
+        k = int(np.argmax(gain))
+        if not gain.flat[k] > 1e-9:
+            break
+        l, i, j = np.unravel_index(k, gain.shape)
+        dd = d[l, i, j]
+        B[h, i], B[l, j] = B[l, j], B[h, i]
+        cost[h, i], cost[l, j] = cost[l, j], cost[h, i]
+        load[h] -= dd
+        load[l] += dd
+    full = n_bins - 1 if cap[-1] < bin_size else n_bins
+    by = list(np.argsort(-load[:full], kind="stable"))
+    seq = []
+    while by:
+        seq.append(by.pop(0))
+        if by:
+            seq.append(by.pop())
+    seq += list(range(full, n_bins))                     # the short bin last
+    out = [int(i) for b in seq for i in B[b] if i >= 0]
+    return np.asarray(out, np.int64)
 
 
 def choose_chunk(n_rels: int, n_rows: int, nnz: int, d: int, target_waves: int = 32768) -> int:
@@ -189,7 +236,7 @@ class DeviceGraph:
                 # one chunk per relation; output chunks of out_chunk relations with balanced
                 # nonzero counts (relation sizes are Zipf-skewed)
                 out_chunk = max(1, -(-len(loc) // STAGED_BINS))
-                perm = snake_bins([c.nnz for c in loc], out_chunk)
+                perm = snake_bins([c.nnz + STAGED_REL_OVERHEAD for c in loc], out_chunk)
                 ids = ids[perm]
                 loc = [loc[i] for i in perm]
                 ch = 1
@@ -704,12 +751,17 @@ class _Layer:
             # here; join before the chunk reduces / epilogues (graph-capturable)
             cur = torch.cuda.current_stream()
             self.side_stream.wait_stream(cur)
+            if STAGED_FIRST:  # the LDS-full staged workgroups claim their CUs first
+                for l in main:
+                    if not isinstance(l, kernels.PreparedEpilogue):
+                        l()
             with torch.cuda.stream(self.side_stream):
                 for l in side:
                     l()
-            for l in main:
-                if not isinstance(l, kernels.PreparedEpilogue):
-                    l()
+            if not STAGED_FIRST:
+                for l in main:
+                    if not isinstance(l, kernels.PreparedEpilogue):
+                        l()
             cur.wait_stream(self.side_stream)
             for l in main:
                 if isinstance(l, kernels.PreparedEpilogue):

@@ -1,5 +1,6 @@
-"""One step's kernel timeline (start/end relative to the step's first launch) from a rocprofv3
---kernel-trace directory: python3 scripts/timeline.py <dir> [first-kernel-substring]."""
+"""One step's kernel timeline (start/end relative to the end of the previous step's last
+kernel) from a rocprofv3 --kernel-trace directory:
+    python3 scripts/timeline.py <dir> [last-kernel-substring] [max kernels]"""
 import csv
 import glob
 import sys
@@ -10,7 +11,7 @@ rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
 i0 = idx[len(idx) // 2]
 t0 = int(rows[i0]["End_Timestamp"])
-for r in rows[i0 + 1:i0 + 16]:
+for r in rows[i0 + 1:i0 + int(sys.argv[3] if len(sys.argv) > 3 else 16)]:
     n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:34]
     s = (int(r["Start_Timestamp"]) - t0) / 1e3
     e = (int(r["End_Timestamp"]) - t0) / 1e3
