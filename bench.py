@@ -247,7 +247,8 @@ def pmc_traffic(config, launch, d, layer=1):
     (profiles/rNN_traffic.json, written by scripts/prof_summary.py from rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE runs of this bench): FETCH_SIZE × 2 (gfx950 counts half of a
     wide streaming read, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, KiB → bytes.  A kernel
-    launched by both layers is split by grid size (layer 1 has the larger grid).  Returns
+    launched by both layers is split by launch class (grid / workgroup / LDS bytes; layer 1,
+    at d = 64, is the class with the larger fetch).  Returns
     (bytes or None, source, the profiled launch's mean duration in ms)."""
     files = sorted(ROOT.glob("profiles/r*_traffic.json"))
     if not files:
@@ -260,12 +261,17 @@ def pmc_traffic(config, launch, d, layer=1):
     if not hit:
         return None, src, None
     e = hit[0]
+    us = e.get("avg_us", 0.0)
     if e.get("by_grid") and len(e["by_grid"]) > 1:
-        grids = sorted(e["by_grid"], key=int)
-        e = e["by_grid"][grids[-1] if layer == 1 else grids[0]]
+        # launch classes (grid/workgroup/LDS): layer 1 (d = 64) fetches the most bytes
+        keys = sorted(e["by_grid"], key=lambda c: e["by_grid"][c].get("fetch_size_kib", 0.0))
+        key = keys[-1] if layer == 1 else keys[0]
+        cls = (e.get("by_launch") or {}).get(key) or {}
+        # the kernel-trace mean of that class's launches that ran alone (as bench.py times it)
+        us = cls.get("alone_avg_us") or cls.get("overlapped_avg_us") or us
+        e = e["by_grid"][key]
     if "fetch_size_kib" not in e or "write_size_kib" not in e:
         return None, src, None
-    us = e.get("avg_us", hit[0].get("avg_us", 0.0))
     return (2.0 * e["fetch_size_kib"] + e["write_size_kib"]) * 1024.0, src, us * 1e-3
 
 

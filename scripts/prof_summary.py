@@ -32,10 +32,55 @@ def pmc(d, by_grid=False):
         return acc
     for r in csv.DictReader(open(f[0])):
         key = (short(r["Kernel_Name"]), r["Counter_Name"])
-        if by_grid:
-            key = key + (int(r.get("Grid_Size", 0) or 0),)
+        if by_grid:  # grid / workgroup / LDS bytes: the two layers differ in at least one
+            key = key + ("%s/%s/%s" % (r.get("Grid_Size", 0) or 0, r.get("Workgroup_Size", 0) or 0,
+                                       r.get("LDS_Block_Size", 0) or 0),)
         acc[key].append(float(r["Counter_Value"]))
     return acc
+
+
+def launches(d):
+    """Per-launch rows of a --kernel-trace directory, keyed by (kernel, grid, workgroup, LDS
+    bytes) — the two layers launch one kernel with different grids or LDS sizes — each split
+    into launches that ran alone and launches that overlapped another kernel (config P runs
+    the staged and the protein-row launches concurrently; bench.py times each layer-1 launch
+    alone, so the "alone" mean is the number its roofline uses)."""
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not f:
+        return {}
+    rows = []
+    for r in csv.DictReader(open(f[0])):
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
+                     int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0),
+                     int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 0)) or 0),
+                     int(r.get("LDS_Block_Size", 0) or 0)))
+    rows.sort()
+    out = {}
+    end_max = 0  # latest end among earlier-starting launches
+    for i, (s, e, k, g, w, lds) in enumerate(rows):
+        overl = end_max > s or (i + 1 < len(rows) and rows[i + 1][0] < e)
+        end_max = max(end_max, e)
+        rec = out.setdefault((k, g, w, lds), {"alone": [], "overlapped": []})
+        rec["overlapped" if overl else "alone"].append((e - s) / 1e3)
+    return out
+
+
+def launch_table(d, top=12):
+    """Markdown table: per (kernel, grid, workgroup, LDS) launch class, mean µs alone / overlapped."""
+    ls = launches(d)
+    if not ls:
+        return
+    tot = {key: sum(v["alone"]) + sum(v["overlapped"]) for key, v in ls.items()}
+    print("Per launch class (from the kernel trace; alone = no other kernel overlapped it):\n")
+    print("| kernel | grid | wg | LDS B | alone: n, mean us | overlapped: n, mean us |")
+    print("|---|---|---|---|---|---|")
+    for key in sorted(tot, key=lambda x: -tot[x])[:top]:
+        k, g, w, lds = key
+        v = ls[key]
+        a = f"{len(v['alone'])}, {sum(v['alone']) / len(v['alone']):.2f}" if v["alone"] else "0, -"
+        o = f"{len(v['overlapped'])}, {sum(v['overlapped']) / len(v['overlapped']):.2f}" if v["overlapped"] else "0, -"
+        print(f"| `{k}` | {g} | {w} | {lds} | {a} | {o} |")
+    print()
 
 
 def traffic_json(root, out):
@@ -54,6 +99,11 @@ def traffic_json(root, out):
             kern.setdefault(k, {}).setdefault("by_grid", {}).setdefault(str(gsz), {})[c.lower() + "_kib"] = sum(v) / len(v)
         for r in stats(os.path.join(root, f"{cfg}_trace")):
             kern.setdefault(short(r["Name"]), {})["avg_us"] = float(r["AverageNs"]) / 1e3
+        for (k, g, w, lds), v in launches(os.path.join(root, f"{cfg}_trace")).items():
+            kern.setdefault(k, {}).setdefault("by_launch", {})[f"{g}/{w}/{lds}"] = {
+                "alone_n": len(v["alone"]), "overlapped_n": len(v["overlapped"]),
+                "alone_avg_us": sum(v["alone"]) / len(v["alone"]) if v["alone"] else None,
+                "overlapped_avg_us": sum(v["overlapped"]) / len(v["overlapped"]) if v["overlapped"] else None}
         rec[cfg] = kern
     json.dump(rec, open(out, "w"), indent=1, sort_keys=True)
 
@@ -82,6 +132,7 @@ def main(root):
                 print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | "
                       f"{float(r['Percentage']):.1f} |")
             print()
+            launch_table(os.path.join(root, f"{cfg}_trace"))
             continue
         bj = os.path.join(root, f"{cfg}_bench.json")
         if os.path.exists(bj):
@@ -114,7 +165,28 @@ def main(root):
             ws = f"{sum(w)/len(w):.1f}" if w else "-"
             print(f"| `{k}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | {fs} | {ws} |")
         print()
+        launch_table(os.path.join(root, f"{cfg}_trace"))
+    lds_table(root)
     config_d(root)
+
+
+def lds_table(root):
+    """Config P: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE per launch class of the LDS kernels."""
+    c = pmc(os.path.join(root, "P_LDS"), by_grid=True)
+    if not c:
+        return
+    print("## config P: LDS bank conflicts (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE)\n")
+    print("| kernel | grid/wg/LDS | launches | conflict cycles | LDS active cycles | ratio |")
+    print("|---|---|---|---|---|---|")
+    for (k, ctr, cls), v in sorted(c.items()):
+        if ctr != "SQ_LDS_BANK_CONFLICT":
+            continue
+        act = c.get((k, "SQ_LDS_IDX_ACTIVE", cls), [])
+        if not act or sum(act) == 0:
+            continue
+        print(f"| `{k}` | {cls} | {len(v)} | {sum(v) / len(v):.4g} | {sum(act) / len(act):.4g} | "
+              f"{sum(v) / sum(act):.3f} |")
+    print()
 
 
 def config_d(root):

@@ -8,7 +8,7 @@ out=gpurun_out/prof_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for cfg in S P; do
-  if [ $cfg = S ]; then steps="--steps 200 --warmup 20 --kernel-reps 200"; else steps="--steps 20 --warmup 3 --kernel-reps 20"; fi
+  if [ $cfg = S ]; then steps="--steps 200 --warmup 20 --kernel-reps 200 --no-extra"; else steps="--steps 20 --warmup 3 --kernel-reps 20"; fi
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${cfg}_trace -o run -- \
     python3 bench.py --config $cfg $steps --no-cpu-baseline > $out/${cfg}_bench.json 2> $out/${cfg}_trace.log
   echo "$cfg trace done"
@@ -19,6 +19,12 @@ for cfg in S P; do
     echo "$cfg $ctr done"
   done
 done
+# the staged kernel's LDS bank-conflict ratio (config P, both layers; one pass, SQ block only)
+timeout -k 10 400 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS --kernel-trace \
+  --output-format csv -d $out/P_LDS -o run -- \
+  python3 bench.py --config P --no-graph --steps 5 --warmup 1 --kernel-reps 3 --no-cpu-baseline \
+  > /dev/null 2> $out/P_LDS.log
+echo "P LDS done"
 for cfg in S P; do
   if [ $cfg = S ]; then steps="--steps 100 --warmup 10"; else steps="--steps 5 --warmup 1 --graph-steps 1"; fi
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/train${cfg}_trace -o run -- \
