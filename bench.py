@@ -102,11 +102,24 @@ def glorot_stack(rng, k, d_in, d_out):
     return rng.uniform(-r, r, size=(k, d_in, d_out)).astype(np.float32)
 
 
-def build_workload(config, rank, world, sharded):
-    from decagon_amd import synthetic
-    from decagon_amd.sharding import RelationShard, torch_allreduce
+def collectives(backend):
+    """(allreduce, allgather) of the sharded step: RCCL called directly on the capturing
+    stream (decagon_amd/rccl.py) for backend nccl, torch.distributed's otherwise (gloo)."""
+    from decagon_amd.sharding import torch_allgather, torch_allreduce
 
-    allreduce = torch_allreduce() if sharded else None
+    if backend == "nccl":
+        from decagon_amd.rccl import world_comm
+
+        return world_comm().collectives()
+    return torch_allreduce(), torch_allgather()
+
+
+def build_workload(config, rank, world, sharded, backend="nccl"):
+    from decagon_amd import synthetic
+    from decagon_amd.sharding import RelationShard
+
+    coll = collectives(backend) if sharded else None
+    allreduce = coll[0] if sharded else None
     if config == "S":
         base = synthetic.load_S()
         graph = synthetic.replicate_sets(base, world) if world > 1 else base
@@ -118,7 +131,7 @@ def build_workload(config, rank, world, sharded):
         graph = synthetic.make_P(seed=0)
         shard = None
         if sharded:
-            shard = RelationShard.polypharmacy(graph, rank, world)
+            shard = RelationShard.polypharmacy(graph, rank, world, collectives=coll)
         scaling = "strong"
         workload = ("P: polypharmacy-shaped 19,085 proteins + 645 drugs, 964 side effects "
                     "(1,932 drug-drug matrices), 2 GCN layers d=64/32 + DEDICOM decoder B=512+512")
@@ -186,7 +199,7 @@ def time_kernel(fn, reps, stream):
         fn()
         stream.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=stream):
+        with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
             for _ in range(reps):
                 fn()
         g.replay()
@@ -217,7 +230,7 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
         run = step
         if use_graph:
             cg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(cg, stream=stream):
+            with torch.cuda.graph(cg, stream=stream, capture_error_mode="thread_local"):
                 for _ in range(G):
                     step()
             cg.replay()
@@ -292,7 +305,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
     kernel's roofline, the whole layer-1 SpMM.  Returns (record fields, graph)."""
     import torch
 
-    graph, shard, scaling, workload = build_workload(config, rank, world, sharded)
+    graph, shard, scaling, workload = build_workload(config, rank, world, sharded, args.backend)
     plan, dg = make_plan(args, graph, shard, device)
     dec = Decoder(graph, plan, device, rank)
 
@@ -335,7 +348,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
                     body()
                     stream.synchronize()
                     gph = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gph, stream=stream):
+                    with torch.cuda.graph(gph, stream=stream, capture_error_mode="thread_local"):
                         body()
                     seq.append(gph.replay)
 
@@ -414,7 +427,7 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
 
     from decagon_amd import kernels, synthetic
     from decagon_amd.scorer import SlotScorer
-    from decagon_amd.sharding import slot_range, torch_allreduce
+    from decagon_amd.sharding import slot_range
 
     c5 = synthetic.make_config5()
     bf = torch.bfloat16
@@ -423,7 +436,8 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
     slots, B, d = Dk.shape[0], c5.batch, E.shape[1]
     s0, s1 = slot_range(slots, rank, world)
     sc = SlotScorer(E, E, R, Dk, up(c5.pos_rows), up(c5.pos_cols), kernels.upload_alias(c5.degrees, device), B,
-                    MARGIN, seed=11, slots=(s0, s1), allreduce=torch_allreduce() if world > 1 else None)
+                    MARGIN, seed=11, slots=(s0, s1),
+                    allreduce=collectives(args.backend)[0] if world > 1 else None)
     stream = torch.cuda.Stream(device)
     G = steps_per_graph(steps, args.graph_steps)
     el = timed_steps(sc, steps, warmup, G, stream, not args.no_graph,
@@ -653,6 +667,10 @@ def main():
         print(json.dumps(out), file=JSON_OUT, flush=True)
     if sharded:
         dist.barrier()
+        from decagon_amd import rccl
+
+        if rccl._COMM is not None:
+            rccl._COMM.destroy()
         dist.destroy_process_group()
 
 

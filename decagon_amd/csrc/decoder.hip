@@ -44,6 +44,7 @@ struct DecTab {
     int64_t ld_row;
     int64_t ld_col;
     int32_t d;
+    int32_t vec4;  // row_table, ld_row and l allow 16-byte loads
 };
 
 // Scores of 32 pairs on one wave: lane i (both halves) names pair i by its row index
@@ -63,15 +64,33 @@ __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, 
     for (int r = 0; r < 16; ++r) part[r] = 0.f;
     if (d == 32) {
         // one k-block, one n-block: every load (G, l, U row, V rows) in flight together, then
-        // the 16 MFMAs — the same k-ordered chain as the general loop below
+        // the 16 MFMAs.  MFMA s takes k = 16h + s from lane half h (the contraction order is
+        // free), so each lane's A operand is 16 contiguous floats of its U row: 4 float4 loads
         float av[16], bv[16], v[16];
+        if (!t.vec4) {
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const int kk = 2 * s + h;
-            bv[s] = t.G[kk * 32 + i];
-            const float a = valid ? u[kk] : 0.f;
-            av[s] = t.l ? a * t.l[kk] : a;
+            for (int s = 0; s < 16; ++s) {
+                const float a = valid ? u[16 * h + s] : 0.f;
+                av[s] = t.l ? a * t.l[16 * h + s] : a;
+            }
+        } else {
+            const float4* u4 = reinterpret_cast<const float4*>(u + 16 * h);
+            const float4* l4 = reinterpret_cast<const float4*>(t.l + 16 * h);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                float4 a4 = valid ? u4[s4] : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (t.l) {
+                    const float4 w4 = l4[s4];
+                    a4 = make_float4(a4.x * w4.x, a4.y * w4.y, a4.z * w4.z, a4.w * w4.w);
+                }
+                av[4 * s4] = a4.x;
+                av[4 * s4 + 1] = a4.y;
+                av[4 * s4 + 2] = a4.z;
+                av[4 * s4 + 3] = a4.w;
+            }
         }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bv[s] = t.G[(16 * h + s) * 32 + i];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int prow = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -154,10 +173,10 @@ __global__ __launch_bounds__(256) void decoder_score_kernel(const DecArgs a) {
 //   pos[b] = score(rows[b], cols[b]),  neg[b] = score(neg_row[b], cols[b]),
 //   loss   = sum_b relu(neg[b] - (pos[b] - margin))
 // One workgroup of two waves per 32 pairs (wave 0 the positive tile, wave 1 the negative
-// tile).  Each workgroup folds its 32 hinge terms, publishes the partial and takes a ticket;
-// the last one (agent-scope release / acquire, cdna_hip_programming.md Guideline 16) adds
-// every partial in block order and resets the ticket counter — fixed order, no float
-// atomics, one launch.
+// tile).  Each workgroup folds its 32 hinge terms, publishes the partial (a write-through sc1
+// store, drained) and takes a ticket; the last one reads every partial with sc1 loads
+// (cdna_hip_programming.md Guideline 16; no L2 write-back or invalidate), adds them in block
+// order and resets the ticket counter — fixed order, no float atomics, one launch.
 struct HingeArgs {
     DecTab t;
     const int32_t* rows;
@@ -177,10 +196,15 @@ struct HingeArgs {
     float margin;
 };
 
+#ifndef DG_DEC_ABL
+#define DG_DEC_ABL 0  // timing ablations only (wrong results): 1 no ticket, 2 no draw, 4 no scores, 8 empty
+#endif
+
 __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
     __shared__ float sc[2][32];
     __shared__ float red[128];
     __shared__ int last;
+    if (DG_DEC_ABL & 8) return;
     const int lane = threadIdx.x & 63;
     const int side = threadIdx.x >> 6;  // 0: positives, 1: negatives
     const int i = lane & 31;
@@ -195,12 +219,19 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
             ridx = a.rows[b];
         else if (a.neg_given)
             ridx = a.neg_given[b];
+        else if (DG_DEC_ABL & 2)
+            ridx = cidx;
         else
             ridx = unigram_draw(a.alias, a.range, a.seed, a.offset + (uint64_t)b);
         if (side == 1 && a.neg_rows_out && h == 0) a.neg_rows_out[b] = ridx;
     }
     float part[16];
-    score_tile(a.t, ridx, cidx, valid, part);
+    if (DG_DEC_ABL & 4) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) part[r] = (float)(ridx + r);
+    } else {
+        score_tile(a.t, ridx, cidx, valid, part);
+    }
     if (i == 0) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -216,21 +247,21 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
         if (lane < 32 && b0 + lane < a.n) term = fmaxf(sc[1][lane] - (sc[0][lane] - a.margin), 0.f);
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) term += __shfl_xor(term, m);
-        if (lane == 0) {
+        if (lane == 0 && (DG_DEC_ABL & 1)) {
             a.partial[blockIdx.x] = term;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            last = 0;
+        } else if (lane == 0) {
+            // hand-off without L2 write-back / invalidate (MI355X_MICROARCH.md "Valid forms",
+            // first row): the partial is stored write-through (sc1) and drained before the
+            // ticket add; the last block reads every partial with sc1 loads
+            __hip_atomic_store(a.partial + blockIdx.x, term, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t t = atomicAdd(a.ticket, 1u);
+            const uint32_t t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             last = (t == gridDim.x - 1) ? 1 : 0;
         }
     }
     __syncthreads();
     if (!last) return;  // block-uniform
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
     float s = 0.f;
     for (int k = threadIdx.x; k < (int)gridDim.x; k += 128)
         s += __hip_atomic_load(a.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -283,15 +314,13 @@ __global__ __launch_bounds__(256) void hinge_multi_kernel(const float* pos, cons
     const float s = block_sum_256(cnt, [&](int q) {
         return fmaxf(neg[p0 + q] - (pos[p0 + q] - margin), 0.f);
     });
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // sc1 partial, drained, then the ticket (decoder_hinge_kernel)
         __hip_atomic_store(partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;  // block-uniform
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
     const float t = block_sum_256((int)gridDim.x, [&](int b) {
         return __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     });
@@ -336,7 +365,8 @@ extern "C" int dg_decoder_score_f32(const float* row_table, int64_t ld_row, cons
     if (!row_table || !col_table || !row_idx || !col_idx || !G || !out) return DG_EINVAL;
     if (ld_row < d || ld_col < d) return DG_EINVAL;
     DecArgs a{};
-    a.t = DecTab{row_table, col_table, G, l, ld_row, ld_col, d};
+    a.t = DecTab{row_table, col_table, G, l, ld_row, ld_col, d,
+                 dg::aligned16(row_table) && (ld_row & 3) == 0 && (!l || dg::aligned16(l))};
     a.row_idx = row_idx;
     a.col_idx = col_idx;
     a.out = out;
@@ -398,7 +428,8 @@ extern "C" int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, cons
     if (!dg::aligned16(workspace)) return DG_EALIGN;
     const int blocks = dg::ceil_div(n, 32);
     HingeArgs a{};
-    a.t = DecTab{row_table, col_table, G, l, ld_row, ld_col, d};
+    a.t = DecTab{row_table, col_table, G, l, ld_row, ld_col, d,
+                 dg::aligned16(row_table) && (ld_row & 3) == 0 && (!l || dg::aligned16(l))};
     a.rows = rows;
     a.cols = cols;
     a.neg_given = neg_rows;

@@ -26,6 +26,9 @@
 #include "common.h"
 #include "dropout.h"
 
+#ifndef DG_FUSED_ABL
+#define DG_FUSED_ABL 0  // timing ablations only (wrong results): 1 no gathers, 8 empty kernels
+#endif
 #ifndef DG_PROJ_UNROLL
 #define DG_PROJ_UNROLL 16  // W loads per batch of the projection chain (measured: 8 → 16 −0.4 µs at S)
 #endif
@@ -79,7 +82,10 @@ struct SpmmArgs {
 };
 
 constexpr int kRowsPerBlock = 4;  // partial mode: 4 waves x 1 (chunk, row)
-constexpr int kUnroll = 8;        // gathers in flight per lane
+#ifndef DG_KUNROLL
+#define DG_KUNROLL 8
+#endif
+constexpr int kUnroll = DG_KUNROLL;  // gathers in flight per lane
 
 // acc = Σ_{p in [beg, end)} val[p] * X[vcol[p]][:], over every wcount-th batch of 64
 // starting at batch wpart.  Returns the folded row in every lane (lane l holds columns
@@ -133,7 +139,9 @@ __device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 const bool ok = qact && (s0 + u * G + sub) < n;
-                xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                xv[u] = ok ? ((DG_FUSED_ABL & 1) ? make_float4(1.f, 1.f, 1.f, 1.f)
+                                                 : *reinterpret_cast<const float4*>(xq + o[u]))
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
                 if (!ok) w[u] = 0.f;
             }
 #pragma unroll
@@ -174,13 +182,22 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
     if (lane < LP && lane * 4 < d) *reinterpret_cast<float4*>(g.out + slot * d + lane * 4) = acc;
 }
 
-// Fused mode (every group of a node type in one chunk): one workgroup per output row r of
-// node type i; W waves per group (i, j) share the row's nonzeros.  The waves of a group
-// meet in LDS, the group's first wave L2-normalises the group sum (layers.py:93), then
-// wave 0 adds the groups in order and applies relu (model.py:75) or not (model.py:88).
+// Fused mode (every group of a node type in one chunk): one workgroup per RPB consecutive
+// output rows of node type i; W waves per (row, group (i, j)) share the row's nonzeros.  The
+// waves of a group meet in LDS, the group's first wave L2-normalises the group sum
+// (layers.py:93), then the row's first wave adds the groups in order and applies relu
+// (model.py:75) or not (model.py:88).
 // Optional projection epilogue (layer 1 only): for every layer-2 group whose source node
 // type is i, P_k[r][:] = out[r][:] · W2_k — the next layer's H_j·W_k (layers.py:113) for
-// this row, a k-ordered fmaf chain exactly like the MFMA path — so layer 2 needs no GEMM.
+// these rows, a k-ordered fmaf chain exactly like the MFMA path — so layer 2 needs no GEMM.
+// A thread owns one (relation, column) of W2 and runs the chains of all RPB rows, so each W2
+// column is read once per RPB rows (the projection reads W2 from L2 and is bound by those
+// bytes: one row per workgroup read ≈40 KB of W2 per 256 B of output).
+#ifndef DG_FUSED_RPB
+#define DG_FUSED_RPB 1  // rows per workgroup, at most (measured at S: 4 rows 10.5 us, 2 rows 9.4, 1 row 9.0-9.2)
+#endif
+constexpr int kFusedRpb = DG_FUSED_RPB;
+
 struct FusedTargetK {
     float* out;
     int32_t n_rows;
@@ -210,14 +227,15 @@ struct FusedArgs {
     int32_t n_projs;
     int32_t d;
     int32_t wpg;  // waves per group
-    int32_t pad;
+    int32_t rpb;  // rows per workgroup (blockDim = 64 · rpb · max groups · wpg)
 };
 
 template <int LP>
 __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
     __shared__ float4 pbuf[16][LP];
-    __shared__ float4 ybuf[DG_MAX_GROUPS][LP];
-    __shared__ float hrow[4 * LP];
+    __shared__ float4 ybuf[kFusedRpb][DG_MAX_GROUPS][LP];
+    __shared__ float hrow[kFusedRpb][4 * LP];
+    if (DG_FUSED_ABL & 8) return;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int b = blockIdx.x;
@@ -225,19 +243,25 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
 #pragma unroll 1
     while (ti + 1 < a.n_targets && b >= a.t[ti + 1].block_begin) ++ti;
     const FusedTargetK& t = a.t[ti];
-    const int r = b - t.block_begin;
     const int d = a.d;
     const int W = a.wpg;
-    const int gl = wave / W;
-    const int part = wave - gl * W;
+    const int RPB = a.rpb;
+    const int wpr = (int)(blockDim.x >> 6) / RPB;  // waves per row slot
+    const int slot = wave / wpr;
+    const int wr = wave - slot * wpr;
+    const int r0 = (b - t.block_begin) * RPB;
+    const int r = r0 + slot;
+    const bool live = r < t.n_rows;  // wave-uniform; every wave still meets every barrier
+    const int gl = wr / W;
+    const int part = wr - gl * W;
     const int q = lane % LP;
-    if (gl < t.g_count) {
+    if (live && gl < t.g_count) {
         const SpmmGroupK& g = a.g[t.g_begin + gl];
         const float4 s = range_sum<LP>(g, g.x, g.rowptr[r], g.rowptr[r + 1], d, part, W);
         if (lane < LP) pbuf[wave][lane] = s;
     }
     __syncthreads();
-    if (gl < t.g_count && part == 0) {
+    if (live && gl < t.g_count && part == 0) {
         float4 s = pbuf[wave][q];
         for (int w = 1; w < W; ++w) dg::add4(s, pbuf[wave + w][q]);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); columns >= d hold zeros
@@ -245,12 +269,12 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
 #pragma unroll
         for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
         const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
-        if (lane < LP) ybuf[gl][lane] = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+        if (lane < LP) ybuf[slot][gl][lane] = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
     }
     __syncthreads();
-    if (wave == 0 && lane < LP) {
-        float4 tot = ybuf[0][lane];
-        for (int g = 1; g < t.g_count; ++g) dg::add4(tot, ybuf[g][lane]);
+    if (live && wr == 0 && lane < LP) {
+        float4 tot = ybuf[slot][0][lane];
+        for (int g = 1; g < t.g_count; ++g) dg::add4(tot, ybuf[slot][g][lane]);
         if (t.relu) {
             tot.x = fmaxf(tot.x, 0.f);
             tot.y = fmaxf(tot.y, 0.f);
@@ -258,9 +282,12 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
             tot.w = fmaxf(tot.w, 0.f);
         }
         if (lane * 4 < d) *reinterpret_cast<float4*>(t.out + (int64_t)r * d + lane * 4) = tot;
-        reinterpret_cast<float4*>(hrow)[lane] = tot;
+        reinterpret_cast<float4*>(hrow[slot])[lane] = tot;
     }
     if (a.n_projs == 0) return;  // launch-uniform
+#ifdef DG_FUSED_NOPROJ  // timing ablation only (wrong results)
+    return;
+#endif
     __syncthreads();
     // every projection output (entry, relation, column) of this target in one index space, so
     // the block's threads run a single load/fmaf chain each instead of one chain per entry
@@ -268,6 +295,7 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
 #pragma unroll 1
     for (int pi = 0; pi < a.n_projs; ++pi)
         if (a.p[pi].target == ti) total += a.p[pi].n_rels * a.p[pi].d_out;
+    const int nr = min(RPB, t.n_rows - r0);  // live rows of this workgroup
 #pragma unroll 1
     for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
         int pi = 0, rem = idx;
@@ -284,10 +312,19 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
         const int c = rem - kk * dout;
         const int rel = pj.rel_map ? pj.rel_map[kk] : kk;
         const float* __restrict__ wcol = pj.w + (int64_t)rel * d * dout + c;
-        float acc = 0.f;
+        float acc[kFusedRpb];
+#pragma unroll
+        for (int s2 = 0; s2 < kFusedRpb; ++s2) acc[s2] = 0.f;
 #pragma unroll DG_PROJ_UNROLL
-        for (int k = 0; k < d; ++k) acc = fmaf(hrow[k], wcol[(int64_t)k * dout], acc);
-        pj.out[((int64_t)rel * t.n_rows + r) * dout + c] = acc;
+        for (int k = 0; k < d; ++k) {
+            const float w = wcol[(int64_t)k * dout];
+#pragma unroll
+            for (int s2 = 0; s2 < kFusedRpb; ++s2) acc[s2] = fmaf(hrow[s2][k], w, acc[s2]);
+        }
+        float* po = pj.out + ((int64_t)rel * t.n_rows + r0) * dout + c;
+#pragma unroll
+        for (int s2 = 0; s2 < kFusedRpb; ++s2)
+            if (s2 < nr) po[(int64_t)s2 * dout] = acc[s2];
     }
 }
 
@@ -622,11 +659,17 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
         k.g_begin = s.g_begin;
         k.g_count = s.g_count;
         k.relu = (s.flags & DG_EPI_RELU) ? 1 : 0;
-        k.block_begin = static_cast<int32_t>(blocks);
-        blocks += s.n_rows;
         max_groups = s.g_count > max_groups ? s.g_count : max_groups;
     }
     if (max_groups * waves_per_group > 16) return DG_EINVAL;  // 1024 threads per workgroup
+    // rows per workgroup: as many row slots as fit 1024 threads (at most kFusedRpb)
+    int rpb = 16 / (max_groups * waves_per_group);
+    rpb = rpb < 1 ? 1 : (rpb > kFusedRpb ? kFusedRpb : rpb);
+    a.rpb = rpb;
+    for (int t = 0; t < n_targets; ++t) {
+        a.t[t].block_begin = static_cast<int32_t>(blocks);
+        blocks += dg::ceil_div(targets[t].n_rows, rpb);
+    }
     for (int i = 0; i < n_projs; ++i) {
         const dg_proj& s = projs[i];
         if (!s.w || !s.out || s.n_rels < 0 || s.d_out < 1 || s.target < 0 || s.target >= n_targets)
@@ -637,7 +680,7 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
     if (blocks > 0x7fffffff) return DG_EINVAL;
     const int lp = dg::lanes_per_row(d);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    dim3 grid(static_cast<unsigned>(blocks)), block(64 * max_groups * waves_per_group);
+    dim3 grid(static_cast<unsigned>(blocks)), block(64 * rpb * max_groups * waves_per_group);
 #define DG_LAUNCH_FUSED(L) hipLaunchKernelGGL(gcn_fused_kernel<L>, grid, block, 0, st, a)
     DG_LP_SWITCH(lp, DG_LAUNCH_FUSED)
 #undef DG_LAUNCH_FUSED

@@ -135,11 +135,18 @@ class RelationShard:
         return RelationShard(rank, world_size, local, allreduce, loads, blocks, allgather)
 
     @staticmethod
-    def polypharmacy(graph, rank: int, world_size: int, comm: bool = True) -> "RelationShard":
+    def polypharmacy(graph, rank: int, world_size: int, comm: bool = True, collectives=None) -> "RelationShard":
         """Config P's shard: proteins row-split, drug-target relations LPT on nonzeros.
-        comm=False: no collectives (a one-GPU timing rehearsal of one rank's share)."""
+        comm=False: no collectives (a one-GPU timing rehearsal of one rank's share);
+        collectives = (allreduce, allgather) to use instead of torch.distributed's (the RCCL
+        communicator of rccl.py for captured steps)."""
         nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
-        ar, ag = (torch_allreduce(), torch_allgather()) if comm else (_no_op, _no_op)
+        if not comm:
+            ar, ag = _no_op, _no_op
+        elif collectives is not None:
+            ar, ag = collectives
+        else:
+            ar, ag = torch_allreduce(), torch_allgather()
         return RelationShard.split(graph.edge_types, graph.n_nodes, nnz, rank, world_size, ar, ag)
 
     @staticmethod
