@@ -29,7 +29,7 @@
 //     relation k+1's slab slice (prefetched into registers during k-1) → the other buffer;
 //     prefetch relation k+2's; load relation k+1's tables
 //     thread i: part = Σ_{m < len[i]} val · xs[col]   (4 × ds_read_b128 + 16 fmaf per nonzero)
-//     a group's segments are summed in lane order by shuffles; its first lane does
+//     a group's segments are folded by a DPP shift tree; its first lane does
 //     acc[row] += part (one writer per row per relation)
 //   out[c][r][16s .. +16) = acc[r]
 // Fixed summation order, no atomics: bitwise reproducible.
@@ -92,6 +92,21 @@ __device__ __forceinline__ void glds16(const float* base, uint32_t voff, uint32_
 // are done; then s_barrier.
 __device__ __forceinline__ void relation_barrier() {
     asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// lane l += lane l + S of its 16-lane row (DPP row_shl:S), where S < the lane's group size
+template <int S>
+__device__ __forceinline__ void fold_step(float4 (&part)[4], int gsz) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float* v = reinterpret_cast<float*>(&part[q]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float o = __int_as_float(
+                __builtin_amdgcn_update_dpp(0, __float_as_int(v[e]), 0x100 + S, 0xF, 0xF, true));
+            if (S < gsz) v[e] += o;
+        }
+    }
 }
 
 __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedArgs a) {
@@ -169,19 +184,15 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         for (int q = 0; q < 4; ++q) u[q] = p[64 * q];
     };
     // a finished relation's sums into the accumulators: a group's segments (consecutive lanes
-    // of this wave) summed in lane order by shuffles, then its first lane adds the row
+    // of this wave) folded by a DPP shift tree, then its first lane adds the row
     auto accumulate = [&](float4 (&part)[4], int vi, int big) {
         const int seg = (vi >> 10) & 7, gsz = ((vi >> 13) & 7) + 1;
-#pragma unroll 1
-        for (int j = 1; j < big; ++j) {
-            float4 o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = dg::shfl4(part[q], min(lane + j, 63));
-            if (seg == 0 && j < gsz) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) dg::add4(part[q], o[q]);
-            }
-        }
+        // a group's gsz (1, 2, 4 or 8) segments sit on lanes from a multiple of gsz, inside one
+        // 16-lane DPP row (staged_layout): a shift-left tree (lane l += lane l + s, s < gsz)
+        // folds them into the first lane — VALU only, no LDS permute
+        if (big > 1) fold_step<1>(part, gsz);
+        if (big > 2) fold_step<2>(part, gsz);
+        if (big > 4) fold_step<4>(part, gsz);
         const int row = vi & 1023;
         if (seg == 0 && row != kDummyRow) {
             float4* ar = acc + row * 4;

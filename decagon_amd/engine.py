@@ -66,7 +66,11 @@ N_WINDOWS = int(os.environ.get("DG_WINDOWS", "2"))
 # node types with at most this many rows finish in the fused row-per-workgroup kernel; larger
 # ones run partial mode + epilogue (one wave per row keeps more gathers in flight)
 FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
-CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "1") != "0"
+# a layer's gather-bound launch beside its LDS-bound staged launch on a second stream: no gain
+# measured (config P step 494.8 us concurrent vs 496.5 sequential; the staged kernel slows by
+# what the other saves) and the fork / join cost ~10 us of idle GPU each at small per-rank
+# shares (8-GPU rehearsal), so one stream by default
+CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "0") != "0"
 STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 
 

@@ -305,23 +305,31 @@ STAGED_DUMMY_ROW = 1023  # vinfo row of a dummy (padding) lane
 STAGED_JM_SPARE = 1024   # zero ints ending jm
 
 
+def _group_sizes(lens: np.ndarray, L: int) -> np.ndarray:
+    """Segments per row for segment length at most L: a power of two (1, 2, 4 or 8), so the
+    kernel combines a group's segments by a DPP shift tree inside one 16-lane row."""
+    need = np.maximum(1, -(-lens // L))
+    return (1 << np.ceil(np.log2(need)).astype(np.int64)).astype(np.int64)
+
+
 def _segment_length(lens: np.ndarray, lanes: int) -> int:
-    """Smallest L >= ceil(max / 8) leaving sum(ceil(lens / L)) virtual rows, with room for
-    the padding lanes of wave boundaries, within `lanes`."""
+    """Smallest L >= ceil(max / 8) leaving sum(group sizes) virtual rows, with room for the
+    alignment padding of groups, within `lanes`."""
     nnz = int(lens.sum())
     L = max(1, -(-nnz // lanes), -(-int(lens.max()) // STAGED_MAX_GROUP))
     budget = lanes - (STAGED_MAX_GROUP - 1) * (-(-lanes // 64))
-    floor = int((lens > 0).sum())
-    while int((-(-lens // L)).sum()) > max(budget, floor):
+    nz = lens[lens > 0]
+    floor = len(nz)
+    while int(_group_sizes(nz, L).sum()) > max(budget, floor):
         L += 1
     return L
 
 
 def _place_groups(glen: np.ndarray, gsize: np.ndarray, lanes: int) -> List[Tuple[int, int]]:
-    """Lane order of groups: descending length, each group inside one 64-lane wave.  Returns
-    [(group index, or -1 for a dummy lane, length)] in lane order — a dummy pads a wave's tail
-    where the next group (of the same length) does not fit and no single of that length is
-    left to fill it."""
+    """Lane order of groups: descending length, each group of size S (a power of two)
+    starting at a lane that is a multiple of S — so it sits inside one 64-lane wave and one
+    16-lane DPP row.  Returns [(group index, or -1 for a dummy lane, length)] in lane order — a
+    dummy pads up to the next aligned lane where no single of that length is left to do so."""
     order = np.lexsort((-gsize, -glen))     # by length desc, then bigger groups first
     out: List[Tuple[int, int]] = []
     pos, i, n = 0, 0, len(order)
@@ -333,7 +341,7 @@ def _place_groups(glen: np.ndarray, gsize: np.ndarray, lanes: int) -> List[Tuple
         multi = [int(g) for g in order[i:j] if gsize[g] > 1]
         single = [int(g) for g in order[i:j] if gsize[g] == 1]
         for g in multi:
-            while int(gsize[g]) > 64 - pos % 64:
+            while pos % int(gsize[g]):
                 out.append((single.pop() if single else -1, ln))
                 pos += 1
             out.append((g, ln))
@@ -370,8 +378,8 @@ def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
             raise ValueError("more nonempty rows than lanes")
         L = (_segment_length(lens, lanes) if split else int(lens.max())) if len(rows_nz) else 1
         while True:
-            S = -(-lens[rows_nz] // L)                        # group size per nonempty row
-            E = -(-lens[rows_nz] // np.maximum(S, 1))         # segment length (padded)
+            S = _group_sizes(lens[rows_nz], L)                # group size per nonempty row
+            E = -(-lens[rows_nz] // S)                        # segment length (padded)
             try:
                 placed = _place_groups(E, S, lanes)
                 break

@@ -43,7 +43,7 @@ def run():
     args = bench.parse.__wrapped__() if hasattr(bench.parse, "__wrapped__") else None
     sys.argv = [sys.argv[0], "--config", "P"]
     args = bench.parse()
-    graph, shard, _, _ = bench.build_workload(args, 0, 1, False)
+    graph, shard, _, _ = bench.build_workload("P", 0, 1, False)
     plan, dg = bench.make_plan(args, graph, shard, torch.device("cuda", 0))
     l1, l2 = plan.spmm_launches
     clock = 100e6  # s_memtime/readcyclecounter ticks (shader clock): report raw and per stage

@@ -199,9 +199,9 @@ def test_alias_table_encodes_the_unigram_distribution():
 
 def test_staged_layout_reproduces_every_relation():
     """The staged layout (sparse.staged_layout) holds each relation exactly: rebuilding A_k
-    from vinfo / woff / rlw / pairs gives the matrix back.  Long rows become groups of at most
-    8 equal-length segments (zero-column padding), groups sit on consecutive lanes of one
-    64-lane wave, lanes are sorted by length, at most `lanes` of them, and every wave's block
+    from vinfo / woff / rlw / pairs gives the matrix back.  Long rows become groups of 2, 4 or
+    8 equal-length segments (zero-column padding), groups sit on consecutive lanes starting at
+    a multiple of their size (inside one 64-lane wave and one 16-lane DPP row), lanes are sorted by length, at most `lanes` of them, and every wave's block
     is dense: lane j's pair at diagonal m sits at woff + 64 m + j (holes are zero pairs)."""
     import scipy.sparse as sp
 
@@ -230,6 +230,7 @@ def test_staged_layout_reproduces_every_relation():
             assert wbig[w] == gsz[64 * w:64 * w + 64].max()
         for i in range(64 * n_w):                                         # groups inside a wave
             if row[i] != 1023 and seg[i] == 0:
+                assert gsz[i] in (1, 2, 4, 8) and i % gsz[i] == 0           # aligned power-of-two group
                 assert i // 64 == (i + gsz[i] - 1) // 64
                 assert np.all(row[i:i + gsz[i]] == row[i]) and np.all(seg[i:i + gsz[i]] == np.arange(gsz[i]))
         got = np.zeros((n_r, n_c), np.float64)
