@@ -494,14 +494,35 @@ def main_train(args):
 
     from decagon_amd import kernels, train
 
-    torch.cuda.set_device(0)
-    device = torch.device("cuda", 0)
-    graph, shard, scaling, workload = build_workload(args.config, 0, 1, False)
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev_index = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    sharded = world > 1 or args.force_shard
+    shard = None
+    if sharded:
+        # relation-sharded training (train.py): every relation whole on one rank (LPT on
+        # nonzeros, no row split), forward all-reduces + the backward's dH1 all-reduce
+        from decagon_amd.sharding import RelationShard
+
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.backend)
+        graph, _, scaling, workload = build_workload(args.config, rank, world, False)
+        nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
+        shard = RelationShard.lpt(graph.edge_types, nnz, rank, world, collectives(args.backend)[0])
+        scaling = "strong"
+    else:
+        graph, _, scaling, workload = build_workload(args.config, 0, 1, False)
     drop = None
     if args.dropout > 0:
         drop = (1.0 - args.dropout, torch.tensor([20180701, 0], dtype=torch.int64, device=device))
         workload += f"; dropout {args.dropout}"
-    plan, dg = make_plan(args, graph, None, device, keep_sums=True, dropout=drop)
+    plan, dg = make_plan(args, graph, shard, device, keep_sums=True, dropout=drop)
     dec = Decoder(graph, plan, device, 0)
     tp = train.TrainPlan(plan, plan.w1, plan.w2, {j: None for j in graph.n_nodes})
     dR = torch.zeros_like(dec.R)
@@ -515,9 +536,9 @@ def main_train(args):
         kernels.scatter_rows(dgrad.row_idx, dgrad.grad_rows, dE[1])
         kernels.scatter_rows(dec.cols, dgrad.grad_cols, dE[1])
 
-    ets = list(graph.edge_types)
-    params = [plan.w1.stacks[et] for et in ets] + [plan.w2.stacks[et] for et in ets] + [dec.R, dec.l]
-    grads = [tp.gW1[et] for et in ets] + [tp.gW2[et] for et in ets] + [dR, dl]
+    pairs = tp.adam_pairs(plan.w1, plan.w2)
+    params = [p for p, _ in pairs] + [dec.R, dec.l]
+    grads = [g for _, g in pairs] + [dR, dl]
     adam = train.AdamState(params, lr=0.001)
     prep = adam.prepared(grads)
 
@@ -533,14 +554,22 @@ def main_train(args):
         step()
         stream.synchronize()
         loss0 = float(f.loss[0])
-    el = timed_steps(step, args.steps, max(0, args.warmup - 1), G, stream, not args.no_graph)
+    el = timed_steps(step, args.steps, max(0, args.warmup - 1), G, stream, not args.no_graph,
+                     dist.barrier if sharded else None)
     loss1 = float(f.loss[0])
     params_n = int(sum(p.numel() for p in params))
+    edges = 2 * dg.total_nnz
+    if sharded:
+        t = torch.tensor([el, float(edges), float(params_n)], dtype=torch.float64, device=device)
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        el, edges, params_n = float(tm[0]), float(t[1]), int(t[2])
     rec = {
         "metric": "GCN training-step edges/sec (forward + backward + Adam), " + ("5-relation synthetic" if args.config == "S" else "polypharmacy-shaped"),
-        "value": 2 * dg.total_nnz * args.steps / el,
+        "value": edges * args.steps / el,
         "unit": "edges/s",
-        "n_gpus": 1,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps,
@@ -550,14 +579,24 @@ def main_train(args):
         "dtype": "f32",
         "data": "synthetic (as the forward bench), random glorot weights, device-sampled negatives",
         "config": {"workload": workload + "; training step: backward + TF-Adam on %d parameters" % params_n,
-                   "nnz_per_layer_total": dg.total_nnz, "parallelism": "1 GPU", "hipgraph": not args.no_graph,
-                   "steps_per_graph": G},
+                   "nnz_per_layer_total": int(edges // 2),
+                   "parallelism": (shard.describe(args.backend) + " + all-reduce of dH1 in the backward"
+                                   if sharded else "1 GPU"),
+                   "hipgraph": not args.no_graph, "steps_per_graph": G},
         "loss_first_step": loss0,
         "loss_last_step": loss1,
         "roofline": None,
         "cpu_baseline": None,
     }
-    print(json.dumps(rec), file=JSON_OUT, flush=True)
+    if rank == 0:
+        print(json.dumps(rec), file=JSON_OUT, flush=True)
+    if sharded:
+        dist.barrier()
+        from decagon_amd import rccl
+
+        if rccl._COMM is not None:
+            rccl._COMM.destroy()
+        dist.destroy_process_group()
 
 
 # ----------------------------------------------------------------------------- rehearsal

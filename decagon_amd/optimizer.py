@@ -269,10 +269,12 @@ class DecagonOptimizer:
         tp.backward(decoder_grad)
         w1, w2 = model.weight_stacks()
         ets = list(model.edge_types)
-        params = [w1.stacks[et] for et in ets] + [w2.stacks[et] for et in ets] + \
-                 [model.edge_type2decoder[et].flat for et in ets]
-        grads = [tp.gW1[et] for et in ets] + [tp.gW2[et] for et in ets] + [dec_grads[et] for et in ets]
+        pairs = tp.adam_pairs(w1, w2)  # whole stacks (one GPU) or the local relations (sharded)
+        params = [p for p, _ in pairs] + [model.edge_type2decoder[et].flat for et in ets]
+        grads = [g for _, g in pairs] + [dec_grads[et] for et in ets]
         if not apply:
+            if tp.sharded:
+                raise NotImplementedError("grads_vars under sharding: each relation's gradient lives on its owner rank")
             return self._grads_vars(model, tp, dec_grads)
         key = ("adam", id(self))
         cache = ctx.session.caches

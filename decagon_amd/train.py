@@ -20,7 +20,17 @@ the backward graph automatically; here it is written out over the forward's save
 Âᵀ of every relation is built once on the host from the uploaded CSR and stored as a
 relation-chunked CSR whose virtual columns index the shared operand dS_ij directly, so the
 transposed SpMM writes dP / dW1 straight in the weight-stack layout [K][n_j][d].
-Scope: one GPU, identity features (sparse-feature and sharded training raise).
+
+Relation-sharded training (N GPUs, sharding.RelationShard.lpt: every relation whole on one
+rank, the forward in flat mode with its two all-reduces): a relation's weights are used only
+by the rank that owns it, so that rank alone computes their gradients and applies Adam to
+them — the gradient and Adam-slot stacks hold the LOCAL relations only ([K_local][…], in
+ascending relation id), no weight gradient is exchanged and Adam's memory and time shard
+with the relations.  The one extra collective is an all-reduce of dH1 (every node type's
+rows, h1 wide) after the layer-2 backward, because dH1_j = Σ_ik dP_ijk·W2_ijkᵀ sums over
+every rank's relations; the decoder and everything after the forward's all-reduces run
+redundantly and identically on every rank.  Row-split node types (sharding.RelationShard.
+split) and dropout are not supported by the sharded backward (they raise).
 """
 from __future__ import annotations
 
@@ -93,8 +103,12 @@ class TrainPlan:
 
     def __init__(self, fwd: ForwardPlan, w1: LayerWeights, w2: LayerWeights,
                  features: Dict[int, Optional[HostCSR]]):
-        if not fwd.keep_sums or fwd.allreduce is not None:
-            raise NotImplementedError("training runs on one GPU over a ForwardPlan(keep_sums=True)")
+        if not fwd.keep_sums:
+            raise NotImplementedError("training runs over a ForwardPlan(keep_sums=True)")
+        self.sharded = fwd.allreduce is not None
+        if self.sharded and (fwd.row_block or fwd.drop_state is not None):
+            raise NotImplementedError("sharded training: relation-sharded plans without dropout only")
+        self.allreduce = fwd.allreduce
         # with dropout (fwd.drop_state), the backward reuses the forward's masks: the draws of the
         # forward's step, regenerated from the same counter-based hash (dropout.hip)
         # sparse features X_j (mono side effects): layer 1's weight gradient is X_jᵀ·(Â_kᵀ·dS1)
@@ -109,7 +123,14 @@ class TrainPlan:
         ets = fwd.edge_types
         self.dE = {i: torch.zeros((n[i], h2), **f32) for i in fwd.targets}
         srcs = sorted({et[1] for et in ets})
-        self.dH1 = {j: torch.zeros((n[j], h1), **f32) for j in srcs}
+        # dH1 of every node type in one flat buffer (sharded: all-reduced after the layer-2 backward)
+        self._dH1_flat = torch.zeros(sum(n[j] for j in n) * h1, **f32)
+        self.dH1, off = {}, 0
+        for j in sorted(n):
+            self.dH1[j] = self._dH1_flat[off:off + n[j] * h1].view(n[j], h1)
+            off += n[j] * h1
+        self.local_ids: Dict[EdgeType, np.ndarray] = {}  # global ids of gW*[et]'s rows
+        self._w2_local = []  # (full W2 stack, ids, compact copy): sharded reduce-GEMM operands
         self.gW1: Dict[EdgeType, torch.Tensor] = {}
         self.gW2: Dict[EdgeType, torch.Tensor] = {}
         specs2, specs1, gemm_w2, gemm_h1 = [], [], [], []
@@ -120,12 +141,21 @@ class TrainPlan:
         for et in ets:
             i, j = et
             grp = g.groups[et]
-            K = grp.K
-            if grp.n_rels != K or grp.host is None:
+            if grp.host is None or (grp.n_rels != grp.K and not self.sharded):
                 raise NotImplementedError("training needs every relation of a group on this device")
             order = np.argsort(grp.rel_ids, kind="stable")
+            ids = np.asarray(grp.rel_ids, np.int64)[order]
+            self.local_ids[et] = ids
+            K = len(ids)  # local relations (all K_ij on one GPU)
+            if K == 0:  # another rank owns every relation of the group: no local gradient
+                self.gW1[et] = torch.zeros((0, n[j] if features.get(j) is None else int(features[j].shape[1]), h1), **f32)
+                self.gW2[et] = torch.zeros((0, h1, h2), **f32)
+                # (the layer's l2-norm backward still writes the group's dS: nothing reads it)
+                self._dS1[et] = torch.zeros((n[i], h1), **f32)
+                self._dS2[et] = torch.zeros((n[i], h2), **f32)
+                continue
             rels = [transpose_csr(grp.host[p]) for p in order]
-            m = merge_chunks(rels, [0] * K, 1, 1)  # chunk k = relation k; vcol = Â row (into dS)
+            m = merge_chunks(rels, [0] * K, 1, 1)  # chunk k = local relation k; vcol = Â row (into dS)
             rp, vc, vv = (torch.from_numpy(m.rowptr).to(dev), torch.from_numpy(m.vcol).to(dev),
                           torch.from_numpy(m.val).to(dev))
             vmax = int(m.vcol.max()) if m.nnz else -1
@@ -133,12 +163,12 @@ class TrainPlan:
             dS1 = torch.zeros((n[i], h1), **f32)
             dP = torch.zeros((K, n[j], h2), **f32)
             self._dS1[et], self._dS2[et] = dS1, dS2
-            self.gW2[et] = torch.zeros_like(w2.stacks[et])
+            self.gW2[et] = torch.zeros((K,) + tuple(w2.stacks[et].shape[1:]), **f32)
             fj = features.get(j)
             F = n[j] if fj is None else int(fj.shape[1])
             self.gW1[et] = torch.zeros((K, F, h1), **f32)
-            if tuple(w1.stacks[et].shape) != (K, F, h1):
-                raise ValueError(f"layer-1 weights of {et} are {tuple(w1.stacks[et].shape)}, expected ({K}, {F}, {h1})")
+            if tuple(w1.stacks[et].shape) != (grp.K, F, h1):
+                raise ValueError(f"layer-1 weights of {et} are {tuple(w1.stacks[et].shape)}, expected ({grp.K}, {F}, {h1})")
             # Âᵀ·dS1 per relation: the weight gradient itself (identity features), or the
             # operand of X_jᵀ·(·) (sparse features)
             g1 = self.gW1[et] if fj is None else torch.zeros((K, n[j], h1), **f32)
@@ -165,7 +195,11 @@ class TrainPlan:
             part = torch.zeros((n_runs, n[j], h1), **f32)
             drop = ((fwd.drop_state, drop_tag(2, fwd.et_index[et]), fwd.keep) if fwd.drop_state is not None
                     else None)
-            gemm_h1.append(kernels.PreparedGemm(dP, (n[j] * h2, h2, 1), w2.stacks[et], (h1 * h2, 1, h2), part,
+            W2 = w2.stacks[et]
+            if K != grp.K:  # sharded: the local relations' W2, gathered each step (Adam moves them)
+                W2 = torch.empty((K,) + tuple(w2.stacks[et].shape[1:]), **f32)
+                self._w2_local.append((w2.stacks[et], torch.from_numpy(ids).to(dev), W2))
+            gemm_h1.append(kernels.PreparedGemm(dP, (n[j] * h2, h2, 1), W2, (h1 * h2, 1, h2), part,
                                                 (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R, drop=drop))
             if fwd.drop_state is not None and fj is None:  # dW1 rows through layer 1's row masks
                 self._w1_drop.append(lambda g=self.gW1[et], tg=drop_tag(1, fwd.et_index[et]):
@@ -184,6 +218,8 @@ class TrainPlan:
         self._gemm_h1 = [kernels.PreparedGemmMulti(c) for c in chunked(gemm_h1)]
         self._epi_h1 = []
         for j, lst in runs.items():
+            if not lst:  # no local relation reads H1_j: its (zeroed) dH1 rows come from the all-reduce
+                continue
             if len(lst) > DG_MAX_GROUPS:
                 raise ValueError(f"more than {DG_MAX_GROUPS} edge types out of node type {j}")
             self._epi_h1.append(kernels.PreparedEpilogue(lst, self.dH1[j], n[j], h1, 0))
@@ -192,9 +228,7 @@ class TrainPlan:
         for i, tets in fwd.targets.items():
             self._l2g2.append(kernels.PreparedL2Grad([(L2.views[et], self._dS2[et]) for et in tets],
                                                      self.dE[i], None, n[i], h2))
-            dy = self.dH1.get(i)
-            if dy is None:  # no layer-2 relation reads H1_i: its gradient is zero
-                dy = self.dH1.setdefault(i, torch.zeros((n[i], h1), **f32))
+            dy = self.dH1[i]  # zero when no layer-2 relation reads H1_i
             self._l2g1.append(kernels.PreparedL2Grad([(L1.views[et], self._dS1[et]) for et in tets],
                                                      dy, fwd.hidden1[i], n[i], h1))
 
@@ -203,6 +237,10 @@ class TrainPlan:
         then both layers' backward into gW2 / gW1."""
         for t in self.dE.values():
             t.zero_()
+        if self.sharded:
+            self._dH1_flat.zero_()  # node types without local layer-2 relations add zeros
+            for full, ids, out in self._w2_local:
+                torch.index_select(full, 0, ids, out=out)
         decoder_grad(self.dE)
         for l in self._l2g2:
             l()
@@ -214,6 +252,8 @@ class TrainPlan:
             gm()
         for e in self._epi_h1:
             e()
+        if self.sharded:
+            self.allreduce(self._dH1_flat)  # dH1_j = Σ over every rank's relations
         for l in self._l2g1:
             l()
         for s in self._spmm1:
@@ -222,3 +262,16 @@ class TrainPlan:
             s()
         for f in self._w1_drop:
             f()
+
+    def adam_pairs(self, w1: LayerWeights, w2: LayerWeights) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+        """(parameter, gradient) of every GCN weight this plan updates: whole stacks on one GPU;
+        the local relations' slices, one pair per relation, when sharded."""
+        out = []
+        for stacks, grads in ((w1.stacks, self.gW1), (w2.stacks, self.gW2)):
+            for et in self.fwd.edge_types:
+                ids = self.local_ids[et]
+                if len(ids) == stacks[et].shape[0]:
+                    out.append((stacks[et], grads[et]))
+                else:
+                    out += [(stacks[et][int(k)], grads[et][c]) for c, k in enumerate(ids)]
+        return out

@@ -152,3 +152,124 @@ def test_sharded_full_size_P_matches_oracle():
     """configs[3]'s plan at full size (19,085 + 645 nodes, 1,932 matrices, ≈23 M nnz) on 2
     ranks: proteins row-split, 1,928 drug×drug relations LPT-sharded (staged kernel)."""
     _check("P", 2)
+
+
+# ---------------------------------------------------------------------------- training
+def _train_rank(rank, world, kind):
+    """One relation-sharded training step (train.py): forward (flat mode, all-reduces), the
+    DEDICOM decoder + hinge on a fixed batch of relation (1,1)_0 with given negatives, the
+    backward (dH1 all-reduce) and TF-Adam on the rank's own relations.  Returns the local
+    gradients by global relation id, the decoder gradients, the updated local weights."""
+    from decagon_amd import kernels, train
+    from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
+    from decagon_amd.sharding import RelationShard, torch_allreduce
+
+    dev = torch.device("cuda", 0)
+    g = _graph(kind)
+    nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
+    shard = RelationShard.lpt(g.edge_types, nnz, rank, world, torch_allreduce())
+    w1, w2 = _weights(g, 5)
+    W1 = LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()})
+    W2 = LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()})
+    dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local)
+    fwd = ForwardPlan(dg, {0: None, 1: None}, W1, W2, 64, 32, shard=shard, keep_sums=True)
+    tp = train.TrainPlan(fwd, W1, W2, {0: None, 1: None})
+    R, l, rows, cols, neg = _train_batch(g)
+    E = fwd.embeddings[1]
+    Rt, lt = torch.from_numpy(R).to(dev), torch.from_numpy(l).to(dev)
+    rows_t, cols_t, neg_t = (torch.from_numpy(x.astype(np.int32)).to(dev) for x in (rows, cols, neg))
+    hinge = kernels.PreparedDecoderHinge(E, E, rows_t, cols_t, Rt, lt, 0.1, neg_rows=neg_t)
+    dR, dl = torch.zeros_like(Rt), torch.zeros_like(lt)
+    dgrad = kernels.PreparedDecoderGrad(E, E, rows_t, cols_t, neg_t, hinge.pos, hinge.neg, Rt, lt, 0.1,
+                                        dG=dR.view(-1), dl=dl)
+
+    def decoder_grad(dE):
+        dgrad()
+        kernels.scatter_rows(dgrad.row_idx, dgrad.grad_rows, dE[1])
+        kernels.scatter_rows(cols_t, dgrad.grad_cols, dE[1])
+
+    pairs = tp.adam_pairs(W1, W2)
+    adam = train.AdamState([p for p, _ in pairs], lr=0.001)
+    prep = adam.prepared([gr for _, gr in pairs])
+    fwd.run()
+    hinge()
+    tp.backward(decoder_grad)
+    torch.cuda.synchronize()
+    grads = {"w1": {}, "w2": {}}
+    for name, gw in (("w1", tp.gW1), ("w2", tp.gW2)):
+        for et, ids in tp.local_ids.items():
+            for c, k in enumerate(ids):
+                grads[name][et[0], et[1], int(k)] = gw[et][c].cpu().numpy()
+    adam.apply(prep)
+    torch.cuda.synchronize()
+    after = {}
+    for name, st in (("w1", W1), ("w2", W2)):
+        for et, ids in tp.local_ids.items():
+            for k in ids:
+                after[name, et[0], et[1], int(k)] = st.stacks[et][int(k)].cpu().numpy()
+    return grads, {"R": dR.cpu().numpy(), "l": dl.cpu().numpy()}, float(hinge.loss[0]), after
+
+
+def _train_batch(g):
+    rng = np.random.default_rng(17)
+    R = rng.uniform(-0.3, 0.3, (32, 32)).astype(np.float32)
+    l = rng.uniform(0.5, 1.5, 32).astype(np.float32)
+    coords = g.adj[1, 1][0][0]
+    pick = coords[rng.choice(len(coords), 128, replace=False)]
+    neg = rng.integers(0, g.n_nodes[1], 128)
+    return R, l, pick[:, 0], pick[:, 1], neg
+
+
+def _train_oracle(kind, g):
+    from oracle import decagon_oracle as orc
+
+    w1, w2 = _weights(g, 5)
+    R, l, rows, cols, neg = _train_batch(g)
+    ets = list(g.edge_types)
+    decoders = {et: "dedicom" for et in ets}
+    rng = np.random.default_rng(1)
+    dec = {et: {"global_interaction": rng.uniform(-0.3, 0.3, (32, 32)),
+                **{"local_variation_%d" % k: rng.uniform(0.5, 1.5, 32) for k in range(K)}}
+           for et, K in g.edge_types.items()}
+    dec[1, 1]["global_interaction"] = R.astype(np.float64)
+    dec[1, 1]["local_variation_0"] = l.astype(np.float64)
+    e = sum(g.edge_types[et] for et in ets[:ets.index((1, 1))])  # flat index of (1,1)_0
+    n = g.n_nodes
+    feats = {t: None for t in n}
+    adj = {et: [(c, v.astype(np.float32).astype(np.float64), s) for c, v, s in mats] for et, mats in g.adj.items()}
+    cost, ref = orc.train_grads(g.edge_types, adj, feats,
+                                {et: [x.astype(np.float64) for x in w] for et, w in w1.items()},
+                                {et: [x.astype(np.float64) for x in w] for et, w in w2.items()},
+                                decoders, dec, 32, np.stack([rows, cols], 1), neg, e, 1, 1, 0.1)
+    return cost, ref, w1, w2
+
+
+def test_sharded_training_step_matches_oracle():
+    """Relation-sharded training on 2 ranks (config S, relations LPT-sharded): every rank's
+    gradients of its own relations and the (replicated) decoder gradients equal the float64
+    oracle's TF-minimize gradients (oracle.train_grads) within 1e-4; every relation is updated
+    by exactly one rank, by one TF-Adam step (oracle.adam_tf) on the device's gradient."""
+    from oracle import decagon_oracle as orc
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    world = 2
+    got = run_ranks(_train_rank, world, ("S",))
+    g = _graph("S")
+    cost, ref, w1, w2 = _train_oracle("S", g)
+    seen = set()
+    for r in range(world):
+        grads, dec, loss, after = got[r]
+        assert abs(loss - cost) <= TOL * abs(cost)
+        assert rel_err(dec["R"], ref["dec"][1, 1]["global_interaction"]) <= TOL
+        assert rel_err(dec["l"], ref["dec"][1, 1]["local_variation_0"]) <= TOL
+        for name, wref, wsrc in (("w1", ref["w1"], w1), ("w2", ref["w2"], w2)):
+            for (i, j, k), gv in grads[name].items():
+                want = wref[i, j][k]
+                scale = np.max(np.abs(want))
+                assert np.max(np.abs(gv - want)) <= TOL * max(scale, 1e-30), (r, name, i, j, k)
+                p1, _, _ = orc.adam_tf(wsrc[i, j][k], gv, np.zeros_like(gv), np.zeros_like(gv), 1)
+                assert np.max(np.abs(after[name, i, j, k] - p1)) <= 1e-6 * max(1.0, np.max(np.abs(p1)))
+                assert (name, i, j, k) not in seen
+                seen.add((name, i, j, k))
+    assert len(seen) == 2 * sum(g.edge_types.values())  # every relation, exactly once
