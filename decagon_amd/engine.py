@@ -508,24 +508,30 @@ class ForwardPlan:
         # row block and one epilogue finishes the block before the exchange
         split_t = [i for i in self.targets if i in self.row_block]
         red = [et for et in rest if et[0] not in self.row_block]
-        flat, views = None, {}
+        flat, views, send, sviews = None, {}, None, {}
         if self.flat_mode and red:
+            # flat (the reduced sums, read by the finishing launch and the backward) and, when
+            # sharded, send (this rank's partial sums, written by its SpMM / reduces): the
+            # all-reduce runs out of place, so the regions of groups without local relations
+            # stay zero from allocation on — no per-step fill
             sizes = [g.groups[et].n_rows * d for et in red]
             flat = torch.zeros(int(sum(sizes)), **f32)
+            send = torch.zeros_like(flat) if self.allreduce is not None else flat
             off = 0
             for et, sz in zip(red, sizes):
                 views[et] = flat[off:off + sz]
+                sviews[et] = send[off:off + sz]
                 off += sz
         partials, specs, staged, reduces = {}, [], [], []
         for et in rest:
             grp = g.groups[et]
             n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
             if flat is not None and et in views and n_out == 1:
-                part = views[et]  # single chunk: the SpMM writes the group sum in place
+                part = sviews[et]  # single chunk: the SpMM writes the group sum in place
             else:
                 part = torch.zeros((max(1, n_out), grp.n_rows, d), **f32)
                 if flat is not None and et in views and grp.n_rels:
-                    reduces.append(kernels.PreparedEpilogue([(part, n_out)], views[et], grp.n_rows, d, 0))
+                    reduces.append(kernels.PreparedEpilogue([(part, n_out)], sviews[et], grp.n_rows, d, 0))
             partials[et] = (part, max(1, n_out))
             if not grp.n_rels:
                 continue
@@ -544,7 +550,7 @@ class ForwardPlan:
             launches.append(kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d))
             self.launch_groups[id(launches[-1])] = spmm_ets[s:s + DG_MAX_GROUPS]
         launches += reduces
-        need_zero = flat is not None and any(g.groups[et].n_rels == 0 for et in red)
+        need_zero = send is flat and flat is not None and any(g.groups[et].n_rels == 0 for et in red)
         epis, local_epis, gathers = [], [], []
         if split_t:
             blocks = []
@@ -580,7 +586,7 @@ class ForwardPlan:
             if tl:
                 epis.append(kernels.PreparedEpilogueMulti(
                     [([partials[et] for et in self.targets[i]], outs[i], n[i]) for i in tl], d, flags))
-        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream,
+        return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream, send,
                       local_epis, gathers, self.allgather)
 
     def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
@@ -709,10 +715,11 @@ class _Layer:
     """The prepared launches of one layer and how to run them."""
 
     def __init__(self, launches, flat, need_zero, allreduce, epilogues, fused_targets, views=None,
-                 side_stream=None, local_epilogues=(), gathers=(), allgather=None):
+                 side_stream=None, send=None, local_epilogues=(), gathers=(), allgather=None):
         self.launches = launches
         self.side_stream = side_stream
         self.flat = flat
+        self.send = flat if send is None else send  # this rank's partial sums (sharded: all-reduced into flat)
         self.views = views or {}  # flat mode: (i,j) -> that group's S_ij, [n_i * d]
         self.need_zero = need_zero
         self.allreduce = allreduce
@@ -730,7 +737,7 @@ class _Layer:
         """The layer's collectives: all-reduce of the relation-sharded sums, then the
         all-gather of the row-split blocks."""
         if self.flat is not None and self.allreduce is not None:
-            self.allreduce(self.flat)
+            self.allreduce(self.send, self.flat)
         for out, blk in self.gathers:
             self.allgather(out, blk)
 

@@ -78,11 +78,15 @@ class RcclComm:
     def _stream() -> int:
         return torch.cuda.current_stream().cuda_stream
 
-    def all_reduce(self, t: torch.Tensor) -> None:
-        """In-place sum over the ranks of a contiguous fp32 device tensor."""
-        if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
-            raise ValueError("RcclComm.all_reduce takes a contiguous fp32 device tensor")
-        _check(_lib().ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), _NCCL_FLOAT32, _NCCL_SUM,
+    def all_reduce(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> None:
+        """Sum over the ranks of a contiguous fp32 device tensor, in place or into `out`."""
+        out = t if out is None else out
+        for x in (t, out):
+            if x.dtype != torch.float32 or not x.is_contiguous() or not x.is_cuda:
+                raise ValueError("RcclComm.all_reduce takes contiguous fp32 device tensors")
+        if out.numel() != t.numel():
+            raise ValueError("RcclComm.all_reduce: out must match t")
+        _check(_lib().ncclAllReduce(t.data_ptr(), out.data_ptr(), t.numel(), _NCCL_FLOAT32, _NCCL_SUM,
                                     self.comm, self._stream()), "ncclAllReduce")
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
@@ -93,7 +97,7 @@ class RcclComm:
         _check(_lib().ncclAllGather(inp.data_ptr(), out.data_ptr(), inp.numel(), _NCCL_FLOAT32, self.comm,
                                     self._stream()), "ncclAllGather")
 
-    def collectives(self) -> Tuple[Callable[[torch.Tensor], None], Callable[[torch.Tensor, torch.Tensor], None]]:
+    def collectives(self) -> Tuple[Callable[..., None], Callable[[torch.Tensor, torch.Tensor], None]]:
         """(allreduce, allgather) with the signatures sharding.RelationShard takes."""
         return self.all_reduce, self.all_gather
 

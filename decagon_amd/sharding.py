@@ -80,7 +80,7 @@ class RelationShard:
     rank: int
     world_size: int
     local: Dict[EdgeType, List[int]]
-    allreduce: Optional[Callable[[torch.Tensor], None]] = None
+    allreduce: Optional[Callable[..., None]] = None  # allreduce(t) in place, allreduce(t, out)
     loads: List[float] = field(default_factory=list)
     # node type -> (first row, end row, padded block) of this rank (row-split node types)
     row_block: Dict[int, Tuple[int, int, int]] = field(default_factory=dict)
@@ -142,7 +142,7 @@ class RelationShard:
         communicator of rccl.py for captured steps)."""
         nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
         if not comm:
-            ar, ag = _no_op, _no_op
+            ar, ag = _no_op_reduce, _no_op
         elif collectives is not None:
             ar, ag = collectives
         else:
@@ -182,12 +182,22 @@ def _no_op(*_a) -> None:
     return None
 
 
+def _no_op_reduce(t: torch.Tensor, out: Optional[torch.Tensor] = None) -> None:
+    """The all-reduce of a one-rank timing rehearsal: out = t (the data path stays valid)."""
+    if out is not None and out is not t:
+        out.copy_(t)
+
+
 def torch_allreduce(group=None) -> Callable[[torch.Tensor], None]:
     """Sum-all-reduce over the default (or given) process group — RCCL when the backend is
     'nccl' on ROCm, gloo on CPU tests."""
     import torch.distributed as dist
 
-    def _ar(t: torch.Tensor) -> None:
+    def _ar(t: torch.Tensor, out: Optional[torch.Tensor] = None) -> None:
+        """Sum over the ranks, in place, or into `out` (t unchanged)."""
+        if out is not None and out is not t:
+            out.copy_(t)
+            t = out
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
     return _ar
