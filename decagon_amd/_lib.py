@@ -21,7 +21,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 20
+ABI_VERSION = 21
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -67,6 +67,10 @@ class DgStagedGroup(ctypes.Structure):
         ("x_rows", c_int32),
         ("jm_len", c_int32),
     ]
+
+
+class DgStagedProj(ctypes.Structure):
+    _fields_ = [("h", c_void_p), ("w", c_void_p), ("h_ld", c_int64), ("din", c_int32), ("pad", c_int32)]
 
 
 class DgProj(ctypes.Structure):
@@ -160,6 +164,7 @@ SIGNATURES = {
                                        ctypes.c_uint32, c_float, c_void_p]),
     "dg_dropout_advance": (c_int32, [c_void_p, c_void_p]),
     "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
+    "dg_spmm_staged_proj_f32": (c_int32, [POINTER(DgStagedGroup), POINTER(DgStagedProj), c_int32, c_int32, c_void_p]),
     "dg_staged_order": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),

@@ -62,6 +62,12 @@ struct StagedGroupK {
     int32_t block_begin;
     int32_t n_blocks;
     int32_t pad;
+    // PROJ form: the slab of relation k is H · W[slab(k)] (H [n_cols][64], W [K][64][d]),
+    // computed in the workgroup on the fp32 MFMA instead of read from x
+    const float* h;
+    const float* w;
+    int32_t h_ld;
+    int32_t pad2;
 };
 
 struct StagedArgs {
@@ -109,6 +115,9 @@ __device__ __forceinline__ void fold_step(float4 (&part)[4], int gsz) {
     }
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool PROJ>
 __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedArgs a) {
     extern __shared__ float4 lds[];
     const int tid = threadIdx.x;
@@ -165,6 +174,42 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
             if (q < n5) glds16(xk, off * 4, dst + q0 * 16);
         }
     };
+    // PROJ: relation i's slab slice computed on the fp32 MFMA — slabᵀ[n][v] = Σ_k W[k][col0 + n]
+    // H[v][k] on v_mfma_f32_16x16x4_f32 (A = W slice: lane l holds W[16q + m][col0 + (l & 15)],
+    // q = l >> 4, for MFMA m; B = Hᵀ: H[v][16q + m] for its tile's row v = 16t + (l & 15); the
+    // contraction order k = 16q + m is free), so lane l ends with slab[v][col0 + 4q .. +3] —
+    // one ds_write_b128 into the buffer's row v.  Wave w makes 16-row tiles w, w + 16, ...; the
+    // W slice (16 floats per lane) is loaded a relation ahead, H rows come from L2.
+    const int pq = lane >> 4, pn = lane & 15;
+    auto load_w = [&](int i, float (&wa)[16]) {
+        const int sl = __builtin_amdgcn_readfirstlane(slb[i]);
+        const float* w = g.w + ((int64_t)sl * 64 + 16 * pq) * d + min(col0 + pn, d - 1);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) wa[m] = w[m * d];
+    };
+    // one 16-row tile at a time (measured: two tiles with interleaved accumulators made the
+    // layer-2 launch 10 us slower — their MFMAs then crowd the gathers of the SIMD's other waves)
+    auto slab_make = [&](int i, const float (&wa)[16]) {
+        float4* buf = xs0 + (i & 1) * a.xs_f4;
+        const int n_tiles = (n_cols + 15) >> 4;
+#pragma unroll 1
+        for (int t = wave; t < n_tiles; t += kMaxThreads / 64) {
+            const int v = 16 * t + pn;
+            const float4* hp = reinterpret_cast<const float4*>(g.h + (int64_t)min(v, n_cols - 1) * g.h_ld + 16 * pq);
+            float4 hv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hv[j] = hp[j];
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[4 * j], hv[j].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[4 * j + 1], hv[j].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[4 * j + 2], hv[j].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[4 * j + 3], hv[j].w, acc, 0, 0, 0);
+            }
+            if (v < n_cols) buf[v * 5 + pq] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
+    };
     // relation i's tables, straight from global memory (L2-resident, read a relation ahead):
     // this wave's pair block (woff, rlw diagonals), its largest group, this lane's vinfo
     // (read unconditionally — jm ends with 1024 spare ints; used only by waves with rlw > 0)
@@ -205,14 +250,24 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         }
     };
 
-    slab_copy(0);
+    float wa[16];  // PROJ: the W slice of the next slab to make
+    if constexpr (PROJ) {
+        load_w(0, wa);
+        slab_make(0, wa);
+        if (nk > 1) load_w(1, wa);
+    } else {
+        slab_copy(0);
+    }
     int woff, rlw, big, vi;
     tables(0, woff, rlw, big, vi);
     woff = __builtin_amdgcn_readfirstlane(woff);
     rlw = __builtin_amdgcn_readfirstlane(rlw);
     int2 un[4];
     pairs4(woff, un);
-    relation_barrier();  // slab 0 complete
+    if constexpr (PROJ)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // slab 0 written
+    else
+        relation_barrier();  // slab 0 complete
 
     float4 part[4];
     int pvi = 0, pbig = 1, prlw = 0;  // the previous relation's lane info (none yet)
@@ -228,11 +283,18 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         // relation i-1's sums (deferred past the barrier: they cover un's latency)
         if (prlw > 0) accumulate(part, pvi, __builtin_amdgcn_readfirstlane(pbig));
         DG_TICK(c_acc);
-        // un (relation i's first diagonals) must arrive before the slab copy is queued behind
-        // it: vmcnt retires in order
-        asm volatile("" :: "v"(un[0].x), "v"(un[0].y), "v"(un[1].x), "v"(un[1].y), "v"(un[2].x),
-                     "v"(un[2].y), "v"(un[3].x), "v"(un[3].y));
-        if (i + 1 < nk) slab_copy(i + 1);  // the other buffer: last read by relation i-1
+        if constexpr (PROJ) {
+            if (i + 1 < nk) {  // the other buffer: last read by relation i-1
+                slab_make(i + 1, wa);
+                if (i + 2 < nk) load_w(i + 2, wa);
+            }
+        } else {
+            // un (relation i's first diagonals) must arrive before the slab copy is queued
+            // behind it: vmcnt retires in order
+            asm volatile("" :: "v"(un[0].x), "v"(un[0].y), "v"(un[1].x), "v"(un[1].y), "v"(un[2].x),
+                         "v"(un[2].y), "v"(un[3].x), "v"(un[3].y));
+            if (i + 1 < nk) slab_copy(i + 1);  // the other buffer: last read by relation i-1
+        }
         DG_TICK(c_put);
         int nwoff, nrlw, nbig, nvi;
         tables(min(i + 1, nk - 1), nwoff, nrlw, nbig, nvi);
@@ -270,7 +332,10 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         vi = nvi;
         // the next relation's first diagonals: the last VMEM ops before the barrier
         pairs4(woff, un);
-        relation_barrier();  // relation i's gathers done; slab i+1 complete
+        if constexpr (PROJ)
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // gathers done; slab i+1 written
+        else
+            relation_barrier();  // relation i's gathers done; slab i+1 complete
         DG_TICK(c_bar);
     }
     if (prlw > 0) accumulate(part, pvi, __builtin_amdgcn_readfirstlane(pbig));
@@ -308,8 +373,9 @@ extern "C" int64_t dg_staged_prof_copy(unsigned long long* host, int64_t max_blo
 }
 #endif
 
-extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_groups, int32_t d,
-                                  void* stream) {
+namespace {
+int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, int32_t n_groups, int32_t d,
+                  void* stream) {
     if (n_groups < 1 || !groups) return DG_EINVAL;
     if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
     if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
@@ -323,11 +389,24 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
         if (s.n_rows < 0 || s.n_cols < 0 || s.n_rels < 0 || s.out_chunk < 1 || s.out_chunk > 64) return DG_EINVAL;
         if (s.n_rows >= kDummyRow || s.n_cols > kMaxThreads) return DG_EINVAL;  // rows fit 10 bits
         if (s.n_rows == 0 || s.n_rels == 0) continue;
-        if (!s.pairs || !s.jm || !s.jmoff || !s.x || !s.out) return DG_EINVAL;
-        if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || !dg::aligned16(s.pairs) || (s.x_ld & 3) || s.x_ld < d)
-            return DG_EALIGN;
-        if ((int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;
+        if (!s.pairs || !s.jm || !s.jmoff || !s.out) return DG_EINVAL;
+        if (!dg::aligned16(s.out) || !dg::aligned16(s.pairs)) return DG_EALIGN;
+        if (projs) {  // slabs from H · W: 64-wide H rows, 16-byte aligned
+            const dg_staged_proj& pj = projs[i];
+            if (!pj.h || !pj.w || pj.din != 64 || pj.h_ld < 64) return DG_EINVAL;
+            if (!dg::aligned16(pj.h) || (pj.h_ld & 3)) return DG_EALIGN;
+            if ((int64_t)s.n_cols * pj.h_ld > 0x7fffffffLL) return DG_EINVAL;
+        } else {
+            if (!s.x) return DG_EINVAL;
+            if (!dg::aligned16(s.x) || (s.x_ld & 3) || s.x_ld < d) return DG_EALIGN;
+            if ((int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;
+        }
         StagedGroupK& k = a.g[a.n_groups++];
+        if (projs) {
+            k.h = projs[i].h;
+            k.w = projs[i].w;
+            k.h_ld = static_cast<int32_t>(projs[i].h_ld);
+        }
         k.pairs = reinterpret_cast<const int2*>(s.pairs);
         k.jm = s.jm;
         k.jmoff = s.jmoff;
@@ -374,9 +453,28 @@ extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_group
     }
 #endif
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    static std::atomic<uint64_t> configured{0};
-    dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel), kLdsBytes, configured);
-    hipLaunchKernelGGL(spmm_staged_kernel, dim3(static_cast<unsigned>(blocks)), dim3(threads),
-                       static_cast<int>(lds), st, a);
+    if (projs) {
+        static std::atomic<uint64_t> configured{0};
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<true>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+                           static_cast<int>(lds), st, a);
+    } else {
+        static std::atomic<uint64_t> configured{0};
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<false>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+                           static_cast<int>(lds), st, a);
+    }
     return dg::launch_status();
+}
+}  // namespace
+
+extern "C" int dg_spmm_staged_f32(const dg_staged_group* groups, int32_t n_groups, int32_t d,
+                                  void* stream) {
+    return staged_launch(groups, nullptr, n_groups, d, stream);
+}
+
+extern "C" int dg_spmm_staged_proj_f32(const dg_staged_group* groups, const dg_staged_proj* projs,
+                                       int32_t n_groups, int32_t d, void* stream) {
+    if (!projs) return DG_EINVAL;
+    return staged_launch(groups, projs, n_groups, d, stream);
 }

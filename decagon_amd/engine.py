@@ -71,6 +71,8 @@ FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
 # what the other saves) and the fork / join cost ~10 us of idle GPU each at small per-rank
 # shares (8-GPU rehearsal), so one stream by default
 CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "0") != "0"
+# layer 2 of staged groups makes its slabs H1_j·W2_k on the MFMA inside the SpMM kernel
+STAGED_PROJ = os.environ.get("DG_STAGED_PROJ", "1") != "0"
 STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 
 
@@ -400,6 +402,11 @@ class ForwardPlan:
         self.embeddings = {i: out_buf(i, h2) for i in self.targets}
 
         # ---- layer-2 projection buffers P_k = H1_j·W2_k (global slabs) ----
+        # staged groups make their slabs H1_j·W2_k in the layer-2 kernel itself
+        # (dg_spmm_staged_proj_f32): no P buffer, no GEMM for them (64-wide H1, no dropout)
+        self.staged_proj = {et for et in self.edge_types
+                            if dgraph.groups[et].staged and dgraph.groups[et].n_rels and h1 == 64
+                            and self.drop_state is None and STAGED_PROJ}
         self.proj: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
@@ -408,7 +415,8 @@ class ForwardPlan:
                 raise ValueError(f"layer-2 weights of {et} are {(K, din, dout)}, expected ({grp.K}, {h1}, {h2})")
             if et[1] not in self.hidden1:
                 raise ValueError(f"node type {et[1]} has no incoming edge type; layer 2 needs hidden1[{et[1]}]")
-            self.proj[et] = torch.empty((K, n[et[1]], h2), **f32)
+            if et not in self.staged_proj:
+                self.proj[et] = torch.empty((K, n[et[1]], h2), **f32)
 
         # a second stream: a layer's gather-bound launch (dg_spmm_groups_f32) runs beside its
         # LDS-bound staged launch (dg_spmm_staged_f32) — different units, no data dependence
@@ -423,7 +431,7 @@ class ForwardPlan:
         # finishes the all-reduced sums) project themselves onto the layer-2 relations
         finished = (set(self.targets) - set(self.row_block)) if self.flat_mode else set(self.fused)
         proj_fused = [et for et in self.edge_types
-                      if dgraph.groups[et].n_rels and et[1] in finished
+                      if dgraph.groups[et].n_rels and et[1] in finished and et not in self.staged_proj
                       and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS and self.drop_state is None]
         if len(proj_fused) > DG_MAX_GROUPS:
             proj_fused = []
@@ -440,7 +448,7 @@ class ForwardPlan:
         self.hdrop: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
-            if not grp.n_rels or et in proj_fused:
+            if not grp.n_rels or et in proj_fused or et in self.staged_proj:
                 continue
             j = et[1]
             W = w2.stacks[et]
@@ -460,7 +468,9 @@ class ForwardPlan:
                 b_map_max=int(grp.rel_ids.max()) if grp.rel_map is not None else None))
         self._gemm2 = drops + [kernels.PreparedGemmMulti(gemms[s:s + DG_MAX_GROUPS])
                                for s in range(0, len(gemms), DG_MAX_GROUPS)]
-        self._layer2 = self._build_layer(self.proj, h2, False, f32)
+        self._layer2 = self._build_layer(self.proj, h2, False, f32,
+                                         staged_proj={et: (self.hidden1[et[1]], w2.stacks[et])
+                                                      for et in self.staged_proj})
 
     # ------------------------------------------------------------------ layer builder
     def _fused_targets(self) -> List[int]:
@@ -476,7 +486,7 @@ class ForwardPlan:
         return kernels.RelGroupSpec(grp.rowptr, grp.vcol, grp.val, x, out, grp.n_rows, grp.n_chunks, d,
                                     grp.K * grp.n_cols, vcol_max=grp.vcol_max)
 
-    def _build_layer(self, xs: Dict[EdgeType, torch.Tensor], d, relu, f32, projs=()):
+    def _build_layer(self, xs: Dict[EdgeType, torch.Tensor], d, relu, f32, projs=(), staged_proj=None):
         """Prepared launches of one layer: fused targets in one dg_gcn_fused_f32 launch; the
         other targets' groups in partial mode + epilogue — with, when sharded, the chunk
         reduce into the all-reduce buffer and the all-reduce before the epilogue."""
@@ -536,9 +546,10 @@ class ForwardPlan:
             if not grp.n_rels:
                 continue
             if grp.staged:
+                sp = (staged_proj or {}).get(et)
                 staged.append(kernels.StagedSpec(
-                    grp.layout, grp.rel_map, xs[et], part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
-                    slab_max=int(grp.rel_ids.max())))
+                    grp.layout, grp.rel_map, xs.get(et), part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
+                    slab_max=int(grp.rel_ids.max()), proj=sp))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
         staged_ets = [et for et in rest if g.groups[et].n_rels and g.groups[et].staged]
@@ -655,14 +666,18 @@ class ForwardPlan:
         return pick(self._layer1), pick(self._layer2)
 
     # ---- accounting (bench / DESIGN.md roofline) ----
-    def group_bytes(self, et: EdgeType, d: int, fused: bool) -> int:
+    def group_bytes(self, et: EdgeType, d: int, fused: bool, layer: int = 1) -> int:
         """Algorithmic bytes of one group's SpMM: its CSR once (4 B per row of each
         relation + 8 B per nonzero), its dense operands once (4·d B per row of each X_k) and,
         in partial mode, its sum S_ij once (4·d B per output row)."""
         grp = self.g.groups[et]
         if not grp.n_rels:
             return 0
-        tot = 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz + 4 * d * grp.n_cols * grp.n_rels
+        tot = 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz
+        if layer == 2 and et in self.staged_proj:  # layer 2 reads H1_j and W2 instead of P_k
+            tot += 4 * self.h1 * (grp.n_cols + d * grp.n_rels)
+        else:
+            tot += 4 * d * grp.n_cols * grp.n_rels
         return tot if fused else tot + 4 * d * grp.n_rows
 
     def launch_bytes(self, launch, layer: int) -> int:
@@ -673,7 +688,7 @@ class ForwardPlan:
         d = self.h1 if layer == 1 else self.h2
         ets = self.launch_groups.get(id(launch), [])
         fused = isinstance(launch, kernels.PreparedFused)
-        tot = sum(self.group_bytes(et, d, fused) for et in ets)
+        tot = sum(self.group_bytes(et, d, fused, layer) for et in ets)
         if fused:
             tot += sum(4 * d * self.g.n_nodes[i] for i in L.fused_targets)
             if layer == 1:
@@ -696,7 +711,10 @@ class ForwardPlan:
             if not grp.n_rels:
                 continue
             tot += 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz
-            tot += 4 * d * grp.n_cols * grp.n_rels
+            if layer == 2 and et in self.staged_proj:  # H1_j and W2 instead of P_k
+                tot += 4 * self.h1 * (grp.n_cols + d * grp.n_rels)
+            else:
+                tot += 4 * d * grp.n_cols * grp.n_rels
             if et[0] not in L.fused_targets:
                 tot += 4 * d * grp.n_rows
         for i in L.fused_targets:

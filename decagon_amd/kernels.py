@@ -19,7 +19,7 @@ import torch
 
 from . import _lib
 from ._lib import (DgAdamSeg, DgEpiGroup, DgFusedTarget, DgGemmDesc, DgL2gGroup, DgProj, DgRelGroup,
-                   DgStagedGroup, check)
+                   DgStagedGroup, DgStagedProj, check)
 
 
 def _stream_ptr(stream: Optional[torch.cuda.Stream] = None) -> int:
@@ -288,13 +288,17 @@ class StagedSpec:
     x_ld: int
     x_rows: int
     slab_max: int = -1            # host-known max(slab) (or n_rels-1 without slab), for checks
+    # (H [n_cols][64], W [K][64][d]): relation k's operand is H·W[slab(k)], made in the kernel
+    # (dg_spmm_staged_proj_f32); x / x_ld / x_rows are then unused
+    proj: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
     def validate(self, d: int) -> None:
         L = self.layout
         for t, nm, dt in ((L.pairs, "pairs", torch.int32), (L.jm, "jm", torch.int32),
-                          (L.jmoff, "jmoff", torch.int32), (self.x, "x", torch.float32),
-                          (self.out, "out", torch.float32)):
+                          (L.jmoff, "jmoff", torch.int32), (self.out, "out", torch.float32)):
             _dev(t, dt, nm)
+        if self.proj is None:
+            _dev(self.x, torch.float32, "x")
         if L.pairs.data_ptr() % 16:
             raise ValueError("pairs must be 16-byte aligned")
         if not (0 < L.n_rows < 1023 and 0 < L.n_cols <= 1024):
@@ -310,10 +314,19 @@ class StagedSpec:
             if self.slab.numel() < L.n_rels:
                 raise ValueError("slab shorter than n_rels")
         smax = self.slab_max if self.slab_max >= 0 else L.n_rels - 1
-        if (smax + 1) * L.n_cols > self.x_rows or self.x.numel() < (self.x_rows - 1) * self.x_ld + d:
-            raise ValueError("dense operand smaller than the slabs address")
-        if self.x_rows * self.x_ld >= 2**31:
-            raise ValueError("dense operand too large for 32-bit gather offsets")
+        if self.proj is not None:
+            h, w = self.proj
+            _dev(h, torch.float32, "proj h")
+            _dev(w, torch.float32, "proj w")
+            if h.dim() != 2 or h.shape[0] < L.n_cols or h.shape[1] != 64 or h.stride(1) != 1 or h.stride(0) % 4:
+                raise ValueError("proj h must be [n_cols][64], rows 16-byte aligned")
+            if w.dim() != 3 or tuple(w.shape[1:]) != (64, d) or not w.is_contiguous() or w.shape[0] <= smax:
+                raise ValueError("proj w must be a contiguous [K][64][d] stack covering the slabs")
+        else:
+            if (smax + 1) * L.n_cols > self.x_rows or self.x.numel() < (self.x_rows - 1) * self.x_ld + d:
+                raise ValueError("dense operand smaller than the slabs address")
+            if self.x_rows * self.x_ld >= 2**31:
+                raise ValueError("dense operand too large for 32-bit gather offsets")
         n_out = -(-L.n_rels // self.out_chunk)
         if self.out.numel() < n_out * L.n_rows * d:
             raise ValueError("staged out too small")
@@ -326,22 +339,33 @@ class PreparedStaged:
         if not 1 <= len(specs) <= _lib.DG_MAX_GROUPS:
             raise ValueError(f"1..{_lib.DG_MAX_GROUPS} groups per launch")
         arr = (DgStagedGroup * len(specs))()
+        proj = specs[0].proj is not None
+        if any((s.proj is not None) != proj for s in specs):
+            raise ValueError("a staged launch's groups are all projected or none")
+        parr = (DgStagedProj * len(specs))() if proj else None
         for i, s in enumerate(specs):
             s.validate(d)
             L, g = s.layout, arr[i]
             g.pairs, g.jm, g.jmoff = L.pairs.data_ptr(), L.jm.data_ptr(), L.jmoff.data_ptr()
             g.slab = s.slab.data_ptr() if s.slab is not None else None
-            g.x = s.x.data_ptr()
+            g.x = s.x.data_ptr() if s.x is not None else None
+            if proj:
+                h, w = s.proj
+                parr[i].h, parr[i].w, parr[i].h_ld, parr[i].din = h.data_ptr(), w.data_ptr(), h.stride(0), 64
             g.out = s.out.data_ptr()
             g.x_ld = s.x_ld
             g.n_rows, g.n_cols, g.n_rels = L.n_rows, L.n_cols, L.n_rels
             g.out_chunk, g.x_rows, g.jm_len = s.out_chunk, s.x_rows, L.jm_len
         self._keep = list(specs)
-        self._arr, self._n, self.d = arr, len(specs), d
-        self._fn = _lib.load().dg_spmm_staged_f32
+        self._arr, self._parr, self._n, self.d = arr, parr, len(specs), d
+        lib = _lib.load()
+        self._fn = lib.dg_spmm_staged_proj_f32 if proj else lib.dg_spmm_staged_f32
 
     def __call__(self, stream=None) -> None:
-        check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_f32")
+        if self._parr is not None:
+            check(self._fn(self._arr, self._parr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_proj_f32")
+        else:
+            check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_f32")
 
 
 def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:

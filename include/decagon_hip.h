@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (19); bumped whenever a struct layout or a signature changes. */
+/* ABI version (21); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -194,6 +194,24 @@ typedef struct dg_staged_group {
 
 int dg_spmm_staged_f32(const dg_staged_group* groups /* HOST */, int32_t n_groups, int32_t d,
                        void* stream);
+
+/* The same SpMM with each relation's dense operand made in the workgroup instead of read:
+ *     X_k = H · W[slab(k)]        (H [n_cols][64] row-major, leading dimension h_ld; W [K][64][d])
+ * — layer 2's projection H1_j · W2_k (layers.py:113) fused into its SpMM (layers.py:114): the
+ * slab slice comes from the fp32 MFMA (exact fp32 products, k summed in a fixed order) into
+ * LDS, so the [K][n_cols][d] operand is never written to or read from HBM.  groups[i].x /
+ * x_ld / x_rows are ignored.  Requirements as dg_spmm_staged_f32, plus din == 64, h and h_ld
+ * 16-byte aligned.  Replaces layers.py:113-116 for such groups. */
+typedef struct dg_staged_proj {
+    const float* h;             /* device, [n_cols][h_ld]                                 */
+    const float* w;             /* device, [K][din][d]                                     */
+    int64_t h_ld;
+    int32_t din;                /* 64                                                      */
+    int32_t pad;
+} dg_staged_proj;
+
+int dg_spmm_staged_proj_f32(const dg_staged_group* groups /* HOST */, const dg_staged_proj* projs /* HOST */,
+                            int32_t n_groups, int32_t d, void* stream);
 
 /* Host-only layout helper: for one relation in CSR (HOST arrays) and its sorted-row order
  * perm[n_rows] (sorted index -> row, lengths descending), rank_out[p] = the diagonal nonzero
