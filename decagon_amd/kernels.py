@@ -316,7 +316,8 @@ class StagedSpec:
         smax = self.slab_max if self.slab_max >= 0 else L.n_rels - 1
         if self.proj is not None:
             h, w = self.proj
-            _dev(h, torch.float32, "proj h")
+            if not (isinstance(h, torch.Tensor) and h.is_cuda and h.dtype == torch.float32):
+                raise ValueError("proj h: float32 device tensor required (rows may be padded)")
             _dev(w, torch.float32, "proj w")
             if h.dim() != 2 or h.shape[0] < L.n_cols or h.shape[1] != 64 or h.stride(1) != 1 or h.stride(0) % 4:
                 raise ValueError("proj h must be [n_cols][64], rows 16-byte aligned")

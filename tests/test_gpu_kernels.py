@@ -449,3 +449,41 @@ def test_spmm_staged(K, d, n_rows, n_cols, density, out_chunk):
     spec.out = out2
     K.PreparedStaged([spec], d)()
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("d", [32, 64, 40])
+@pytest.mark.parametrize("n_rows,n_cols,density,out_chunk", [
+    (150, 137, 0.03, 5),     # a partial last 16-row projection tile, empty rows
+    (300, 137, 0.45, 4),     # long rows, split into segments
+    (645, 645, 0.3, 3),      # config P's shape: 41 tiles over 16 waves
+    (64, 880, 0.01, 23),     # 55 tiles (up to 4 per wave)
+])
+def test_spmm_staged_projected(K, d, n_rows, n_cols, density, out_chunk):
+    """dg_spmm_staged_proj_f32: relation k's operand H·W[slab(k)] made on the MFMA inside the
+    kernel, against the float64 Σ_k A_k·(H·W_slab(k)); H with a padded leading dimension."""
+    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, staged_layout
+
+    rng = np.random.default_rng(7 * d + n_rows + n_cols)
+    nrel, total = 23, 30
+    mats = [_rand_csr(rng, n_rows, n_cols, density, empty_rows=0.1) for _ in range(nrel)]
+    mats[5] = sp.csr_matrix((n_rows, n_cols), dtype=np.float32)
+    slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
+    lay = staged_layout([coo_to_csr(*sparse_to_tuple(x)) for x in mats], K.staged_order)
+    dev = K.StagedDevice.upload(lay, "cuda")
+    Hp = rng.standard_normal((n_cols, 68)).astype(np.float32)   # leading dimension 68
+    W = rng.standard_normal((total, 64, d)).astype(np.float32)
+    h = torch.from_numpy(Hp).cuda()[:, :64]
+    n_out = -(-nrel // out_chunk)
+    out = torch.zeros((n_out, n_rows, d), device="cuda")
+    spec = K.StagedSpec(dev, torch.from_numpy(slabs).cuda(), None, out, out_chunk, d, 0,
+                        slab_max=int(slabs.max()), proj=(h, torch.from_numpy(W).cuda()))
+    K.PreparedStaged([spec], d)()
+    H = Hp[:, :64].astype(np.float64)
+    want = np.zeros((n_out, n_rows, d))
+    for k, x in enumerate(mats):
+        want[k // out_chunk] += x @ (H @ W[slabs[k]].astype(np.float64))
+    assert rel_err(out.cpu().numpy(), want) <= 1e-5
+    out2 = torch.zeros_like(out)
+    spec.out = out2
+    K.PreparedStaged([spec], d)()
+    assert torch.equal(out, out2)
