@@ -12,13 +12,15 @@
 // Layout (decagon_amd/sparse.py: staged_layout): per relation, a long row becomes a group of
 // ≤ 8 equal-length segments ("virtual rows", zero-padded), groups sorted by length and kept
 // inside one 64-lane wave, and each wave's nonzeros a dense diagonal-major block [rlw][64]
-// (rlw a multiple of 4, holes zero pairs).  Thread i owns virtual row i, so at diagonal m the
+// (rlw a multiple of 4; holes are zero pairs on one of sixteen zero columns, one per bank
+// class, so a hole never collides with a nonzero's bank slot).  Thread i owns virtual row i, so at diagonal m the
 // 64 threads of a wave read 64 consecutive (col, value) pairs — one coalesced 512-byte load
 // straight from global memory at woff + 64m + lane, no table and no test, prefetched four
 // diagonals ahead in registers (the next relation's first four before the barrier).  The
-// relation tables (woff, rlw, vinfo) come from global memory a relation ahead.  Each row's
-// nonzeros are ordered on the host (layout.cpp) so the 16 lanes of a ds_read_b128 group mostly
-// gather from distinct bank slots.
+// relation tables (woff, rlw, vinfo) come from global memory a relation ahead.  Each lane's
+// nonzeros are placed on diagonals by the host (layout.cpp: a bipartite edge colouring per
+// ds_read_b128 lane group) so the group's 16 lanes gather from distinct bank slots wherever
+// the relation allows.
 //
 // Workgroup = 1024 threads, one per (output chunk c, 16-float column slice s), ONE barrier per
 // relation: the slab slice X_slab(k)[:, 16s .. +16) and k's tables live in one of two LDS
@@ -76,6 +78,9 @@ struct StagedArgs {
     int32_t d;
     int32_t xs_f4;     // float4 slots of one slab buffer (+ the zero column)
     int32_t acc_f4;    // float4 slots of the accumulator
+    int32_t acc_st;    // float4 slots per accumulator row: 5 (80 B, bank slot (5·row + j) mod 16,
+                       // a bijection of row & 15) when LDS allows, else 4
+    int32_t pad;
 #ifdef DG_STAGED_PROF
     unsigned long long* prof;  // per block, per wave: kProfSlots counters (see DG_TICK below)
 #endif
@@ -152,8 +157,10 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
 
     for (int i = tid; i <= nk; i += T) jof[i] = g.jmoff[k0 + i];
     for (int i = tid; i < nk; i += T) slb[i] = g.slab ? g.slab[k0 + i] : k0 + i;
-    for (int i = tid; i < n_rows * 4; i += T) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < 8) xs0[(tid >> 2) * a.xs_f4 + n_cols * 5 + (tid & 3)] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int ast = a.acc_st;
+    for (int i = tid; i < n_rows * ast; i += T) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // the sixteen zero columns n_cols .. n_cols + 15 (one per bank class) that holes read
+    if (tid < 128) xs0[(tid >> 6) * a.xs_f4 + (n_cols + ((tid >> 2) & 15)) * 5 + (tid & 3)] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
 
     // relation i's slab slice -> buffer i & 1 by glds: slot q of the buffer (column v = q / 5,
@@ -165,8 +172,10 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         const float* xk = g.x + (int64_t)__builtin_amdgcn_readfirstlane(slb[i]) * n_cols * g.x_ld + col0;
         const uint32_t dst = lds0 + (i & 1) * a.xs_f4 * 16;
         const int n5 = n_cols * 5;
-#pragma unroll 1
-        for (int q0 = 64 * wave; q0 < n5; q0 += 64 * 16) {
+        // unrolled (n_cols <= 1024: at most five rounds): the copies issue back to back
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const int q0 = 64 * wave + 1024 * r;
             const int q = q0 + lane;
             const int v = (q * 52429) >> 18;  // q / 5 (q < 5120)
             const int j = min(q - 5 * v, 3);
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         if (big > 4) fold_step<4>(part, gsz);
         const int row = vi & 1023;
         if (seg == 0 && row != kDummyRow) {
-            float4* ar = acc + row * 4;
+            float4* ar = acc + row * ast;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float4 o = ar[j];
@@ -355,7 +364,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     for (int q = tid; q < n_rows * 4; q += T) {
         const int r = q >> 2, j = q & 3;
         if (col0 + 4 * j < d)
-            *reinterpret_cast<float4*>(g.out + ((int64_t)c * n_rows + r) * d + col0 + 4 * j) = acc[q];
+            *reinterpret_cast<float4*>(g.out + ((int64_t)c * n_rows + r) * d + col0 + 4 * j) = acc[r * ast + j];
     }
 }
 
@@ -433,10 +442,20 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
     if (blocks == 0) return DG_OK;
     if (blocks > 0x7fffffff) return DG_EINVAL;
     const int threads = kMaxThreads;  // one thread per virtual row (staged_layout: at most 1024)
-    a.xs_f4 = (max_cols + 1) * 5;     // + the zero column
+    a.xs_f4 = (max_cols + 16) * 5;    // + the sixteen zero columns
+    a.acc_st = 4;
     a.acc_f4 = max_rows * 4;
-    const int64_t lds = 2 * (int64_t)a.xs_f4 * 16 + kMetaInts * 4 + (int64_t)a.acc_f4 * 16;
+    int64_t lds = 2 * (int64_t)a.xs_f4 * 16 + kMetaInts * 4 + (int64_t)a.acc_f4 * 16;
     if (lds > kLdsBytes) return DG_EINVAL;
+#ifndef DG_STAGED_ACC4  // A/B builds: 64-byte accumulator rows
+    // 80-byte accumulator rows when they fit: a wave's row updates (rows of consecutive virtual
+    // rows) then spread over the 16 bank slots instead of 4 (64-byte rows: slot (4·row + j) mod 16)
+    if (lds + (int64_t)max_rows * 16 <= kLdsBytes) {
+        a.acc_st = 5;
+        a.acc_f4 = max_rows * 5;
+        lds += (int64_t)max_rows * 16;
+    }
+#endif
 #ifdef DG_STAGED_PROF
     {
         static unsigned long long* buf = nullptr;

@@ -267,7 +267,7 @@ class DeviceGraph:
             g.staged, g.out_chunk = staged, out_chunk
             g.host = loc  # local relations in device order (the backward builds Âᵀ from them)
             if staged:
-                lay = staged_layout(loc, kernels.staged_order,
+                lay = staged_layout(loc, kernels.staged_block,
                                     split=os.environ.get("DG_STAGED_SPLIT", "1") != "0")
                 g.layout = kernels.StagedDevice.upload(lay, device)
             self.groups[et] = g

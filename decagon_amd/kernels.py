@@ -234,16 +234,19 @@ class PreparedFused:
                        self.wpg, self.d, _stream_ptr(stream)), "dg_gcn_fused_f32")
 
 
-def staged_order(csr, perm: np.ndarray) -> np.ndarray:
-    """Diagonal of each nonzero of one relation (CSR order) for the staged layout: the
-    library's bank-conflict-avoiding order (dg_staged_order, host-only)."""
-    rowptr = np.ascontiguousarray(csr.rowptr, np.int32)
-    col = np.ascontiguousarray(csr.col, np.int32)
-    perm = np.ascontiguousarray(perm, np.int32)
-    rank = np.zeros(len(col), np.int32)
-    check(_lib.load().dg_staged_order(rowptr.ctypes.data, col.ctypes.data, len(rowptr) - 1,
-                                      perm.ctypes.data, rank.ctypes.data), "dg_staged_order")
-    return rank
+def staged_block(lrowptr: np.ndarray, lcol: np.ndarray, lval: np.ndarray, rlw: np.ndarray,
+                 n_cols: int) -> np.ndarray:
+    """One relation's pair block of the staged layout with the library's bank-conflict-avoiding
+    diagonals and hole columns (dg_staged_block, host-only).  Lanes as a CSR over 64·waves
+    virtual rows; returns pairs [sum(rlw)·64, 2] int32."""
+    lrowptr = np.ascontiguousarray(lrowptr, np.int32)
+    lcol = np.ascontiguousarray(lcol, np.int32)
+    lval = np.ascontiguousarray(lval, np.float32)
+    rlw = np.ascontiguousarray(rlw, np.int32)
+    pairs = np.zeros((int(rlw.sum()) * 64, 2), np.int32)
+    check(_lib.load().dg_staged_block(lrowptr.ctypes.data, lcol.ctypes.data, lval.ctypes.data, len(lrowptr) - 1,
+                                      rlw.ctypes.data, n_cols, pairs.ctypes.data), "dg_staged_block")
+    return pairs
 
 
 @dataclass
@@ -271,9 +274,10 @@ STAGED_JM_SPARE = 1024
 
 
 def staged_lds_bytes(n_rows: int, n_cols: int) -> int:
-    """LDS of one staged workgroup (mirrors dg_spmm_staged_f32): two slab buffers of n_cols + 1
-    columns 80 B apart, 1 KiB of chunk tables, n_rows 64-byte accumulators."""
-    return 2 * (n_cols + 1) * 80 + 1024 + n_rows * 64
+    """LDS of one staged workgroup (mirrors dg_spmm_staged_f32): two slab buffers of n_cols + 16
+    columns 80 B apart (the slab rows, then sixteen zero columns), 1 KiB of chunk tables,
+    n_rows 64-byte accumulators (80-byte rows when LDS has room)."""
+    return 2 * (n_cols + 16) * 80 + 1024 + n_rows * 64
 
 
 @dataclass

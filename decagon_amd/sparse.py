@@ -9,6 +9,7 @@ float64 -> float32 exactly as the placeholder's dtype does.
 """
 from __future__ import annotations
 
+import os
 from collections import namedtuple
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence, Tuple
@@ -277,7 +278,8 @@ class StagedLayout:
     lane j at diagonal m sits at woff_w + 64m + j and the kernel loads it with no table or test.
     A group's segments are summed within the wave in lane order.
 
-      pairs [n_pairs, 2] int32   (column, fp32 value bits), relations and waves back to back
+      pairs [n_pairs, 2] int32   (column, fp32 value bits), relations and waves back to back;
+                                 holes read one of sixteen zero columns (n_cols + z, value 0)
       jm    int32                per relation at jmoff[k]: [n_waves, largest group, 0, 0],
                                  (then STAGED_JM_SPARE zeros ending the array)
                                  woff[16] (absolute pair offset of each wave's block),
@@ -355,13 +357,14 @@ def _place_groups(glen: np.ndarray, gsize: np.ndarray, lanes: int) -> List[Tuple
     return out
 
 
-def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
+def staged_layout(csrs: Sequence[HostCSR], block: Optional[Callable] = None,
                   lanes: int = 1024, split: bool = True) -> StagedLayout:
     """Build the staged layout of relations `csrs` (all one shape, local columns) with at
     most `lanes` virtual rows per relation (split=False: one virtual row per nonempty row).
-    `order(csr, perm) -> rank` places each nonzero of a (virtual-row) CSR on a diagonal
-    (default: feed order); the device path passes the library's bank-conflict-avoiding
-    order (kernels.staged_order)."""
+    `block(lrowptr, lcol, lval, rlw, n_cols) -> pairs` fills a relation's pair block from its
+    lanes (a CSR over virtual rows) and the waves' diagonals; the device path passes the
+    library's bank-conflict-avoiding builder (kernels.staged_block: each nonzero's diagonal,
+    each hole's zero column).  Default: feed order, holes on column n_cols."""
     if not csrs:
         raise ValueError("empty relation group")
     n_r, n_c = csrs[0].shape
@@ -369,6 +372,12 @@ def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
         raise ValueError("staged groups need n_rows < 1023, n_cols <= 1024")
     pairs_parts, jm_parts, jmoff = [], [], [0]
     base = 0
+    # the block builder (C, GIL released) runs on a thread pool while the lanes of the next
+    # relations are laid out here
+    pool = None
+    if block is not None and len(csrs) > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=max(1, min(16, len(os.sched_getaffinity(0)))))
     for c in csrs:
         if c.shape != (n_r, n_c):
             raise ValueError("all relations of a group must share one shape")
@@ -410,25 +419,25 @@ def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
         woff = np.zeros(16, np.int64)
         woff[:n_w] = base + np.concatenate([[0], np.cumsum(rlw * 64)[:-1]]) if n_w else 0
         n_pairs = int(rlw.sum()) * 64
-        rel_pairs = np.zeros((n_pairs, 2), np.int32)
-        rel_pairs[:, 0] = n_c  # padding: the zero column, value 0
-        if c.nnz:
-            # the lanes' real nonzeros as a CSR over lanes (each a contiguous piece of its row)
-            n_l = n_w * 64
-            vrowptr = np.zeros(n_l + 1, np.int64)
-            np.cumsum(lcnt, out=vrowptr[1:])
-            vr = np.repeat(np.arange(n_l), lcnt)
-            src = np.repeat(np.asarray(lst + [0] * pad_l, np.int64), lcnt) + (np.arange(len(vr)) - vrowptr[:-1][vr])
-            vcol = np.ascontiguousarray(c.col[src], np.int32)
-            vval = np.ascontiguousarray(np.asarray(c.val, np.float32)[src])
-            if order is None:
+        # the lanes' real nonzeros as a CSR over lanes (each a contiguous piece of its row)
+        n_l = n_w * 64
+        vrowptr = np.zeros(n_l + 1, np.int64)
+        np.cumsum(lcnt, out=vrowptr[1:])
+        vr = np.repeat(np.arange(n_l), lcnt)
+        src = np.repeat(np.asarray(lst + [0] * pad_l, np.int64), lcnt) + (np.arange(len(vr)) - vrowptr[:-1][vr])
+        vcol = np.ascontiguousarray(c.col[src], np.int32)
+        vval = np.ascontiguousarray(np.asarray(c.val, np.float32)[src])
+        if block is not None and n_w:
+            args = (vrowptr, vcol, vval, rlw, n_c)
+            rel_pairs = pool.submit(block, *args) if pool is not None else block(*args)
+        else:
+            rel_pairs = np.zeros((n_pairs, 2), np.int32)
+            rel_pairs[:, 0] = n_c  # padding: the zero column, value 0
+            if c.nnz:
                 rank = np.arange(len(src), dtype=np.int64) - vrowptr[:-1][vr]
-            else:
-                rank = np.asarray(order(HostCSR(vrowptr.astype(np.int32), vcol, vval, (n_l, n_c)),
-                                        np.arange(n_l)), np.int64)
-            dst = woff[vr >> 6] - base + rank * 64 + (vr & 63)
-            rel_pairs[dst, 0] = vcol
-            rel_pairs[dst, 1] = vval.view(np.int32)
+                dst = woff[vr >> 6] - base + rank * 64 + (vr & 63)
+                rel_pairs[dst, 0] = vcol
+                rel_pairs[dst, 1] = vval.view(np.int32)
         pairs_parts.append(rel_pairs)
         big = int(max(lgs)) if n_v else 1
         # per wave: diagonals (low 16 bits) and its largest group (bits 16+): a wave whose
@@ -442,6 +451,11 @@ def staged_layout(csrs: Sequence[HostCSR], order: Optional[Callable] = None,
         jm_parts.append(seg.astype(np.int32))
         jmoff.append(jmoff[-1] + len(seg))
         base += n_pairs
+    for k, part in enumerate(pairs_parts):
+        if hasattr(part, "result"):  # a block still being built
+            pairs_parts[k] = np.asarray(part.result(), np.int32).reshape(-1, 2)
+    if pool is not None:
+        pool.shutdown()
     if base >= 2**31:
         raise ValueError("group exceeds int32 indexing")
     # at least one 4-diagonal block: waves without pairs read block 0 unconditionally

@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (21); bumped whenever a struct layout or a signature changes. */
+/* ABI version (22); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -159,8 +159,8 @@ int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
  *     out[c][r][:] = sum_{k in chunk c} sum_{p in row r of A_k} val[p] * X[slab(k)*n_cols + col[p]][:]
  *
  * Layout (built on the host by decagon_amd/sparse.py: staged_layout): per relation, a long
- * row becomes a group of <= 8 equal-length segments (virtual rows; padding pairs have column
- * n_cols and value 0), at most 1024 virtual rows (16 waves of 64 lanes) sorted by length
+ * row becomes a group of <= 8 equal-length segments (virtual rows; padding pairs read one
+ * of sixteen zero columns n_cols .. n_cols + 15, value 0), at most 1024 virtual rows (16 waves of 64 lanes) sorted by length
  * with each group inside one wave; wave w's pairs form a dense block [rlw_w][64] (rlw_w a
  * multiple of 4; holes are padding pairs), lane j's pair at diagonal m at woff_w + 64 m + j:
  *   pairs      [n_pairs][2] int32: (column, fp32 value bits), relations and waves back to
@@ -213,13 +213,17 @@ typedef struct dg_staged_proj {
 int dg_spmm_staged_proj_f32(const dg_staged_group* groups /* HOST */, const dg_staged_proj* projs /* HOST */,
                             int32_t n_groups, int32_t d, void* stream);
 
-/* Host-only layout helper: for one relation in CSR (HOST arrays) and its sorted-row order
- * perm[n_rows] (sorted index -> row, lengths descending), rank_out[p] = the diagonal nonzero
- * p is placed on.  Each row's nonzeros are ordered so that the rows sharing a ds_read_b128
- * lane group in the staged kernel read different LDS bank slots at every diagonal where
- * possible (a fixed order: the row sums change only by rounding, deterministically). */
-int dg_staged_order(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
-                    const int32_t* perm, int32_t* rank_out);
+/* Host-only layout helper: one relation's pair block of the staged layout.  Its lanes
+ * (virtual rows; n_lanes = 64 x waves) are given as a CSR over lanes (HOST arrays: lrowptr
+ * [n_lanes + 1], lcol / lval the lanes' nonzeros in any order), rlw[wave] the wave's diagonals
+ * (>= its longest lane).  Fills pairs [sum rlw x 64][2] (wave w's block after the blocks of
+ * waves < w; lane j's pair at diagonal m at 64 m + j: (column, fp32 value bits); holes
+ * (n_cols + z, 0) with z < 16).  The diagonal of each nonzero and the zero column of each
+ * hole are chosen so that the lanes of each ds_read_b128 lane group read different bank
+ * slots at every diagonal where the relation allows (a fixed order: the row sums change only
+ * by rounding, deterministically). */
+int dg_staged_block(const int32_t* lrowptr, const int32_t* lcol, const float* lval, int32_t n_lanes,
+                    const int32_t* rlw, int32_t n_cols, int32_t* pairs);
 
 /* --------------------------------------------------------------------------------------
  * GCN epilogue (T4 tail + T5 + T6):  for one node type i with groups g = (i, j_1..j_m),

@@ -197,12 +197,15 @@ def test_alias_table_encodes_the_unigram_distribution():
         alias_table(np.zeros(4))
 
 
-def test_staged_layout_reproduces_every_relation():
+@pytest.mark.parametrize("builder", ["feed", "library"])
+def test_staged_layout_reproduces_every_relation(builder):
     """The staged layout (sparse.staged_layout) holds each relation exactly: rebuilding A_k
     from vinfo / woff / rlw / pairs gives the matrix back.  Long rows become groups of 2, 4 or
     8 equal-length segments (zero-column padding), groups sit on consecutive lanes starting at
     a multiple of their size (inside one 64-lane wave and one 16-lane DPP row), lanes are sorted by length, at most `lanes` of them, and every wave's block
-    is dense: lane j's pair at diagonal m sits at woff + 64 m + j (holes are zero pairs)."""
+    is dense: lane j's pair at diagonal m sits at woff + 64 m + j (holes are zero pairs).  With
+    the library's block builder (kernels.staged_block) a lane's nonzeros may sit on any of its
+    wave's diagonals and holes read one of the sixteen zero columns n_c .. n_c + 15."""
     import scipy.sparse as sp
 
     from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, staged_layout
@@ -212,7 +215,11 @@ def test_staged_layout_reproduces_every_relation():
     mats = [sp.random(n_r, n_c, density=dn, random_state=int(rng.integers(1 << 30)), format="csr",
                       dtype=np.float32) for dn in (0.3, 0.0, 0.05, 0.9)]
     lanes = 256
-    lay = staged_layout([coo_to_csr(*sparse_to_tuple(m)) for m in mats], lanes=lanes)
+    block = None
+    if builder == "library":
+        from decagon_amd import kernels
+        block = kernels.staged_block
+    lay = staged_layout([coo_to_csr(*sparse_to_tuple(m)) for m in mats], block, lanes=lanes)
     vals = lay.pairs[:, 1].view(np.float32)
     covered = np.zeros(len(lay.pairs), bool)
     for k, m in enumerate(mats):
@@ -244,10 +251,12 @@ def test_staged_layout_reproduces_every_relation():
                 for mm in range(rlw[w]):
                     p = woff[w] + 64 * mm + j
                     c = lay.pairs[p, 0]
-                    if c == n_c:
-                        assert vals[p] == 0.0                             # padding pair
+                    if c >= n_c:
+                        assert c < n_c + (16 if block else 1) and vals[p] == 0.0   # padding pair
                         continue
-                    assert mm < vlen[i] and row[i] != 1023 and got[row[i], c] == 0
+                    # (the library's colouring may place a lane's nonzero on any of the
+                    # wave's diagonals; feed order keeps them on the lane's first vlen)
+                    assert (block is not None or mm < vlen[i]) and row[i] != 1023 and got[row[i], c] == 0
                     got[row[i], c] = vals[p]
         np.testing.assert_array_equal(got, m.toarray())
     assert covered.all()

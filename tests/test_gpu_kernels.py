@@ -432,7 +432,7 @@ def test_spmm_staged(K, d, n_rows, n_cols, density, out_chunk):
     mats = [_rand_csr(rng, n_rows, n_cols, density, empty_rows=0.1) for _ in range(nrel)]
     mats[3] = sp.csr_matrix((n_rows, n_cols), dtype=np.float32)  # an empty relation
     slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
-    lay = staged_layout([coo_to_csr(*sparse_to_tuple(x)) for x in mats], K.staged_order)
+    lay = staged_layout([coo_to_csr(*sparse_to_tuple(x)) for x in mats], K.staged_block)
     dev = K.StagedDevice.upload(lay, "cuda")
     X = rng.standard_normal((total, n_cols, d)).astype(np.float32)
     n_out = -(-nrel // out_chunk)
@@ -468,7 +468,7 @@ def test_spmm_staged_projected(K, d, n_rows, n_cols, density, out_chunk):
     mats = [_rand_csr(rng, n_rows, n_cols, density, empty_rows=0.1) for _ in range(nrel)]
     mats[5] = sp.csr_matrix((n_rows, n_cols), dtype=np.float32)
     slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
-    lay = staged_layout([coo_to_csr(*sparse_to_tuple(x)) for x in mats], K.staged_order)
+    lay = staged_layout([coo_to_csr(*sparse_to_tuple(x)) for x in mats], K.staged_block)
     dev = K.StagedDevice.upload(lay, "cuda")
     Hp = rng.standard_normal((n_cols, 68)).astype(np.float32)   # leading dimension 68
     W = rng.standard_normal((total, 64, d)).astype(np.float32)
