@@ -409,10 +409,39 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
     }
     if sharded:
         rec["rank_ms_per_step"] = el * 1e3 / steps
+        if args.backend == "nccl" and use_graph:
+            rec["phases"] = phase_times(plan, dec, stream, dist, min(kernel_reps, 20))
     del plan, dec
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return rec, graph
+
+
+def phase_times(plan, dec, stream, dist, reps):
+    """The sharded step taken apart on this rank (every rank runs the same sequence): each
+    compute phase between two collectives and each exchange (the layer's RCCL all-reduce /
+    all-gather), each timed alone as `reps` back-to-back launches in one hipGraph; and the
+    bytes each exchange moves.  compute + exchange ≈ the step (the step also pays the
+    boundaries between them); the max over ranks of each is reported."""
+    import torch
+
+    phases = plan.phases()
+    last = max(i for i, (kind, _) in enumerate(phases) if kind == "compute")
+    out = {"compute_us": [], "exchange_us": [], "exchange_bytes": []}
+    layers = [L for L in (plan._layer1, plan._layer2) if L.has_exchange]
+    for i, (kind, fn) in enumerate(phases):
+        body = (lambda fn=fn: (fn(), dec())) if i == last else fn
+        out["compute_us" if kind == "compute" else "exchange_us"].append(time_kernel(body, reps, stream) * 1e3)
+    for L in layers:
+        nb = 0 if L.flat is None or L.allreduce is None else 4 * L.flat.numel()
+        out["exchange_bytes"].append({"allreduce": nb, "allgather": sum(4 * o.numel() for o, _ in L.gathers)})
+    t = torch.tensor(out["compute_us"] + out["exchange_us"], dtype=torch.float64, device=stream.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n_c = len(out["compute_us"])
+    out["compute_us"], out["exchange_us"] = t[:n_c].tolist(), t[n_c:].tolist()
+    out["compute_total_us"] = sum(out["compute_us"])
+    out["exchange_total_us"] = sum(out["exchange_us"])
+    return out
 
 
 # ----------------------------------------------------------------------------- config 5

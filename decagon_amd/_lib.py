@@ -26,6 +26,7 @@ DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
 DG_GROUP_DROPOUT = 2
+DG_GROUP_DENSE_ROWS = 4  # dg_gcn_fused_f32 only: row r of the group's sum is x[r]
 DG_MAX_ADAM_SEGS = 32
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}

@@ -257,7 +257,12 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
     const int q = lane % LP;
     if (live && gl < t.g_count) {
         const SpmmGroupK& g = a.g[t.g_begin + gl];
-        const float4 s = range_sum<LP>(g, g.x, g.rowptr[r], g.rowptr[r + 1], d, part, W);
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!g.rowptr) {  // DG_GROUP_DENSE_ROWS: the sum is x[r] (the group's first wave loads it)
+            if (part == 0 && q * 4 < d) s = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.x_ld + q * 4);
+        } else {
+            s = range_sum<LP>(g, g.x, g.rowptr[r], g.rowptr[r + 1], d, part, W);
+        }
         if (lane < LP) pbuf[wave][lane] = s;
     }
     __syncthreads();
@@ -555,9 +560,23 @@ extern "C" int32_t dg_abi_version(void) { return 22; }
 namespace {
 
 // Validate one descriptor and copy it into the kernel form.  Returns DG_OK or an error.
-int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k, bool allow_shared = false) {
+int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k, bool allow_shared = false,
+                  bool allow_dense = false) {
     if (s.n_rows < 0 || s.n_chunks < 1 || s.x_rows < 0) return DG_EINVAL;
-    if (s.flags & ~(DG_GROUP_SHARED_PATTERN | DG_GROUP_DROPOUT)) return DG_EINVAL;
+    if (s.flags & ~(DG_GROUP_SHARED_PATTERN | DG_GROUP_DROPOUT | DG_GROUP_DENSE_ROWS)) return DG_EINVAL;
+    if (s.flags & DG_GROUP_DENSE_ROWS) {  // row r of the sum is x[r]: no adjacency
+        if (!allow_dense || s.flags != DG_GROUP_DENSE_ROWS || s.n_chunks != 1 || s.x_rows < s.n_rows || !s.x)
+            return DG_EINVAL;
+        if (!dg::aligned16(s.x) || (s.x_ld & 3)) return DG_EALIGN;
+        if (s.x_ld < d || (int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;
+        k = SpmmGroupK{};
+        k.x = s.x;
+        k.x_ld = static_cast<int32_t>(s.x_ld);
+        k.n_rows = s.n_rows;
+        k.n_chunks = 1;
+        k.drop_keep = 1.f;
+        return DG_OK;  // k.rowptr == nullptr marks the dense form in the kernel
+    }
     if ((s.flags & DG_GROUP_SHARED_PATTERN) && !allow_shared) return DG_EINVAL;
     if (s.flags & DG_GROUP_DROPOUT) {  // per-chunk masks of a shared pattern only
         if (!(s.flags & DG_GROUP_SHARED_PATTERN) || !s.drop_state || s.drop_stride < 0) return DG_EINVAL;
@@ -641,7 +660,7 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
     a.wpg = waves_per_group;
     for (int i = 0; i < n_groups; ++i) {
         if (groups[i].n_chunks != 1) return DG_EINVAL;  // fused mode: the whole group is one chunk
-        const int rc = convert_group(groups[i], d, false, a.g[i]);
+        const int rc = convert_group(groups[i], d, false, a.g[i], false, true);
         if (rc != DG_OK) return rc;
     }
     int64_t blocks = 0;

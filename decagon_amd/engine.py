@@ -322,7 +322,7 @@ class ForwardPlan:
             self.keep, self.drop_state = float(dropout[0]), dropout[1]
         # flat mode: every group's pre-normalisation sum S_ij lands in one flat buffer per
         # layer (all-reduced when sharded; kept for the backward when training), and one fused
-        # launch over identity "adjacencies" finishes every node type from it
+        # launch over dense-rows groups (DG_GROUP_DENSE_ROWS) finishes every node type from it
         self.flat_mode = allreduce is not None or keep_sums
         self.keep_sums = keep_sums
         self.sums_mode = False  # set below: partial mode whose epilogue also writes each S_ij
@@ -560,7 +560,6 @@ class ForwardPlan:
         for s in range(0, len(specs), DG_MAX_GROUPS):
             launches.append(kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d))
             self.launch_groups[id(launches[-1])] = spmm_ets[s:s + DG_MAX_GROUPS]
-        launches += reduces
         need_zero = send is flat and flat is not None and any(g.groups[et].n_rels == 0 for et in red)
         epis, local_epis, gathers = [], [], []
         if split_t:
@@ -571,12 +570,28 @@ class ForwardPlan:
                 r0 = self.shard.rank * blk
                 blocks.append(([partials[et] for et in self.targets[i]], pad[r0:r0 + (b - a)], b - a))
                 gathers.append((pad, pad[r0:r0 + blk]))
+            # the relation-sharded node types' chunk reduces ride in the same launch: a target
+            # whose groups write their pre-normalisation sums into the send buffer (its
+            # finished rows go to a scratch buffer, unread) — one launch per layer instead of two
+            red_t = [i for i in self.targets if i not in self.row_block
+                     and any(et in views and g.groups[et].n_rels and partials[et][1] > 1 for et in self.targets[i])]
+            n_groups = sum(len(self.targets[i]) for i in split_t + red_t)
+            if reduces and len(split_t) + len(red_t) <= 8 and n_groups <= DG_MAX_GROUPS:
+                for i in red_t:
+                    grp_parts = []
+                    for et in self.targets[i]:
+                        part, nc = partials[et][:2]
+                        reduced = et in views and g.groups[et].n_rels and nc > 1
+                        grp_parts.append((part, nc, sviews[et] if reduced else None))
+                    blocks.append((grp_parts, torch.empty((n[i], d), **f32), n[i]))
+                reduces = []
             local_epis.append(kernels.PreparedEpilogueMulti(blocks, d, flags))
+        launches += reduces
         if flat is not None:
-            # sharded: the all-reduced group sums S_ij are finished by ONE fused launch over
-            # identity "adjacencies" (row r gathers S_ij[r] with weight 1.0f: exact), so the
-            # l2norm, Σ_j, relu and (layer 1) the layer-2 projections of every node type run in
-            # one kernel after the exchange
+            # sharded: the all-reduced group sums S_ij are finished by ONE fused launch whose
+            # groups are the dense rows S_ij[r] themselves (DG_GROUP_DENSE_ROWS), so the l2norm,
+            # Σ_j, relu and (layer 1) the layer-2 projections of every node type run in one
+            # kernel after the exchange
             tl = [i for i in self.targets if i not in self.row_block]
             pspecs = []
             for tgt_node, pj in projs:
@@ -601,18 +616,10 @@ class ForwardPlan:
                       local_epis, gathers, self.allgather)
 
     def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
-        """A group spec whose 'adjacency' is the identity of node type i (one nonzero 1.0f per
-        row): the fused kernel then reads the dense rows x[r] as the group sums."""
+        """A group spec with no adjacency (DG_GROUP_DENSE_ROWS): the fused kernel reads the dense
+        rows x[r] as the group sums."""
         n_i = self.g.n_nodes[i]
-        if not hasattr(self, "_eye"):
-            self._eye = {}
-        if i not in self._eye:
-            dev = self.g.device
-            self._eye[i] = (torch.arange(n_i + 1, dtype=torch.int32, device=dev),
-                            torch.arange(n_i, dtype=torch.int32, device=dev),
-                            torch.ones(n_i, dtype=torch.float32, device=dev))
-        rp, vc, vv = self._eye[i]
-        return kernels.RelGroupSpec(rp, vc, vv, x, None, n_i, 1, d, n_i, vcol_max=n_i - 1)
+        return kernels.RelGroupSpec(None, None, None, x, None, n_i, 1, d, n_i, dense=True)
 
     def run_layer1(self) -> None:
         for p in self._pre:

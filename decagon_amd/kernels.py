@@ -62,8 +62,19 @@ class RelGroupSpec:
                                   # (device state {seed, step}, stream tag, keep) — chunk c scales
                                   # nonzero p by mask element c·nnz + (drop_index[p] or p)
     drop_index: Optional[torch.Tensor] = None
+    dense: bool = False           # DG_GROUP_DENSE_ROWS (dg_gcn_fused_f32 only): row r of the sum
+                                  # is x[r]; rowptr / vcol / val unused (may be None)
 
     def validate(self, d: int, need_out: bool = True) -> None:
+        if self.dense:
+            _dev(self.x, torch.float32, "x")
+            if self.n_chunks != 1 or self.shared or self.drop is not None:
+                raise ValueError("a dense-rows group is one chunk, no shared pattern, no dropout")
+            if self.x_ld < d or self.x_ld % 4:
+                raise ValueError("x_ld must be >= d and a multiple of 4")
+            if self.x_rows < self.n_rows or (self.n_rows and self.x.numel() < (self.n_rows - 1) * self.x_ld + d):
+                raise ValueError("x smaller than the group's rows")
+            return
         _dev(self.rowptr, torch.int32, "rowptr")
         _dev(self.vcol, torch.int32, "vcol")
         _dev(self.val, torch.float32, "val")
@@ -108,6 +119,13 @@ class RelGroupSpec:
 
 
 def _fill_group(g, s: RelGroupSpec) -> None:
+    if s.dense:
+        g.rowptr = g.vcol = g.val = g.out = None
+        g.x = s.x.data_ptr()
+        g.x_ld, g.n_rows, g.n_chunks, g.x_rows = s.x_ld, s.n_rows, 1, s.x_rows
+        g.flags = _lib.DG_GROUP_DENSE_ROWS
+        g.drop_state = g.drop_index = None
+        return
     g.rowptr = s.rowptr.data_ptr()
     g.vcol = s.vcol.data_ptr() if s.vcol.numel() else None
     g.val = s.val.data_ptr() if s.val.numel() else None

@@ -71,7 +71,8 @@ typedef struct dg_rel_group {
     int32_t x_rows;             /* rows of X addressable (bound on vcol); per chunk when  */
                                 /* DG_GROUP_SHARED_PATTERN is set                         */
     int32_t flags;              /* 0, or DG_GROUP_SHARED_PATTERN [| DG_GROUP_DROPOUT]      */
-                                /* (dg_spmm_groups_f32 only)                              */
+                                /* (dg_spmm_groups_f32 only), or DG_GROUP_DENSE_ROWS       */
+                                /* (dg_gcn_fused_f32 only)                                */
     uint32_t drop_tag;          /* DG_GROUP_DROPOUT: mask stream of the group             */
     float drop_keep;            /* DG_GROUP_DROPOUT: keep probability in (0, 1]           */
     int32_t drop_stride;        /* DG_GROUP_DROPOUT: mask elements per chunk (the nnz of  */
@@ -93,6 +94,12 @@ typedef struct dg_rel_group {
  * of every relation (layers.py:23-31, :88), each relation its own draw, the backward X_jᵀ·G_k
  * (drop_index: the transposed pattern's nonzeros mapped to the forward's) on the same masks. */
 #define DG_GROUP_DROPOUT 2
+
+/* dg_gcn_fused_f32 only: the group has no adjacency — row r of its sum IS row r of X
+ * (x[r * x_ld ..], n_chunks == 1, x_rows >= n_rows; rowptr / vcol / val unused, may be NULL).
+ * The sharded forward finishes its all-reduced pre-normalisation sums S_ij this way
+ * (layers.py:92-93 after the cross-rank Σ_k), without an identity CSR's two dependent loads. */
+#define DG_GROUP_DENSE_ROWS 4
 
 int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
                        int32_t d, void* stream);

@@ -1,7 +1,8 @@
 """Cycle breakdown of dg_spmm_staged_f32 on config P (profiling aid).
 
-Build (here):   python scripts/staged_prof.py build     -> scripts/prof_build/libdecagon_hip_prof.so
-Run (GPU box):  python scripts/staged_prof.py run [bins]
+Build (here):   python scripts/staged_prof.py build [NAME -DFLAG ...]
+                                 -> scripts/prof_build/libdecagon_hip_prof[_NAME].so
+Run (GPU box):  python scripts/staged_prof.py run [bins]   (DG_PROF_LIB=<.so> for a named build)
 Per wave of each workgroup: cycles at the relation barrier, filling the other buffers and
 issuing the next prefetch, reading the relation tables, gathering, and accumulating; printed
 per relation as means over blocks, one column per wave, for layer 1 and layer 2.
@@ -20,13 +21,17 @@ def build():
     sys.path.insert(0, str(ROOT))
     from decagon_amd import _build
     OUT.parent.mkdir(exist_ok=True)
+    out, flags = OUT, []
+    if len(sys.argv) > 2:
+        out = OUT.with_name(f"libdecagon_hip_prof_{sys.argv[2]}.so")
+        flags = sys.argv[3:]
     cmd = [_build.hipcc(), "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared", "-DDG_STAGED_PROF",
-           f"-I{ROOT / 'include'}", f"-I{_build.CSRC}", "-o", str(OUT), *map(str, _build._sources())]
+           *flags, f"-I{ROOT / 'include'}", f"-I{_build.CSRC}", "-o", str(out), *map(str, _build._sources())]
     subprocess.run(cmd, check=True)
 
 
 def run():
-    os.environ["DG_LIB"] = str(OUT)
+    os.environ["DG_LIB"] = os.environ.get("DG_PROF_LIB", str(OUT))
     os.environ["DG_STAGED"] = "1"
     if len(sys.argv) > 2:
         os.environ["DG_STAGED_BINS"] = sys.argv[2]
