@@ -86,6 +86,7 @@ class RelationShard:
     row_block: Dict[int, Tuple[int, int, int]] = field(default_factory=dict)
     # allgather(out [world * blk, d], inp = out[rank * blk:(rank + 1) * blk]) — in place
     allgather: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None
+    scheme: str = "relations LPT-sharded"  # how the relations were dealt (describe())
 
     @staticmethod
     def lpt(edge_types: Dict[EdgeType, int], rel_cost: Dict[EdgeType, Sequence[float]], rank: int,
@@ -155,7 +156,7 @@ class RelationShard:
         """Weak scaling: the graph holds world_size relation sets; rank r owns set r, i.e.
         relations [r*K_ij, (r+1)*K_ij) of every group."""
         local = {et: list(range(rank * k, (rank + 1) * k)) for et, k in edge_types_per_rank.items()}
-        return RelationShard(rank, world_size, local, allreduce)
+        return RelationShard(rank, world_size, local, allreduce, scheme="one relation set per GPU")
 
     def local_csr(self, csr: Dict[EdgeType, Sequence]) -> Dict[EdgeType, list]:
         """The graph's per-group relation lists with the relations of other ranks replaced by
@@ -173,7 +174,7 @@ class RelationShard:
     def describe(self, backend: str = "nccl") -> str:
         lib = "RCCL" if backend == "nccl" else backend
         rs = ", ".join(f"node type {t} row-split" for t in sorted(self.row_block))
-        return (f"x{self.world_size}: relations LPT-sharded" + (f", {rs}" if rs else "")
+        return (f"x{self.world_size}: {self.scheme}" + (f", {rs}" if rs else "")
                 + f"; {lib} all-reduce of the relation-sharded sums"
                 + (" + all-gather of the row-split rows" if rs else "") + " per layer")
 
