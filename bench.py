@@ -12,8 +12,9 @@ included — SURVEY §8d).  Inputs are resident in HBM before timing (uploaded o
 Workloads (BASELINE.json configs):
   S (default, configs[1]): main.py's 5-relation / 10-matrix synthetic, the exact
      reference-normalised adjacencies (decagon_amd/data/synthetic_S_adj.npz), d = 64/32,
-     fp32.  At N GPUs the graph holds N relation sets, one per GPU (weak scaling); each layer
-     all-reduces the per-(i,j) pre-normalisation sums over RCCL.
+     fp32.  At N GPUs the graph holds N relation sets, one per GPU (weak scaling); every node
+     type is row-split — each rank finishes its row block over all N sets in the fused kernel
+     and the blocks are all-gathered over RCCL (two all-gathers per step, no all-reduce).
   P (configs[2]/[3]): polypharmacy-shaped 19,085 + 645 nodes, 964 side effects ⇒ 1,932
      drug-drug matrices, ≈23 M nnz; at N GPUs the drug×drug relations are LPT-sharded and the
      protein rows row-split (strong scaling, sharding.py).
@@ -80,7 +81,7 @@ def parse(argv=None):
                     help="N > 1 over RCCL: capture the whole step, collectives included, in one "
                          "hipGraph (graph), or replay the compute phases between eager collectives")
     ap.add_argument("--simulate-world", type=int, default=0,
-                    help="config P: time each rank's share of an N-GPU sharded step on this one GPU, "
+                    help="config P / S: time each rank's share of an N-GPU sharded step on this one GPU, "
                          "collectives replaced by no-ops (prints per-rank step times and the bytes each "
                          "collective would move)")
     ap.add_argument("--simulate-rank", type=int, default=-1,
@@ -123,7 +124,16 @@ def build_workload(config, rank, world, sharded, backend="nccl"):
     if config == "S":
         base = synthetic.load_S()
         graph = synthetic.replicate_sets(base, world) if world > 1 else base
-        shard = RelationShard.blocks(base.edge_types, rank, world, allreduce) if sharded else None
+        shard = None
+        if sharded:
+            # weak scaling: the graph holds one relation set per GPU; every node type is
+            # row-split (each rank finishes its row block over every set's relations in the
+            # fused kernel, then the blocks are all-gathered — no all-reduce of sums)
+            nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
+            shard = RelationShard.split(graph.edge_types, graph.n_nodes, nnz, rank, world, allreduce,
+                                        coll[1], row_split_min=1)
+            shard.chunks = dict(graph.edge_types)  # one chunk per group: the fused kernel's form
+            shard.fused_rows = True
         scaling = "weak"
         workload = ("S: main.py 5-relation / 10-matrix synthetic (reference-normalised, 105,974 nnz "
                     "per relation set), 2 GCN layers d=64/32 + DEDICOM decoder B=512+512")
@@ -146,8 +156,9 @@ def make_plan(args, graph, shard, device, keep_sums=False, dropout=None):
     csr = graph.csr()
     if shard is not None:  # only local relations need host CSR / upload
         csr = shard.local_csr(csr)
+    chunk = args.chunk if shard is None or shard.chunks is None else shard.chunks
     dg = DeviceGraph(graph.edge_types, csr, device, None if shard is None else shard.local,
-                     chunk=args.chunk, target_waves=args.target_waves,
+                     chunk=chunk, target_waves=args.target_waves,
                      row_block=None if shard is None else shard.row_block)
     rng = np.random.default_rng(1234)
     n = graph.n_nodes
@@ -630,24 +641,34 @@ def main_train(args):
 
 # ----------------------------------------------------------------------------- rehearsal
 def main_simulate(args):
-    """One GPU standing in for each rank of an N-GPU config-P step in turn: the rank's shard
-    (proteins row-split, drug×drug relations LPT-sharded) with the collectives replaced by
-    no-ops, timed as the bench times a step.  max over ranks + the collectives' time is the
-    N-GPU step; the bytes each collective moves are printed beside it."""
+    """One GPU standing in for each rank of an N-GPU step in turn: the rank's shard (config P:
+    proteins row-split, drug×drug relations LPT-sharded; config S: N relation sets, every node
+    type row-split and finished in the fused kernel) with the collectives replaced by no-ops,
+    timed as the bench times a step.  max over ranks + the collectives' time is the N-GPU step
+    (DESIGN §6); the bytes each collective moves are printed beside it."""
     import torch
 
     from decagon_amd import synthetic
-    from decagon_amd.sharding import RelationShard
+    from decagon_amd.sharding import RelationShard, _no_op, _no_op_reduce
 
     torch.cuda.set_device(0)
     device = torch.device("cuda", 0)
     N = args.simulate_world
-    graph = synthetic.make_P(seed=0)
+    if args.config == "S":
+        graph = synthetic.replicate_sets(synthetic.load_S(), N)
+    else:
+        graph = synthetic.make_P(seed=0)
     stream = torch.cuda.Stream(device)
     G = steps_per_graph(args.steps, args.graph_steps)
     ranks = []
     for r in (range(N) if args.simulate_rank < 0 else [args.simulate_rank]):
-        shard = RelationShard.polypharmacy(graph, r, N, comm=False)
+        if args.config == "S":
+            nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
+            shard = RelationShard.split(graph.edge_types, graph.n_nodes, nnz, r, N, _no_op_reduce, _no_op,
+                                        row_split_min=1)
+            shard.chunks, shard.fused_rows = dict(graph.edge_types), True
+        else:
+            shard = RelationShard.polypharmacy(graph, r, N, comm=False)
         plan, dg = make_plan(args, graph, shard, device)
         dec = Decoder(graph, plan, device, r)
 
@@ -669,7 +690,7 @@ def main_simulate(args):
         del plan, dec, dg
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-    rec = {"metric": "config P sharded-step rehearsal on one GPU (collectives not run)", "world": N,
+    rec = {"metric": f"config {args.config} sharded-step rehearsal on one GPU (collectives not run)", "world": N,
            "steps": args.steps, "warmup": args.warmup, "steps_per_graph": G,
            "max_rank_ms_per_step": max(x["ms_per_step"] for x in ranks), "ranks": ranks}
     print(json.dumps(rec), file=JSON_OUT, flush=True)

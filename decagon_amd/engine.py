@@ -474,10 +474,23 @@ class ForwardPlan:
 
     # ------------------------------------------------------------------ layer builder
     def _fused_targets(self) -> List[int]:
-        if self.flat_mode:
+        """Node types one dg_gcn_fused_f32 launch finishes: at most FUSED_MAX_ROWS (local) rows,
+        every group one chunk (and not staged).  Sharded plans finish only row-split node types
+        this way, when the shard asks for it (`fused_rows`: their rows are complete on this
+        rank; relation-sharded ones need the all-reduce first), and the sharded backward takes
+        none."""
+        if self.flat_mode and (self.keep_sums or not self.row_block
+                               or not getattr(self.shard, "fused_rows", False)):
             return []
+
+        def rows(i):
+            if i in self.row_block:
+                return self.row_block[i][1] - self.row_block[i][0]
+            return self.g.n_nodes[i]
+
         return [i for i, ets in self.targets.items()
-                if self.g.n_nodes[i] <= FUSED_MAX_ROWS
+                if (not self.flat_mode or i in self.row_block)
+                and 0 < rows(i) <= FUSED_MAX_ROWS
                 and all(self.g.groups[et].n_chunks == 1 and self.g.groups[et].n_rels > 0
                         and not self.g.groups[et].staged for et in ets)]
 
@@ -495,28 +508,45 @@ class ForwardPlan:
         outs = self.hidden1 if relu else self.embeddings
         launches: List[Callable[[], None]] = []
         fused_t = self.fused
+        gathers = []
         if fused_t:
             # waves per group: small launches (latency-bound) split the densest row group's
             # batches of 64 over up to two waves; big launches have parallelism to spare
             avg = max(g.groups[et].nnz / max(1, g.groups[et].n_rows) for i in fused_t for et in self.targets[i])
             max_groups = max(len(self.targets[i]) for i in fused_t)
-            rows = sum(n[i] for i in fused_t)
-            wpg = 1 if rows >= 4096 else int(max(1, min(2, 16 // max_groups, math.ceil(avg / 64.0))))
+            rows = sum(g.groups[self.targets[i][0]].n_rows for i in fused_t)
+            # (row blocks of N relation sets — config S's weak scaling — have N times longer
+            # rows over 1/N of the rows: up to 16 waves per row there; measured at N = 8, rank
+            # 0's layer 1: 27.0 µs at 2 waves per group)
+            cap = 16 // max_groups if self.row_block else 2
+            wpg = 1 if rows >= 4096 else int(max(1, min(cap, 16 // max_groups, math.ceil(avg / 64.0))))
             if os.environ.get("DG_WPG"):  # tuning override
                 wpg = max(1, min(int(os.environ["DG_WPG"]), 16 // max_groups))
             pspecs = []
             for tgt_node, pj in projs:
-                pj.target = fused_t.index(tgt_node)
-                pspecs.append(pj)
-            launches.append(kernels.PreparedFused(
-                [(outs[i], n[i], [self._spec(et, xs[et], None, d) for et in self.targets[i]], relu)
-                 for i in fused_t], d, pspecs, wpg))
+                if tgt_node in fused_t:  # (sharded: the finishing launch projects the others)
+                    pj.target = fused_t.index(tgt_node)
+                    pspecs.append(pj)
+            tgts = []
+            for i in fused_t:
+                out, rows_i = outs[i], n[i]
+                if i in self.row_block:
+                    # a row-split node type (sharded): this rank's block, finished in place in the
+                    # padded output, then all-gathered
+                    a, b, blk = self.row_block[i]
+                    pad = self._pad[i, d]
+                    r0 = self.shard.rank * blk
+                    out, rows_i = pad[r0:r0 + (b - a)], b - a
+                    gathers.append((pad, pad[r0:r0 + blk]))
+                tgts.append((out, rows_i, [self._spec(et, xs[et], None, d) for et in self.targets[i]], relu))
+            launches.append(kernels.PreparedFused(tgts, d, pspecs, wpg))
             self.launch_groups[id(launches[-1])] = [et for i in fused_t for et in self.targets[i]]
         rest = [et for et in self.edge_types if et[0] not in fused_t]
         flags = DG_EPI_L2NORM | (DG_EPI_RELU if relu else 0)
-        # row-split node types (sharded): their groups run in partial mode over this rank's
-        # row block and one epilogue finishes the block before the exchange
-        split_t = [i for i in self.targets if i in self.row_block]
+        # row-split node types (sharded) not finished by the fused launch: their groups run in
+        # partial mode over this rank's row block and one epilogue finishes the block before
+        # the exchange
+        split_t = [i for i in self.targets if i in self.row_block and i not in fused_t]
         red = [et for et in rest if et[0] not in self.row_block]
         flat, views, send, sviews = None, {}, None, {}
         if self.flat_mode and red:
@@ -561,7 +591,7 @@ class ForwardPlan:
             launches.append(kernels.PreparedSpmm(specs[s:s + DG_MAX_GROUPS], d))
             self.launch_groups[id(launches[-1])] = spmm_ets[s:s + DG_MAX_GROUPS]
         need_zero = send is flat and flat is not None and any(g.groups[et].n_rels == 0 for et in red)
-        epis, local_epis, gathers = [], [], []
+        epis, local_epis = [], []
         if split_t:
             blocks = []
             for i in split_t:
@@ -673,6 +703,12 @@ class ForwardPlan:
         return pick(self._layer1), pick(self._layer2)
 
     # ---- accounting (bench / DESIGN.md roofline) ----
+    def _out_rows(self, i: int) -> int:
+        """Rows of node type i this plan finishes (a row-split rank: its block)."""
+        if i in self.row_block:
+            return self.row_block[i][1] - self.row_block[i][0]
+        return self.g.n_nodes[i]
+
     def group_bytes(self, et: EdgeType, d: int, fused: bool, layer: int = 1) -> int:
         """Algorithmic bytes of one group's SpMM: its CSR once (4 B per row of each
         relation + 8 B per nonzero), its dense operands once (4·d B per row of each X_k) and,
@@ -697,7 +733,7 @@ class ForwardPlan:
         fused = isinstance(launch, kernels.PreparedFused)
         tot = sum(self.group_bytes(et, d, fused, layer) for et in ets)
         if fused:
-            tot += sum(4 * d * self.g.n_nodes[i] for i in L.fused_targets)
+            tot += sum(4 * d * self._out_rows(i) for i in L.fused_targets)
             if layer == 1:
                 for pj in launch._keep[2]:
                     K, din, dout = pj.w.shape
@@ -725,7 +761,7 @@ class ForwardPlan:
             if et[0] not in L.fused_targets:
                 tot += 4 * d * grp.n_rows
         for i in L.fused_targets:
-            tot += 4 * d * self.g.n_nodes[i]
+            tot += 4 * d * self._out_rows(i)
         if layer == 1:
             for f in L.launches:
                 if isinstance(f, kernels.PreparedFused):

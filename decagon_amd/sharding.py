@@ -87,6 +87,12 @@ class RelationShard:
     # allgather(out [world * blk, d], inp = out[rank * blk:(rank + 1) * blk]) — in place
     allgather: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None
     scheme: str = "relations LPT-sharded"  # how the relations were dealt (describe())
+    # relations per chunk the plan should use per edge type (None: the plan's policy) — a
+    # row-split plan whose blocks the fused kernel finishes needs one chunk per group
+    chunks: Optional[Dict[EdgeType, int]] = None
+    # row-split node types finished by the fused SpMM kernel over their row block (one chunk
+    # per group; config S's weak scaling) instead of partial mode + an epilogue
+    fused_rows: bool = False
 
     @staticmethod
     def lpt(edge_types: Dict[EdgeType, int], rel_cost: Dict[EdgeType, Sequence[float]], rank: int,
@@ -174,6 +180,9 @@ class RelationShard:
     def describe(self, backend: str = "nccl") -> str:
         lib = "RCCL" if backend == "nccl" else backend
         rs = ", ".join(f"node type {t} row-split" for t in sorted(self.row_block))
+        shared = any(t not in self.row_block for et in self.local for t in [et[0]])
+        if self.row_block and not shared:
+            return f"x{self.world_size}: every node type row-split; {lib} all-gather of the finished rows per layer"
         return (f"x{self.world_size}: {self.scheme}" + (f", {rs}" if rs else "")
                 + f"; {lib} all-reduce of the relation-sharded sums"
                 + (" + all-gather of the row-split rows" if rs else "") + " per layer")

@@ -5,7 +5,9 @@ device; the 8-GPU RCCL run is the driver's).  Every rank must end with the full 
 embeddings, equal to oracle/decagon_oracle.py's restatement of the reference forward
 (decagon/deep/layers.py:85-118, model.py:64-88) within 1e-4 relative — for
 
-  * config S, relations LPT-sharded (BASELINE configs[1] on N GPUs);
+  * config S, relations LPT-sharded;
+  * config S's weak-scaling form (bench.py at N GPUs): one relation set per rank, every node
+    type row-split and finished in the fused kernel, the blocks all-gathered, on 2 and 3 ranks;
   * a scaled-down config P with the proteins row-split and the drug×drug relations
     LPT-sharded into the LDS-staged kernel (configs[3]'s plan), on 2 and 3 ranks (uneven
     row blocks, a short last block);
@@ -32,11 +34,13 @@ def _weights(g, seed, s1=0.1, s2=0.3):
     return w1, w2
 
 
-def _graph(kind):
+def _graph(kind, world=1):
     from decagon_amd import synthetic
 
     if kind == "S":
         return synthetic.load_S()
+    if kind == "S-rows":
+        return synthetic.replicate_sets(synthetic.load_S(), world)
     if kind == "P-small":
         return synthetic.make_P(seed=3, n_proteins=1500, n_drugs=150, n_side_effects=60, ppi_edges=12000,
                                 target_edges=1200)
@@ -49,6 +53,12 @@ def _shard(kind, g, rank, world):
     nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
     if kind == "S":
         return RelationShard.lpt(g.edge_types, nnz, rank, world, torch_allreduce())
+    if kind == "S-rows":
+        sh = RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
+                                 row_split_min=1)
+        sh.chunks = dict(g.edge_types)
+        sh.fused_rows = True
+        return sh
     return RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
                                row_split_min=1000)
 
@@ -57,16 +67,17 @@ def _rank(rank, world, kind):
     from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
 
     dev = torch.device("cuda", 0)
-    g = _graph(kind)
+    g = _graph(kind, world)
     shard = _shard(kind, g, rank, world)
     w1, w2 = _weights(g, 5)
-    dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local, row_block=shard.row_block)
+    dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local, row_block=shard.row_block,
+                     chunk=shard.chunks)
     plan = ForwardPlan(dg, {0: None, 1: None},
                        LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
                        LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, 32,
                        shard=shard)
     info = {"row_split": sorted(shard.row_block), "staged": dg.groups[(1, 1)].staged,
-            "local": {et: len(v) for et, v in shard.local.items()}}
+            "local": {et: len(v) for et, v in shard.local.items()}, "fused": sorted(plan.fused)}
     plan.run()
     torch.cuda.synchronize()
 
@@ -120,11 +131,13 @@ def _check(kind, world):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     got = run_ranks(_rank, world, (kind,))
-    g = _graph(kind)
+    g = _graph(kind, world)
     h1, emb = _oracle(kind, g)
     for r in range(world):
         info, eager, graphed = got[r]
-        if kind != "S":
+        if kind == "S-rows":
+            assert info["row_split"] == [0, 1] and info["fused"] == [0, 1], info  # fused row blocks
+        elif kind != "S":
             assert info["row_split"] == [0], info          # proteins row-split
             assert info["staged"], info                    # drug×drug in the LDS-staged kernel
         for form in (eager, graphed):
@@ -133,14 +146,23 @@ def _check(kind, world):
                 assert rel_err(form[1][t], emb[t]) <= TOL, (r, "embeddings", t)
         for t in (0, 1):  # the graph-captured phases reproduce the eager forward bit for bit
             assert np.array_equal(eager[0][t], graphed[0][t]) and np.array_equal(eager[1][t], graphed[1][t])
-    # every relation of a relation-sharded group is owned by exactly one rank
+    # every relation of a relation-sharded group is owned by exactly one rank; a row-split
+    # group's relations by every rank (each over its row block)
+    split = got[0][0]["row_split"]
     for et in g.edge_types:
         owned = sum(got[r][0]["local"][et] for r in range(world))
-        assert owned == (g.edge_types[et] * (world if kind != "S" and et[0] == 0 else 1))
+        assert owned == (g.edge_types[et] * (world if et[0] in split else 1))
 
 
 def test_sharded_S_forward_matches_oracle():
     _check("S", 2)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_weak_scaling_S_row_split_matches_oracle(world):
+    """bench.py's config S at N GPUs: N relation sets, every node type row-split and finished
+    in the fused kernel over all N sets' relations, blocks all-gathered."""
+    _check("S-rows", world)
 
 
 @pytest.mark.parametrize("world", [2, 3])
