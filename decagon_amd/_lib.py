@@ -7,6 +7,7 @@ package fails loudly instead of silently running on the CPU.
 from __future__ import annotations
 
 import ctypes
+import threading
 import os
 from pathlib import Path
 from ctypes import POINTER, c_float, c_int32, c_int64, c_uint64, c_void_p
@@ -210,6 +211,7 @@ SIGNATURES = {
 }
 
 _LIB = None
+_LOAD_LOCK = threading.Lock()  # staged_layout's thread pool may make the first call
 
 
 class KernelError(RuntimeError):
@@ -221,6 +223,13 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
+    with _LOAD_LOCK:
+        if _LIB is None:
+            _LIB = _load(build_if_missing)
+    return _LIB
+
+
+def _load(build_if_missing: bool) -> ctypes.CDLL:
     override = os.environ.get("DG_LIB")  # an instrumented build (scripts/staged_prof.py)
     path = Path(override) if override else _build.lib_path()
     if not override and (not path.exists() or (build_if_missing and _build.needs_build())):
@@ -235,7 +244,6 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     got = lib.dg_abi_version()
     if got != ABI_VERSION:
         raise ImportError(f"libdecagon_hip ABI {got} != expected {ABI_VERSION}; rebuild")
-    _LIB = lib
     return lib
 
 

@@ -268,6 +268,7 @@ class DeviceGraph:
             g.host = loc  # local relations in device order (the backward builds Âᵀ from them)
             if staged:
                 lay = staged_layout(loc, kernels.staged_block,
+                                    lanes=int(os.environ.get("DG_STAGED_LANES", "1024")),
                                     split=os.environ.get("DG_STAGED_SPLIT", "1") != "0")
                 g.layout = kernels.StagedDevice.upload(lay, device)
             self.groups[et] = g
