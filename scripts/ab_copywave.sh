@@ -1,7 +1,8 @@
-# A/B of the staged kernel's copy-wave form (config P): default build vs DG_STAGED_COPYWAVE
+# A/B of the staged kernel's copy-wave form (config P): default build vs DG_STAGED_COPYWAVE=1/2/3
 # build with the layout's lanes at 960 (wave 15 left without pairs) and at 1024; then the
 # staged parity tests on the variant.  Usage on the box: bash scripts/ab_copywave.sh <tag>
 set -o pipefail
+# Build the variants first: python scripts/variants.py build cwN -DDG_STAGED_COPYWAVE=N (N = 1, 2, 3)
 out=gpurun_out/${1:-abcw}; mkdir -p $out
 run() {  # name, env...
   local name=$1; shift
