@@ -11,134 +11,15 @@
 // accumulator column by l[j]·V[p][j] and the 32 lanes of a half-wave fold the row sums with
 // a shuffle butterfly.  Nothing of size B×B is formed.
 #include "common.h"
+#include "decoder_tile.h"
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-// Draw #idx of the counter-based unigram sampler from a Walker alias table: entry j holds
-// {acceptance probability (float bits), alias index}.  One 64-bit hash gives the column j
-// (high 32 bits, scaled by range) and the 24-bit acceptance uniform (low bits): one 8-byte
-// load per draw, no search.
-__device__ __forceinline__ int unigram_draw(const uint2* table, int range, uint64_t seed,
-                                            uint64_t idx) {
-    const uint64_t h = splitmix64(seed ^ splitmix64(idx));
-    const int j = (int)(((h >> 32) * (uint64_t)range) >> 32);
-    const float u = (float)(h & 0xFFFFFFu) * (1.0f / 16777216.0f);
-    const uint2 e = table[j];
-    return u < __uint_as_float(e.x) ? j : (int)e.y;
-}
-
-struct DecTab {
-    const float* row_table;
-    const float* col_table;
-    const float* G;
-    const float* l;
-    int64_t ld_row;
-    int64_t ld_col;
-    int32_t d;
-    int32_t vec4;  // row_table, ld_row and l allow 16-byte loads
-};
-
-// Scores of 32 pairs on one wave: lane i (both halves) names pair i by its row index
-// `ridx` (into row_table) and column index `cidx` (into col_table); `valid` masks pairs
-// past the end.  T = (U∘l)·G runs on v_mfma_f32_32x32x2_f32 in k-blocks of 32 whose A/B
-// fragments are loaded up front (one memory round trip per block, not per k-step); then
-// score[p] = Σ_j T[p][j]·l[j]·V[p][j] is folded over the 32 lanes of each half-wave.
-// Returns the score of pair (r&3)+8(r>>2)+4h in part[r] of lane 0 / 32.
-__device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, bool valid,
-                                           float (&part)[16]) {
-    const int lane = threadIdx.x & 63;
-    const int i = lane & 31;
-    const int h = lane >> 5;
-    const int d = t.d;
-    const float* u = t.row_table + (int64_t)ridx * t.ld_row;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) part[r] = 0.f;
-    if (d == 32) {
-        // one k-block, one n-block: every load (G, l, U row, V rows) in flight together, then
-        // the 16 MFMAs.  MFMA s takes k = 16h + s from lane half h (the contraction order is
-        // free), so each lane's A operand is 16 contiguous floats of its U row: 4 float4 loads
-        float av[16], bv[16], v[16];
-        if (!t.vec4) {
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const float a = valid ? u[16 * h + s] : 0.f;
-                av[s] = t.l ? a * t.l[16 * h + s] : a;
-            }
-        } else {
-            const float4* u4 = reinterpret_cast<const float4*>(u + 16 * h);
-            const float4* l4 = reinterpret_cast<const float4*>(t.l + 16 * h);
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                float4 a4 = valid ? u4[s4] : make_float4(0.f, 0.f, 0.f, 0.f);
-                if (t.l) {
-                    const float4 w4 = l4[s4];
-                    a4 = make_float4(a4.x * w4.x, a4.y * w4.y, a4.z * w4.z, a4.w * w4.w);
-                }
-                av[4 * s4] = a4.x;
-                av[4 * s4 + 1] = a4.y;
-                av[4 * s4 + 2] = a4.z;
-                av[4 * s4 + 3] = a4.w;
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < 16; ++s) bv[s] = t.G[(16 * h + s) * 32 + i];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int prow = (r & 3) + 8 * (r >> 2) + 4 * h;
-            v[r] = t.col_table[(int64_t)__shfl(cidx, prow) * t.ld_col + i];
-        }
-        const float lj = t.l ? t.l[i] : 1.0f;
-        f32x16 acc = {};
-#pragma unroll
-        for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) part[r] = fmaf(acc[r] * lj, v[r], 0.f);
-    }
-#pragma unroll 1
-    for (int n0 = 0; d != 32 && n0 < d; n0 += 32) {
-        f32x16 acc = {};
-#pragma unroll 1
-        for (int k0 = 0; k0 < d; k0 += 32) {
-            float av[16], bv[16];
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const int kk = k0 + 2 * s + h;
-                float a = valid ? u[kk] : 0.f;
-                if (t.l) a *= t.l[kk];
-                av[s] = a;
-                bv[s] = t.G[(int64_t)kk * d + n0 + i];
-            }
-#pragma unroll
-            for (int s = 0; s < 16; ++s)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
-        }
-        const int j = n0 + i;
-        const float lj = t.l ? t.l[j] : 1.0f;
-        float v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int prow = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int c = __shfl(cidx, prow);  // lane prow names pair prow
-            v[r] = t.col_table[(int64_t)c * t.ld_col + j];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) part[r] = fmaf(acc[r] * lj, v[r], part[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-#pragma unroll
-        for (int m = 1; m < 32; m <<= 1) part[r] += __shfl_xor(part[r], m);
-    }
-}
+using dg::DecTab;
+using dg::f32x16;
+using dg::score_tile;
+using dg::splitmix64;
+using dg::unigram_draw;
 
 struct DecArgs {
     DecTab t;

@@ -25,6 +25,7 @@
 // the next layer's projection of the finished row.
 #include "common.h"
 #include "dropout.h"
+#include "decoder_tile.h"
 
 #ifndef DG_FUSED_ABL
 #define DG_FUSED_ABL 0  // timing ablations only (wrong results): 1 no gathers, 8 empty kernels
@@ -230,15 +231,17 @@ struct FusedArgs {
     int32_t rpb;  // rows per workgroup (blockDim = 64 · rpb · max groups · wpg)
 };
 
-template <int LP>
-__global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
+// The fused layer for workgroup b.  kPublish (the layer-2 + decoder launch): the finished rows
+// are stored write-through (sc1), every storing wave drains them, and after the workgroup
+// barrier one lane adds 1 to arrival shard b % 8 (cdna_hip_programming.md Guideline 16 R1: the
+// decoder workgroups poll the shards and read the rows with sc1 loads).
+template <int LP, bool kPublish>
+__device__ __forceinline__ void fused_body(const FusedArgs& a, const int b, uint32_t* arrive) {
     __shared__ float4 pbuf[16][LP];
     __shared__ float4 ybuf[kFusedRpb][DG_MAX_GROUPS][LP];
     __shared__ float hrow[kFusedRpb][4 * LP];
-    if (DG_FUSED_ABL & 8) return;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int b = blockIdx.x;
     int ti = 0;
 #pragma unroll 1
     while (ti + 1 < a.n_targets && b >= a.t[ti + 1].block_begin) ++ti;
@@ -286,8 +289,24 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
             tot.z = fmaxf(tot.z, 0.f);
             tot.w = fmaxf(tot.w, 0.f);
         }
-        if (lane * 4 < d) *reinterpret_cast<float4*>(t.out + (int64_t)r * d + lane * 4) = tot;
+        if (lane * 4 < d) {
+            float* o = t.out + (int64_t)r * d + lane * 4;
+            if (kPublish) {
+                const float v[4] = {tot.x, tot.y, tot.z, tot.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    __hip_atomic_store((dg::gf32*)(o + e), v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                *reinterpret_cast<float4*>(o) = tot;
+            }
+        }
         reinterpret_cast<float4*>(hrow[slot])[lane] = tot;
+    }
+    if (kPublish) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_add(arrive + 32 * (b & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (a.n_projs == 0) return;  // launch-uniform
 #ifdef DG_FUSED_NOPROJ  // timing ablation only (wrong results)
@@ -331,6 +350,155 @@ __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
         for (int s2 = 0; s2 < kFusedRpb; ++s2)
             if (s2 < nr) po[(int64_t)s2 * dout] = acc[s2];
     }
+}
+
+template <int LP>
+__global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
+    if (DG_FUSED_ABL & 8) return;
+    fused_body<LP, false>(a, blockIdx.x, nullptr);
+}
+
+// Layer 2 + decoder + hinge in one launch (config S, one GPU; optimizer.py:37-57, :116-120 on
+// the embeddings model.py:85-88 just produced): the workgroups past the fused layer's score
+// 32-pair tiles of the batch — waves 2s / 2s+1 the positives / negatives of tile s — exactly
+// as decoder_hinge_kernel does, after waiting for every layer workgroup's arrival.  They sit at
+// the end of the grid and never hold a layer workgroup back (those wait for nothing); the
+// wait is bounded (a timeout sets a sticky word instead of hanging).
+// Workspace (uint32): arrival shard s at [32 s] (s < 8, one per 128-B line), the ticket at
+// [256], the timeout word at [257], the decoder workgroups' hinge partials from [260].
+constexpr int kStepTicket = 256;
+constexpr int kStepTimeout = 257;
+constexpr int kStepPartial = 260;
+constexpr uint32_t kStepSpinMax = 1u << 22;
+
+struct StepHingeK {
+    dg::DecTab t;
+    const int32_t* rows;
+    const int32_t* cols;
+    const int32_t* neg_given;
+    const uint2* alias;
+    float* pos;
+    float* neg;
+    int32_t* neg_rows_out;
+    float* loss;
+    uint32_t* ws;
+    uint64_t seed;
+    uint64_t offset;
+    int32_t range;
+    int32_t n;
+    float margin;
+    int32_t fused_blocks;
+    int32_t dec_blocks;
+    int32_t pad;
+};
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+__device__ __forceinline__ void step_hinge_body(const StepHingeK& h, const int blk) {
+    __shared__ float sc[8][2][32];
+    __shared__ float red[8];
+    __shared__ int last;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int tiles = (int)(blockDim.x >> 7);  // two waves per 32-pair tile
+    const int ts = wave >> 1;
+    const int side = wave & 1;  // 0: positives, 1: negatives
+    const bool act = ts < tiles;  // wave-uniform (an odd last wave idles)
+    const int i = lane & 31;
+    const int hh = lane >> 5;
+    const int b0 = (blk * tiles + ts) * 32;
+    const int b = b0 + i;
+    const bool valid = act && b < h.n;
+    // the batch and the negative draws need no embedding: they overlap the layer
+    int ridx = 0, cidx = 0;
+    if (valid) {
+        cidx = h.cols[b];
+        if (side == 0)
+            ridx = h.rows[b];
+        else if (h.neg_given)
+            ridx = h.neg_given[b];
+        else
+            ridx = dg::unigram_draw(h.alias, h.range, h.seed, h.offset + (uint64_t)b);
+        if (side == 1 && h.neg_rows_out && hh == 0) h.neg_rows_out[b] = ridx;
+    }
+    if (wave == 0) {  // ONE wave polls the eight arrival shards (relaxed sc1 loads)
+        uint32_t spins = 0;
+#pragma unroll 1
+        for (;;) {
+            uint32_t c = lane < 8 ? __hip_atomic_load((gu32*)(h.ws + 32 * lane), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0u;
+#pragma unroll
+            for (int m = 1; m < 8; m <<= 1) c += __shfl_xor(c, m);
+            c = __shfl(c, 0);
+            if (c >= (uint32_t)h.fused_blocks) break;
+            if (++spins > kStepSpinMax) {
+                if (lane == 0)
+                    __hip_atomic_store((gu32*)(h.ws + kStepTimeout), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();  // the other waves load the rows only after the poll matched
+    float part[16];
+    if (act) {
+        dg::score_tile<true>(h.t, ridx, cidx, valid, part);
+        if (i == 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int q = (r & 3) + 8 * (r >> 2) + 4 * hh;
+                const float v = (b0 + q < h.n) ? part[r] : 0.f;
+                sc[ts][side][q] = v;
+                if (b0 + q < h.n) (side == 0 ? h.pos : h.neg)[b0 + q] = v;
+            }
+        }
+    }
+    __syncthreads();
+    if (act && side == 0) {
+        float term = 0.f;
+        if (lane < 32 && b0 + lane < h.n) term = fmaxf(sc[ts][1][lane] - (sc[ts][0][lane] - h.margin), 0.f);
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) term += __shfl_xor(term, m);
+        if (lane == 0) red[ts] = term;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float p = 0.f;
+        for (int s = 0; s < tiles; ++s) p += red[s];  // tile order
+        // partial stored write-through and drained before the ticket (decoder_hinge_kernel)
+        __hip_atomic_store((dg::gf32*)(reinterpret_cast<float*>(h.ws) + kStepPartial + blk), p, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(h.ws + kStepTicket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (tk == (uint32_t)h.dec_blocks - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last) return;  // block-uniform
+    if (threadIdx.x >= 64) return;
+    float s = 0.f;  // lane l sums partials l, l + 64, ...; a butterfly folds the lanes (fixed order)
+    for (int k = lane; k < h.dec_blocks; k += 64)
+        s += __hip_atomic_load((dg::gf32*)(reinterpret_cast<float*>(h.ws) + kStepPartial + k), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
+    if (lane == 0) {
+        h.loss[0] = s;
+        // every decoder workgroup has passed its poll (its ticket came after it) and every layer
+        // workgroup has arrived: reset the words for the next launch
+        __hip_atomic_store((gu32*)(h.ws + kStepTicket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int sh = 0; sh < 8; ++sh)
+            __hip_atomic_store((gu32*)(h.ws + 32 * sh), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int LP>
+__global__ __launch_bounds__(512) void gcn_fused_hinge_kernel(const FusedArgs a, const StepHingeK h) {
+    if ((int)blockIdx.x < h.fused_blocks)
+        fused_body<LP, true>(a, blockIdx.x, h.ws);
+    else
+        step_hinge_body(h, (int)blockIdx.x - h.fused_blocks);
 }
 
 struct EpiGroupK {
@@ -554,7 +722,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 22; }
+extern "C" int32_t dg_abi_version(void) { return 23; }
 
 
 namespace {
@@ -642,17 +810,17 @@ extern "C" int dg_spmm_groups_f32(const dg_rel_group* groups, int32_t n_groups, 
     return dg::launch_status();
 }
 
-extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
-                                const dg_fused_target* targets, int32_t n_targets,
-                                const dg_proj* projs, int32_t n_projs, int32_t waves_per_group,
-                                int32_t d, void* stream) {
+namespace {
+// The fused launch's arguments, grid and workgroup size (dg_gcn_fused_f32's checks).
+int prep_fused(const dg_rel_group* groups, int32_t n_groups, const dg_fused_target* targets, int32_t n_targets,
+               const dg_proj* projs, int32_t n_projs, int32_t waves_per_group, int32_t d, FusedArgs& a,
+               int64_t& blocks, int& threads) {
     if (n_groups < 1 || !groups || n_targets < 1 || !targets) return DG_EINVAL;
     if (n_groups > DG_MAX_GROUPS || n_targets > DG_MAX_GROUPS || n_projs > DG_MAX_GROUPS)
         return DG_ETOOMANY;
     if (n_projs < 0 || (n_projs > 0 && !projs)) return DG_EINVAL;
     if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
     if (waves_per_group < 1) return DG_EINVAL;
-    FusedArgs a{};
     a.d = d;
     a.n_groups = n_groups;
     a.n_targets = n_targets;
@@ -663,7 +831,7 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
         const int rc = convert_group(groups[i], d, false, a.g[i], false, true);
         if (rc != DG_OK) return rc;
     }
-    int64_t blocks = 0;
+    blocks = 0;
     int max_groups = 1;
     for (int t = 0; t < n_targets; ++t) {
         const dg_fused_target& s = targets[t];
@@ -695,14 +863,79 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
             return DG_EINVAL;
         a.p[i] = ProjK{s.w, s.rel_map, s.out, s.n_rels, s.target, s.d_out, 0};
     }
-    if (blocks == 0) return DG_OK;
     if (blocks > 0x7fffffff) return DG_EINVAL;
+    threads = 64 * rpb * max_groups * waves_per_group;
+    return DG_OK;
+}
+}  // namespace
+
+extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
+                                const dg_fused_target* targets, int32_t n_targets,
+                                const dg_proj* projs, int32_t n_projs, int32_t waves_per_group,
+                                int32_t d, void* stream) {
+    FusedArgs a{};
+    int64_t blocks = 0;
+    int threads = 0;
+    const int rc = prep_fused(groups, n_groups, targets, n_targets, projs, n_projs, waves_per_group, d, a, blocks,
+                              threads);
+    if (rc != DG_OK) return rc;
+    if (blocks == 0) return DG_OK;
     const int lp = dg::lanes_per_row(d);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    dim3 grid(static_cast<unsigned>(blocks)), block(64 * rpb * max_groups * waves_per_group);
+    dim3 grid(static_cast<unsigned>(blocks)), block(threads);
 #define DG_LAUNCH_FUSED(L) hipLaunchKernelGGL(gcn_fused_kernel<L>, grid, block, 0, st, a)
     DG_LP_SWITCH(lp, DG_LAUNCH_FUSED)
 #undef DG_LAUNCH_FUSED
+    return dg::launch_status();
+}
+
+extern "C" int dg_gcn_fused_hinge_f32(const dg_rel_group* groups, int32_t n_groups,
+                                      const dg_fused_target* targets, int32_t n_targets,
+                                      const dg_proj* projs, int32_t n_projs, int32_t waves_per_group,
+                                      int32_t d, const dg_hinge_desc* hd, void* stream) {
+    FusedArgs a{};
+    int64_t blocks = 0;
+    int threads = 0;
+    const int rc = prep_fused(groups, n_groups, targets, n_targets, projs, n_projs, waves_per_group, d, a, blocks,
+                              threads);
+    if (rc != DG_OK) return rc;
+    if (!hd) return DG_EINVAL;
+    const dg_hinge_desc& q = *hd;
+    if (q.n < 1 || q.d <= 0 || (q.d % 32) || q.d > 256) return DG_EINVAL;
+    if (!q.row_table || !q.col_table || !q.rows || !q.cols || !q.G || !q.pos || !q.neg || !q.loss || !q.workspace)
+        return DG_EINVAL;
+    if (!q.neg_rows && (!q.alias_table || q.range < 1)) return DG_EINVAL;
+    if (q.ld_row < q.d || q.ld_col < q.d) return DG_EINVAL;
+    if (!dg::aligned16(q.workspace)) return DG_EALIGN;
+    if (threads < 128 || threads > 512) return DG_EINVAL;  // two waves per 32-pair tile; <= 512 threads
+    const int tiles = threads >> 7;
+    const int64_t dec_blocks = dg::ceil_div(q.n, 32 * tiles);
+    if (blocks + dec_blocks > 0x7fffffff) return DG_EINVAL;
+    StepHingeK h{};
+    h.t = dg::DecTab{q.row_table, q.col_table, q.G, q.l, q.ld_row, q.ld_col, q.d,
+                     dg::aligned16(q.row_table) && (q.ld_row & 3) == 0 && (!q.l || dg::aligned16(q.l))};
+    h.rows = q.rows;
+    h.cols = q.cols;
+    h.neg_given = q.neg_rows;
+    h.alias = reinterpret_cast<const uint2*>(q.alias_table);
+    h.pos = q.pos;
+    h.neg = q.neg;
+    h.neg_rows_out = q.neg_rows_out;
+    h.loss = q.loss;
+    h.ws = reinterpret_cast<uint32_t*>(q.workspace);
+    h.seed = q.seed;
+    h.offset = q.offset;
+    h.range = q.range;
+    h.n = q.n;
+    h.margin = q.margin;
+    h.fused_blocks = static_cast<int32_t>(blocks);
+    h.dec_blocks = static_cast<int32_t>(dec_blocks);
+    const int lp = dg::lanes_per_row(d);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(blocks + dec_blocks)), block(threads);
+#define DG_LAUNCH_FH(L) hipLaunchKernelGGL(gcn_fused_hinge_kernel<L>, grid, block, 0, st, a, h)
+    DG_LP_SWITCH(lp, DG_LAUNCH_FH)
+#undef DG_LAUNCH_FH
     return dg::launch_status();
 }
 

@@ -666,6 +666,22 @@ class ForwardPlan:
         self.run_layer1()
         self.run_layer2()
 
+    def fold_hinge(self, hinge: "kernels.PreparedDecoderHinge") -> bool:
+        """Run `hinge` (the decoder step on this plan's embeddings) inside layer 2's launch
+        (dg_gcn_fused_hinge_f32) when layer 2 is one fused launch with nothing after it (one
+        GPU, every node type fused: config S); then the caller must not launch `hinge` itself.
+        Returns whether it folded."""
+        L = self._layer2
+        if (self.shard is not None or L.has_exchange or L.epilogues or L.local_epilogues or L.need_zero
+                or len(L.launches) != 1 or not isinstance(L.launches[0], kernels.PreparedFused)):
+            return False
+        f = L.launches[0]
+        if not 2 <= f.block_threads() <= 8:
+            return False
+        L.launches = [kernels.PreparedFusedHinge(f, hinge)]
+        self.folded_hinge = L.launches[0]
+        return True
+
     def phases(self) -> List[Tuple[str, Callable[[], None]]]:
         """The forward as alternating ("compute", fn) / ("exchange", fn) phases: the device
         launches between two collectives form one compute phase (capturable into one
@@ -699,7 +715,7 @@ class ForwardPlan:
     @property
     def spmm_launches(self):
         """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""
-        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged)
+        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged, kernels.PreparedFusedHinge)
         pick = lambda L: [l for l in L.launches if isinstance(l, kinds)]
         return pick(self._layer1), pick(self._layer2)
 

@@ -148,6 +148,7 @@ def _fill_group(g, s: RelGroupSpec) -> None:
         g.drop_index = s.drop_index.data_ptr() if s.drop_index is not None else None
 
 
+FUSED_RPB = 1  # spmm.hip kFusedRpb: rows per fused workgroup, at most
 SPMM_LDS_MAX_ROWS = 160 * 1024 // 144  # dg_spmm_groups_lds_f32: operand rows staged in LDS
 
 
@@ -245,7 +246,13 @@ class PreparedFused:
         self._garr, self._tarr, self._parr = garr, tarr, parr
         self._ng, self._nt, self._np, self.d = len(specs), len(targets), len(projs), d
         self.wpg = waves_per_group
+        self._max_groups = max_groups
         self._fn = _lib.load().dg_gcn_fused_f32
+
+    def block_threads(self) -> int:
+        """Waves per workgroup of this launch (dg_gcn_fused_f32's rows-per-workgroup rule)."""
+        rpb = max(1, min(FUSED_RPB, 16 // (self._max_groups * self.wpg)))
+        return rpb * self._max_groups * self.wpg
 
     def __call__(self, stream=None) -> None:
         check(self._fn(self._garr, self._ng, self._tarr, self._nt, self._parr if self._np else None, self._np,
@@ -798,6 +805,43 @@ class PreparedDecoderHinge:
         a = list(self._args)
         a[9], a[10] = self.seed & (2**64 - 1), self.offset & (2**64 - 1)
         check(self._fn(*a, _stream_ptr(stream)), "dg_decoder_hinge_f32")
+
+
+class PreparedFusedHinge:
+    """dg_gcn_fused_hinge_f32: a PreparedFused layer and a PreparedDecoderHinge step in ONE
+    launch (the decoder workgroups wait in-launch for the layer's rows).  Same buffers and the
+    same outputs as running `fused` then `hinge` (the loss summed in another fixed order);
+    `timeouts()` reads the sticky word the in-launch wait sets if it ever gives up."""
+
+    WS_WORDS = 260  # arrival shards, ticket, timeout word; the partials follow
+
+    def __init__(self, fused: "PreparedFused", hinge: "PreparedDecoderHinge"):
+        if not 2 <= fused.block_threads() <= 8:
+            raise ValueError("the fused layer's workgroup must have 2..8 waves (128..512 threads)")
+        self.fused, self.hinge = fused, hinge
+        a = hinge._args
+        n = a[11]
+        dev = hinge.pos.device
+        self._ws = torch.zeros(self.WS_WORDS + 4 + -(-n // 32), device=dev, dtype=torch.int32)
+        self.desc = _lib.DgHingeDesc()
+        self._fn = _lib.load().dg_gcn_fused_hinge_f32
+
+    def _fill(self) -> None:
+        a, q = self.hinge._args, self.desc
+        (q.row_table, q.ld_row, q.col_table, q.ld_col, q.rows, q.cols, q.neg_rows, q.alias_table, q.range) = a[:9]
+        q.seed, q.offset = self.hinge.seed & (2**64 - 1), self.hinge.offset & (2**64 - 1)
+        q.n, q.G, q.l, q.d, q.margin = a[11], a[12], a[13], a[14], a[15]
+        q.pos, q.neg, q.neg_rows_out, q.loss = a[16], a[17], a[18], a[19]
+        q.workspace = self._ws.data_ptr()
+
+    def timeouts(self) -> int:
+        return int(self._ws[257].item())
+
+    def __call__(self, stream=None) -> None:
+        f = self.fused
+        self._fill()
+        check(self._fn(f._garr, f._ng, f._tarr, f._nt, f._parr if f._np else None, f._np, f.wpg, f.d,
+                       ctypes.byref(self.desc), _stream_ptr(stream)), "dg_gcn_fused_hinge_f32")
 
 
 # --------------------------------------------------------------------------------------
