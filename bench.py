@@ -59,6 +59,9 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
     ap.add_argument("--no-fold", action="store_true",
                     help="launch the decoder step on its own instead of inside layer 2's launch")
+    ap.add_argument("--fold", choices=["step", "layer2", "none"], default="step",
+                    help="config S on one GPU: the whole step in one launch (step), layer 2 + decoder "
+                         "in one launch (layer2), or three launches (none)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per form")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
@@ -204,6 +207,11 @@ class Decoder:
         self.folded = plan.fold_hinge(self.fused)
         return self.folded
 
+    def fold_step(self, plan) -> bool:
+        """The whole forward step in one launch (dg_gcn_step_f32) when the plan allows it."""
+        self.folded = plan.fold_step(self.fused)
+        return self.folded
+
     def __call__(self):
         if not getattr(self, "folded", False):
             self.fused()
@@ -328,7 +336,9 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
     graph, shard, scaling, workload = build_workload(config, rank, world, sharded, args.backend)
     plan, dg = make_plan(args, graph, shard, device)
     dec = Decoder(graph, plan, device, rank)
-    folded = False if args.no_fold else dec.fold(plan)
+    mode_fold = "none" if args.no_fold else args.fold
+    folded = {"none": lambda: False, "layer2": lambda: dec.fold(plan), "step": lambda: dec.fold_step(plan)}[mode_fold]()
+    folded = mode_fold if folded else False
 
     def step():
         plan.run()
@@ -427,7 +437,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
                         "frac": l1_bytes / (l1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "edges_per_s": dg.total_nnz / (l1_ms * 1e-3)},
         "spmm_layer2_ms": k2_ms,
-        "decoder_in_layer2_launch": folded,  # spmm_layer2_ms then includes the decoder step
+        "folded": folded,  # "layer2": spmm_layer2_ms includes the decoder; "step": one launch per step
     }
     if folded and plan.folded_hinge.timeouts():
         raise RuntimeError("the in-launch decoder wait timed out (dg_gcn_fused_hinge_f32)")

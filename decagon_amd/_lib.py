@@ -94,6 +94,12 @@ class DgHingeDesc(ctypes.Structure):
                 ("workspace", c_void_p)]
 
 
+class DgFusedLayer(ctypes.Structure):
+    _fields_ = [("groups", POINTER(DgRelGroup)), ("n_groups", c_int32), ("n_targets", c_int32),
+                ("targets", POINTER(DgFusedTarget)), ("projs", POINTER(DgProj)), ("n_projs", c_int32),
+                ("waves_per_group", c_int32), ("d", c_int32), ("reserved", c_int32)]
+
+
 class DgEpiGroup(ctypes.Structure):
     _fields_ = [("partial", c_void_p), ("sum_out", c_void_p), ("n_chunks", c_int32), ("reserved", c_int32)]
 
@@ -166,6 +172,7 @@ SIGNATURES = {
         [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, POINTER(DgProj), c_int32, c_int32,
          c_int32, POINTER(DgHingeDesc), c_void_p],
     ),
+    "dg_gcn_step_f32": (c_int32, [POINTER(DgFusedLayer), POINTER(DgFusedLayer), POINTER(DgHingeDesc), c_void_p]),
     "dg_gcn_epilogue_multi_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, c_void_p]),
     "dg_gcn_epilogue_f32": (
         c_int32,

@@ -69,14 +69,15 @@ __device__ __forceinline__ float4 ld_emb4(const float* p) {
 // fragments are loaded up front (one memory round trip per block, not per k-step); then
 // score[p] = Σ_j T[p][j]·l[j]·V[p][j] is folded over the 32 lanes of each half-wave.
 // Returns the score of pair (r&3)+8(r>>2)+4h in part[r] of lane 0 / 32.  kSc1: every load of
-// row_table / col_table is an sc1 load (the tables were written in this launch).
-template <bool kSc1 = false>
+// row_table / col_table is an sc1 load (the tables were written in this launch).  kD: the width
+// when known at compile time (only that path is compiled: fewer registers), else 0.
+template <bool kSc1 = false, int kD = 0>
 __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, bool valid,
                                            float (&part)[16]) {
     const int lane = threadIdx.x & 63;
     const int i = lane & 31;
     const int h = lane >> 5;
-    const int d = t.d;
+    const int d = kD ? kD : t.d;
     const float* u = t.row_table + (int64_t)ridx * t.ld_row;
 #pragma unroll
     for (int r = 0; r < 16; ++r) part[r] = 0.f;

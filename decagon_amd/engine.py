@@ -663,6 +663,10 @@ class ForwardPlan:
         self._layer2.run()
 
     def run(self) -> None:
+        step = getattr(self, "folded_step", None)
+        if step is not None:
+            step()
+            return
         self.run_layer1()
         self.run_layer2()
 
@@ -680,6 +684,25 @@ class ForwardPlan:
             return False
         L.launches = [kernels.PreparedFusedHinge(f, hinge)]
         self.folded_hinge = L.launches[0]
+        return True
+
+    def fold_step(self, hinge: "kernels.PreparedDecoderHinge") -> bool:
+        """The whole step in one launch (dg_gcn_step_f32): layer 1, layer 2 and `hinge`, when
+        both layers are one fused launch each with nothing between or after them (one GPU,
+        every node type fused, projections in layer 1's epilogue: config S).  Then run()
+        launches only that (and the caller must not launch `hinge`); the per-layer launches
+        stay available to time alone.  Returns whether it folded."""
+        L1, L2 = self._layer1, self._layer2
+        plain = lambda L: (not L.has_exchange and not L.epilogues and not L.local_epilogues and not L.need_zero
+                           and len(L.launches) == 1 and isinstance(L.launches[0], kernels.PreparedFused))
+        if self.shard is not None or self._pre or self._gemm2 or not plain(L1) or not plain(L2):
+            return False
+        f1, f2 = L1.launches[0], L2.launches[0]
+        if (f1.d != 64 or f2.d != 32 or f2._np or f1.block_threads() != f2.block_threads()
+                or not 2 <= f1.block_threads() <= 8 or any(s.dense for s in f2._keep[0])):
+            return False
+        self.folded_step = kernels.PreparedStep(f1, f2, hinge)
+        self.folded_hinge = self.folded_step
         return True
 
     def phases(self) -> List[Tuple[str, Callable[[], None]]]:

@@ -193,6 +193,30 @@ typedef struct dg_hinge_desc {
                                 /* before the first call (the launch leaves it re-armed)     */
 } dg_hinge_desc;
 
+/* The whole config-S forward step in ONE launch: layer 1 (fused, with the layer-2 projection
+ * epilogue), layer 2 (fused, reading those projections) and the decoder step of
+ * dg_gcn_fused_hinge_f32 — each stage's workgroups after the previous stage's in the grid, each
+ * waiting in-launch (bounded) for the previous stage's published bytes.  Results equal
+ * dg_gcn_fused_f32(layer1), dg_gcn_fused_f32(layer2), dg_decoder_hinge_f32 (the loss in another
+ * fixed order).  Requirements: layer1.d == 64, layer2.d == 32, layer2 without projections and
+ * without DG_GROUP_DENSE_ROWS groups, layer-2 operands < 2 GB, both layers' workgroups of the
+ * same size in 128..512 threads; workspace >= 2064 + 4*ceil(n/32) bytes, zeroed before the
+ * first call.  Replaces layers.py:70-118 + model.py:64-88 + optimizer.py:37-57, :116-120. */
+typedef struct dg_fused_layer {
+    const dg_rel_group* groups;     /* HOST */
+    int32_t n_groups;
+    int32_t n_targets;
+    const dg_fused_target* targets; /* HOST */
+    const dg_proj* projs;           /* HOST, may be NULL */
+    int32_t n_projs;
+    int32_t waves_per_group;
+    int32_t d;
+    int32_t reserved;
+} dg_fused_layer;
+
+int dg_gcn_step_f32(const dg_fused_layer* layer1 /* HOST */, const dg_fused_layer* layer2 /* HOST */,
+                    const dg_hinge_desc* hinge /* HOST */, void* stream);
+
 int dg_gcn_fused_hinge_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
                            const dg_fused_target* targets /* HOST */, int32_t n_targets,
                            const dg_proj* projs /* HOST, may be NULL */, int32_t n_projs,

@@ -27,7 +27,7 @@ def _plan_S():
         r = np.sqrt(6.0 / (a + b))
         return torch.from_numpy(rng.uniform(-r, r, size=(k, a, b)).astype(np.float32)).cuda()
 
-    dgr = DeviceGraph(g.edge_types, g.csr(), "cuda", None)
+    dgr = DeviceGraph(g.edge_types, g.csr(), torch.device("cuda"), None)
     w1 = LayerWeights({et: glorot(K, g.n_nodes[et[1]], 64) for et, K in g.edge_types.items()})
     w2 = LayerWeights({et: glorot(K, 64, 32) for et, K in g.edge_types.items()})
     plan = ForwardPlan(dgr, {j: None for j in g.n_nodes}, w1, w2, 64, 32)
@@ -168,7 +168,7 @@ def test_fold_refused_where_it_does_not_apply():
         pytest.skip("no HIP device")
     g = synthetic.make_P(seed=3, n_proteins=5000, n_drugs=60, n_side_effects=6)
     rng = np.random.default_rng(0)
-    dgr = DeviceGraph(g.edge_types, g.csr(), "cuda", None)
+    dgr = DeviceGraph(g.edge_types, g.csr(), torch.device("cuda"), None)
     mk = lambda K_, a, b: torch.from_numpy(rng.uniform(-0.1, 0.1, (K_, a, b)).astype(np.float32)).cuda()
     w1 = LayerWeights({et: mk(K_, g.n_nodes[et[1]], 64) for et, K_ in g.edge_types.items()})
     w2 = LayerWeights({et: mk(K_, 64, 32) for et, K_ in g.edge_types.items()})
@@ -176,3 +176,65 @@ def test_fold_refused_where_it_does_not_apply():
     E = plan.embeddings
     op = _hinge(K, g, rng, E[1], E[1], 32, 64, given=True)
     assert not plan.fold_hinge(op)
+
+
+def _step_ref(plan, op):
+    plan.run()
+    op()
+    projs = [pj.out for pj in plan._layer1.launches[0]._keep[2]]
+    outs = [plan.hidden1[0], plan.hidden1[1], plan.embeddings[0], plan.embeddings[1]] + projs
+    return outs, _snap(outs, op)
+
+
+@pytest.mark.parametrize("given", [False, True])
+@pytest.mark.parametrize("n", [512, 1300])
+def test_whole_step_in_one_launch(n, given):
+    """dg_gcn_step_f32: layer 1 (+ the layer-2 projections), layer 2 and the decoder step in
+    one launch equal the three launches — hidden1, the projections, the embeddings, negatives
+    and scores bit for bit — launch after launch, and the scores match the oracle."""
+    from decagon_amd import kernels as K
+
+    g, plan, rng = _plan_S()
+    E = plan.embeddings
+    op = _hinge(K, g, rng, E[1], E[0], 32, n, given)
+    outs, ref = _step_ref(plan, op)
+    assert plan.fold_step(op)
+    for _ in range(3):
+        for t in outs + [op.pos, op.neg, op.loss]:
+            t.fill_(float("nan"))
+        plan.run()
+        got = _snap(outs, op)
+        for a, b in zip(ref[:-1], got[:-1]):
+            assert np.array_equal(a, b)
+        assert abs(got[-1] - ref[-1]) <= 1e-6 * max(1.0, abs(ref[-1]))
+    assert plan.folded_step.timeouts() == 0
+    _check_oracle(op, E[1], E[0])
+
+
+def test_whole_step_hipgraph_replays():
+    """The one-launch step captured G times into a hipGraph and replayed back to back."""
+    from decagon_amd import kernels as K
+
+    g, plan, rng = _plan_S()
+    E = plan.embeddings
+    op = _hinge(K, g, rng, E[1], E[1], 32, 512)
+    outs, ref = _step_ref(plan, op)
+    assert plan.fold_step(op)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        plan.run()
+        s.synchronize()
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg, stream=s, capture_error_mode="thread_local"):
+            for _ in range(10):
+                plan.run()
+        for _ in range(5):
+            for t in outs:
+                t.fill_(float("nan"))
+            cg.replay()
+    s.synchronize()
+    got = _snap(outs, op)
+    for a, b in zip(ref[:-1], got[:-1]):
+        assert np.array_equal(a, b)
+    assert abs(got[-1] - ref[-1]) <= 1e-6 * max(1.0, abs(ref[-1]))
+    assert plan.folded_step.timeouts() == 0
