@@ -57,11 +57,10 @@ def parse(argv=None):
                     help="S / P: the GCN forward step (metric: edges/s); D: config 5, bf16 DEDICOM "
                          "scoring of every drug-drug slot's batch (metric: scored pairs/s)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
-    ap.add_argument("--no-fold", action="store_true",
-                    help="launch the decoder step on its own instead of inside layer 2's launch")
-    ap.add_argument("--fold", choices=["step", "layer2", "none"], default="step",
-                    help="config S on one GPU: the whole step in one launch (step), layer 2 + decoder "
-                         "in one launch (layer2), or three launches (none)")
+    ap.add_argument("--fold", choices=["step", "layer2", "none"], default="none",
+                    help="config S on one GPU: three launches (none, the default: measured fastest), "
+                         "layer 2 + decoder in one launch (layer2), or the whole step in one launch "
+                         "(step) — in-launch waits instead of kernel boundaries (DESIGN §5)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per form")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
@@ -336,7 +335,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
     graph, shard, scaling, workload = build_workload(config, rank, world, sharded, args.backend)
     plan, dg = make_plan(args, graph, shard, device)
     dec = Decoder(graph, plan, device, rank)
-    mode_fold = "none" if args.no_fold else args.fold
+    mode_fold = args.fold
     folded = {"none": lambda: False, "layer2": lambda: dec.fold(plan), "step": lambda: dec.fold_step(plan)}[mode_fold]()
     folded = mode_fold if folded else False
 

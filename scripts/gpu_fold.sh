@@ -12,6 +12,7 @@ for v in step.a layer2.a none.a step.b layer2.b none.b; do
     > $out/S_$v.json 2> $out/S_$v.err || exit $?
   python -c "import json,sys; r=json.load(open('$out/S_$v.json')); print('$v', r['ms_per_step']*1e3, 'us/step', r['spmm_layer2_ms']*1e3, r['folded'])"
 done
+[ "$2" = quick ] && exit 0
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?; tail -5 $out/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err
