@@ -82,15 +82,19 @@ struct SpmmArgs {
     int32_t d;
 };
 
-constexpr int kRowsPerBlock = 4;  // partial mode: 4 waves x 1 (chunk, row)
+#ifndef DG_ROWS_PER_WAVE
+#define DG_ROWS_PER_WAVE 2
+#endif
+// partial mode: 4 waves x kRowsPerWave consecutive (chunk, row) items; a wave issues every row's
+// pointers and first (vcol, val) batch before it gathers the first row, so the later rows' two
+// dependent loads hide under the earlier rows' gathers
+constexpr int kRowsPerWave = DG_ROWS_PER_WAVE;
+constexpr int kRowsPerBlock = 4 * kRowsPerWave;
 #ifndef DG_KUNROLL
 #define DG_KUNROLL 8
 #endif
 constexpr int kUnroll = DG_KUNROLL;  // gathers in flight per lane
 
-// acc = Σ_{p in [beg, end)} val[p] * X[vcol[p]][:], over every wcount-th batch of 64
-// starting at batch wpart.  Returns the folded row in every lane (lane l holds columns
-// 4(l%LP) .. 4(l%LP)+3).
 typedef __attribute__((address_space(1))) uint32_t gu32;
 constexpr uint32_t kStepSpinMax = 1u << 22;
 
@@ -132,13 +136,30 @@ struct WaitK {
     uint32_t* tmo;         // sticky timeout word
 };
 
+// The first batch of 64 (vcol, val) pairs of a range (batch wpart): lane l holds pair l.
+__device__ __forceinline__ void range_head(const SpmmGroupK& g, int beg, int end, int wpart, uint32_t dkey,
+                                           uint32_t dbase, int& vc, float& vv) {
+    const int lane = threadIdx.x & 63;
+    const int base = beg + wpart * 64;
+    vc = 0;
+    vv = 0.f;
+    if (base + lane < end) {
+        vc = g.vcol[base + lane];
+        vv = g.val[base + lane];
+        if (g.drop_state) vv *= drop_mul(g, dkey, dbase, base + lane);
+    }
+}
+
+// acc = Σ_{p in [beg, end)} val[p] * X[vcol[p]][:], over every wcount-th batch of 64
+// starting at batch wpart, whose first batch (vc, vv) range_head loaded.  Returns the folded
+// row in every lane (lane l holds columns 4(l%LP) .. 4(l%LP)+3).
 // kStep (a layer whose operand X the previous layer of the SAME launch wrote write-through):
 // the wave loads its first (vcol, val) batch — bytes no workgroup of the launch writes — then
 // waits for the producer's arrivals, and every gather of X is an sc1 buffer load.
 template <int LP, bool kStep = false>
-__device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb, int beg, int end, int d,
-                                            int wpart = 0, int wcount = 1, uint32_t dkey = 0,
-                                            uint32_t dbase = 0, const WaitK* wk = nullptr) {
+__device__ __forceinline__ float4 range_body(const SpmmGroupK& g, const float* xb, int beg, int end, int d,
+                                             int wpart, int wcount, uint32_t dkey, uint32_t dbase, int vc,
+                                             float vv, const WaitK* wk = nullptr) {
     constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
@@ -150,13 +171,6 @@ __device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const int stride = wcount * 64;
     int base = beg + wpart * 64;
-    int vc = 0;
-    float vv = 0.f;
-    if (base + lane < end) {
-        vc = vcolp[base + lane];
-        vv = valp[base + lane];
-        if (g.drop_state) vv *= drop_mul(g, dkey, dbase, base + lane);
-    }
     __amdgpu_buffer_rsrc_t xr;
     if constexpr (kStep) {
         wave_wait(wk->poll, wk->target, wk->tmo);
@@ -209,6 +223,16 @@ __device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb
     return acc;
 }
 
+template <int LP, bool kStep = false>
+__device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb, int beg, int end, int d,
+                                            int wpart = 0, int wcount = 1, uint32_t dkey = 0,
+                                            uint32_t dbase = 0, const WaitK* wk = nullptr) {
+    int vc;
+    float vv;
+    range_head(g, beg, end, wpart, dkey, dbase, vc, vv);
+    return range_body<LP, kStep>(g, xb, beg, end, d, wpart, wcount, dkey, dbase, vc, vv, wk);
+}
+
 // Partial mode: one wave per (chunk, row); writes out[c][r][:].
 template <int LP>
 __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
@@ -226,16 +250,29 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
     const int item = (lb & 7) * per + (lb >> 3);
     if (item >= g.n_chunks * g.row_blocks) return;
     const int c = item / g.row_blocks;
-    const int r = (item - c * g.row_blocks) * kRowsPerBlock + wave;
-    if (r >= g.n_rows) return;  // wave-uniform; no barriers in this kernel
+    const int r0 = (item - c * g.row_blocks) * kRowsPerBlock + wave * kRowsPerWave;
+    if (r0 >= g.n_rows) return;  // wave-uniform; no barriers in this kernel
     const int d = args.d;
-    const int64_t slot = (int64_t)c * g.n_rows + r;
+    const int64_t slot0 = (int64_t)c * g.n_rows + r0;
     // shared pattern: every chunk reads rowptr[r] over its own X slab
-    const int64_t ps = g.chunk_x ? r : slot;
+    const int64_t ps0 = g.chunk_x ? r0 : slot0;
     const uint32_t dkey = g.drop_state ? dg::drop_key(g.drop_state, g.drop_tag) : 0u;
-    const float4 acc = range_sum<LP>(g, g.x + c * g.chunk_x, g.rowptr[ps], g.rowptr[ps + 1], d, 0, 1, dkey,
-                                     (uint32_t)c * (uint32_t)g.drop_stride);
-    if (lane < LP && lane * 4 < d) *reinterpret_cast<float4*>(g.out + slot * d + lane * 4) = acc;
+    const uint32_t dbase = (uint32_t)c * (uint32_t)g.drop_stride;
+    const int nr = min(kRowsPerWave, g.n_rows - r0);  // this wave's rows (the last wave may hold fewer)
+    int rp[kRowsPerWave + 1];
+#pragma unroll
+    for (int j = 0; j <= kRowsPerWave; ++j) rp[j] = g.rowptr[ps0 + min(j, nr)];
+    int vc[kRowsPerWave];
+    float vv[kRowsPerWave];
+#pragma unroll
+    for (int j = 0; j < kRowsPerWave; ++j) range_head(g, rp[j], rp[j + 1], 0, dkey, dbase, vc[j], vv[j]);
+#pragma unroll
+    for (int j = 0; j < kRowsPerWave; ++j) {
+        if (j >= nr) break;
+        const float4 acc = range_body<LP>(g, g.x + c * g.chunk_x, rp[j], rp[j + 1], d, 0, 1, dkey, dbase, vc[j],
+                                          vv[j]);
+        if (lane < LP && lane * 4 < d) *reinterpret_cast<float4*>(g.out + (slot0 + j) * d + lane * 4) = acc;
+    }
 }
 
 // Fused mode (every group of a node type in one chunk): one workgroup per RPB consecutive
