@@ -531,7 +531,7 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
         "loss": float(sc.loss[0]),
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / BF16_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "decoder_bf16_kernel<256, true>", "kernel_ms": k_ms,
+                     "kernel": "decoder_bf16_paired_kernel<256, true>", "kernel_ms": k_ms,
                      "algorithmic_flops": n * flop_pair},
     }
 

@@ -666,10 +666,15 @@ def decoder_score(row_table: torch.Tensor, col_table: torch.Tensor, row_idx: tor
 def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: torch.Tensor,
                        cols: torch.Tensor, G: torch.Tensor, l_table: Optional[torch.Tensor] = None,
                        rel: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-                       stream=None) -> torch.Tensor:
+                       stream=None, paired: bool = False) -> torch.Tensor:
     """bf16 DEDICOM scores of pairs (rows[p], cols[p]) of relations rel[p] (dg_decoder_score_bf16):
-    uᵀ·D_k·G·D_k·v with bf16 tables / G / diagonals and fp32 accumulation (config 5)."""
+    uᵀ·D_k·G·D_k·v with bf16 tables / G / diagonals and fp32 accumulation (config 5).
+    paired: the caller promises pair p and pair p + n/2 share the column and the relation (a
+    positive and its negative); dg_decoder_score_bf16_paired scores them together, reading cols
+    and rel of the first half only."""
     n = rows.numel()
+    if paired and (n % 2 or cols.numel() != n or (rel is not None and rel.numel() != n)):
+        raise ValueError("paired scoring needs an even number of pairs, cols / rel of the same length")
     d = G.shape[0]
     for t, nm in ((row_table, "row_table"), (col_table, "col_table"), (G, "G")):
         _dev(t, torch.bfloat16, nm)
@@ -687,11 +692,11 @@ def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: t
         raise ValueError("tables must have d contiguous columns")
     if out is None:
         out = torch.empty(n, device=rows.device, dtype=torch.float32)
-    check(_lib.load().dg_decoder_score_bf16(
+    name = "dg_decoder_score_bf16_paired" if paired else "dg_decoder_score_bf16"
+    check(getattr(_lib.load(), name)(
         row_table.data_ptr(), row_table.stride(0), col_table.data_ptr(), col_table.stride(0), rows.data_ptr(),
-        cols.data_ptr(), rel.data_ptr() if rel is not None else None, n, G.data_ptr(),
-        l_table.data_ptr() if l_table is not None else None, d, out.data_ptr(), _stream_ptr(stream)),
-        "dg_decoder_score_bf16")
+        cols.data_ptr(), rel.data_ptr() if rel is not None else None, n // 2 if paired else n, G.data_ptr(),
+        l_table.data_ptr() if l_table is not None else None, d, out.data_ptr(), _stream_ptr(stream)), name)
     return out
 
 

@@ -75,8 +75,9 @@ class SlotScorer:
         kernels.unigram_sample(self.alias, self.n, self.seed, self.s0 * self.batch, out=self.neg_rows)
 
     def score(self) -> None:
+        # positives then negatives, a negative keeping its positive's column and relation
         kernels.decoder_score_bf16(self.E_row, self.E_col, self.rows, self.cols, self.R, self.D, self.rel,
-                                   out=self.out)
+                                   out=self.out, paired=True)
 
     def hinge(self) -> None:
         kernels.hinge_loss(self.pos, self.neg, self.margin, out=self.loss, workspace=self._ws)

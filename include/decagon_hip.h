@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (23); bumped whenever a struct layout or a signature changes. */
+/* ABI version (24); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -417,6 +417,17 @@ int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint1
                           int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
                           const int32_t* rel_idx, int32_t n_pairs, const uint16_t* G,
                           const uint16_t* l_table, int32_t d, float* out, void* stream);
+
+/* The same scores for config 5's layout: pairs p < n_half and p + n_half (a positive and its
+ * negative, optimizer.py:37-57) share the column and the relation, so col_idx / rel_idx are read
+ * for the first half only (row_idx, out hold 2*n_half entries).  One wave scores both pairs of
+ * a batch entry: every Rᵀ fragment it reads from LDS feeds two MFMAs, and the shared v and D_k
+ * rows are loaded once.  Same bf16 operands and k order as dg_decoder_score_bf16; the epilogue
+ * sums the n's in another fixed order (fp32 rounding apart, the same scores). */
+int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
+                                 int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
+                                 const int32_t* rel_idx, int32_t n_half, const uint16_t* G,
+                                 const uint16_t* l_table, int32_t d, float* out, void* stream);
 
 /* Fused decoder step (T8 + T9 + T11 + T12 in one launch):
  *   neg_row[b] = neg_rows[b] if neg_rows != NULL, else draw (offset + b) of the alias

@@ -332,6 +332,40 @@ def test_decoder_score_bf16(K, d):
     assert rel_err(got2, want2) <= 1e-4
 
 
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("n_half", [32 * 40 + 13, 7, 4096])
+def test_decoder_score_bf16_paired(K, d, n_half):
+    """dg_decoder_score_bf16_paired (config 5's positive / negative layout: pair p and p + n_half
+    share the column and the relation) against the unpaired kernel (same operands and k order;
+    the epilogue's n order differs: fp32 rounding) and the float64 restatement; ragged tails,
+    relations mixed within a tile, with and without the diagonals."""
+    rng = np.random.default_rng(d + n_half)
+    n_r, n_c, n_rel = 300, 200, 7
+    bf = torch.bfloat16
+    E_r = torch.from_numpy(rng.standard_normal((n_r, d)).astype(np.float32)).to(bf)
+    E_c = torch.from_numpy(rng.standard_normal((n_c, d)).astype(np.float32)).to(bf)
+    R = torch.from_numpy((rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)).to(bf)
+    Dk = torch.from_numpy(rng.standard_normal((n_rel, d)).astype(np.float32)).to(bf)
+    rows = rng.integers(0, n_r, 2 * n_half).astype(np.int32)
+    c1 = rng.integers(0, n_c, n_half).astype(np.int32)
+    r1 = rng.integers(0, n_rel, n_half).astype(np.int32)
+    cols, rel = np.concatenate([c1, c1]), np.concatenate([r1, r1])
+    dv = lambda x: torch.from_numpy(x).cuda()
+    for L in (Dk, None):
+        args = (E_r.cuda(), E_c.cuda(), dv(rows), dv(cols), R.cuda(), None if L is None else L.cuda(), dv(rel))
+        got = K.decoder_score_bf16(*args, paired=True).cpu().numpy()
+        ref = K.decoder_score_bf16(*args).cpu().numpy()
+        assert rel_err(got, ref) <= 1e-5
+        u = E_r.float().numpy()[rows]
+        v = E_c.float().numpy()[cols]
+        dk = L.float().numpy()[rel] if L is not None else np.ones_like(u)
+        a = torch.from_numpy((u * dk).astype(np.float32)).to(bf).double().numpy()
+        want = np.einsum("pi,in,pn->p", a, R.double().numpy(), dk.astype(np.float64) * v.astype(np.float64))
+        assert rel_err(got, want) <= 1e-4
+    with pytest.raises(ValueError):
+        K.decoder_score_bf16(E_r.cuda(), E_c.cuda(), dv(rows[:-1]), dv(cols[:-1]), R.cuda(), paired=True)
+
+
 def test_losses(K):
     rng = np.random.default_rng(5)
     pos = rng.standard_normal(1000).astype(np.float32)
