@@ -824,19 +824,18 @@ class PreparedFusedHinge:
         if not 2 <= fused.block_threads() <= 8:
             raise ValueError("the fused layer's workgroup must have 2..8 waves (128..512 threads)")
         self.fused, self.hinge = fused, hinge
-        a = hinge._args
-        n = a[11]
-        dev = hinge.pos.device
-        self._ws = torch.zeros(self.WS_WORDS + 4 + -(-n // 32), device=dev, dtype=torch.int32)
+        n = hinge.pos.numel()
+        self._ws = torch.zeros(self.WS_WORDS + 4 + -(-n // 32), device=hinge.pos.device, dtype=torch.int32)
         self.desc = _lib.DgHingeDesc()
         self._fn = _lib.load().dg_gcn_fused_hinge_f32
 
     def _fill(self) -> None:
-        a, q = self.hinge._args, self.desc
-        (q.row_table, q.ld_row, q.col_table, q.ld_col, q.rows, q.cols, q.neg_rows, q.alias_table, q.range) = a[:9]
+        """The descriptor from the hinge's dg_decoder_hinge_f32 argument list (same order as
+        that signature), the current seed / offset and this launch's workspace."""
+        q = self.desc
+        (q.row_table, q.ld_row, q.col_table, q.ld_col, q.rows, q.cols, q.neg_rows, q.alias_table, q.range,
+         _seed, _offset, q.n, q.G, q.l, q.d, q.margin, q.pos, q.neg, q.neg_rows_out, q.loss, _ws) = self.hinge._args
         q.seed, q.offset = self.hinge.seed & (2**64 - 1), self.hinge.offset & (2**64 - 1)
-        q.n, q.G, q.l, q.d, q.margin = a[11], a[12], a[13], a[14], a[15]
-        q.pos, q.neg, q.neg_rows_out, q.loss = a[16], a[17], a[18], a[19]
         q.workspace = self._ws.data_ptr()
 
     def timeouts(self) -> int:
