@@ -57,10 +57,6 @@ def parse(argv=None):
                     help="S / P: the GCN forward step (metric: edges/s); D: config 5, bf16 DEDICOM "
                          "scoring of every drug-drug slot's batch (metric: scored pairs/s)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
-    ap.add_argument("--fold", choices=["step", "layer2", "none"], default="none",
-                    help="config S on one GPU: three launches (none, the default: measured fastest), "
-                         "layer 2 + decoder in one launch (layer2), or the whole step in one launch "
-                         "(step) — in-launch waits instead of kernel boundaries (DESIGN §5)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per form")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
@@ -200,20 +196,8 @@ class Decoder:
         self.fused = kernels.PreparedDecoderHinge(self.E, self.E, self.rows, self.cols, self.R, self.l,
                                                   MARGIN, alias=self.alias, seed=7)
 
-    def fold(self, plan) -> bool:
-        """Run the decoder step inside layer 2's fused launch when the plan allows it (config
-        S on one GPU: dg_gcn_fused_hinge_f32); then calling self launches nothing."""
-        self.folded = plan.fold_hinge(self.fused)
-        return self.folded
-
-    def fold_step(self, plan) -> bool:
-        """The whole forward step in one launch (dg_gcn_step_f32) when the plan allows it."""
-        self.folded = plan.fold_step(self.fused)
-        return self.folded
-
     def __call__(self):
-        if not getattr(self, "folded", False):
-            self.fused()
+        self.fused()
 
 
 def time_kernel(fn, reps, stream):
@@ -335,9 +319,6 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
     graph, shard, scaling, workload = build_workload(config, rank, world, sharded, args.backend)
     plan, dg = make_plan(args, graph, shard, device)
     dec = Decoder(graph, plan, device, rank)
-    mode_fold = args.fold
-    folded = {"none": lambda: False, "layer2": lambda: dec.fold(plan), "step": lambda: dec.fold_step(plan)}[mode_fold]()
-    folded = mode_fold if folded else False
 
     def step():
         plan.run()
@@ -436,10 +417,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
                         "frac": l1_bytes / (l1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "edges_per_s": dg.total_nnz / (l1_ms * 1e-3)},
         "spmm_layer2_ms": k2_ms,
-        "folded": folded,  # "layer2": spmm_layer2_ms includes the decoder; "step": one launch per step
     }
-    if folded and plan.folded_hinge.timeouts():
-        raise RuntimeError("the in-launch decoder wait timed out (dg_gcn_fused_hinge_f32)")
     if sharded:
         rec["rank_ms_per_step"] = el * 1e3 / steps
         if args.backend == "nccl" and use_graph:

@@ -10,8 +10,9 @@ __version__ = "0.1.0"
 
 from . import flags  # noqa: F401
 from .flags import FLAGS  # noqa: F401
-from .graph import (InvalidArgumentError, Node, Operation, Placeholder, Session, Variable,  # noqa: F401
-                    float32, global_variables, global_variables_initializer, int32, name_scope, placeholder,
+from .graph import (Graph, InvalidArgumentError, Node, Operation, Placeholder, Session, Variable,  # noqa: F401
+                    float32, get_default_graph, global_variables, global_variables_initializer, int32,
+                    name_scope, placeholder, reset_default_graph,
                     placeholder_with_default, sparse_placeholder)
 from .inits import set_random_seed  # noqa: F401
 from .layers import (BilinearDecoder, DEDICOMDecoder, DistMultDecoder,  # noqa: F401

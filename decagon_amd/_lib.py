@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 24
+ABI_VERSION = 25
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -83,21 +83,6 @@ class DgProj(ctypes.Structure):
 class DgFusedTarget(ctypes.Structure):
     _fields_ = [("out", c_void_p), ("n_rows", c_int32), ("g_begin", c_int32), ("g_count", c_int32),
                 ("flags", c_int32)]
-
-
-class DgHingeDesc(ctypes.Structure):
-    _fields_ = [("row_table", c_void_p), ("col_table", c_void_p), ("ld_row", c_int64), ("ld_col", c_int64),
-                ("rows", c_void_p), ("cols", c_void_p), ("neg_rows", c_void_p), ("alias_table", c_void_p),
-                ("range", c_int32), ("n", c_int32), ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64),
-                ("G", c_void_p), ("l", c_void_p), ("d", c_int32), ("margin", ctypes.c_float),
-                ("pos", c_void_p), ("neg", c_void_p), ("neg_rows_out", c_void_p), ("loss", c_void_p),
-                ("workspace", c_void_p)]
-
-
-class DgFusedLayer(ctypes.Structure):
-    _fields_ = [("groups", POINTER(DgRelGroup)), ("n_groups", c_int32), ("n_targets", c_int32),
-                ("targets", POINTER(DgFusedTarget)), ("projs", POINTER(DgProj)), ("n_projs", c_int32),
-                ("waves_per_group", c_int32), ("d", c_int32), ("reserved", c_int32)]
 
 
 class DgEpiGroup(ctypes.Structure):
@@ -167,12 +152,6 @@ SIGNATURES = {
         [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, POINTER(DgProj), c_int32, c_int32,
          c_int32, c_void_p],
     ),
-    "dg_gcn_fused_hinge_f32": (
-        c_int32,
-        [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, POINTER(DgProj), c_int32, c_int32,
-         c_int32, POINTER(DgHingeDesc), c_void_p],
-    ),
-    "dg_gcn_step_f32": (c_int32, [POINTER(DgFusedLayer), POINTER(DgFusedLayer), POINTER(DgHingeDesc), c_void_p]),
     "dg_gcn_epilogue_multi_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, c_void_p]),
     "dg_gcn_epilogue_f32": (
         c_int32,

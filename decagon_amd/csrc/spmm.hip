@@ -25,7 +25,6 @@
 // the next layer's projection of the finished row.
 #include "common.h"
 #include "dropout.h"
-#include "decoder_tile.h"
 
 #ifndef DG_FUSED_ABL
 #define DG_FUSED_ABL 0  // timing ablations only (wrong results): 1 no gathers, 8 empty kernels
@@ -95,47 +94,6 @@ constexpr int kRowsPerBlock = 4 * kRowsPerWave;
 #endif
 constexpr int kUnroll = DG_KUNROLL;  // gathers in flight per lane
 
-typedef __attribute__((address_space(1))) uint32_t gu32;
-constexpr uint32_t kStepSpinMax = 1u << 22;
-
-// One wave waits until the eight arrival shards at `poll` (one per 128-B line) sum to `target`
-// (relaxed sc1 polls; cdna_hip_programming.md Guideline 16 R1: this wave's later sc1 loads of
-// the published bytes need no acquire).  Bounded: a timeout sets *tmo and returns.
-__device__ __forceinline__ void wave_wait(const uint32_t* poll, uint32_t target, uint32_t* tmo) {
-    const int lane = threadIdx.x & 63;
-    uint32_t spins = 0;
-#pragma unroll 1
-    for (;;) {
-        uint32_t c = lane < 8 ? __hip_atomic_load((gu32*)(const_cast<uint32_t*>(poll) + 32 * lane), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)
-                              : 0u;
-#pragma unroll
-        for (int m = 1; m < 8; m <<= 1) c += __shfl_xor(c, m);
-        c = __shfl(c, 0);
-        if (c >= target) return;
-        if (++spins > kStepSpinMax) {
-            if (lane == 0) __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-// A wave-uniform buffer resource over p (32-bit byte offsets; the host bounds the operand).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
-                                             0x7fffffff, 0x00020000);
-}
-
-struct WaitK {
-    const uint32_t* poll;  // arrival shards of the producing layer
-    uint32_t target;       // its workgroup count
-    uint32_t* tmo;         // sticky timeout word
-};
-
 // The first batch of 64 (vcol, val) pairs of a range (batch wpart): lane l holds pair l.
 __device__ __forceinline__ void range_head(const SpmmGroupK& g, int beg, int end, int wpart, uint32_t dkey,
                                            uint32_t dbase, int& vc, float& vv) {
@@ -153,13 +111,10 @@ __device__ __forceinline__ void range_head(const SpmmGroupK& g, int beg, int end
 // acc = Σ_{p in [beg, end)} val[p] * X[vcol[p]][:], over every wcount-th batch of 64
 // starting at batch wpart, whose first batch (vc, vv) range_head loaded.  Returns the folded
 // row in every lane (lane l holds columns 4(l%LP) .. 4(l%LP)+3).
-// kStep (a layer whose operand X the previous layer of the SAME launch wrote write-through):
-// the wave loads its first (vcol, val) batch — bytes no workgroup of the launch writes — then
-// waits for the producer's arrivals, and every gather of X is an sc1 buffer load.
-template <int LP, bool kStep = false>
+template <int LP>
 __device__ __forceinline__ float4 range_body(const SpmmGroupK& g, const float* xb, int beg, int end, int d,
                                              int wpart, int wcount, uint32_t dkey, uint32_t dbase, int vc,
-                                             float vv, const WaitK* wk = nullptr) {
+                                             float vv) {
     constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
@@ -171,11 +126,6 @@ __device__ __forceinline__ float4 range_body(const SpmmGroupK& g, const float* x
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const int stride = wcount * 64;
     int base = beg + wpart * 64;
-    __amdgpu_buffer_rsrc_t xr;
-    if constexpr (kStep) {
-        wave_wait(wk->poll, wk->target, wk->tmo);
-        xr = wave_rsrc(xb);
-    }
 #pragma unroll 1
     for (; base < end; base += stride) {
         const int n = min(64, end - base);
@@ -203,15 +153,9 @@ __device__ __forceinline__ float4 range_body(const SpmmGroupK& g, const float* x
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 const bool ok = qact && (s0 + u * G + sub) < n;
-                if constexpr (kStep) {
-                    xv[u] = ok ? __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                xr, (o[u] + q * 4) * 4, 0, 16 /* sc1 */))
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-                } else {
-                    xv[u] = ok ? ((DG_FUSED_ABL & 1) ? make_float4(1.f, 1.f, 1.f, 1.f)
-                                                     : *reinterpret_cast<const float4*>(xq + o[u]))
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-                }
+                xv[u] = ok ? ((DG_FUSED_ABL & 1) ? make_float4(1.f, 1.f, 1.f, 1.f)
+                                                 : *reinterpret_cast<const float4*>(xq + o[u]))
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
                 if (!ok) w[u] = 0.f;
             }
 #pragma unroll
@@ -223,14 +167,14 @@ __device__ __forceinline__ float4 range_body(const SpmmGroupK& g, const float* x
     return acc;
 }
 
-template <int LP, bool kStep = false>
+template <int LP>
 __device__ __forceinline__ float4 range_sum(const SpmmGroupK& g, const float* xb, int beg, int end, int d,
                                             int wpart = 0, int wcount = 1, uint32_t dkey = 0,
-                                            uint32_t dbase = 0, const WaitK* wk = nullptr) {
+                                            uint32_t dbase = 0) {
     int vc;
     float vv;
     range_head(g, beg, end, wpart, dkey, dbase, vc, vv);
-    return range_body<LP, kStep>(g, xb, beg, end, d, wpart, wcount, dkey, dbase, vc, vv, wk);
+    return range_body<LP>(g, xb, beg, end, d, wpart, wcount, dkey, dbase, vc, vv);
 }
 
 // Partial mode: one wave per (chunk, row); writes out[c][r][:].
@@ -323,17 +267,9 @@ struct FusedArgs {
     int32_t rpb;  // rows per workgroup (blockDim = 64 · rpb · max groups · wpg)
 };
 
-// The fused layer for workgroup b.  kPub publishes what a later stage of the SAME launch reads:
-// bit 1 the finished rows, bit 2 the projection outputs — stored write-through (sc1), drained
-// by every storing wave, then after the workgroup barrier one lane adds 1 to arrival shard
-// b % 8 of `arrive` (cdna_hip_programming.md Guideline 16 R1: consumers poll the shards and read
-// the bytes with sc1 loads).  kWait: the layer's operand was published by the previous stage
-// (range_sum's step form waits for it).
-template <int LP, int kPub, bool kWait = false>
-__device__ __forceinline__ void fused_body(const FusedArgs& a, const int b, uint32_t* arrive,
-                                           const WaitK* wk = nullptr) {
-    constexpr bool kPubRows = (kPub & 1) != 0;
-    constexpr bool kPubProj = (kPub & 2) != 0;
+// The fused layer for workgroup b.
+template <int LP>
+__device__ __forceinline__ void fused_body(const FusedArgs& a, const int b) {
     __shared__ float4 pbuf[16][LP];
     __shared__ float4 ybuf[kFusedRpb][DG_MAX_GROUPS][LP];
     __shared__ float hrow[kFusedRpb][4 * LP];
@@ -361,7 +297,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, const int b, uint
         if (!g.rowptr) {  // DG_GROUP_DENSE_ROWS: the sum is x[r] (the group's first wave loads it)
             if (part == 0 && q * 4 < d) s = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.x_ld + q * 4);
         } else {
-            s = range_sum<LP, kWait>(g, g.x, g.rowptr[r], g.rowptr[r + 1], d, part, W, 0, 0, wk);
+            s = range_sum<LP>(g, g.x, g.rowptr[r], g.rowptr[r + 1], d, part, W);
         }
         if (lane < LP) pbuf[wave][lane] = s;
     }
@@ -386,24 +322,8 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, const int b, uint
             tot.z = fmaxf(tot.z, 0.f);
             tot.w = fmaxf(tot.w, 0.f);
         }
-        if (lane * 4 < d) {
-            float* o = t.out + (int64_t)r * d + lane * 4;
-            if (kPubRows) {
-                const float v[4] = {tot.x, tot.y, tot.z, tot.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    __hip_atomic_store((dg::gf32*)(o + e), v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                *reinterpret_cast<float4*>(o) = tot;
-            }
-        }
+        if (lane * 4 < d) *reinterpret_cast<float4*>(t.out + (int64_t)r * d + lane * 4) = tot;
         reinterpret_cast<float4*>(hrow[slot])[lane] = tot;
-    }
-    if (kPub && (!kPubProj || a.n_projs == 0)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(arrive + 32 * (b & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (a.n_projs == 0) return;  // launch-uniform
 #ifdef DG_FUSED_NOPROJ  // timing ablation only (wrong results)
@@ -446,185 +366,15 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, const int b, uint
 #pragma unroll
         for (int s2 = 0; s2 < kFusedRpb; ++s2) {
             if (s2 >= nr) continue;
-            if (kPubProj)
-                __hip_atomic_store((dg::gf32*)(po + (int64_t)s2 * dout), acc[s2], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            else
-                po[(int64_t)s2 * dout] = acc[s2];
+            po[(int64_t)s2 * dout] = acc[s2];
         }
-    }
-    if (kPubProj) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(arrive + 32 * (b & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 template <int LP>
 __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
     if (DG_FUSED_ABL & 8) return;
-    fused_body<LP, 0>(a, blockIdx.x, nullptr);
-}
-
-// Layer 2 + decoder + hinge in one launch (config S, one GPU; optimizer.py:37-57, :116-120 on
-// the embeddings model.py:85-88 just produced): the workgroups past the fused layer's score
-// 32-pair tiles of the batch — waves 2s / 2s+1 the positives / negatives of tile s — exactly
-// as decoder_hinge_kernel does, after waiting for every layer workgroup's arrival.  They sit at
-// the end of the grid and never hold a layer workgroup back (those wait for nothing); the
-// wait is bounded (a timeout sets a sticky word instead of hanging).
-// Workspace (uint32): arrival shard s at [32 s] (s < 8, one per 128-B line), the ticket at
-// [256], the timeout word at [257], the decoder workgroups' hinge partials from [260].
-constexpr int kStepTicket = 256;
-constexpr int kStepTimeout = 257;
-constexpr int kStepPartial = 260;
-// dg_gcn_step_f32's workspace: layer 1's shards at [32 s], layer 2's at [256 + 32 s], the ticket
-// at [512], the timeout word at [513], the partials from [516]
-constexpr int kStep2Set2 = 256;
-constexpr int kStep2Ticket = 512;
-constexpr int kStep2Timeout = 513;
-constexpr int kStep2Partial = 516;
-
-struct StepHingeK {
-    dg::DecTab t;
-    const int32_t* rows;
-    const int32_t* cols;
-    const int32_t* neg_given;
-    const uint2* alias;
-    float* pos;
-    float* neg;
-    int32_t* neg_rows_out;
-    float* loss;
-    uint32_t* poll;       // arrival shards the decoder waits on
-    uint32_t* reset2;     // another shard set to re-arm at the end, or NULL
-    uint32_t* ticket;
-    uint32_t* tmo;
-    float* partial;
-    uint64_t seed;
-    uint64_t offset;
-    int32_t range;
-    int32_t n;
-    float margin;
-    int32_t fused_blocks;  // the arrivals to wait for
-    int32_t dec_blocks;
-    int32_t pad;
-};
-
-template <int kD>
-__device__ __forceinline__ void step_hinge_body(const StepHingeK& h, const int blk) {
-    __shared__ float sc[8][2][32];
-    __shared__ float red[8];
-    __shared__ int last;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int tiles = (int)(blockDim.x >> 7);  // two waves per 32-pair tile
-    const int ts = wave >> 1;
-    const int side = wave & 1;  // 0: positives, 1: negatives
-    const bool act = ts < tiles;  // wave-uniform (an odd last wave idles)
-    const int i = lane & 31;
-    const int hh = lane >> 5;
-    const int b0 = (blk * tiles + ts) * 32;
-    const int b = b0 + i;
-    const bool valid = act && b < h.n;
-    // the batch and the negative draws need no embedding: they overlap the layer
-    int ridx = 0, cidx = 0;
-    if (valid) {
-        cidx = h.cols[b];
-        if (side == 0)
-            ridx = h.rows[b];
-        else if (h.neg_given)
-            ridx = h.neg_given[b];
-        else
-            ridx = dg::unigram_draw(h.alias, h.range, h.seed, h.offset + (uint64_t)b);
-        if (side == 1 && h.neg_rows_out && hh == 0) h.neg_rows_out[b] = ridx;
-    }
-    if (wave == 0) wave_wait(h.poll, (uint32_t)h.fused_blocks, h.tmo);  // ONE wave polls
-    __syncthreads();  // the other waves load the rows only after the poll matched
-    float part[16];
-    if (act) {
-        dg::score_tile<true, kD>(h.t, ridx, cidx, valid, part);
-        if (i == 0) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int q = (r & 3) + 8 * (r >> 2) + 4 * hh;
-                const float v = (b0 + q < h.n) ? part[r] : 0.f;
-                sc[ts][side][q] = v;
-                if (b0 + q < h.n) (side == 0 ? h.pos : h.neg)[b0 + q] = v;
-            }
-        }
-    }
-    __syncthreads();
-    if (act && side == 0) {
-        float term = 0.f;
-        if (lane < 32 && b0 + lane < h.n) term = fmaxf(sc[ts][1][lane] - (sc[ts][0][lane] - h.margin), 0.f);
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) term += __shfl_xor(term, m);
-        if (lane == 0) red[ts] = term;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float p = 0.f;
-        for (int s = 0; s < tiles; ++s) p += red[s];  // tile order
-        // partial stored write-through and drained before the ticket (decoder_hinge_kernel)
-        __hip_atomic_store((dg::gf32*)(h.partial + blk), p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(h.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (tk == (uint32_t)h.dec_blocks - 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (!last) return;  // block-uniform
-    if (threadIdx.x >= 64) return;
-    float s = 0.f;  // lane l sums partials l, l + 64, ...; a butterfly folds the lanes (fixed order)
-    for (int k = lane; k < h.dec_blocks; k += 64)
-        s += __hip_atomic_load((dg::gf32*)(h.partial + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
-    if (lane == 0) {
-        h.loss[0] = s;
-        // every decoder workgroup has passed its poll (its ticket came after it) and every layer
-        // workgroup has arrived: reset the words for the next launch
-        __hip_atomic_store((gu32*)h.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int sh = 0; sh < 8; ++sh) {
-            __hip_atomic_store((gu32*)(h.poll + 32 * sh), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (h.reset2)
-                __hip_atomic_store((gu32*)(h.reset2 + 32 * sh), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// kD: the decoder width when it is 32 (that path alone: 128 VGPRs, so the layer's workgroups
-// keep the plain kernel's residency), else 0
-template <int LP, int kD>
-__global__ __launch_bounds__(1024) void gcn_fused_hinge_kernel(const FusedArgs a, const StepHingeK h) {
-    // the decoder workgroups first: resident from the start, their batch loads and draws
-    // overlap the layer; they are few, so they never keep a layer workgroup from a CU
-    if ((int)blockIdx.x < h.dec_blocks)
-        step_hinge_body<kD>(h, (int)blockIdx.x);
-    else
-        fused_body<LP, 1>(a, (int)blockIdx.x - h.dec_blocks, h.poll);
-}
-
-// The whole config-S forward step in one launch (layers.py:70-118, model.py:64-88,
-// optimizer.py:37-57 and :116-120): workgroups [0, n1) run layer 1 and publish its projections
-// P_k (layer 2's operand), [n1, n1 + n2) run layer 2 — each wave loads its first pair batch,
-// waits for layer 1's n1 arrivals, gathers P with sc1 loads — and publish the embeddings, the
-// rest are the decoder step waiting for layer 2's n2 arrivals.  Stages sit in grid order, so a
-// waiting workgroup is never dispatched ahead of one it waits for on the same XCD.
-template <int LP1, int LP2>
-__global__ __launch_bounds__(1024) void gcn_step_kernel(const FusedArgs a1, const FusedArgs a2, const StepHingeK h,
-                                                      const int32_t n1) {
-    // grid order: the decoder workgroups (few; they wait for layer 2), layer 1, layer 2 (waits
-    // for layer 1) — a waiting workgroup never precedes one it waits for in dispatch order
-    const int b = (int)blockIdx.x - h.dec_blocks;
-    if (b < 0) {
-        step_hinge_body<32>(h, (int)blockIdx.x);
-    } else if (b < n1) {
-        fused_body<LP1, 2>(a1, b, h.reset2);
-    } else {
-        const WaitK wk{h.reset2, (uint32_t)n1, h.tmo};
-        fused_body<LP2, 1, true>(a2, b - n1, h.poll, &wk);
-    }
+    fused_body<LP>(a, blockIdx.x);
 }
 
 struct EpiGroupK {
@@ -848,7 +598,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 24; }
+extern "C" int32_t dg_abi_version(void) { return 25; }
 
 
 namespace {
@@ -1012,123 +762,6 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
 #define DG_LAUNCH_FUSED(L) hipLaunchKernelGGL(gcn_fused_kernel<L>, grid, block, 0, st, a)
     DG_LP_SWITCH(lp, DG_LAUNCH_FUSED)
 #undef DG_LAUNCH_FUSED
-    return dg::launch_status();
-}
-
-namespace {
-int fill_hinge(const dg_hinge_desc& q, StepHingeK& h);
-}  // namespace
-
-extern "C" int dg_gcn_fused_hinge_f32(const dg_rel_group* groups, int32_t n_groups,
-                                      const dg_fused_target* targets, int32_t n_targets,
-                                      const dg_proj* projs, int32_t n_projs, int32_t waves_per_group,
-                                      int32_t d, const dg_hinge_desc* hd, void* stream) {
-    FusedArgs a{};
-    int64_t blocks = 0;
-    int threads = 0;
-    const int rc = prep_fused(groups, n_groups, targets, n_targets, projs, n_projs, waves_per_group, d, a, blocks,
-                              threads);
-    if (rc != DG_OK) return rc;
-    if (!hd) return DG_EINVAL;
-    const dg_hinge_desc& q = *hd;
-    if (q.n < 1 || q.d <= 0 || (q.d % 32) || q.d > 256) return DG_EINVAL;
-    if (!q.row_table || !q.col_table || !q.rows || !q.cols || !q.G || !q.pos || !q.neg || !q.loss || !q.workspace)
-        return DG_EINVAL;
-    if (!q.neg_rows && (!q.alias_table || q.range < 1)) return DG_EINVAL;
-    if (q.ld_row < q.d || q.ld_col < q.d) return DG_EINVAL;
-    if (!dg::aligned16(q.workspace)) return DG_EALIGN;
-    if (threads < 128 || threads > 512) return DG_EINVAL;  // two waves per 32-pair tile; <= 512 threads
-    const int tiles = threads >> 7;
-    const int64_t dec_blocks = dg::ceil_div(q.n, 32 * tiles);
-    if (blocks + dec_blocks > 0x7fffffff) return DG_EINVAL;
-    StepHingeK h{};
-    const int hrc = fill_hinge(q, h);
-    if (hrc != DG_OK) return hrc;
-    uint32_t* ws = reinterpret_cast<uint32_t*>(q.workspace);
-    h.poll = ws;
-    h.reset2 = nullptr;
-    h.ticket = ws + kStepTicket;
-    h.tmo = ws + kStepTimeout;
-    h.partial = reinterpret_cast<float*>(ws + kStepPartial);
-    h.fused_blocks = static_cast<int32_t>(blocks);
-    h.dec_blocks = static_cast<int32_t>(dec_blocks);
-    const int lp = dg::lanes_per_row(d);
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    dim3 grid(static_cast<unsigned>(blocks + dec_blocks)), block(threads);
-#define DG_LAUNCH_FH(L)                                                                  \
-    if (q.d == 32)                                                                       \
-        hipLaunchKernelGGL((gcn_fused_hinge_kernel<L, 32>), grid, block, 0, st, a, h);   \
-    else                                                                                 \
-        hipLaunchKernelGGL((gcn_fused_hinge_kernel<L, 0>), grid, block, 0, st, a, h)
-    DG_LP_SWITCH(lp, DG_LAUNCH_FH)
-#undef DG_LAUNCH_FH
-    return dg::launch_status();
-}
-
-namespace {
-int fill_hinge(const dg_hinge_desc& q, StepHingeK& h) {
-    if (q.n < 1 || q.d <= 0 || (q.d % 32) || q.d > 256) return DG_EINVAL;
-    if (!q.row_table || !q.col_table || !q.rows || !q.cols || !q.G || !q.pos || !q.neg || !q.loss || !q.workspace)
-        return DG_EINVAL;
-    if (!q.neg_rows && (!q.alias_table || q.range < 1)) return DG_EINVAL;
-    if (q.ld_row < q.d || q.ld_col < q.d) return DG_EINVAL;
-    if (!dg::aligned16(q.workspace)) return DG_EALIGN;
-    h.t = dg::DecTab{q.row_table, q.col_table, q.G, q.l, q.ld_row, q.ld_col, q.d,
-                     dg::aligned16(q.row_table) && (q.ld_row & 3) == 0 && (!q.l || dg::aligned16(q.l))};
-    h.rows = q.rows;
-    h.cols = q.cols;
-    h.neg_given = q.neg_rows;
-    h.alias = reinterpret_cast<const uint2*>(q.alias_table);
-    h.pos = q.pos;
-    h.neg = q.neg;
-    h.neg_rows_out = q.neg_rows_out;
-    h.loss = q.loss;
-    h.seed = q.seed;
-    h.offset = q.offset;
-    h.range = q.range;
-    h.n = q.n;
-    h.margin = q.margin;
-    return DG_OK;
-}
-}  // namespace
-
-extern "C" int dg_gcn_step_f32(const dg_fused_layer* l1, const dg_fused_layer* l2, const dg_hinge_desc* hd,
-                               void* stream) {
-    if (!l1 || !l2 || !hd) return DG_EINVAL;
-    FusedArgs a1{}, a2{};
-    int64_t n1 = 0, n2 = 0;
-    int t1 = 0, t2 = 0;
-    int rc = prep_fused(l1->groups, l1->n_groups, l1->targets, l1->n_targets, l1->projs, l1->n_projs,
-                        l1->waves_per_group, l1->d, a1, n1, t1);
-    if (rc != DG_OK) return rc;
-    rc = prep_fused(l2->groups, l2->n_groups, l2->targets, l2->n_targets, l2->projs, l2->n_projs,
-                    l2->waves_per_group, l2->d, a2, n2, t2);
-    if (rc != DG_OK) return rc;
-    if (l1->d != 64 || l2->d != 32 || l2->n_projs != 0 || hd->d != 32) return DG_EINVAL;  // the <16, 8> instance
-    if (t1 != t2 || t1 < 128 || t1 > 512) return DG_EINVAL;
-    for (int i = 0; i < l2->n_groups; ++i) {
-        const dg_rel_group& g = l2->groups[i];
-        // gathers use 32-bit buffer offsets; dense-row groups would read unpublished rows
-        if (!g.rowptr || (g.flags & DG_GROUP_DENSE_ROWS) || (int64_t)g.x_rows * g.x_ld * 4 >= (1ll << 31))
-            return DG_EINVAL;
-    }
-    StepHingeK h{};
-    rc = fill_hinge(*hd, h);
-    if (rc != DG_OK) return rc;
-    const int tiles = t1 >> 7;
-    const int64_t dec_blocks = dg::ceil_div(hd->n, 32 * tiles);
-    if (n1 + n2 + dec_blocks > 0x7fffffff) return DG_EINVAL;
-    uint32_t* ws = reinterpret_cast<uint32_t*>(hd->workspace);
-    h.reset2 = ws;                 // layer 1's arrivals (layer 2 waits on them)
-    h.poll = ws + kStep2Set2;      // layer 2's arrivals (the decoder waits on them)
-    h.ticket = ws + kStep2Ticket;
-    h.tmo = ws + kStep2Timeout;
-    h.partial = reinterpret_cast<float*>(ws + kStep2Partial);
-    h.fused_blocks = static_cast<int32_t>(n2);
-    h.dec_blocks = static_cast<int32_t>(dec_blocks);
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL((gcn_step_kernel<16, 8>), dim3(static_cast<unsigned>(n1 + n2 + dec_blocks)), dim3(t1), 0, st,
-                       a1, a2, h, static_cast<int32_t>(n1));
     return dg::launch_status();
 }
 

@@ -390,17 +390,18 @@ class ForwardPlan:
 
         # row-split node types: the full output rows live in a buffer padded to world × block
         # rows (this rank finishes its block in place, the all-gather fills the rest)
+        # (keyed by node type and layer: h1 == h2 must not share a buffer)
         self._pad: Dict[Tuple[int, int], torch.Tensor] = {}
 
-        def out_buf(i, d):
+        def out_buf(i, d, layer):
             if i not in self.row_block:
                 return torch.empty((n[i], d), **f32)
             pad = torch.empty((self.world * self.row_block[i][2], d), **f32)
-            self._pad[i, d] = pad
+            self._pad[i, layer] = pad
             return pad[:n[i]]
 
-        self.hidden1 = {i: out_buf(i, h1) for i in self.targets}
-        self.embeddings = {i: out_buf(i, h2) for i in self.targets}
+        self.hidden1 = {i: out_buf(i, h1, 1) for i in self.targets}
+        self.embeddings = {i: out_buf(i, h2, 2) for i in self.targets}
 
         # ---- layer-2 projection buffers P_k = H1_j·W2_k (global slabs) ----
         # staged groups make their slabs H1_j·W2_k in the layer-2 kernel itself
@@ -535,7 +536,7 @@ class ForwardPlan:
                     # a row-split node type (sharded): this rank's block, finished in place in the
                     # padded output, then all-gathered
                     a, b, blk = self.row_block[i]
-                    pad = self._pad[i, d]
+                    pad = self._pad[i, 1 if relu else 2]
                     r0 = self.shard.rank * blk
                     out, rows_i = pad[r0:r0 + (b - a)], b - a
                     gathers.append((pad, pad[r0:r0 + blk]))
@@ -597,7 +598,7 @@ class ForwardPlan:
             blocks = []
             for i in split_t:
                 a, b, blk = self.row_block[i]
-                pad = self._pad[i, d]
+                pad = self._pad[i, 1 if relu else 2]
                 r0 = self.shard.rank * blk
                 blocks.append(([partials[et] for et in self.targets[i]], pad[r0:r0 + (b - a)], b - a))
                 gathers.append((pad, pad[r0:r0 + blk]))
@@ -663,47 +664,8 @@ class ForwardPlan:
         self._layer2.run()
 
     def run(self) -> None:
-        step = getattr(self, "folded_step", None)
-        if step is not None:
-            step()
-            return
         self.run_layer1()
         self.run_layer2()
-
-    def fold_hinge(self, hinge: "kernels.PreparedDecoderHinge") -> bool:
-        """Run `hinge` (the decoder step on this plan's embeddings) inside layer 2's launch
-        (dg_gcn_fused_hinge_f32) when layer 2 is one fused launch with nothing after it (one
-        GPU, every node type fused: config S); then the caller must not launch `hinge` itself.
-        Returns whether it folded."""
-        L = self._layer2
-        if (self.shard is not None or L.has_exchange or L.epilogues or L.local_epilogues or L.need_zero
-                or len(L.launches) != 1 or not isinstance(L.launches[0], kernels.PreparedFused)):
-            return False
-        f = L.launches[0]
-        if not 2 <= f.block_threads() <= 8:
-            return False
-        L.launches = [kernels.PreparedFusedHinge(f, hinge)]
-        self.folded_hinge = L.launches[0]
-        return True
-
-    def fold_step(self, hinge: "kernels.PreparedDecoderHinge") -> bool:
-        """The whole step in one launch (dg_gcn_step_f32): layer 1, layer 2 and `hinge`, when
-        both layers are one fused launch each with nothing between or after them (one GPU,
-        every node type fused, projections in layer 1's epilogue: config S).  Then run()
-        launches only that (and the caller must not launch `hinge`); the per-layer launches
-        stay available to time alone.  Returns whether it folded."""
-        L1, L2 = self._layer1, self._layer2
-        plain = lambda L: (not L.has_exchange and not L.epilogues and not L.local_epilogues and not L.need_zero
-                           and len(L.launches) == 1 and isinstance(L.launches[0], kernels.PreparedFused))
-        if self.shard is not None or self._pre or self._gemm2 or not plain(L1) or not plain(L2):
-            return False
-        f1, f2 = L1.launches[0], L2.launches[0]
-        if (f1.d != 64 or f2.d != 32 or f2._np or f1.block_threads() != f2.block_threads()
-                or not 2 <= f1.block_threads() <= 8 or any(s.dense for s in f2._keep[0])):
-            return False
-        self.folded_step = kernels.PreparedStep(f1, f2, hinge)
-        self.folded_hinge = self.folded_step
-        return True
 
     def phases(self) -> List[Tuple[str, Callable[[], None]]]:
         """The forward as alternating ("compute", fn) / ("exchange", fn) phases: the device
@@ -738,7 +700,7 @@ class ForwardPlan:
     @property
     def spmm_launches(self):
         """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""
-        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged, kernels.PreparedFusedHinge)
+        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged)
         pick = lambda L: [l for l in L.launches if isinstance(l, kinds)]
         return pick(self._layer1), pick(self._layer2)
 

@@ -83,7 +83,35 @@ def placeholder_with_default(value, shape=None, name=None) -> Placeholder:
     return Placeholder(None, shape, name, default=value, has_default=True)
 
 
-_VARIABLES: list = []  # weak references to every Variable, in creation order (TF's GLOBAL_VARIABLES)
+class Graph:
+    """tf.Graph: here only the owner of a variable collection (TF's GLOBAL_VARIABLES), so that
+    global_variables() / global_variables_initializer() cover the variables of one graph, not
+    every model the process ever built.  Variables join the default graph at creation."""
+
+    def __init__(self):
+        self._variables: list = []  # weak references, in creation order
+
+    @contextlib.contextmanager
+    def as_default(self):
+        global _DEFAULT
+        prev, _DEFAULT = _DEFAULT, self
+        try:
+            yield self
+        finally:
+            _DEFAULT = prev
+
+
+_DEFAULT = Graph()
+
+
+def get_default_graph() -> Graph:
+    return _DEFAULT
+
+
+def reset_default_graph() -> None:
+    """tf.reset_default_graph: later variables go to a fresh graph."""
+    global _DEFAULT
+    _DEFAULT = Graph()
 
 
 class Variable(Node):
@@ -95,7 +123,7 @@ class Variable(Node):
         super().__init__(name)
         self.tensor = tensor
         self.initializer = initializer
-        _VARIABLES.append(weakref.ref(self))
+        _DEFAULT._variables.append(weakref.ref(self))
 
     @property
     def shape(self):
@@ -244,21 +272,26 @@ def name_scope(name: str):
 
 
 def global_variables() -> list:
-    """Every live Variable, in creation order (tf.global_variables)."""
-    live = [r() for r in _VARIABLES]
-    _VARIABLES[:] = [r for r, v in zip(list(_VARIABLES), live) if v is not None]
+    """The default graph's live Variables, in creation order (tf.global_variables)."""
+    reg = _DEFAULT._variables
+    live = [r() for r in reg]
+    reg[:] = [r for r, v in zip(list(reg), live) if v is not None]
     return [v for v in live if v is not None]
 
 
 def global_variables_initializer() -> Operation:
     """tf.global_variables_initializer (main.py:286, DecagonTrainer.py:49): running it
-    re-draws every variable from its initializer (glorot, inits.py:5-12 — in place, so the
-    prepared kernels keep their buffers) and resets the optimizer slots the session holds
-    (Adam's m, v and beta powers are TF variables too).  Variables are also initialised at
-    construction, so a model is usable without running it."""
+    re-draws the variables of the default graph that existed when it was created — as TF's
+    op groups the initializers of the collection at creation — from their initializers
+    (glorot, inits.py:5-12 — in place, so the prepared kernels keep their buffers), and resets
+    the optimizer slots the session holds (Adam's m, v and beta powers are TF variables too).
+    Variables are also initialised at construction, so a model is usable without running it."""
+    refs = [weakref.ref(v) for v in global_variables()]
+
     def fn(ctx):
-        for v in global_variables():
-            if v.initializer is not None:
+        for r in refs:
+            v = r()
+            if v is not None and v.initializer is not None:
                 v.load(v.initializer())
         ctx.session.reset_optimizer_slots()
         return None

@@ -812,78 +812,6 @@ class PreparedDecoderHinge:
         check(self._fn(*a, _stream_ptr(stream)), "dg_decoder_hinge_f32")
 
 
-class PreparedFusedHinge:
-    """dg_gcn_fused_hinge_f32: a PreparedFused layer and a PreparedDecoderHinge step in ONE
-    launch (the decoder workgroups wait in-launch for the layer's rows).  Same buffers and the
-    same outputs as running `fused` then `hinge` (the loss summed in another fixed order);
-    `timeouts()` reads the sticky word the in-launch wait sets if it ever gives up."""
-
-    WS_WORDS = 260  # arrival shards, ticket, timeout word; the partials follow
-
-    def __init__(self, fused: "PreparedFused", hinge: "PreparedDecoderHinge"):
-        if not 2 <= fused.block_threads() <= 8:
-            raise ValueError("the fused layer's workgroup must have 2..8 waves (128..512 threads)")
-        self.fused, self.hinge = fused, hinge
-        n = hinge.pos.numel()
-        self._ws = torch.zeros(self.WS_WORDS + 4 + -(-n // 32), device=hinge.pos.device, dtype=torch.int32)
-        self.desc = _lib.DgHingeDesc()
-        self._fn = _lib.load().dg_gcn_fused_hinge_f32
-
-    def _fill(self) -> None:
-        """The descriptor from the hinge's dg_decoder_hinge_f32 argument list (same order as
-        that signature), the current seed / offset and this launch's workspace."""
-        q = self.desc
-        (q.row_table, q.ld_row, q.col_table, q.ld_col, q.rows, q.cols, q.neg_rows, q.alias_table, q.range,
-         _seed, _offset, q.n, q.G, q.l, q.d, q.margin, q.pos, q.neg, q.neg_rows_out, q.loss, _ws) = self.hinge._args
-        q.seed, q.offset = self.hinge.seed & (2**64 - 1), self.hinge.offset & (2**64 - 1)
-        q.workspace = self._ws.data_ptr()
-
-    def timeouts(self) -> int:
-        return int(self._ws[257].item())
-
-    def _layer_desc(self, f: "PreparedFused") -> "_lib.DgFusedLayer":
-        from ctypes import POINTER, cast
-
-        L = _lib.DgFusedLayer()
-        L.groups, L.n_groups = cast(f._garr, POINTER(DgRelGroup)), f._ng
-        L.targets, L.n_targets = cast(f._tarr, POINTER(DgFusedTarget)), f._nt
-        L.projs = cast(f._parr, POINTER(DgProj)) if f._np else None
-        L.n_projs, L.waves_per_group, L.d = f._np, f.wpg, f.d
-        return L
-
-    def __call__(self, stream=None) -> None:
-        f = self.fused
-        self._fill()
-        check(self._fn(f._garr, f._ng, f._tarr, f._nt, f._parr if f._np else None, f._np, f.wpg, f.d,
-                       ctypes.byref(self.desc), _stream_ptr(stream)), "dg_gcn_fused_hinge_f32")
-
-
-class PreparedStep(PreparedFusedHinge):
-    """dg_gcn_step_f32: layer 1 (fused, with the layer-2 projection epilogue), layer 2 (fused)
-    and the decoder step in ONE launch, each stage waiting in-launch for the previous one.
-    Same buffers and outputs as the three launches (the loss in another fixed order)."""
-
-    WS_WORDS = 516  # two arrival-shard sets, ticket, timeout word; the partials follow
-
-    def __init__(self, fused1: "PreparedFused", fused2: "PreparedFused", hinge: "PreparedDecoderHinge"):
-        if fused1.d != 64 or fused2.d != 32 or fused2._np:
-            raise ValueError("dg_gcn_step_f32 takes layer 1 at d = 64 and layer 2 at d = 32 without projections")
-        if fused1.block_threads() != fused2.block_threads():
-            raise ValueError("both layers' workgroups must have the same size")
-        super().__init__(fused2, hinge)
-        self.fused1 = fused1
-        self._l1, self._l2 = self._layer_desc(fused1), self._layer_desc(fused2)
-        self._fn = _lib.load().dg_gcn_step_f32
-
-    def timeouts(self) -> int:
-        return int(self._ws[513].item())
-
-    def __call__(self, stream=None) -> None:
-        self._fill()
-        check(self._fn(ctypes.byref(self._l1), ctypes.byref(self._l2), ctypes.byref(self.desc),
-                       _stream_ptr(stream)), "dg_gcn_step_f32")
-
-
 # --------------------------------------------------------------------------------------
 # Training step (train.hip): decoder gradient, gather-gradient scatter, l2-norm backward, Adam
 # --------------------------------------------------------------------------------------

@@ -192,6 +192,7 @@ class DecagonModel(Model):
                             dropout=(keep, self.dropout_state(ctx)) if keep < 1.0 else None)
             hit = (dg, feats, p)
             cache.put(key, hit, torch.cuda.memory_allocated(ctx.session.device) - before)
+            p.cache_ref = (cache, key)  # later allocations for this plan (its TrainPlan) are charged to it
         return hit[2]
 
     def _forward(self, ctx: RunContext) -> ForwardPlan:

@@ -206,7 +206,11 @@ class DecagonOptimizer:
             feats = {j: runtime.feature_csr(ctx, model.inputs[j]) if j in model.inputs else None
                      for j in fwd.g.n_nodes}
             w1, w2 = model.weight_stacks()
+            before = torch.cuda.memory_allocated(ctx.session.device)
             plans[id(self)] = train.TrainPlan(fwd, w1, w2, feats)
+            ref = getattr(fwd, "cache_ref", None)
+            if ref is not None:  # the backward's buffers count against the plan's LRU entry
+                ref[0].add_bytes(ref[1], torch.cuda.memory_allocated(ctx.session.device) - before)
         return fwd, plans[id(self)]
 
     def _decoder_grads(self, ctx: RunContext, model, e: int, rt: int, ct: int):
@@ -276,16 +280,17 @@ class DecagonOptimizer:
             if tp.sharded:
                 raise NotImplementedError("grads_vars under sharding: each relation's gradient lives on its owner rank")
             return self._grads_vars(model, tp, dec_grads)
+        # the Adam slots belong to the variables (session-wide); the prepared launch, which holds
+        # this plan's gradient buffers, lives on the TrainPlan, so evicting the plan frees both
         key = ("adam", id(self))
         cache = ctx.session.caches
         if key not in cache:
-            st = train.AdamState(params, lr=float(FLAGS.learning_rate))
-            cache[key] = (st, {})
-        st, prepared = cache[key]
-        pk = tuple(g.data_ptr() for g in grads)
-        if pk not in prepared:
-            prepared[pk] = st.prepared(grads)
-        st.apply(prepared[pk])
+            cache[key] = train.AdamState(params, lr=float(FLAGS.learning_rate))
+        st = cache[key]
+        prep = getattr(tp, "adam_prepared", None)
+        if prep is None or prep[0] is not st:
+            tp.adam_prepared = prep = (st, st.prepared(grads))
+        st.apply(prep[1])
         return None
 
     def _grads_vars(self, model, tp, dec_grads):

@@ -92,8 +92,15 @@ class RcclComm:
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         """out = the ranks' equal blocks in rank order; `inp` may be this rank's block of `out`
         (in place, as RCCL allows)."""
-        if out.dtype != torch.float32 or inp.dtype != torch.float32 or out.numel() != inp.numel() * self.world:
-            raise ValueError("RcclComm.all_gather: fp32 tensors, out = world x inp")
+        for x in (out, inp):
+            if x.dtype != torch.float32 or not x.is_contiguous() or not x.is_cuda:
+                raise ValueError("RcclComm.all_gather takes contiguous fp32 device tensors")
+        if out.numel() != inp.numel() * self.world:
+            raise ValueError("RcclComm.all_gather: out must hold world x inp elements")
+        # in place: inp must be exactly this rank's block of out (RCCL reads it from there)
+        lo, hi = out.data_ptr(), out.data_ptr() + 4 * out.numel()
+        if lo <= inp.data_ptr() < hi and inp.data_ptr() != lo + 4 * self.rank * inp.numel():
+            raise ValueError("RcclComm.all_gather: an in-place input must be this rank's block of out")
         _check(_lib().ncclAllGather(inp.data_ptr(), out.data_ptr(), inp.numel(), _NCCL_FLOAT32, self.comm,
                                     self._stream()), "ncclAllGather")
 

@@ -98,6 +98,21 @@ class ByteLRU:
             if self.on_evict is not None:
                 self.on_evict(k, v)
 
+    def add_bytes(self, key, nbytes: int) -> None:
+        """Charge `nbytes` more to a cached entry (memory allocated for it after insertion),
+        evicting least recently used entries past the cap as put() does."""
+        hit = self._d.get(key)
+        if hit is None:
+            return
+        self._d[key] = (hit[0], hit[1] + int(nbytes))
+        self.bytes += int(nbytes)
+        self._d.move_to_end(key)
+        while self.bytes > self.cap and len(self._d) > 1:
+            k, (v, nb) = self._d.popitem(last=False)
+            self.bytes -= nb
+            if self.on_evict is not None:
+                self.on_evict(k, v)
+
     def pop(self, key) -> None:
         hit = self._d.pop(key, None)
         if hit is not None:

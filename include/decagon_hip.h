@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (24); bumped whenever a struct layout or a signature changes. */
+/* ABI version (25); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -157,71 +157,6 @@ int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
                      const dg_fused_target* targets /* HOST */, int32_t n_targets,
                      const dg_proj* projs /* HOST, may be NULL */, int32_t n_projs,
                      int32_t waves_per_group, int32_t d, void* stream);
-
-/* The same fused layer and, in the SAME launch, the decoder step of dg_decoder_hinge_f32 on the
- * rows it produces (config S's layer 2 + DEDICOM/DistMult/bilinear scores + hinge loss in one
- * launch instead of two: one kernel boundary fewer, and the batch loads and negative draws
- * overlap the layer).  Extra workgroups after the layer's score 32-pair tiles (two waves per
- * tile; the layer's workgroup must have 128..512 threads) once every layer workgroup has
- * published its rows (write-through stores + an arrival counter, read back with sc1 loads —
- * no dispatch-order assumption; the wait is bounded and a timeout sets workspace word 257).
- * Results equal dg_gcn_fused_f32 followed by dg_decoder_hinge_f32, except the loss, which
- * sums the same hinge terms in another fixed order.  row_table / col_table may be outputs of
- * this launch.  Replaces layers.py:109-118 + model.py:85-88 + optimizer.py:37-57, :116-120. */
-typedef struct dg_hinge_desc {
-    const float* row_table;     /* device, row embeddings (ld_row floats apart)              */
-    const float* col_table;     /* device, column embeddings                                 */
-    int64_t ld_row;
-    int64_t ld_col;
-    const int32_t* rows;        /* device, [n] positive row indices                          */
-    const int32_t* cols;        /* device, [n] column indices                                */
-    const int32_t* neg_rows;    /* device, [n] given negatives, or NULL: drawn from alias    */
-    const uint32_t* alias_table;/* device, [range][2] Walker alias table (dg_unigram_sample)  */
-    int32_t range;
-    int32_t n;
-    uint64_t seed;
-    uint64_t offset;
-    const float* G;             /* device, [d][d] */
-    const float* l;             /* device, [d] or NULL */
-    int32_t d;                  /* multiple of 32, <= 256 */
-    float margin;
-    float* pos;                 /* device, [n] */
-    float* neg;                 /* device, [n] */
-    int32_t* neg_rows_out;      /* device, [n] or NULL */
-    float* loss;                /* device, [1] */
-    void* workspace;            /* device, >= 1040 + 4*ceil(n/32) bytes, 16-B aligned, zeroed */
-                                /* before the first call (the launch leaves it re-armed)     */
-} dg_hinge_desc;
-
-/* The whole config-S forward step in ONE launch: layer 1 (fused, with the layer-2 projection
- * epilogue), layer 2 (fused, reading those projections) and the decoder step of
- * dg_gcn_fused_hinge_f32 — each stage's workgroups after the previous stage's in the grid, each
- * waiting in-launch (bounded) for the previous stage's published bytes.  Results equal
- * dg_gcn_fused_f32(layer1), dg_gcn_fused_f32(layer2), dg_decoder_hinge_f32 (the loss in another
- * fixed order).  Requirements: layer1.d == 64, layer2.d == 32, layer2 without projections and
- * without DG_GROUP_DENSE_ROWS groups, layer-2 operands < 2 GB, both layers' workgroups of the
- * same size in 128..512 threads; workspace >= 2064 + 4*ceil(n/32) bytes, zeroed before the
- * first call.  Replaces layers.py:70-118 + model.py:64-88 + optimizer.py:37-57, :116-120. */
-typedef struct dg_fused_layer {
-    const dg_rel_group* groups;     /* HOST */
-    int32_t n_groups;
-    int32_t n_targets;
-    const dg_fused_target* targets; /* HOST */
-    const dg_proj* projs;           /* HOST, may be NULL */
-    int32_t n_projs;
-    int32_t waves_per_group;
-    int32_t d;
-    int32_t reserved;
-} dg_fused_layer;
-
-int dg_gcn_step_f32(const dg_fused_layer* layer1 /* HOST */, const dg_fused_layer* layer2 /* HOST */,
-                    const dg_hinge_desc* hinge /* HOST */, void* stream);
-
-int dg_gcn_fused_hinge_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
-                           const dg_fused_target* targets /* HOST */, int32_t n_targets,
-                           const dg_proj* projs /* HOST, may be NULL */, int32_t n_projs,
-                           int32_t waves_per_group, int32_t d, const dg_hinge_desc* hinge /* HOST */,
-                           void* stream);
 
 /* --------------------------------------------------------------------------------------
  * LDS-staged relation SpMM for groups of many relations over a narrow column space

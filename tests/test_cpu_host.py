@@ -333,3 +333,35 @@ def test_global_variables_initializer_redraws_in_place():
     changed = [not np.array_equal(before[id(v)][1], v.eval()) for v in mine]
     assert all(v.tensor.data_ptr() == before[id(v)][0] for v in mine)   # in place
     assert sum(changed) == len(mine) and reset == [1]
+
+
+def test_global_variables_are_scoped_to_their_graph():
+    """TF's GLOBAL_VARIABLES belong to one graph, and the initializer op groups the variables
+    that existed when it was created: a model built in another graph (or after the op) is
+    not re-drawn."""
+    import decagon_amd as dg
+
+    et = {(0, 0): 1, (0, 1): 1, (1, 0): 1, (1, 1): 2}
+    dec = {(0, 0): "bilinear", (0, 1): "bilinear", (1, 0): "bilinear", (1, 1): "dedicom"}
+
+    class _S:
+        def reset_optimizer_slots(self):
+            pass
+
+    class _Ctx:
+        session = _S()
+
+    g_a, g_b = dg.Graph(), dg.Graph()
+    with g_a.as_default():
+        a = dg.DecagonModel(dg.construct_placeholders(et), {0: 12, 1: 8}, {0: 12, 1: 8}, et, dec)
+        init_a = dg.global_variables_initializer()
+        assert dg.get_default_graph() is g_a
+    with g_b.as_default():
+        b = dg.DecagonModel(dg.construct_placeholders(et), {0: 12, 1: 8}, {0: 12, 1: 8}, et, dec)
+        vb = {k: v.eval().copy() for k, v in b.layers1[0, 0].vars.items()}
+        assert all(any(v is x for x in dg.global_variables()) for v in b.layers1[0, 0].vars.values())
+        assert not any(v is x for x in dg.global_variables() for v in a.layers1[0, 0].vars.values())
+    va = {k: v.eval().copy() for k, v in a.layers1[0, 0].vars.items()}
+    init_a._fn(_Ctx())
+    assert all(not np.array_equal(va[k], v.eval()) for k, v in a.layers1[0, 0].vars.items())
+    assert all(np.array_equal(vb[k], v.eval()) for k, v in b.layers1[0, 0].vars.items())
