@@ -170,8 +170,9 @@ SIGNATURES = {
     "dg_staged_block": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
-    "dg_decoder_score_bf16_paired": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
-                                        c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "dg_slot_scores_bf16": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
+                                      c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32,
+                                      c_int64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p]),
     "dg_decoder_hinge_f32": (
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,

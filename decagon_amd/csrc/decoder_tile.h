@@ -1,5 +1,5 @@
 // One wave's 32-pair decoder tile and the counter-based unigram draw, shared by decoder.hip
-// (the decoder launches) and spmm.hip (the layer-2 + decoder launch of config S).
+// (the decoder launches) and slot_scorer.hip (config 5's draws).
 //
 // Replaces (paths relative to the reference root):
 //   DecagonOptimizer.batch_predict + tf.diag_part     decagon/deep/optimizer.py:51-57, :63-85

@@ -141,26 +141,45 @@ def replicate_sets(g: SyntheticGraph, copies: int) -> SyntheticGraph:
 class Config5:
     """BASELINE configs[4]'s scorer inputs (float32 here; the bench and tests round them to
     bf16): d = 256 drug embeddings, the global R, one D_k per drug-drug relation slot, B
-    positive pairs per slot (slot-major) and the drug degrees the sampler follows."""
+    positive pairs per slot (slot-major, edges of the slot's relation) and each slot's drug
+    degrees, which its negatives follow (optimizer.py:38-47 samples relation k's negatives
+    from degrees[i][k])."""
 
     E: np.ndarray
     R: np.ndarray
     D: np.ndarray
     pos_rows: np.ndarray
     pos_cols: np.ndarray
-    degrees: np.ndarray
+    degrees: np.ndarray  # [n_slots, n_drugs]
     batch: int
 
 
 def make_config5(seed: int = 5, n_drugs: int = 645, n_slots: int = 1928, d: int = 256, batch: int = 512) -> Config5:
+    """Slots are config P's drug-drug relations: relation r (1-based, r <= n_slots/2) has
+    max(500, ⌊28,568·r^-0.31⌋) undirected edges, slot r + n_slots/2 is its
+    transpose (same degrees); each slot's positives are B of its edges."""
     rng = np.random.default_rng(seed)
     E = (rng.standard_normal((n_drugs, d)) / 4).astype(np.float32)
     r = np.sqrt(6.0 / (2 * d))
     R = rng.uniform(-r, r, (d, d)).astype(np.float32)
     r = np.sqrt(6.0 / (d + 1))
     D = rng.uniform(-r, r, (n_slots, d)).astype(np.float32)
-    n = n_slots * batch
-    pos_rows = rng.integers(0, n_drugs, n).astype(np.int32)
-    pos_cols = rng.integers(0, n_drugs, n).astype(np.int32)
-    degrees = rng.integers(1, 200, n_drugs).astype(np.float64)
+    half = n_slots // 2 if n_slots > 1 else n_slots
+    degrees = np.zeros((n_slots, n_drugs), np.float64)
+    pos_rows = np.empty(n_slots * batch, np.int32)
+    pos_cols = np.empty(n_slots * batch, np.int32)
+    edges = {}
+    for k in range(n_slots):
+        rel = k % half
+        if rel not in edges:
+            size = max(500, int(28568 * (rel + 1) ** -0.31))
+            a = rng.integers(0, n_drugs, size)
+            b = rng.integers(0, n_drugs, size)
+            keep = a != b
+            edges[rel] = (a[keep], b[keep])
+        src, dst = edges[rel] if k < half else edges[rel][::-1]  # slot k + half: the transpose
+        degrees[k] = np.bincount(src, minlength=n_drugs) + np.bincount(dst, minlength=n_drugs)
+        pick = rng.integers(0, src.size, batch)
+        pos_rows[k * batch:(k + 1) * batch] = src[pick]
+        pos_cols[k * batch:(k + 1) * batch] = dst[pick]
     return Config5(E, R, D, pos_rows, pos_cols, degrees, batch)

@@ -42,6 +42,27 @@ def rel_err(got, want) -> float:
     return float(np.max(np.abs(got - want)) / den)
 
 
+def alias_draws(table, seed, idx):
+    """Host restatement of the device's counter-based alias draw (decoder_tile.h unigram_draw):
+    h = splitmix64(seed ^ splitmix64(idx)); column j = ((h >> 32)·range) >> 32; accept j when
+    the 24-bit uniform of h's low bits is below its probability, else its alias."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+    def sm(z):
+        z = (z + np.uint64(0x9E3779B97F4A7C15)) & M
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M
+        return z ^ (z >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        h = sm(np.uint64(seed) ^ sm(np.asarray(idx, np.uint64)))
+    rng_ = np.uint64(table.shape[0])
+    j = (((h >> np.uint64(32)) * rng_) >> np.uint64(32)).astype(np.int64)
+    u = (h & np.uint64(0xFFFFFF)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    q = table[:, 0].view(np.float32)
+    return np.where(u < q[j], j, table[j, 1].astype(np.int64)).astype(np.int32)
+
+
 # ---------------------------------------------------------------- multi-rank tests (gloo)
 def _rank_entry(fn, rank, world, port, q, args):
     """Child process of run_ranks: gloo group, fn(rank, world, *args) -> payload, reported

@@ -11,7 +11,11 @@ embeddings, equal to oracle/decagon_oracle.py's restatement of the reference for
   * a scaled-down config P with the proteins row-split and the drug×drug relations
     LPT-sharded into the LDS-staged kernel (configs[3]'s plan), on 2 and 3 ranks (uneven
     row blocks, a short last block);
-  * config P at full size on 2 ranks (configs[3], every output row).
+  * config P at full size on 2 and 8 ranks (configs[3], every output row; 8 is the partition
+    the driver's 8-GPU run executes: 241 staged drug×drug relations and a 2,386-row protein
+    block per rank);
+  * config S's weak-scaling form and the scaled-down P at 4 and 8 ranks;
+  * h1 == h2 on a row-split graph (each layer keeps its own padded output).
 
 Each is run eagerly and as the bench's N > 1 form (each compute phase captured in a
 hipGraph, the collectives eager between replays).
@@ -26,11 +30,11 @@ torch = pytest.importorskip("torch")
 TOL = 1e-4
 
 
-def _weights(g, seed, s1=0.1, s2=0.3):
+def _weights(g, seed, s1=0.1, s2=0.3, h2=32):
     rng = np.random.default_rng(seed)
     n = g.n_nodes
     w1 = {et: rng.uniform(-s1, s1, (K, n[et[1]], 64)).astype(np.float32) for et, K in g.edge_types.items()}
-    w2 = {et: rng.uniform(-s2, s2, (K, 64, 32)).astype(np.float32) for et, K in g.edge_types.items()}
+    w2 = {et: rng.uniform(-s2, s2, (K, 64, h2)).astype(np.float32) for et, K in g.edge_types.items()}
     return w1, w2
 
 
@@ -63,18 +67,18 @@ def _shard(kind, g, rank, world):
                                row_split_min=1000)
 
 
-def _rank(rank, world, kind):
+def _rank(rank, world, kind, h2=32):
     from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
 
     dev = torch.device("cuda", 0)
     g = _graph(kind, world)
     shard = _shard(kind, g, rank, world)
-    w1, w2 = _weights(g, 5)
+    w1, w2 = _weights(g, 5, h2=h2)
     dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local, row_block=shard.row_block,
                      chunk=shard.chunks)
     plan = ForwardPlan(dg, {0: None, 1: None},
                        LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
-                       LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, 32,
+                       LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, h2,
                        shard=shard)
     info = {"row_split": sorted(shard.row_block), "staged": dg.groups[(1, 1)].staged,
             "local": {et: len(v) for et, v in shard.local.items()}, "fused": sorted(plan.fused)}
@@ -108,12 +112,12 @@ def _rank(rank, world, kind):
     return info, eager, grab()
 
 
-def _oracle(kind, g):
+def _oracle(kind, g, h2=32):
     import scipy.sparse as sp
 
     from oracle import decagon_oracle as orc
 
-    w1, w2 = _weights(g, 5)
+    w1, w2 = _weights(g, 5, h2=h2)
     if kind == "P":
         csr = {et: [sp.csr_matrix((v.astype(np.float32).astype(np.float64), (c[:, 0], c[:, 1])), shape=s)
                     for c, v, s in mats] for et, mats in g.adj.items()}
@@ -127,19 +131,22 @@ def _oracle(kind, g):
                                {et: [x.astype(np.float64) for x in w] for et, w in w2.items()})
 
 
-def _check(kind, world):
+def _check(kind, world, h2=32):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    got = run_ranks(_rank, world, (kind,))
+    got = run_ranks(_rank, world, (kind, h2))
     g = _graph(kind, world)
-    h1, emb = _oracle(kind, g)
+    h1, emb = _oracle(kind, g, h2)
     for r in range(world):
         info, eager, graphed = got[r]
         if kind == "S-rows":
             assert info["row_split"] == [0, 1] and info["fused"] == [0, 1], info  # fused row blocks
         elif kind != "S":
             assert info["row_split"] == [0], info          # proteins row-split
-            assert info["staged"], info                    # drug×drug in the LDS-staged kernel
+            # drug×drug in the LDS-staged kernel whenever the rank holds enough of them (P-small
+            # at 4 / 8 ranks leaves 30 / 15 per rank: those run in the partial-mode SpMM)
+            from decagon_amd.engine import STAGED_MIN_RELS
+            assert info["staged"] == (info["local"][1, 1] >= STAGED_MIN_RELS), info
         for form in (eager, graphed):
             for t in (0, 1):
                 assert rel_err(form[0][t], h1[t]) <= TOL, (r, "hidden1", t)
@@ -158,22 +165,30 @@ def test_sharded_S_forward_matches_oracle():
     _check("S", 2)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_weak_scaling_S_row_split_matches_oracle(world):
     """bench.py's config S at N GPUs: N relation sets, every node type row-split and finished
     in the fused kernel over all N sets' relations, blocks all-gathered."""
     _check("S-rows", world)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_P_shaped_row_split_matches_oracle(world):
     _check("P-small", world)
 
 
-def test_sharded_full_size_P_matches_oracle():
+def test_sharded_row_split_equal_layer_widths():
+    """h1 == h2 on a row-split graph: hidden1 and the embeddings keep separate padded
+    buffers (the layer-2 operand is not overwritten by the layer-2 output)."""
+    _check("P-small", 2, h2=64)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_full_size_P_matches_oracle(world):
     """configs[3]'s plan at full size (19,085 + 645 nodes, 1,932 matrices, ≈23 M nnz) on 2
-    ranks: proteins row-split, 1,928 drug×drug relations LPT-sharded (staged kernel)."""
-    _check("P", 2)
+    and 8 ranks: proteins row-split, 1,928 drug×drug relations LPT-sharded (staged kernel) —
+    at 8, the partition of the driver's 8-GPU run."""
+    _check("P", world)
 
 
 # ---------------------------------------------------------------------------- training
