@@ -46,10 +46,12 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build libdecagon_hip.so)")
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile every csrc/*.hip into decagon_amd/lib/libdecagon_hip.so for gfx950."""
-    out = lib_path()
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, defines=(), out: Path = None) -> Path:
+    """Compile every csrc/*.hip into decagon_amd/lib/libdecagon_hip.so for gfx950 (or, with
+    `defines` such as "DG_SLOT_ABL=1", a variant build into `out`: A/B and ablation runs load
+    it through DG_LIB)."""
+    out = lib_path() if out is None else Path(out)
+    if not force and not defines and not needs_build():
         return out
     LIBDIR.mkdir(parents=True, exist_ok=True)
     tmp = out.with_suffix(".so.tmp")
@@ -64,6 +66,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         "-Wno-pass-failed",
         f"-I{INCLUDE}",
         f"-I{CSRC}",
+        *[f"-D{d}" for d in defines],
         "-o",
         str(tmp),
         *[str(s) for s in _sources()],
@@ -80,4 +83,10 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+
+    # python -m decagon_amd._build [NAME DEFINE ...]: a variant lib/var_NAME.so
+    if len(sys.argv) > 2:
+        print(build(force=True, defines=sys.argv[2:], out=LIBDIR / f"var_{sys.argv[1]}.so"))
+    else:
+        print(build(force=True, verbose=True))

@@ -170,9 +170,8 @@ SIGNATURES = {
     "dg_staged_block": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
-    "dg_slot_scores_bf16": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
-                                      c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32,
-                                      c_int64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p]),
+    "dg_decoder_score_bf16_paired": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                        c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "dg_decoder_hinge_f32": (
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
@@ -207,6 +206,8 @@ SIGNATURES = {
                                          c_int64, c_void_p]),
     "dg_rank_metrics_f32": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int64,
                                       c_void_p]),
+    "dg_unigram_sample_slots": (c_int32, [c_void_p, c_int32, c_int64, c_int32, c_int32, c_int32, ctypes.c_uint64,
+                                          c_void_p, c_void_p]),
     "dg_unigram_sample": (
         c_int32,
         [c_void_p, c_int32, c_int32, c_uint64, c_uint64, c_void_p, c_void_p],

@@ -235,6 +235,17 @@ __global__ __launch_bounds__(256) void unigram_sample_kernel(const uint2* table,
     out[idx] = unigram_draw(table, range, seed, offset + (uint64_t)idx);
 }
 
+// one table per relation slot: draw i is draw slot0*batch + i of slot (slot0 + i / batch)'s table
+__global__ __launch_bounds__(256) void unigram_sample_slots_kernel(const uint2* table, int range, int64_t stride,
+                                                                   int slot0, int batch, int n, uint64_t seed,
+                                                                   int32_t* out) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n) return;
+    const int slot = slot0 + idx / batch;
+    out[idx] = unigram_draw(table + (int64_t)slot * stride, range, seed,
+                            (uint64_t)slot0 * (uint64_t)batch + (uint64_t)idx);
+}
+
 }  // namespace
 
 extern "C" int dg_decoder_score_f32(const float* row_table, int64_t ld_row, const float* col_table,
@@ -291,6 +302,19 @@ extern "C" int dg_unigram_sample(const uint32_t* alias_table, int32_t range, int
     hipLaunchKernelGGL(unigram_sample_kernel, dim3(dg::ceil_div(n, 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream),
                        reinterpret_cast<const uint2*>(alias_table), range, n, seed, offset, out);
+    return dg::launch_status();
+}
+
+extern "C" int dg_unigram_sample_slots(const uint32_t* alias_table, int32_t range, int64_t alias_stride,
+                                       int32_t slot0, int32_t batch, int32_t n, uint64_t seed, int32_t* out,
+                                       void* stream) {
+    if (range < 1 || n < 0 || batch < 1 || slot0 < 0 || alias_stride < 0 || !alias_table || (n > 0 && !out))
+        return DG_EINVAL;
+    if (alias_stride > 0 && alias_stride < range) return DG_EINVAL;
+    if (n == 0) return DG_OK;
+    hipLaunchKernelGGL(unigram_sample_slots_kernel, dim3(dg::ceil_div(n, 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint2*>(alias_table), range,
+                       alias_stride, slot0, batch, n, seed, out);
     return dg::launch_status();
 }
 

@@ -666,11 +666,15 @@ def decoder_score(row_table: torch.Tensor, col_table: torch.Tensor, row_idx: tor
 def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: torch.Tensor,
                        cols: torch.Tensor, G: torch.Tensor, l_table: Optional[torch.Tensor] = None,
                        rel: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-                       stream=None) -> torch.Tensor:
+                       stream=None, paired: bool = False) -> torch.Tensor:
     """bf16 DEDICOM scores of pairs (rows[p], cols[p]) of relations rel[p] (dg_decoder_score_bf16):
-    uᵀ·D_k·G·D_k·v with bf16 tables / G / diagonals and fp32 accumulation, any mix of pairs
-    and relations (config 5's slot layout has its own kernel: slot_scores_bf16)."""
+    uᵀ·D_k·G·D_k·v with bf16 tables / G / diagonals and fp32 accumulation (config 5).
+    paired: the caller promises pair p and pair p + n/2 share the column and the relation (a
+    positive and its negative); dg_decoder_score_bf16_paired scores them together, reading cols
+    and rel of the first half only."""
     n = rows.numel()
+    if paired and (n % 2 or cols.numel() != n or (rel is not None and rel.numel() != n)):
+        raise ValueError("paired scoring needs an even number of pairs, cols / rel of the same length")
     d = G.shape[0]
     for t, nm in ((row_table, "row_table"), (col_table, "col_table"), (G, "G")):
         _dev(t, torch.bfloat16, nm)
@@ -688,53 +692,11 @@ def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: t
         raise ValueError("tables must have d contiguous columns")
     if out is None:
         out = torch.empty(n, device=rows.device, dtype=torch.float32)
-    check(_lib.load().dg_decoder_score_bf16(
+    name = "dg_decoder_score_bf16_paired" if paired else "dg_decoder_score_bf16"
+    check(getattr(_lib.load(), name)(
         row_table.data_ptr(), row_table.stride(0), col_table.data_ptr(), col_table.stride(0), rows.data_ptr(),
-        cols.data_ptr(), rel.data_ptr() if rel is not None else None, n, G.data_ptr(),
-        l_table.data_ptr() if l_table is not None else None, d, out.data_ptr(), _stream_ptr(stream)),
-        "dg_decoder_score_bf16")
-    return out
-
-
-def slot_scores_bf16(row_table: torch.Tensor, col_table: torch.Tensor, Rt: torch.Tensor, D: torch.Tensor,
-                     pos_rows: torch.Tensor, pos_cols: torch.Tensor, batch: int, slot0: int,
-                     alias: torch.Tensor, seed: int, neg_rows: torch.Tensor, out: torch.Tensor,
-                     stream=None) -> torch.Tensor:
-    """Config 5's slot scorer (dg_slot_scores_bf16): for each local slot s of n_slots =
-    pos_rows.numel() / batch (global id slot0 + s), draw its negatives from its own alias table
-    (alias: int32 [n_tables, range, 2], one table per GLOBAL slot, or [range, 2] shared) and
-    score its positives and negatives with Rt = Rᵀ (bf16 [d][d]) and D_k = D[slot0 + s].
-    out: fp32 [2·n_slots·batch] (positives, then negatives)."""
-    for t, nm in ((row_table, "row_table"), (col_table, "col_table"), (Rt, "Rt"), (D, "D")):
-        _dev(t, torch.bfloat16, nm)
-    for t, nm in ((pos_rows, "pos_rows"), (pos_cols, "pos_cols"), (alias, "alias"), (neg_rows, "neg_rows")):
-        _dev(t, torch.int32, nm)
-    _dev(out, torch.float32, "out")
-    d = Rt.shape[0]
-    n = pos_rows.numel()
-    if n % batch or pos_cols.numel() != n or neg_rows.numel() < n or out.numel() < 2 * n:
-        raise ValueError("slot_scores_bf16: pos_rows / pos_cols hold n_slots·batch pairs; neg_rows, out sized to match")
-    if Rt.shape != (d, d) or not Rt.is_contiguous() or D.dim() != 2 or D.shape[1] != d or not D.is_contiguous():
-        raise ValueError("slot_scores_bf16: Rt must be a contiguous [d, d], D a contiguous [n, d] bf16 tensor")
-    n_slots = n // batch
-    if slot0 < 0 or slot0 + n_slots > D.shape[0]:
-        raise ValueError("slot range outside D")
-    if alias.dim() == 3:
-        if alias.shape[0] < slot0 + n_slots or alias.shape[2] != 2 or not alias.is_contiguous():
-            raise ValueError("per-slot alias tables must be a contiguous [n_slots_total, range, 2] tensor")
-        rng, stride = alias.shape[1], alias.shape[1]
-    elif alias.dim() == 2 and alias.shape[1] == 2:
-        rng, stride = alias.shape[0], 0
-    else:
-        raise ValueError("alias must be [range, 2] or [n_slots, range, 2]")
-    for t in (row_table, col_table):
-        if t.shape[1] != d or t.stride(1) != 1:
-            raise ValueError("tables must have d contiguous columns")
-    check(_lib.load().dg_slot_scores_bf16(
-        row_table.data_ptr(), row_table.stride(0), row_table.shape[0], col_table.data_ptr(), col_table.stride(0),
-        col_table.shape[0], Rt.data_ptr(), D.data_ptr(), d, pos_rows.data_ptr(), pos_cols.data_ptr(), n_slots,
-        batch, slot0, alias.data_ptr(), rng, stride, seed & (2**64 - 1), neg_rows.data_ptr(), out.data_ptr(),
-        _stream_ptr(stream)), "dg_slot_scores_bf16")
+        cols.data_ptr(), rel.data_ptr() if rel is not None else None, n // 2 if paired else n, G.data_ptr(),
+        l_table.data_ptr() if l_table is not None else None, d, out.data_ptr(), _stream_ptr(stream)), name)
     return out
 
 
@@ -792,6 +754,30 @@ def unigram_sample(table: torch.Tensor, n: int, seed: int, offset: int,
     check(_lib.load().dg_unigram_sample(table.data_ptr(), table.shape[0], n, seed & (2**64 - 1),
                                          offset & (2**64 - 1), out.data_ptr(), _stream_ptr(stream)),
           "dg_unigram_sample")
+    return out
+
+
+def unigram_sample_slots(table: torch.Tensor, slot0: int, batch: int, n: int, seed: int,
+                         out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """n draws, draw i from the alias table of relation slot slot0 + i // batch (table: int32
+    [n_slots, range, 2], one per GLOBAL slot; or a shared [range, 2]) — counter slot0·batch + i,
+    so the draws do not depend on how slots are dealt to ranks (dg_unigram_sample_slots)."""
+    _dev(table, torch.int32, "alias table")
+    if table.dim() == 3 and table.shape[2] == 2 and table.is_contiguous():
+        rng, stride = table.shape[1], table.shape[1]
+        if slot0 + -(-n // batch) > table.shape[0]:
+            raise ValueError("slot range outside the alias tables")
+    elif table.dim() == 2 and table.shape[1] == 2:
+        rng, stride = table.shape[0], 0
+    else:
+        raise ValueError("alias tables must be [n_slots, range, 2] (contiguous) or [range, 2]")
+    if out is None:
+        out = torch.empty(n, device=table.device, dtype=torch.int32)
+    _dev(out, torch.int32, "out")
+    if out.numel() < n:
+        raise ValueError("out too small")
+    check(_lib.load().dg_unigram_sample_slots(table.data_ptr(), rng, stride, slot0, batch, n, seed & (2**64 - 1),
+                                               out.data_ptr(), _stream_ptr(stream)), "dg_unigram_sample_slots")
     return out
 
 

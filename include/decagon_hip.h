@@ -364,16 +364,19 @@ int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint1
  * the bf16 operand), D_k = D[slot0 + s].  Rt is Rᵀ (Rt[n][k] = R[k][n]), bf16 [d][d]; tables and
  * D are bf16 rows.  Per slot the product E·(D_k∘R) is computed once for every row of the row
  * table (32-row tiles on the bf16 MFMA) and each pair is a dot with it.  d == 256,
- * n_rows <= 1024, n_cols <= 65535, 2*batch <= 2048, 1 <= range <= n_rows.
+ * n_rows <= 1024, n_cols <= 65535, batch <= 512, 1 <= range <= n_rows.
  * Replaces optimizer.py:38-47 (fixed_unigram_candidate_sampler, per relation's degrees) and
  * :51-57 / :63-85 (batch_predict pos / neg, G = R, L = D_k: model.py:130-134). */
-int dg_slot_scores_bf16(const uint16_t* row_table, int64_t ld_row, int32_t n_rows,
-                        const uint16_t* col_table, int64_t ld_col, int32_t n_cols,
-                        const uint16_t* Rt, const uint16_t* D, int32_t d,
-                        const int32_t* pos_rows, const int32_t* pos_cols, int32_t n_slots,
-                        int32_t batch, int32_t slot0, const uint32_t* alias_table, int32_t range,
-                        int64_t alias_stride, uint64_t seed, int32_t* neg_rows, float* out,
-                        void* stream);
+/* The same scores for config 5's layout: pairs p < n_half and p + n_half (a positive and its
+ * negative, optimizer.py:37-57) share the column and the relation, so col_idx / rel_idx are read
+ * for the first half only (row_idx, out hold 2*n_half entries).  One wave scores both pairs of
+ * a batch entry: every Rᵀ fragment it reads from LDS feeds two MFMAs, and the shared v and D_k
+ * rows are loaded once.  Same bf16 operands and k order as dg_decoder_score_bf16; the epilogue
+ * sums the n's in another fixed order (fp32 rounding apart, the same scores). */
+int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
+                                 int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
+                                 const int32_t* rel_idx, int32_t n_half, const uint16_t* G,
+                                 const uint16_t* l_table, int32_t d, float* out, void* stream);
 
 /* Fused decoder step (T8 + T9 + T11 + T12 in one launch):
  *   neg_row[b] = neg_rows[b] if neg_rows != NULL, else draw (offset + b) of the alias
@@ -530,6 +533,14 @@ int dg_rank_metrics_ex_f32(const float* pos, int32_t n_pos, const float* neg, in
  * -------------------------------------------------------------------------------------- */
 int dg_unigram_sample(const uint32_t* alias_table, int32_t range, int32_t n, uint64_t seed,
                       uint64_t offset, int32_t* out, void* stream);
+
+/* The same draws with one table per relation slot (optimizer.py:38-47 samples relation k's
+ * negatives from ITS degrees, degrees[i][k]): draw i < n is draw slot0*batch + i of the table
+ * of slot slot0 + i / batch, at alias_table + (slot0 + i / batch) * alias_stride entries
+ * (alias_stride 0: one shared table, = dg_unigram_sample with offset slot0*batch). */
+int dg_unigram_sample_slots(const uint32_t* alias_table, int32_t range, int64_t alias_stride,
+                            int32_t slot0, int32_t batch, int32_t n, uint64_t seed, int32_t* out,
+                            void* stream);
 
 #ifdef __cplusplus
 }

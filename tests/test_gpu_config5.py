@@ -4,7 +4,7 @@ d = 256 bf16 DEDICOM decoder, then the hinge loss (decagon_amd.scorer.SlotScorer
 bench.py runs it) — against a float64 restatement of the reference's scores
 (decagon/deep/optimizer.py:51-57, 63-85 with G = R, L = D_k: model.py:130-134) and hinge
 (optimizer.py:116-120) over EVERY pair, with the same bf16 operand rounding as the kernel
-(inputs rounded to bf16; D_k[k]·R[k][n] rounded to bf16 as the MFMA's operand; fp32 after).
+(inputs rounded to bf16; u∘D_k rounded to bf16 as the MFMA's operand; fp32 accumulation).
 
 The negatives are read back from the device: each slot's are exactly the restated alias draws
 of THAT slot's degree^0.75 table (fixed_unigram_candidate_sampler over degrees[i][k],
@@ -36,19 +36,20 @@ def _scorer(device, slots=None, allreduce=None):
 
 
 def _restated_scores(c5, rows, cols):
-    """float64 uᵀ·(D_k∘R)·D_k·v on the bf16-rounded inputs, D_k[k]·R[k][n] rounded to bf16 (the
-    MFMA operand); pairs slot-major, B per slot."""
+    """float64 uᵀ·D_k·R·D_k·v on the bf16-rounded inputs, u∘D_k rounded to bf16 (the MFMA
+    operand); pairs slot-major, B per slot."""
     bf = torch.bfloat16
-    E = torch.from_numpy(c5.E).to(bf).double().numpy()
+    E = torch.from_numpy(c5.E).to(bf).float().numpy()
     R = torch.from_numpy(c5.R).to(bf).double().numpy()
-    D = torch.from_numpy(c5.D).to(bf).double().numpy()
-    B = c5.batch
+    D = torch.from_numpy(c5.D).to(bf).float().numpy()
+    rel = np.repeat(np.arange(D.shape[0]), c5.batch)
     out = np.empty(len(rows))
-    for k in range(D.shape[0]):
-        Bk = torch.from_numpy(D[k][:, None] * R).to(bf).double().numpy()
-        T = E @ Bk                                                      # every drug's row, once
-        sl = slice(k * B, (k + 1) * B)
-        out[sl] = np.einsum("pn,pn->p", T[rows[sl]], D[k] * E[cols[sl]])
+    step = 1 << 16
+    for s in range(0, len(rows), step):
+        r, c, k = rows[s:s + step], cols[s:s + step], rel[s:s + step]
+        a = torch.from_numpy(E[r] * D[k]).to(bf).double().numpy()          # the MFMA operand
+        b = D[k].astype(np.float64) * E[c].astype(np.float64)
+        out[s:s + step] = np.einsum("pn,pn->p", a @ R, b)
     return out
 
 

@@ -332,61 +332,67 @@ def test_decoder_score_bf16(K, d):
     assert rel_err(got2, want2) <= 1e-4
 
 
-@pytest.mark.parametrize("n_rows,n_cols,batch,slot0,n_slots,per_slot", [
-    (645, 645, 512, 0, 6, True),     # config 5's shape (few slots)
-    (33, 200, 37, 3, 5, True),       # ragged last tile, odd batch, a slot sub-range, other col table
-    (1024, 40, 1024, 1, 2, False),   # 32 full tiles, the largest batch, one shared table
-    (1, 1, 3, 0, 2, True),           # one row
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("n_half", [32 * 40 + 13, 7, 4096])
+def test_decoder_score_bf16_paired(K, d, n_half):
+    """dg_decoder_score_bf16_paired (config 5's positive / negative layout: pair p and p + n_half
+    share the column and the relation) against the unpaired kernel (same operands and k order;
+    the epilogue's n order differs: fp32 rounding) and the float64 restatement; ragged tails,
+    relations mixed within a tile, with and without the diagonals."""
+    rng = np.random.default_rng(d + n_half)
+    n_r, n_c, n_rel = 300, 200, 7
+    bf = torch.bfloat16
+    E_r = torch.from_numpy(rng.standard_normal((n_r, d)).astype(np.float32)).to(bf)
+    E_c = torch.from_numpy(rng.standard_normal((n_c, d)).astype(np.float32)).to(bf)
+    R = torch.from_numpy((rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)).to(bf)
+    Dk = torch.from_numpy(rng.standard_normal((n_rel, d)).astype(np.float32)).to(bf)
+    rows = rng.integers(0, n_r, 2 * n_half).astype(np.int32)
+    c1 = rng.integers(0, n_c, n_half).astype(np.int32)
+    r1 = rng.integers(0, n_rel, n_half).astype(np.int32)
+    cols, rel = np.concatenate([c1, c1]), np.concatenate([r1, r1])
+    dv = lambda x: torch.from_numpy(x).cuda()
+    for L in (Dk, None):
+        args = (E_r.cuda(), E_c.cuda(), dv(rows), dv(cols), R.cuda(), None if L is None else L.cuda(), dv(rel))
+        got = K.decoder_score_bf16(*args, paired=True).cpu().numpy()
+        ref = K.decoder_score_bf16(*args).cpu().numpy()
+        assert rel_err(got, ref) <= 1e-5
+        u = E_r.float().numpy()[rows]
+        v = E_c.float().numpy()[cols]
+        dk = L.float().numpy()[rel] if L is not None else np.ones_like(u)
+        a = torch.from_numpy((u * dk).astype(np.float32)).to(bf).double().numpy()
+        want = np.einsum("pi,in,pn->p", a, R.double().numpy(), dk.astype(np.float64) * v.astype(np.float64))
+        assert rel_err(got, want) <= 1e-4
+    with pytest.raises(ValueError):
+        K.decoder_score_bf16(E_r.cuda(), E_c.cuda(), dv(rows[:-1]), dv(cols[:-1]), R.cuda(), paired=True)
+
+
+@pytest.mark.parametrize("range_,batch,slot0,n_slots,per_slot", [
+    (645, 512, 0, 7, True),      # config 5's tables
+    (33, 37, 3, 5, True),        # odd batch, a slot sub-range
+    (1, 3, 0, 2, True),          # one row
+    (200, 64, 2, 3, False),      # one shared table (= dg_unigram_sample at offset slot0·batch)
 ])
-def test_slot_scores_bf16(K, n_rows, n_cols, batch, slot0, n_slots, per_slot):
-    """dg_slot_scores_bf16 (config 5's scorer) against float64: the negatives are exactly the
-    restated alias draws of each slot's own table (counter (slot0 + s)·batch + i), every score
-    equals uᵀ·(D_k∘R)_bf16·D_k·v over the same bf16 inputs (the products D_k[k]·R[k][n]
-    rounded to bf16 as the MFMA operand, fp32 after) within 1e-4.  Rows concentrated in one
-    tile exercise the bucket overflow past the prefetched rounds."""
+def test_unigram_sample_slots(K, range_, batch, slot0, n_slots, per_slot):
+    """dg_unigram_sample_slots: draw i of slot slot0 + i // batch is exactly the restated alias
+    draw (conftest.alias_draws) of THAT slot's table at counter slot0·batch + i — per-relation
+    degree distributions (optimizer.py:38-47), independent of how slots are dealt to ranks."""
     from decagon_amd.sampling import alias_table
 
-    d = 256
-    rng = np.random.default_rng(n_rows + batch)
-    bf = torch.bfloat16
-    E_r = torch.from_numpy((rng.standard_normal((n_rows, d)) / 4).astype(np.float32)).to(bf)
-    E_c = torch.from_numpy((rng.standard_normal((n_cols, d)) / 4).astype(np.float32)).to(bf)
-    R = torch.from_numpy(rng.uniform(-0.1, 0.1, (d, d)).astype(np.float32)).to(bf)
-    total = slot0 + n_slots + 1
-    Dk = torch.from_numpy(rng.uniform(-1, 1, (total, d)).astype(np.float32)).to(bf)
-    n = n_slots * batch
-    pr = rng.integers(0, n_rows, n).astype(np.int32)
-    pr[: batch // 2] = rng.integers(0, min(n_rows, 32), batch // 2)  # one crowded tile in slot 0
-    pc = rng.integers(0, n_cols, n).astype(np.int32)
-    degs = [rng.integers(0, 50, n_rows).astype(np.float64) + (k % 3 == 0) for k in range(total)]
-    for dg_ in degs:
-        dg_[0] += 1  # a positive sum
+    rng = np.random.default_rng(range_ + batch)
+    total = slot0 + n_slots
+    degs = [rng.integers(0, 40, range_).astype(np.float64) for _ in range(total)]
+    for x in degs:
+        x[rng.integers(0, range_)] += 1  # a positive sum
     tabs = np.stack([alias_table(x) for x in degs]) if per_slot else alias_table(degs[0])
-    dv = lambda x: torch.from_numpy(x).cuda()
-    neg = torch.full((n,), -1, dtype=torch.int32, device="cuda")
-    out = torch.full((2 * n,), float("nan"), device="cuda")
-    Rt = R.t().contiguous().cuda()
-    K.slot_scores_bf16(E_r.cuda(), E_c.cuda(), Rt, Dk.cuda(), dv(pr), dv(pc), batch, slot0,
-                       dv(tabs.view(np.int32)), 99, neg, out)
-    neg_h = neg.cpu().numpy()
+    n = n_slots * batch
+    got = K.unigram_sample_slots(torch.from_numpy(tabs.view(np.int32)).cuda(), slot0, batch, n, 1234).cpu().numpy()
     for s in range(n_slots):
         tab = tabs[slot0 + s] if per_slot else tabs
-        idx = (slot0 + s) * batch + np.arange(batch)
-        assert np.array_equal(neg_h[s * batch:(s + 1) * batch], alias_draws(tab, 99, idx)), s
-    got = out.cpu().numpy()
-    Ef, Cf, Rf, Df = (x.float().numpy().astype(np.float64) for x in (E_r, E_c, R, Dk))
-    want = np.empty(2 * n)
-    for s in range(n_slots):
-        dk = Df[slot0 + s]
-        Bs = torch.from_numpy((dk[:, None] * Rf).astype(np.float32)).to(bf).double().numpy()  # the operand
-        for half, rows in ((0, pr), (1, neg_h)):
-            sl = slice(s * batch, (s + 1) * batch)
-            T = Ef[rows[sl]] @ Bs
-            want[half * n + s * batch: half * n + (s + 1) * batch] = np.einsum("pn,pn->p", T, dk * Cf[pc[sl]])
-    assert rel_err(got, want) <= 1e-4
-    with pytest.raises(ValueError):  # a batch that does not divide the pairs
-        K.slot_scores_bf16(E_r.cuda(), E_c.cuda(), Rt, Dk.cuda(), dv(pr[:-1]), dv(pc[:-1]), batch, slot0,
-                           dv(tabs.view(np.int32)), 99, neg, out)
+        idx = slot0 * batch + s * batch + np.arange(batch)
+        assert np.array_equal(got[s * batch:(s + 1) * batch], alias_draws(tab, 1234, idx)), s
+    if not per_slot:  # the shared-table form is dg_unigram_sample's stream
+        one = K.unigram_sample(torch.from_numpy(tabs.view(np.int32)).cuda(), n, 1234, slot0 * batch).cpu().numpy()
+        assert np.array_equal(got, one)
 
 
 def test_losses(K):
