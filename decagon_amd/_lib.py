@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 25
+ABI_VERSION = 26
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -164,6 +164,10 @@ SIGNATURES = {
                                       c_void_p]),
     "dg_dropout_elems_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
                                        ctypes.c_uint32, c_float, c_void_p]),
+    "dg_dropout_rows_map_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_int32, c_int32, c_void_p,
+                                          ctypes.c_uint32, ctypes.c_float, c_void_p]),
+    "dg_dropout_elems_map_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
+                                           ctypes.c_uint32, ctypes.c_float, c_void_p]),
     "dg_dropout_advance": (c_int32, [c_void_p, c_void_p]),
     "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_staged_proj_f32": (c_int32, [POINTER(DgStagedGroup), POINTER(DgStagedProj), c_int32, c_int32, c_void_p]),

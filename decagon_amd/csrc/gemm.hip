@@ -103,11 +103,12 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
             t = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, t, 0, 0, 0);
         }
         if (drop) {
-            // Σ_b M_b∘(A_b·B_b): element (row, col) of batch b carries mask bit (b·m + row)·n + col
+            // Σ_b M_b∘(A_b·B_b): element (row, col) of batch b carries mask bit (bb·m + row)·n + col
+            // (bb = b_map[b]: a relation shard's batch b is global relation bb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const uint32_t idx = static_cast<uint32_t>(((int64_t)b * g.m + mrow) * g.n + col);
+                const uint32_t idx = static_cast<uint32_t>(((int64_t)bb * g.m + mrow) * g.n + col);
                 dsum[r] += t[r] * dg::keep_scale(dkey, idx, g.drop_keep);
             }
         }
@@ -130,7 +131,9 @@ __global__ __launch_bounds__(256) void gemm_f32_generic(const GemmArgs args) {
 // the order c = 16h + s (s = MFMA step, h = lane half) — a permutation of the same sum — so
 // each lane reads 16 contiguous floats of its row (4 float4 loads) instead of 16 scattered
 // ones.  A wave computes a 32-row tile against all n (≤ 64: NT tiles) for its run of batches;
-// with a dropout descriptor each batch product is masked before it joins the run's sum.
+// with a dropout descriptor each batch product is masked before it joins the run's sum.  With a
+// batch map, batch b reads B_{map(b)} and carries mask bits of batch map(b) (A and the run
+// index stay unmapped).
 template <int NT>
 __global__ __launch_bounds__(256) void gemm_f32_reduce_k32(const GemmArgs args) {
     int tb, bblk;
@@ -153,6 +156,7 @@ __global__ __launch_bounds__(256) void gemm_f32_reduce_k32(const GemmArgs args) 
     // the next batch's fragments are loaded while the current batch's MFMAs run
     float4 a4[4], b4[NT][4];
     auto load = [&](int b) {
+        const int bb = g.b_map ? g.b_map[b] : b;
         const float* A = g.a + b * g.a_bs + (int64_t)(row_ok ? row : 0) * g.a_sm + 16 * h;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(256) void gemm_f32_reduce_k32(const GemmArgs args) 
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const int col = t * 32 + i;
-            const float* B = g.b + b * g.b_bs + (int64_t)(col < g.n ? col : 0) * g.b_sn + 16 * h;
+            const float* B = g.b + bb * g.b_bs + (int64_t)(col < g.n ? col : 0) * g.b_sn + 16 * h;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 b4[t][q] = col < g.n ? *reinterpret_cast<const float4*>(B + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -190,12 +194,13 @@ __global__ __launch_bounds__(256) void gemm_f32_reduce_k32(const GemmArgs args) 
             }
         }
         if (drop) {
+            const int bb = g.b_map ? g.b_map[b] : b;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int mrow = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const uint32_t idx = static_cast<uint32_t>(((int64_t)b * g.m + mrow) * g.n + t * 32 + i);
+                    const uint32_t idx = static_cast<uint32_t>(((int64_t)bb * g.m + mrow) * g.n + t * 32 + i);
                     sum[t][r] += acc[t][r] * dg::keep_scale(dkey, idx, g.drop_keep);
                 }
         } else {
@@ -569,9 +574,9 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
         // wave amortises its A fragment over up to 16 relations.
         int bpw = 1;
         while (bpw < 16 && (int64_t)g.tile_blocks * 4 * dg::ceil_div(d->batch, bpw * 2) >= 8192) bpw *= 2;
-        if (d->reduce < 0 || (d->reduce > 0 && d->b_map)) return DG_EINVAL;
+        if (d->reduce < 0) return DG_EINVAL;
         if (d->drop_state && (d->reduce <= 0 || !(d->drop_keep > 0.f && d->drop_keep <= 1.f))) return DG_EINVAL;
-        if (d->drop_state && (int64_t)d->batch * d->m * d->n >= 0xFFFFFFFFLL) return DG_EINVAL;
+        if (d->drop_state && !d->b_map && (int64_t)d->batch * d->m * d->n >= 0xFFFFFFFFLL) return DG_EINVAL;
         g.reduce = d->reduce > 0 ? 1 : 0;
         g.drop_state = d->drop_state;
         g.drop_tag = d->drop_tag;

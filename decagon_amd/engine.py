@@ -312,14 +312,12 @@ class ForwardPlan:
             raise ValueError("a row-split device graph needs its RelationShard (with an all-gather)")
         if shard is not None and allreduce is None:
             raise ValueError("a RelationShard needs its all-reduce")
-        if self.row_block and keep_sums:
-            raise NotImplementedError("training with row-split node types is not on the HIP path")
         # dropout (training): (keep probability, device state {seed, step}); every forward
         # draws new masks (the step advances first), the backward reuses them
+        # (sharded: a relation's masks are keyed by its GLOBAL id, so every rank — and one GPU —
+        # masks it identically; each rank masks its own relations only)
         self.keep, self.drop_state = 1.0, None
         if dropout is not None and float(dropout[0]) < 1.0:
-            if allreduce is not None or self.row_block:
-                raise NotImplementedError("dropout with a sharded forward is not on the HIP path")
             self.keep, self.drop_state = float(dropout[0]), dropout[1]
         # flat mode: every group's pre-normalisation sum S_ij lands in one flat buffer per
         # layer (all-reduced when sharded; kept for the backward when training), and one fused
@@ -368,9 +366,15 @@ class ForwardPlan:
                 if self.drop_state is not None:
                     # dropout_sparse on the identity (layers.py:87-88): relation k's operand is W1_k
                     # with rows kept / scaled by 1/keep — a masked copy of the stack per forward
+                    # (sharded: of the local relations' slabs only, at their global positions)
                     xd = torch.empty_like(W)
-                    self._pre.append(lambda W=W, xd=xd, t=drop_tag(1, self.et_index[et]):
-                                     kernels.dropout_rows(W, xd, self.drop_state, t, self.keep))
+                    t = drop_tag(1, self.et_index[et])
+                    if grp.rel_map is None:
+                        self._pre.append(lambda W=W, xd=xd, t=t: kernels.dropout_rows(W, xd, self.drop_state, t,
+                                                                                      self.keep))
+                    elif grp.n_rels:
+                        self._pre.append(lambda W=W, xd=xd, t=t, m=grp.rel_map, F=F: kernels.dropout_rows_map(
+                            W, xd, m, F, self.drop_state, t, self.keep, True, True))
                     x1[et] = xd
                 continue
             if fj.shape[0] != n[j] or fj.shape[1] != F:
@@ -455,14 +459,25 @@ class ForwardPlan:
             j = et[1]
             W = w2.stacks[et]
             if self.drop_state is not None:
-                # tf.nn.dropout(H1_j) drawn per relation (layers.py:111-113): H_k = M_k∘H1_j/keep
-                hd = torch.empty((grp.K, n[j], h1), **f32)
+                # tf.nn.dropout(H1_j) drawn per relation (layers.py:111-113): H_k = M_k∘H1_j/keep,
+                # one slab per LOCAL relation in ascending relation id (the backward's dP order;
+                # sharded: slab b is relation sorted_ids[b], its mask drawn under that global id),
+                # projected into P's global slabs
+                hd = torch.empty((grp.n_rels, n[j], h1), **f32)
                 self.hdrop[et] = hd
-                drops.append(lambda j=j, hd=hd, t=drop_tag(2, self.et_index[et]):
-                             kernels.dropout_elems(self.hidden1[j], hd, self.drop_state, t, self.keep))
+                t = drop_tag(2, self.et_index[et])
+                sids = np.sort(grp.rel_ids).astype(np.int32)
+                smap = None if np.array_equal(sids, np.arange(grp.K)) else torch.from_numpy(sids).to(dev)
+                if smap is None:
+                    drops.append(lambda j=j, hd=hd, t=t: kernels.dropout_elems(self.hidden1[j], hd, self.drop_state,
+                                                                               t, self.keep))
+                else:
+                    drops.append(lambda j=j, hd=hd, t=t, m=smap: kernels.dropout_elems_map(
+                        self.hidden1[j], hd, m, self.drop_state, t, self.keep))
                 gemms.append(kernels.PreparedGemm(
                     hd, (n[j] * h1, h1, 1), W, (h1 * h2, h2, 1), self.proj[et], (n[j] * h2, h2, 1),
-                    n[j], h2, h1, grp.n_rels))
+                    n[j], h2, h1, grp.n_rels, b_map=smap, b_batches=W.shape[0],
+                    b_map_max=int(sids.max()) if smap is not None else None))
                 continue
             gemms.append(kernels.PreparedGemm(
                 self.hidden1[j], (0, h1, 1), W, (h1 * h2, h2, 1), self.proj[et], (n[j] * h2, h2, 1),
@@ -600,7 +615,14 @@ class ForwardPlan:
                 a, b, blk = self.row_block[i]
                 pad = self._pad[i, 1 if relu else 2]
                 r0 = self.shard.rank * blk
-                blocks.append(([partials[et] for et in self.targets[i]], pad[r0:r0 + (b - a)], b - a))
+                parts = [partials[et] for et in self.targets[i]]
+                if self.keep_sums:
+                    # training: the epilogue also keeps each group's pre-normalisation sum S_ij over
+                    # this rank's block rows (the backward's l2-norm gradient reads them)
+                    for n_, et in enumerate(self.targets[i]):
+                        views[et] = torch.empty((b - a) * d, **f32)
+                        parts[n_] = (parts[n_][0], parts[n_][1], views[et])
+                blocks.append((parts, pad[r0:r0 + (b - a)], b - a))
                 gathers.append((pad, pad[r0:r0 + blk]))
             # the relation-sharded node types' chunk reduces ride in the same launch: a target
             # whose groups write their pre-normalisation sums into the send buffer (its

@@ -532,8 +532,8 @@ class PreparedGemm:
         if m and n and k and batch:
             if a.numel() < span(a_strides, m, k) or b.numel() < span(b_strides, k, n, nb_b):
                 raise ValueError("gemm operand too small for its strides")
-        if reduce < 0 or (reduce and b_map is not None):
-            raise ValueError("batch-reduce mode takes no b_map")
+        if reduce < 0:
+            raise ValueError("reduce must be >= 0")
         n_out = -(-batch // reduce) if reduce else nb_b
         if m and n and batch and c.numel() < span(c_strides, m, n, n_out):
             raise ValueError("gemm output too small for its strides")
@@ -557,6 +557,8 @@ class PreparedGemm:
                 raise ValueError("the dropout mask applies in batch-reduce mode")
             if state.dtype != torch.int64 or not state.is_cuda:
                 raise ValueError("dropout state: int64 device tensor {seed, step}")
+            if nb_b * m * n >= 2**32:
+                raise ValueError("dropout mask indices are 32-bit: (mapped) batches·m·n < 2^32")
             desc.drop_state, desc.drop_tag, desc.drop_keep = state.data_ptr(), int(tag), float(keep_p)
         self._desc = desc
         self._keep = (a, b, c, sa, sc, b_map, drop)
@@ -1010,6 +1012,45 @@ def dropout_elems(src: torch.Tensor, out: torch.Tensor, state: torch.Tensor, tag
         raise ValueError("dropout_elems: shapes")
     check(_lib.load().dg_dropout_elems_f32(src.data_ptr(), out.data_ptr(), K, n, d, state.data_ptr(), tag, keep,
                                            _stream_ptr(stream)), "dg_dropout_elems_f32")
+
+
+def dropout_rows_map(inp: torch.Tensor, out: torch.Tensor, rel_map: torch.Tensor, rows_per_slab: int,
+                     state: torch.Tensor, tag: int, keep: float, in_global: bool, out_global: bool,
+                     stream=None) -> None:
+    """Row masks of a relation shard: local slab b (rows_per_slab rows) is global relation
+    rel_map[b] and takes its mask bits; in / out addressed at global slabs (in_global /
+    out_global) or local ones (dg_dropout_rows_map_f32)."""
+    _dev(inp, torch.float32, "in")
+    _dev(out, torch.float32, "out")
+    _dev(rel_map, torch.int32, "rel_map")
+    _drop_state(state)
+    d = inp.shape[-1]
+    n_map = rel_map.numel()
+    for t, glob in ((inp, in_global), (out, out_global)):
+        slabs = t.numel() // (rows_per_slab * d) if rows_per_slab else 0
+        need = (int(rel_map.max()) + 1) if (glob and n_map) else n_map
+        if t.shape[-1] != d or slabs < need:
+            raise ValueError("dropout_rows_map: operand too small for its slabs")
+    check(_lib.load().dg_dropout_rows_map_f32(inp.data_ptr(), out.data_ptr(), rel_map.data_ptr(), n_map,
+                                              rows_per_slab, d, (1 if in_global else 0) | (2 if out_global else 0),
+                                              state.data_ptr(), tag, keep, _stream_ptr(stream)),
+          "dg_dropout_rows_map_f32")
+
+
+def dropout_elems_map(src: torch.Tensor, out: torch.Tensor, rel_map: torch.Tensor, state: torch.Tensor, tag: int,
+                      keep: float, stream=None) -> None:
+    """out[b] = src ∘ M_{rel_map[b]} / keep (src [n][d], out [K_local][n][d]): the per-relation
+    tf.nn.dropout masks of a relation shard (dg_dropout_elems_map_f32)."""
+    _dev(src, torch.float32, "src")
+    _dev(out, torch.float32, "out")
+    _dev(rel_map, torch.int32, "rel_map")
+    _drop_state(state)
+    K, n, d = out.shape
+    if tuple(src.shape) != (n, d) or rel_map.numel() != K:
+        raise ValueError("dropout_elems_map: shapes")
+    check(_lib.load().dg_dropout_elems_map_f32(src.data_ptr(), out.data_ptr(), rel_map.data_ptr(), K, n, d,
+                                               state.data_ptr(), tag, keep, _stream_ptr(stream)),
+          "dg_dropout_elems_map_f32")
 
 
 def dropout_advance(state: torch.Tensor, stream=None) -> None:

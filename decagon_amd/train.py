@@ -29,8 +29,14 @@ ascending relation id), no weight gradient is exchanged and Adam's memory and ti
 with the relations.  The one extra collective is an all-reduce of dH1 (every node type's
 rows, h1 wide) after the layer-2 backward, because dH1_j = Σ_ik dP_ijk·W2_ijkᵀ sums over
 every rank's relations; the decoder and everything after the forward's all-reduces run
-redundantly and identically on every rank.  Row-split node types (sharding.RelationShard.
-split) and dropout are not supported by the sharded backward (they raise).
+redundantly and identically on every rank.  With dropout every relation's masks are drawn
+under its global id (dropout.hip's mapped forms), so each rank's forward and backward mask its
+relations exactly as one GPU does.  Row-split node types (sharding.RelationShard.split) are
+handled too: a rank holds rows [a, b) of every relation into the node type, so its l2-norm
+gradient runs over its block (dE / dH1 rows a..b, the S_ij block sums its epilogue kept), its
+Âᵀ·dS products are partial weight gradients summed by one all-reduce per such relation stack
+after the backward (PPI: 9.8 MB), and every rank applies the same Adam step to those weights;
+their dH1 contributions join the existing dH1 all-reduce.
 """
 from __future__ import annotations
 
@@ -106,8 +112,6 @@ class TrainPlan:
         if not fwd.keep_sums:
             raise NotImplementedError("training runs over a ForwardPlan(keep_sums=True)")
         self.sharded = fwd.allreduce is not None
-        if self.sharded and (fwd.row_block or fwd.drop_state is not None):
-            raise NotImplementedError("sharded training: relation-sharded plans without dropout only")
         self.allreduce = fwd.allreduce
         # with dropout (fwd.drop_state), the backward reuses the forward's masks: the draws of the
         # forward's step, regenerated from the same counter-based hash (dropout.hip)
@@ -130,7 +134,12 @@ class TrainPlan:
             self.dH1[j] = self._dH1_flat[off:off + n[j] * h1].view(n[j], h1)
             off += n[j] * h1
         self.local_ids: Dict[EdgeType, np.ndarray] = {}  # global ids of gW*[et]'s rows
-        self._w2_local = []  # (full W2 stack, ids, compact copy): sharded reduce-GEMM operands
+        # row-split node types (sharding.RelationShard.split): this rank holds rows [a, b) of every
+        # relation into them, so its Âᵀ·dS products over those rows are PARTIAL weight
+        # gradients — all-reduced after the backward (every rank then applies the same Adam step)
+        rb = dict(fwd.row_block)
+        rows_of = lambda i: (rb[i][1] - rb[i][0]) if i in rb else n[i]  # noqa: E731
+        self._rowsplit_grads: List[torch.Tensor] = []
         self.gW1: Dict[EdgeType, torch.Tensor] = {}
         self.gW2: Dict[EdgeType, torch.Tensor] = {}
         specs2, specs1, gemm_w2, gemm_h1 = [], [], [], []
@@ -147,6 +156,9 @@ class TrainPlan:
             ids = np.asarray(grp.rel_ids, np.int64)[order]
             self.local_ids[et] = ids
             K = len(ids)  # local relations (all K_ij on one GPU)
+            # sharded: local relation c (ascending id) is global relation ids[c] — the batch map of
+            # the W2 reads and of the dropout masks
+            idmap = None if np.array_equal(ids, np.arange(grp.K)) else torch.from_numpy(ids.astype(np.int32)).to(dev)
             if K == 0:  # another rank owns every relation of the group: no local gradient
                 self.gW1[et] = torch.zeros((0, n[j] if features.get(j) is None else int(features[j].shape[1]), h1), **f32)
                 self.gW2[et] = torch.zeros((0, h1, h2), **f32)
@@ -159,8 +171,8 @@ class TrainPlan:
             rp, vc, vv = (torch.from_numpy(m.rowptr).to(dev), torch.from_numpy(m.vcol).to(dev),
                           torch.from_numpy(m.val).to(dev))
             vmax = int(m.vcol.max()) if m.nnz else -1
-            dS2 = torch.zeros((n[i], h2), **f32)
-            dS1 = torch.zeros((n[i], h1), **f32)
+            dS2 = torch.zeros((rows_of(i), h2), **f32)
+            dS1 = torch.zeros((rows_of(i), h1), **f32)
             dP = torch.zeros((K, n[j], h2), **f32)
             self._dS1[et], self._dS2[et] = dS1, dS2
             self.gW2[et] = torch.zeros((K,) + tuple(w2.stacks[et].shape[1:]), **f32)
@@ -172,8 +184,10 @@ class TrainPlan:
             # Âᵀ·dS1 per relation: the weight gradient itself (identity features), or the
             # operand of X_jᵀ·(·) (sparse features)
             g1 = self.gW1[et] if fj is None else torch.zeros((K, n[j], h1), **f32)
-            specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, n[i], vcol_max=vmax))
-            specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, g1, n[j], K, h1, n[i], vcol_max=vmax))
+            specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, rows_of(i), vcol_max=vmax))
+            specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, g1, n[j], K, h1, rows_of(i), vcol_max=vmax))
+            if i in rb:
+                self._rowsplit_grads += [self.gW1[et], self.gW2[et]]
             if fj is not None:  # X_jᵀ's pattern shared by the K chunks, chunk k reading G_k
                 xt, perm = transpose_csr(fj, with_perm=True)
                 drop = None
@@ -195,15 +209,19 @@ class TrainPlan:
             part = torch.zeros((n_runs, n[j], h1), **f32)
             drop = ((fwd.drop_state, drop_tag(2, fwd.et_index[et]), fwd.keep) if fwd.drop_state is not None
                     else None)
-            W2 = w2.stacks[et]
-            if K != grp.K:  # sharded: the local relations' W2, gathered each step (Adam moves them)
-                W2 = torch.empty((K,) + tuple(w2.stacks[et].shape[1:]), **f32)
-                self._w2_local.append((w2.stacks[et], torch.from_numpy(ids).to(dev), W2))
+            W2 = w2.stacks[et]  # (sharded: read at the local relations' global slabs)
             gemm_h1.append(kernels.PreparedGemm(dP, (n[j] * h2, h2, 1), W2, (h1 * h2, 1, h2), part,
-                                                (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R, drop=drop))
+                                                (n[j] * h1, h1, 1), n[j], h1, h2, K, reduce=R, drop=drop,
+                                                b_map=idmap, b_batches=grp.K,
+                                                b_map_max=int(ids.max()) if idmap is not None else None))
             if fwd.drop_state is not None and fj is None:  # dW1 rows through layer 1's row masks
-                self._w1_drop.append(lambda g=self.gW1[et], tg=drop_tag(1, fwd.et_index[et]):
-                                     kernels.dropout_rows(g, g, fwd.drop_state, tg, fwd.keep))
+                tg = drop_tag(1, fwd.et_index[et])
+                if idmap is None:
+                    self._w1_drop.append(lambda g=self.gW1[et], tg=tg:
+                                         kernels.dropout_rows(g, g, fwd.drop_state, tg, fwd.keep))
+                else:
+                    self._w1_drop.append(lambda g=self.gW1[et], tg=tg, m=idmap, F=F: kernels.dropout_rows_map(
+                        g, g, m, F, fwd.drop_state, tg, fwd.keep, False, False))
             runs[j].append((part, n_runs))
         chunked = lambda xs: [xs[s:s + DG_MAX_GROUPS] for s in range(0, len(xs), DG_MAX_GROUPS)]  # noqa: E731
         # Âᵀ·dS: operands small enough for LDS (the drug side) take the LDS-staged form
@@ -226,11 +244,12 @@ class TrainPlan:
         L1, L2 = fwd._layer1, fwd._layer2
         self._l2g2, self._l2g1 = [], []
         for i, tets in fwd.targets.items():
+            a, b = (rb[i][0], rb[i][1]) if i in rb else (0, n[i])  # (row-split: this rank's block)
             self._l2g2.append(kernels.PreparedL2Grad([(L2.views[et], self._dS2[et]) for et in tets],
-                                                     self.dE[i], None, n[i], h2))
-            dy = self.dH1[i]  # zero when no layer-2 relation reads H1_i
+                                                     self.dE[i][a:b], None, b - a, h2))
+            dy = self.dH1[i][a:b]  # zero when no layer-2 relation reads H1_i
             self._l2g1.append(kernels.PreparedL2Grad([(L1.views[et], self._dS1[et]) for et in tets],
-                                                     dy, fwd.hidden1[i], n[i], h1))
+                                                     dy, fwd.hidden1[i][a:b], b - a, h1))
 
     def backward(self, decoder_grad) -> None:
         """dE ← decoder_grad(dE) (it adds the decoder's row gradients into the zeroed dE),
@@ -239,8 +258,6 @@ class TrainPlan:
             t.zero_()
         if self.sharded:
             self._dH1_flat.zero_()  # node types without local layer-2 relations add zeros
-            for full, ids, out in self._w2_local:
-                torch.index_select(full, 0, ids, out=out)
         decoder_grad(self.dE)
         for l in self._l2g2:
             l()
@@ -262,6 +279,8 @@ class TrainPlan:
             s()
         for f in self._w1_drop:
             f()
+        for gr in self._rowsplit_grads:  # row-split groups: Σ over the ranks' row blocks
+            self.allreduce(gr)
 
     def adam_pairs(self, w1: LayerWeights, w2: LayerWeights) -> List[Tuple[torch.Tensor, torch.Tensor]]:
         """(parameter, gradient) of every GCN weight this plan updates: whole stacks on one GPU;

@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (25); bumped whenever a struct layout or a signature changes. */
+/* ABI version (26); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -300,7 +300,7 @@ typedef struct dg_gemm_desc {
     int64_t b_bs, b_sk, b_sn;
     int64_t c_bs, c_sm, c_sn;
     int32_t m, n, k, batch;
-    int32_t reduce;             /* 0, or R > 0: batch-reduce mode (below); b_map must be NULL */
+    int32_t reduce;             /* 0, or R > 0: batch-reduce mode (below; b_map maps B and the mask) */
     uint32_t drop_tag;          /* batch-reduce with dropout: mask stream tag */
     const uint64_t* drop_state; /* NULL, or the device dropout state {seed, step} (below) */
     float drop_keep;            /* keep probability when drop_state != NULL */
@@ -317,7 +317,10 @@ int dg_gemm_f32(const dg_gemm_desc* descs /* HOST array */, int32_t n_desc, void
  * as partial sums that dg_gcn_epilogue_f32 (no flags) adds up.  With drop_state != NULL each
  * batch product is first multiplied element-wise by its dropout mask (mask element
  * (b·m + row)·n + col of stream drop_tag, scaled by 1/keep, as dg_dropout_elems_f32 draws it):
- *     C_q = Σ_b M_b∘(A_b·B_b)   — the gradient through tf.nn.dropout (layers.py:112). */
+ *     C_q = Σ_b M_b∘(A_b·B_b)   — the gradient through tf.nn.dropout (layers.py:112).
+ * With b_map in batch-reduce mode, batch b reads B at b_map[b] and takes the mask of batch
+ * b_map[b] (a rank's relation shard: local batch b is global relation b_map[b]); A and the run
+ * index are not mapped. */
 
 /* Batched Aᵀ·B over a long reduction (the weight gradient H_jᵀ·dP_k, backward of
  * layers.py:113):  C_b[m][n] = Σ_{r < rows} A[b*a_bs + r*lda + m] · B[b*b_bs + r*ldb + n],  C
@@ -495,6 +498,16 @@ int dg_dropout_rows_f32(const float* in, float* out, int64_t n_rows, int32_t d, 
  * independently for each of the K relations.  K·n_rows·d < 2^32. */
 int dg_dropout_elems_f32(const float* src, float* out, int32_t K, int32_t n_rows, int32_t d,
                          const uint64_t* state, uint32_t tag, float keep, void* stream);
+/* Relation-mapped forms for a rank's relation shard (sharding.py): local slab b is global
+ * relation rel_map[b] and draws THAT relation's mask bits (the bits the unmapped forms draw
+ * for it).  Rows: slab b is rows_per_slab rows; flags bit 1 / bit 2 address `in` / `out` at
+ * slab rel_map[b] (else b).  Elems: out[b] = src ∘ M_{rel_map[b]} (out local, contiguous). */
+int dg_dropout_rows_map_f32(const float* in, float* out, const int32_t* rel_map, int32_t n_map,
+                            int64_t rows_per_slab, int32_t d, int32_t flags, const uint64_t* state,
+                            uint32_t tag, float keep, void* stream);
+int dg_dropout_elems_map_f32(const float* src, float* out, const int32_t* rel_map, int32_t K,
+                             int32_t n_rows, int32_t d, const uint64_t* state, uint32_t tag, float keep,
+                             void* stream);
 int dg_dropout_advance(uint64_t* state, void* stream);
 
 /* --------------------------------------------------------------------------------------

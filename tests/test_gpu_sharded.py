@@ -192,24 +192,33 @@ def test_sharded_full_size_P_matches_oracle(world):
 
 
 # ---------------------------------------------------------------------------- training
-def _train_rank(rank, world, kind):
-    """One relation-sharded training step (train.py): forward (flat mode, all-reduces), the
-    DEDICOM decoder + hinge on a fixed batch of relation (1,1)_0 with given negatives, the
-    backward (dH1 all-reduce) and TF-Adam on the rank's own relations.  Returns the local
-    gradients by global relation id, the decoder gradients, the updated local weights."""
+def _train_rank(rank, world, kind, split=False, dropout=0.0):
+    """One sharded training step (train.py): forward (flat mode: all-reduces, and with `split`
+    the proteins row-split — all-gathers), the DEDICOM decoder + hinge on a fixed batch of
+    relation (1,1)_0 with given negatives, the backward (dH1 all-reduce; row-split groups'
+    partial weight gradients all-reduced) and TF-Adam on the rank's relations, with dropout
+    masks drawn under each relation's global id.  Returns the local gradients by global
+    relation id, the decoder gradients, the loss and the updated local weights."""
     from decagon_amd import kernels, train
     from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
-    from decagon_amd.sharding import RelationShard, torch_allreduce
+    from decagon_amd.sharding import RelationShard, torch_allgather, torch_allreduce
 
     dev = torch.device("cuda", 0)
     g = _graph(kind)
     nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
-    shard = RelationShard.lpt(g.edge_types, nnz, rank, world, torch_allreduce())
+    if split:
+        shard = RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
+                                    row_split_min=1000)
+    else:
+        shard = RelationShard.lpt(g.edge_types, nnz, rank, world, torch_allreduce())
     w1, w2 = _weights(g, 5)
     W1 = LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()})
     W2 = LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()})
-    dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local)
-    fwd = ForwardPlan(dg, {0: None, 1: None}, W1, W2, 64, 32, shard=shard, keep_sums=True)
+    dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local, row_block=shard.row_block)
+    drop = None
+    if dropout > 0:
+        drop = (1.0 - dropout, torch.tensor([20180701, 0], dtype=torch.int64, device=dev))
+    fwd = ForwardPlan(dg, {0: None, 1: None}, W1, W2, 64, 32, shard=shard, keep_sums=True, dropout=drop)
     tp = train.TrainPlan(fwd, W1, W2, {0: None, 1: None})
     R, l, rows, cols, neg = _train_batch(g)
     E = fwd.embeddings[1]
@@ -244,7 +253,8 @@ def _train_rank(rank, world, kind):
         for et, ids in tp.local_ids.items():
             for k in ids:
                 after[name, et[0], et[1], int(k)] = st.stacks[et][int(k)].cpu().numpy()
-    return grads, {"R": dR.cpu().numpy(), "l": dl.cpu().numpy()}, float(hinge.loss[0]), after
+    info = {"row_split": sorted(shard.row_block)}
+    return grads, {"R": dR.cpu().numpy(), "l": dl.cpu().numpy()}, float(hinge.loss[0]), after, info
 
 
 def _train_batch(g):
@@ -257,8 +267,9 @@ def _train_batch(g):
     return R, l, pick[:, 0], pick[:, 1], neg
 
 
-def _train_oracle(kind, g):
+def _train_oracle(kind, g, dropout=0.0):
     from oracle import decagon_oracle as orc
+    from test_cpu_train_oracle import _masks
 
     w1, w2 = _weights(g, 5)
     R, l, rows, cols, neg = _train_batch(g)
@@ -274,29 +285,37 @@ def _train_oracle(kind, g):
     n = g.n_nodes
     feats = {t: None for t in n}
     adj = {et: [(c, v.astype(np.float32).astype(np.float64), s) for c, v, s in mats] for et, mats in g.adj.items()}
+    drop1, drop2 = _masks(g.edge_types, adj, 1.0 - dropout, step=1) if dropout > 0 else (None, None)
     cost, ref = orc.train_grads(g.edge_types, adj, feats,
                                 {et: [x.astype(np.float64) for x in w] for et, w in w1.items()},
                                 {et: [x.astype(np.float64) for x in w] for et, w in w2.items()},
-                                decoders, dec, 32, np.stack([rows, cols], 1), neg, e, 1, 1, 0.1)
+                                decoders, dec, 32, np.stack([rows, cols], 1), neg, e, 1, 1, 0.1,
+                                drop1=drop1, drop2=drop2)
     return cost, ref, w1, w2
 
 
-def test_sharded_training_step_matches_oracle():
-    """Relation-sharded training on 2 ranks (config S, relations LPT-sharded): every rank's
-    gradients of its own relations and the (replicated) decoder gradients equal the float64
-    oracle's TF-minimize gradients (oracle.train_grads) within 1e-4; every relation is updated
-    by exactly one rank, by one TF-Adam step (oracle.adam_tf) on the device's gradient."""
+@pytest.mark.parametrize("kind,split,dropout", [("S", False, 0.0), ("S", False, 0.1), ("P-small", True, 0.1),
+                                                ("P-small", True, 0.0)])
+def test_sharded_training_step_matches_oracle(kind, split, dropout):
+    """Sharded training on 2 ranks: config S relations LPT-sharded (with and without the
+    reference's default dropout 0.1, main.py:305-308), and the scaled-down config P with its
+    proteins row-split (the multi-GPU plan of config P, optimizer.py:108-114 on it).  Every
+    rank's gradients of its relations and the (replicated) decoder gradients equal the float64
+    oracle's TF-minimize gradients (oracle.train_grads, on the same dropout masks) within 1e-4;
+    a relation-sharded relation is updated by exactly one rank, a row-split group's relations
+    by every rank identically (all-reduced gradients), each by one TF-Adam step (oracle.adam_tf)."""
     from oracle import decagon_oracle as orc
 
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     world = 2
-    got = run_ranks(_train_rank, world, ("S",))
-    g = _graph("S")
-    cost, ref, w1, w2 = _train_oracle("S", g)
-    seen = set()
+    got = run_ranks(_train_rank, world, (kind, split, dropout))
+    g = _graph(kind)
+    cost, ref, w1, w2 = _train_oracle(kind, g, dropout)
+    seen = {}
     for r in range(world):
-        grads, dec, loss, after = got[r]
+        grads, dec, loss, after, info = got[r]
+        assert info["row_split"] == ([0] if split else []), info
         assert abs(loss - cost) <= TOL * abs(cost)
         assert rel_err(dec["R"], ref["dec"][1, 1]["global_interaction"]) <= TOL
         assert rel_err(dec["l"], ref["dec"][1, 1]["local_variation_0"]) <= TOL
@@ -307,6 +326,9 @@ def test_sharded_training_step_matches_oracle():
                 assert np.max(np.abs(gv - want)) <= TOL * max(scale, 1e-30), (r, name, i, j, k)
                 p1, _, _ = orc.adam_tf(wsrc[i, j][k], gv, np.zeros_like(gv), np.zeros_like(gv), 1)
                 assert np.max(np.abs(after[name, i, j, k] - p1)) <= 1e-6 * max(1.0, np.max(np.abs(p1)))
-                assert (name, i, j, k) not in seen
-                seen.add((name, i, j, k))
-    assert len(seen) == 2 * sum(g.edge_types.values())  # every relation, exactly once
+                key = (name, i, j, k)
+                if key in seen:  # only a row-split group's relations live on several ranks
+                    assert split and i in info["row_split"], key
+                    assert np.array_equal(seen[key], after[key]), key
+                seen[key] = after[name, i, j, k]
+    assert len(seen) == 2 * sum(g.edge_types.values())  # every relation

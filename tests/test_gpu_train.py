@@ -439,6 +439,46 @@ def test_gemm_batch_reduce_with_dropout_mask():
         assert rel_err(got[q], ref) <= 1e-5
 
 
+def test_mapped_dropout_masks_and_reduce_gemm():
+    """A relation shard's masks (dg_dropout_rows_map_f32 / dg_dropout_elems_map_f32 and the
+    batch-mapped batch-reduce GEMM): local slab b carries global relation map[b]'s bits, the
+    bits the unmapped kernels (and oracle.dropout_scale) draw for it."""
+    from decagon_amd import kernels
+
+    dev = _dev()
+    state = torch.tensor([4242, 2], dtype=torch.int64, device=dev)
+    K, F, d = 9, 37, 8
+    ids = np.array([1, 4, 5, 8], np.int32)
+    m = torch.from_numpy(ids).to(dev)
+    W = torch.from_numpy(np.random.default_rng(3).standard_normal((K, F, d)).astype(np.float32)).to(dev)
+    full = torch.empty_like(W)
+    kernels.dropout_rows(W, full, state, 31, 0.7)
+    glob = torch.zeros_like(W)
+    kernels.dropout_rows_map(W, glob, m, F, state, 31, 0.7, True, True)
+    loc = W[m.long()].clone()
+    kernels.dropout_rows_map(loc, loc, m, F, state, 31, 0.7, False, False)
+    src = torch.from_numpy(np.random.default_rng(4).standard_normal((F, 64)).astype(np.float32)).to(dev)
+    el_full = torch.empty((K, F, 64), device=dev)
+    kernels.dropout_elems(src, el_full, state, 32, 0.7)
+    el_loc = torch.empty((len(ids), F, 64), device=dev)
+    kernels.dropout_elems_map(src, el_loc, m, state, 32, 0.7)
+    # batch-reduce GEMM over the local relations, W2 read at their global slabs, masks mapped
+    rng = np.random.default_rng(5)
+    dP = torch.from_numpy(rng.standard_normal((len(ids), F, 32)).astype(np.float32)).to(dev)
+    W2 = torch.from_numpy(rng.standard_normal((K, 64, 32)).astype(np.float32)).to(dev)
+    out = torch.zeros((1, F, 64), device=dev)
+    kernels.PreparedGemm(dP, (F * 32, 32, 1), W2, (64 * 32, 1, 32), out, (F * 64, 64, 1), F, 64, 32, len(ids),
+                         reduce=len(ids), drop=(state, 32, 0.7), b_map=m, b_batches=K, b_map_max=8)()
+    torch.cuda.synchronize()
+    assert np.array_equal(glob.cpu().numpy()[ids], full.cpu().numpy()[ids])
+    assert np.array_equal(loc.cpu().numpy(), full.cpu().numpy()[ids])
+    assert np.array_equal(el_loc.cpu().numpy(), el_full.cpu().numpy()[ids])
+    mk = orc.dropout_scale(4242, 2, 32, K * F * 64, 0.7).reshape(K, F, 64).astype(np.float64)
+    want = sum(mk[k] * (dP[b].cpu().numpy().astype(np.float64) @ W2[k].cpu().numpy().T.astype(np.float64))
+               for b, k in enumerate(ids))
+    assert rel_err(out.cpu().numpy()[0], want) <= 1e-5
+
+
 def test_grads_vars_with_dropout_match_oracle(golden_S):
     """The training step at FLAGS.dropout = 0.1 (main.py:235, :307): every gradient against the
     oracle on the same masks (the device's draw for step 1, regenerated by the oracle)."""
