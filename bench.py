@@ -545,18 +545,15 @@ def main_train(args):
     sharded = world > 1 or args.force_shard
     shard = None
     if sharded:
-        # relation-sharded training (train.py): every relation whole on one rank (LPT on
-        # nonzeros, no row split), forward all-reduces + the backward's dH1 all-reduce
-        from decagon_amd.sharding import RelationShard
-
+        # sharded training (train.py) on the forward bench's partition: config S one relation set
+        # per GPU with every node type row-split, config P proteins row-split + drug×drug
+        # relations LPT-sharded — the forward's exchanges, the backward's dH1 all-reduce and the
+        # row-split groups' gradient all-reduce
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.backend)
-        graph, _, scaling, workload = build_workload(args.config, rank, world, False)
-        nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
-        shard = RelationShard.lpt(graph.edge_types, nnz, rank, world, collectives(args.backend)[0])
-        scaling = "strong"
+        graph, shard, scaling, workload = build_workload(args.config, rank, world, True, args.backend)
     else:
         graph, _, scaling, workload = build_workload(args.config, 0, 1, False)
     drop = None
@@ -621,8 +618,8 @@ def main_train(args):
         "data": "synthetic (as the forward bench), random glorot weights, device-sampled negatives",
         "config": {"workload": workload + "; training step: backward + TF-Adam on %d parameters" % params_n,
                    "nnz_per_layer_total": int(edges // 2),
-                   "parallelism": (shard.describe(args.backend) + " + all-reduce of dH1 in the backward"
-                                   if sharded else "1 GPU"),
+                   "parallelism": (shard.describe(args.backend) + " + all-reduce of dH1 (and of the row-split "
+                                   "groups' weight gradients) in the backward" if sharded else "1 GPU"),
                    "hipgraph": not args.no_graph, "steps_per_graph": G},
         "loss_first_step": loss0,
         "loss_last_step": loss1,
