@@ -127,13 +127,10 @@ def build_workload(config, rank, world, sharded, backend="nccl"):
         shard = None
         if sharded:
             # weak scaling: the graph holds one relation set per GPU; every node type is
-            # row-split (each rank finishes its row block over every set's relations in the
-            # fused kernel, then the blocks are all-gathered — no all-reduce of sums)
-            nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
-            shard = RelationShard.split(graph.edge_types, graph.n_nodes, nnz, rank, world, allreduce,
-                                        coll[1], row_split_min=1)
-            shard.chunks = dict(graph.edge_types)  # one chunk per group: the fused kernel's form
-            shard.fused_rows = True
+            # row-split (each rank finishes its row block over every set's relations —
+            # dg_spmm_seg_f32 + the epilogue, layer 2 reassociated — then the blocks are
+            # all-gathered: no all-reduce of sums)
+            shard = RelationShard.weak_sets(graph.edge_types, graph.n_nodes, rank, world, allreduce, coll[1])
         scaling = "weak"
         workload = ("S: main.py 5-relation / 10-matrix synthetic (reference-normalised, 105,974 nnz "
                     "per relation set), 2 GCN layers d=64/32 + DEDICOM decoder B=512+512")
@@ -159,7 +156,8 @@ def make_plan(args, graph, shard, device, keep_sums=False, dropout=None):
     chunk = args.chunk if shard is None or shard.chunks is None else shard.chunks
     dg = DeviceGraph(graph.edge_types, csr, device, None if shard is None else shard.local,
                      chunk=chunk, target_waves=args.target_waves,
-                     row_block=None if shard is None else shard.row_block)
+                     row_block=None if shard is None else shard.row_block,
+                     segments=shard is not None and shard.seg_rows)
     rng = np.random.default_rng(1234)
     n = graph.n_nodes
     w1 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, n[et[1]], H1)).to(device)
@@ -641,7 +639,7 @@ def main_train(args):
 def main_simulate(args):
     """One GPU standing in for each rank of an N-GPU step in turn: the rank's shard (config P:
     proteins row-split, drug×drug relations LPT-sharded; config S: N relation sets, every node
-    type row-split and finished in the fused kernel) with the collectives replaced by no-ops,
+    type row-split — RelationShard.weak_sets) with the collectives replaced by no-ops,
     timed as the bench times a step.  max over ranks + the collectives' time is the N-GPU step
     (DESIGN §6); the bytes each collective moves are printed beside it."""
     import torch
@@ -661,10 +659,7 @@ def main_simulate(args):
     ranks = []
     for r in (range(N) if args.simulate_rank < 0 else [args.simulate_rank]):
         if args.config == "S":
-            nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
-            shard = RelationShard.split(graph.edge_types, graph.n_nodes, nnz, r, N, _no_op_reduce, _no_op,
-                                        row_split_min=1)
-            shard.chunks, shard.fused_rows = dict(graph.edge_types), True
+            shard = RelationShard.weak_sets(graph.edge_types, graph.n_nodes, r, N, _no_op_reduce, _no_op)
         else:
             shard = RelationShard.polypharmacy(graph, r, N, comm=False)
         plan, dg = make_plan(args, graph, shard, device)

@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 26
+ABI_VERSION = 27
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -68,6 +68,26 @@ class DgStagedGroup(ctypes.Structure):
         ("out_chunk", c_int32),
         ("x_rows", c_int32),
         ("jm_len", c_int32),
+    ]
+
+
+class DgSegGroup(ctypes.Structure):
+    _fields_ = [
+        ("rowptr", c_void_p),
+        ("seg", c_void_p),
+        ("vcol", c_void_p),
+        ("val", c_void_p),
+        ("slab", c_void_p),
+        ("x", c_void_p),
+        ("w", c_void_p),
+        ("out", c_void_p),
+        ("x_ld", c_int64),
+        ("n_rows", c_int32),
+        ("n_cols", c_int32),
+        ("n_chunks", c_int32),
+        ("chunk", c_int32),
+        ("n_rels", c_int32),
+        ("x_rows", c_int32),
     ]
 
 
@@ -142,6 +162,7 @@ SIGNATURES = {
     "dg_abi_version": (c_int32, []),
     "dg_spmm_groups_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_groups_lds_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
+    "dg_spmm_seg_f32": (c_int32, [POINTER(DgSegGroup), c_int32, c_int32, c_int32, c_void_p]),
     "dg_spmm_csr_f32": (
         c_int32,
         [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32,

@@ -1,0 +1,237 @@
+// Relation-segment SpMM for gfx950 (MI355X): one wave per (row, relation) — the sharded
+// config-S form (one relation set per GPU, every node type row-split).
+//
+// Reference ops replaced (paths relative to the reference root):
+//   tf.sparse_tensor_dense_matmul(adj_mats[edge_type][k], x)  decagon/deep/layers.py:90, :114
+//   tf.matmul(x, weights_k)                                    decagon/deep/layers.py:113
+//   tf.add_n(outputs) over a chunk of relations               decagon/deep/layers.py:92, :116
+//
+// Why: at N GPUs a rank owns n/N rows of every node type, each carrying N relation sets.  One
+// workgroup per row (dg_gcn_fused_f32) leaves most CUs idle at 113 rows per rank, and the layer-2
+// operands H1_j·W2_k of every relation would have to be projected on every rank (all of H1 is
+// gathered; the projection of a source row is needed by every rank whose rows it touches).
+// Here the item is (chunk, row) with one wave per relation of the chunk, and layer 2 is
+// reassociated,
+//     Σ_k Â_k[r]·(H1·W2_k) = Σ_k (Â_k[r]·H1)·W2_k,
+// so a rank gathers the shared 64-wide H1 rows and projects only the aggregates of its own rows.
+//
+// Per wave (row r, relation t of chunk c):
+//   [W: issue the 8 float4 loads of this lane's W2 slice, before the pairs]
+//   pairs of the segment (one coalesced load of ≤ 64), 8 gathers in flight per lane
+//   (LP lanes per gathered row, 64/LP nonzeros per step), a shuffle butterfly → y = Â_k[r]·X
+//   [W: y through the wave's LDS slot to the matvec layout (lane: output float4 l&7, input
+//    slice 8(l>>3) .. +8), 32 fmaf, a butterfly over the 8 slices → z = y·W_k]
+// then the chunk's waves add their rows in relation order (LDS, one barrier) and the first
+// wave of the row writes out[c][r].  Fixed order, no atomics: bitwise reproducible.
+#include "common.h"
+
+namespace {
+
+struct SegGroupK {
+    const int32_t* rowptr;
+    const int32_t* seg;
+    const int32_t* vcol;
+    const float* val;
+    const int32_t* slab;
+    const float* x;
+    const float* w;
+    float* out;
+    int32_t x_ld;
+    int32_t n_rows;
+    int32_t n_cols;
+    int32_t n_chunks;
+    int32_t chunk;
+    int32_t n_rels;
+    int32_t rpb;         // rows per workgroup: 16 / chunk
+    int32_t row_blocks;
+    int32_t block_begin;
+    int32_t n_blocks;
+};
+
+struct SegArgs {
+    SegGroupK g[DG_MAX_GROUPS];
+    int32_t n_groups;
+    int32_t pad;
+};
+
+constexpr int kSegUnroll = 8;  // gathers in flight per lane
+
+// y = Σ_{p in [beg, end)} val[p] · X[vcol[p]] (X row v at xb + v·x_ld), folded: every lane
+// holds float4 (lane % LP) of the row.
+template <int LP>
+__device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, const float* __restrict__ val,
+                                             const float* xb, int x_ld, int beg, int end) {
+    constexpr int G = dg::kWave / LP;
+    const int lane = threadIdx.x & 63;
+    const int sub = lane / LP;
+    const float* xq = xb + (lane % LP) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int base = beg; base < end; base += 64) {
+        const int n = min(64, end - base);
+        int vc = 0;
+        float vv = 0.f;
+        if (lane < n) {
+            vc = vcol[base + lane];
+            vv = val[base + lane];
+        }
+        const int eoff = vc * x_ld;
+#pragma unroll 1
+        for (int s0 = 0; s0 < n; s0 += kSegUnroll * G) {
+            int o[kSegUnroll];
+            float w[kSegUnroll];
+#pragma unroll
+            for (int u = 0; u < kSegUnroll; ++u) {
+                const int src = (s0 + u * G + sub) & 63;
+                o[u] = __shfl(eoff, src);
+                w[u] = __shfl(vv, src);
+            }
+            float4 xv[kSegUnroll];
+#pragma unroll
+            for (int u = 0; u < kSegUnroll; ++u) {
+                const bool ok = s0 + u * G + sub < n;
+                xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (!ok) w[u] = 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kSegUnroll; ++u) dg::fma4(acc, w[u], xv[u]);
+        }
+    }
+#pragma unroll
+    for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+    return acc;
+}
+
+// PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.
+template <int LP, bool PROJ>
+__global__ __launch_bounds__(1024) void spmm_seg_kernel(const SegArgs a) {
+    constexpr int DOUT4 = PROJ ? 8 : LP;  // float4s of an output row
+    __shared__ float4 ybuf[16][16];
+    __shared__ float4 zbuf[16][DOUT4];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    int gi = 0;
+#pragma unroll 1
+    while (gi + 1 < a.n_groups && (int)blockIdx.x >= a.g[gi + 1].block_begin) ++gi;
+    const SegGroupK& g = a.g[gi];
+    // XCD-contiguous item map (block lb runs on XCD lb % 8): one chunk's rows stay on few XCDs
+    const int lb = blockIdx.x - g.block_begin;
+    const int per = g.n_blocks >> 3;
+    const int item = (lb & 7) * per + (lb >> 3);
+    if (item >= g.n_chunks * g.row_blocks) return;  // workgroup-uniform, before any barrier
+    const int c = item / g.row_blocks;
+    const int r0 = (item - c * g.row_blocks) * g.rpb;
+    const int slot = wave / g.chunk;
+    const int t = wave - slot * g.chunk;
+    const int r = r0 + slot;
+    const bool row_ok = slot < g.rpb && r < g.n_rows;
+    const int k = c * g.chunk + t;
+    float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row_ok && k < g.n_rels) {  // wave-uniform
+        const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
+        const int beg = g.seg[si];
+        const int end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
+        if constexpr (PROJ) {
+            const int s = g.slab ? g.slab[k] : k;
+            // this lane's W_s slice: rows 8(l>>3) .. +8, columns 4(l&7) .. +4
+            const float* W = g.w + (int64_t)s * (64 * 32) + (lane >> 3) * (8 * 32) + (lane & 7) * 4;
+            float4 wv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wv[i] = *reinterpret_cast<const float4*>(W + i * 32);
+            // H is shared by the relations: vcol = s·n_cols + col addresses row col
+            const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;
+            const float4 y = seg_gather<16>(g.vcol, g.val, xb, g.x_ld, beg, end);
+            if (lane < 16) ybuf[wave][lane] = y;
+            __builtin_amdgcn_wave_barrier();
+            const int ms = lane >> 3;
+            const float4 ya = ybuf[wave][2 * ms];
+            const float4 yb = ybuf[wave][2 * ms + 1];
+            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            dg::fma4(z, ya.x, wv[0]);
+            dg::fma4(z, ya.y, wv[1]);
+            dg::fma4(z, ya.z, wv[2]);
+            dg::fma4(z, ya.w, wv[3]);
+            dg::fma4(z, yb.x, wv[4]);
+            dg::fma4(z, yb.y, wv[5]);
+            dg::fma4(z, yb.z, wv[6]);
+            dg::fma4(z, yb.w, wv[7]);
+            dg::add4(z, dg::shfl_xor4(z, 8));
+            dg::add4(z, dg::shfl_xor4(z, 16));
+            dg::add4(z, dg::shfl_xor4(z, 32));
+            res = z;
+        } else {
+            res = seg_gather<LP>(g.vcol, g.val, g.x, g.x_ld, beg, end);
+        }
+    }
+    if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
+    __syncthreads();
+    if (row_ok && t == 0 && lane < DOUT4) {
+        float4 s = zbuf[wave][lane];
+        for (int u = 1; u < g.chunk; ++u) dg::add4(s, zbuf[wave + u][lane]);
+        *reinterpret_cast<float4*>(g.out + ((int64_t)c * g.n_rows + r) * (4 * DOUT4) + 4 * lane) = s;
+    }
+}
+
+}  // namespace
+
+extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out,
+                               void* stream) {
+    if (n_groups < 0 || (n_groups > 0 && groups == nullptr)) return DG_EINVAL;
+    if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
+    bool proj = false;
+    if (d_in == 64 && d_out == 32)
+        proj = true;
+    else if (!(d_in == d_out && (d_in == 32 || d_in == 64)))
+        return DG_EINVAL;
+    SegArgs args{};
+    int64_t blocks = 0;
+    int ng = 0;
+    for (int i = 0; i < n_groups; ++i) {
+        const dg_seg_group& s = groups[i];
+        if (s.n_rows < 0 || s.n_chunks < 1 || s.chunk < 1 || s.chunk > 16 || s.n_rels < 0 || s.n_cols < 0 ||
+            s.x_rows < 0)
+            return DG_EINVAL;
+        if ((int64_t)s.n_chunks * s.chunk < s.n_rels || (int64_t)(s.n_chunks - 1) * s.chunk >= s.n_rels)
+            return DG_EINVAL;  // every chunk holds at least one relation
+        if ((s.w != nullptr) != proj) return DG_EINVAL;  // a weight stack exactly when d_in != d_out
+        if (s.n_rows == 0 || s.n_rels == 0) continue;
+        if (!s.rowptr || !s.seg || !s.x || !s.out) return DG_EINVAL;
+        if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || (s.x_ld & 3)) return DG_EALIGN;
+        if (proj && !dg::aligned16(s.w)) return DG_EALIGN;
+        if (s.x_ld < d_in) return DG_EINVAL;
+        if ((int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;  // 32-bit gather offsets
+        SegGroupK& k = args.g[ng++];
+        k.rowptr = s.rowptr;
+        k.seg = s.seg;
+        k.vcol = s.vcol;
+        k.val = s.val;
+        k.slab = s.slab;
+        k.x = s.x;
+        k.w = s.w;
+        k.out = s.out;
+        k.x_ld = static_cast<int32_t>(s.x_ld);
+        k.n_rows = s.n_rows;
+        k.n_cols = s.n_cols;
+        k.n_chunks = s.n_chunks;
+        k.chunk = s.chunk;
+        k.n_rels = s.n_rels;
+        k.rpb = 16 / s.chunk;
+        k.row_blocks = dg::ceil_div(s.n_rows, k.rpb);
+        const int64_t items = (int64_t)s.n_chunks * k.row_blocks;
+        k.n_blocks = static_cast<int32_t>(8 * ((items + 7) / 8));
+        k.block_begin = static_cast<int32_t>(blocks);
+        blocks += k.n_blocks;
+        if (blocks > 0x7fffffff) return DG_EINVAL;
+    }
+    args.n_groups = ng;
+    if (blocks == 0) return DG_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(blocks)), block(1024);
+    if (proj)
+        hipLaunchKernelGGL((spmm_seg_kernel<16, true>), grid, block, 0, st, args);
+    else if (d_in == 64)
+        hipLaunchKernelGGL((spmm_seg_kernel<16, false>), grid, block, 0, st, args);
+    else
+        hipLaunchKernelGGL((spmm_seg_kernel<8, false>), grid, block, 0, st, args);
+    return dg::launch_status();
+}

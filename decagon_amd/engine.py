@@ -30,7 +30,7 @@ import torch
 
 from . import kernels
 from ._lib import DG_EPI_L2NORM, DG_EPI_RELU, DG_MAX_GROUPS
-from .sparse import HostCSR, MergedCSR, merge_chunks, merge_windows, staged_layout
+from .sparse import HostCSR, MergedCSR, chunk_segments, merge_chunks, merge_windows, staged_layout
 
 EdgeType = Tuple[int, int]
 
@@ -206,7 +206,9 @@ class DeviceGraph:
     def __init__(self, edge_types: Dict[EdgeType, int], adj: Dict[EdgeType, Sequence[Optional[HostCSR]]],
                  device: torch.device, local: Optional[Dict[EdgeType, Sequence[int]]] = None,
                  chunk=None, target_waves: int = 32768, d_policy: int = 64,
-                 row_block: Optional[Dict[int, Tuple[int, int, int]]] = None):
+                 row_block: Optional[Dict[int, Tuple[int, int, int]]] = None, segments: bool = False):
+        """segments: also upload each chunk-merged group's segment starts (sparse.chunk_segments)
+        for dg_spmm_seg_f32 — groups of at most 16 relations per chunk."""
         self.edge_types = dict(edge_types)
         self.device = device
         self.groups: Dict[EdgeType, DeviceGroup] = {}
@@ -266,6 +268,8 @@ class DeviceGraph:
                 g.rel_map = torch.from_numpy(ids).to(device)
             g.staged, g.out_chunk = staged, out_chunk
             g.host = loc  # local relations in device order (the backward builds Âᵀ from them)
+            if segments and loc and not staged and not windows and m.chunk <= 16:
+                g.seg = torch.from_numpy(chunk_segments(loc, m)).to(device)
             if staged:
                 lay = staged_layout(loc, kernels.staged_block,
                                     lanes=int(os.environ.get("DG_STAGED_LANES", "1024")),
@@ -344,6 +348,16 @@ class ForwardPlan:
             else:
                 self.flat_mode = True
         n = dgraph.n_nodes
+        # config S's weak scaling (RelationShard.weak_sets form "seg"): every node type row-split,
+        # its groups in dg_spmm_seg_f32 (one wave per (row, relation), one chunk per relation
+        # set) + the epilogue, and layer 2 reassociated, Σ_k (Â_k·H1_j)·W2_k — no projection
+        # GEMM over every relation on every rank (forward only: the backward keeps the sums)
+        self.seg_mode = (shard is not None and getattr(shard, "seg_rows", False) and not keep_sums
+                         and self.drop_state is None and h1 == 64 and h2 == 32
+                         and all(et[0] in self.row_block for et in self.edge_types)
+                         and all(g.seg is not None or not g.n_rels for g in dgraph.groups.values()))
+        # (otherwise such a shard runs the same chunks in dg_spmm_groups_f32 + the epilogue,
+        # with the projection GEMM)
 
         # ---- layer-1 dense operand: W1 (identity features) or X_j·W1_k (sparse features) ----
         self._pre: List[Callable[[], None]] = []
@@ -413,6 +427,8 @@ class ForwardPlan:
         self.staged_proj = {et for et in self.edge_types
                             if dgraph.groups[et].staged and dgraph.groups[et].n_rels and h1 == 64
                             and self.drop_state is None and STAGED_PROJ}
+        self.seg_proj = {et for et in self.edge_types
+                         if self.seg_mode and dgraph.groups[et].n_rels and h1 == 64 and h2 == 32}
         self.proj: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
@@ -421,7 +437,7 @@ class ForwardPlan:
                 raise ValueError(f"layer-2 weights of {et} are {(K, din, dout)}, expected ({grp.K}, {h1}, {h2})")
             if et[1] not in self.hidden1:
                 raise ValueError(f"node type {et[1]} has no incoming edge type; layer 2 needs hidden1[{et[1]}]")
-            if et not in self.staged_proj:
+            if et not in self.staged_proj and et not in self.seg_proj:
                 self.proj[et] = torch.empty((K, n[et[1]], h2), **f32)
 
         # a second stream: a layer's gather-bound launch (dg_spmm_groups_f32) runs beside its
@@ -454,7 +470,7 @@ class ForwardPlan:
         self.hdrop: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
-            if not grp.n_rels or et in proj_fused or et in self.staged_proj:
+            if not grp.n_rels or et in proj_fused or et in self.staged_proj or et in self.seg_proj:
                 continue
             j = et[1]
             W = w2.stacks[et]
@@ -487,7 +503,8 @@ class ForwardPlan:
                                for s in range(0, len(gemms), DG_MAX_GROUPS)]
         self._layer2 = self._build_layer(self.proj, h2, False, f32,
                                          staged_proj={et: (self.hidden1[et[1]], w2.stacks[et])
-                                                      for et in self.staged_proj})
+                                                      for et in self.staged_proj},
+                                         seg_w={et: (self.hidden1[et[1]], w2.stacks[et]) for et in self.seg_proj})
 
     # ------------------------------------------------------------------ layer builder
     def _fused_targets(self) -> List[int]:
@@ -516,7 +533,14 @@ class ForwardPlan:
         return kernels.RelGroupSpec(grp.rowptr, grp.vcol, grp.val, x, out, grp.n_rows, grp.n_chunks, d,
                                     grp.K * grp.n_cols, vcol_max=grp.vcol_max)
 
-    def _build_layer(self, xs: Dict[EdgeType, torch.Tensor], d, relu, f32, projs=(), staged_proj=None):
+    def _seg_spec(self, et, x: torch.Tensor, out, w=None) -> kernels.SegSpec:
+        grp = self.g.groups[et]
+        return kernels.SegSpec(grp.rowptr, grp.seg, grp.vcol, grp.val, x, out, grp.n_rows, grp.n_cols, grp.n_chunks,
+                               grp.chunk, grp.n_rels, x.stride(-2),
+                               grp.K * grp.n_cols, vcol_max=grp.vcol_max, w=w, slab=grp.rel_map,
+                               slab_max=int(grp.rel_ids.max()) if grp.n_rels else -1)
+
+    def _build_layer(self, xs: Dict[EdgeType, torch.Tensor], d, relu, f32, projs=(), staged_proj=None, seg_w=None):
         """Prepared launches of one layer: fused targets in one dg_gcn_fused_f32 launch; the
         other targets' groups in partial mode + epilogue — with, when sharded, the chunk
         reduce into the all-reduce buffer and the all-reduce before the epilogue."""
@@ -579,7 +603,7 @@ class ForwardPlan:
                 views[et] = flat[off:off + sz]
                 sviews[et] = send[off:off + sz]
                 off += sz
-        partials, specs, staged, reduces = {}, [], [], []
+        partials, specs, staged, reduces, segs = {}, [], [], [], []
         for et in rest:
             grp = g.groups[et]
             n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
@@ -597,8 +621,17 @@ class ForwardPlan:
                 staged.append(kernels.StagedSpec(
                     grp.layout, grp.rel_map, xs.get(et), part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
                     slab_max=int(grp.rel_ids.max()), proj=sp))
+            elif self.seg_mode:
+                segs.append(self._seg_spec(et, *seg_w[et], out=part) if et in (seg_w or {})
+                            else self._seg_spec(et, xs[et], part))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
+        if segs:
+            d_in = self.h1 if seg_w else d
+            seg_ets = [et for et in rest if g.groups[et].n_rels]
+            for s in range(0, len(segs), DG_MAX_GROUPS):
+                launches.append(kernels.PreparedSeg(segs[s:s + DG_MAX_GROUPS], d_in, d))
+                self.launch_groups[id(launches[-1])] = seg_ets[s:s + DG_MAX_GROUPS]
         staged_ets = [et for et in rest if g.groups[et].n_rels and g.groups[et].staged]
         spmm_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged]
         for s in range(0, len(staged), DG_MAX_GROUPS):
@@ -722,7 +755,7 @@ class ForwardPlan:
     @property
     def spmm_launches(self):
         """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""
-        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged)
+        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged, kernels.PreparedSeg)
         pick = lambda L: [l for l in L.launches if isinstance(l, kinds)]
         return pick(self._layer1), pick(self._layer2)
 
@@ -741,7 +774,7 @@ class ForwardPlan:
         if not grp.n_rels:
             return 0
         tot = 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz
-        if layer == 2 and et in self.staged_proj:  # layer 2 reads H1_j and W2 instead of P_k
+        if layer == 2 and (et in self.staged_proj or et in self.seg_proj):  # H1_j and W2 instead of P_k
             tot += 4 * self.h1 * (grp.n_cols + d * grp.n_rels)
         else:
             tot += 4 * d * grp.n_cols * grp.n_rels
@@ -778,7 +811,7 @@ class ForwardPlan:
             if not grp.n_rels:
                 continue
             tot += 4 * (grp.n_rels * grp.n_rows + 1) + 8 * grp.nnz
-            if layer == 2 and et in self.staged_proj:  # H1_j and W2 instead of P_k
+            if layer == 2 and (et in self.staged_proj or et in self.seg_proj):  # H1_j and W2 instead of P_k
                 tot += 4 * self.h1 * (grp.n_cols + d * grp.n_rels)
             else:
                 tot += 4 * d * grp.n_cols * grp.n_rels

@@ -179,6 +179,102 @@ class PreparedSpmm:
 
 
 @dataclass
+class SegSpec:
+    """One group of dg_spmm_seg_f32 (decagon_hip.h): the chunk-merged CSR, its segment starts
+    (sparse.chunk_segments) and, for the reassociated layer 2, the weight stack w with each
+    local relation's slab."""
+
+    rowptr: torch.Tensor          # int32 [n_chunks*n_rows + 1]
+    seg: torch.Tensor             # int32 [n_chunks*n_rows*chunk]
+    vcol: torch.Tensor            # int32 [nnz]
+    val: torch.Tensor             # float32 [nnz]
+    x: torch.Tensor               # float32: stacked X (no w) or H [n_cols, x_ld]
+    out: torch.Tensor             # float32 [n_chunks, n_rows, d_out]
+    n_rows: int
+    n_cols: int
+    n_chunks: int
+    chunk: int
+    n_rels: int
+    x_ld: int
+    x_rows: int                   # bound on vcol
+    vcol_max: int = -1
+    w: Optional[torch.Tensor] = None      # float32 [K, 64, 32]
+    slab: Optional[torch.Tensor] = None   # int32 [n_rels] (None: relation k is slab k)
+    slab_max: int = -1
+
+    def validate(self, d_in: int, d_out: int) -> None:
+        for t, what in ((self.rowptr, "rowptr"), (self.seg, "seg"), (self.vcol, "vcol")):
+            _dev(t, torch.int32, what)
+        _dev(self.val, torch.float32, "val")
+        _dev(self.x, torch.float32, "x")
+        _dev(self.out, torch.float32, "out")
+        if not 1 <= self.chunk <= 16:
+            raise ValueError("chunk must be in [1, 16]")
+        if not (self.n_chunks - 1) * self.chunk < self.n_rels <= self.n_chunks * self.chunk:
+            raise ValueError("every chunk must hold at least one relation")
+        if self.rowptr.numel() < self.n_chunks * self.n_rows + 1:
+            raise ValueError("rowptr too short")
+        if self.seg.numel() < self.n_chunks * self.n_rows * self.chunk:
+            raise ValueError("seg too short")
+        if self.vcol.numel() != self.val.numel():
+            raise ValueError("vcol/val length mismatch")
+        if self.vcol_max >= self.x_rows:
+            raise ValueError(f"vcol reaches row {self.vcol_max} of a {self.x_rows}-row operand")
+        if self.x_ld < d_in or self.x_ld % 4:
+            raise ValueError("x_ld must be >= d_in and a multiple of 4")
+        if self.x_rows * self.x_ld >= 2**31:
+            raise ValueError("dense operand too large for 32-bit gather offsets")
+        if self.out.numel() < self.n_chunks * self.n_rows * d_out:
+            raise ValueError("out too small for [n_chunks, n_rows, d_out]")
+        if self.w is None:
+            if self.n_rows and self.x_rows and self.x.numel() < (self.x_rows - 1) * self.x_ld + d_in:
+                raise ValueError("x smaller than x_rows rows")
+            return
+        _dev(self.w, torch.float32, "w")
+        K = self.w.shape[0]
+        if tuple(self.w.shape[1:]) != (64, 32) or (d_in, d_out) != (64, 32):
+            raise ValueError("the reassociated form takes a [K, 64, 32] stack (d_in 64, d_out 32)")
+        if self.x_rows > K * self.n_cols:
+            raise ValueError("vcol bound beyond the stack's slabs")
+        if self.x.numel() < (self.n_cols - 1) * self.x_ld + 64:
+            raise ValueError("H smaller than n_cols rows")
+        if self.slab is not None:
+            _dev(self.slab, torch.int32, "slab")
+            if self.slab.numel() < self.n_rels or not 0 <= self.slab_max < K:
+                raise ValueError("slab map must index inside w")
+        elif self.n_rels > K:
+            raise ValueError("n_rels > K")
+
+
+class PreparedSeg:
+    """A fixed dg_spmm_seg_f32 launch (every group with w, or none)."""
+
+    def __init__(self, specs: Sequence[SegSpec], d_in: int, d_out: int):
+        if len(specs) > _lib.DG_MAX_GROUPS:
+            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups per launch")
+        if len({s.w is None for s in specs}) > 1:
+            raise ValueError("every group of a launch has a weight stack, or none")
+        arr = (_lib.DgSegGroup * max(1, len(specs)))()
+        for i, s in enumerate(specs):
+            s.validate(d_in, d_out)
+            g = arr[i]
+            g.rowptr, g.seg = s.rowptr.data_ptr(), s.seg.data_ptr()
+            g.vcol = s.vcol.data_ptr() if s.vcol.numel() else None
+            g.val = s.val.data_ptr() if s.val.numel() else None
+            g.slab = s.slab.data_ptr() if s.slab is not None else None
+            g.x, g.out = s.x.data_ptr(), s.out.data_ptr()
+            g.w = s.w.data_ptr() if s.w is not None else None
+            g.x_ld, g.n_rows, g.n_cols, g.n_chunks = s.x_ld, s.n_rows, s.n_cols, s.n_chunks
+            g.chunk, g.n_rels, g.x_rows = s.chunk, s.n_rels, s.x_rows
+        self.specs = list(specs)
+        self._arr, self._n, self.d_in, self.d_out = arr, len(specs), d_in, d_out
+        self._fn = _lib.load().dg_spmm_seg_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(self._arr, self._n, self.d_in, self.d_out, _stream_ptr(stream)), "dg_spmm_seg_f32")
+
+
+@dataclass
 class ProjSpec:
     """Projection epilogue of a fused launch: out[kk] = row · w[rel_map[kk] or kk]."""
 

@@ -6,16 +6,17 @@ until the per-(i,j) sum Σ_k, which must be complete before the row L2 normalisa
 (decagon/deep/layers.py:92-93); after it, the layer's rows are independent.  Two ways to
 split a node type's work follow from that, and a plan uses both:
 
-  relation-sharded  (small node types: the 645 drugs, config S's genes and drugs)
+  relation-sharded  (small node types: the 645 drugs)
       each rank owns a subset of the relations of every group into the node type (LPT over
-      nonzero counts, or whole relation sets — one per GPU in the weak-scaling bench), writes
+      nonzero counts), writes
       its partial pre-normalisation sums S_ij into one flat buffer and the ranks all-reduce
       it (one RCCL all-reduce per layer); every rank then finishes those rows redundantly.
   row-split         (node types of >= ROW_SPLIT_MIN rows: the 19,085 proteins)
       each rank owns a contiguous block of the node type's rows for EVERY relation into it,
       so its S_ij rows are complete locally: it normalises and finishes its block, and the
       blocks are all-gathered (padded to equal size) into the full hidden1 / embeddings that
-      the next layer's gathers and the decoder read.
+      the next layer's gathers and the decoder read.  Config S's weak scaling (N relation
+      sets over the same nodes) row-splits every node type (RelationShard.weak_sets).
 
 Per layer the exchange is therefore one all-reduce of the relation-sharded node types' sums
 (config P: 2 × 645 × d floats) plus one all-gather of the row-split node types' finished
@@ -29,6 +30,7 @@ relation map of dg_rel_group / dg_gemm_desc, without copies.
 from __future__ import annotations
 
 import heapq
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -93,6 +95,9 @@ class RelationShard:
     # row-split node types finished by the fused SpMM kernel over their row block (one chunk
     # per group; config S's weak scaling) instead of partial mode + an epilogue
     fused_rows: bool = False
+    # row-split node types in dg_spmm_seg_f32 + the epilogue, layer 2 reassociated (config S's
+    # weak scaling at N GPUs; `chunks` then holds the relations per set)
+    seg_rows: bool = False
 
     @staticmethod
     def lpt(edge_types: Dict[EdgeType, int], rel_cost: Dict[EdgeType, Sequence[float]], rank: int,
@@ -157,12 +162,31 @@ class RelationShard:
         return RelationShard.split(graph.edge_types, graph.n_nodes, nnz, rank, world_size, ar, ag)
 
     @staticmethod
-    def blocks(edge_types_per_rank: Dict[EdgeType, int], rank: int, world_size: int,
-               allreduce=None) -> "RelationShard":
-        """Weak scaling: the graph holds world_size relation sets; rank r owns set r, i.e.
-        relations [r*K_ij, (r+1)*K_ij) of every group."""
-        local = {et: list(range(rank * k, (rank + 1) * k)) for et, k in edge_types_per_rank.items()}
-        return RelationShard(rank, world_size, local, allreduce, scheme="one relation set per GPU")
+    def weak_sets(edge_types: Dict[EdgeType, int], n_nodes: Dict[int, int], rank: int, world_size: int,
+                  allreduce=None, allgather=None, form: Optional[str] = None) -> "RelationShard":
+        """Config S's weak scaling (synthetic.replicate_sets): the graph holds world_size relation
+        sets over the same nodes, set r at relations [r·K, (r+1)·K) of every group (K = the
+        group's relations per set).  Every node type is row-split: each rank finishes its row
+        block over every set's relations and the blocks are all-gathered — no all-reduce.
+        form "seg" (default; DG_S_ROWS_FORM overrides): one chunk per relation set, the blocks in
+        dg_spmm_seg_f32 (one wave per (row, relation), layer 2 reassociated so no rank projects
+        every relation) + the epilogue; "fused": one chunk per group in dg_gcn_fused_f32 (one
+        workgroup per row) with the layer-2 projection GEMM over every relation on every rank."""
+        form = form or os.environ.get("DG_S_ROWS_FORM", "seg")
+        if form not in ("seg", "fused"):
+            raise ValueError(f"unknown weak-scaling form {form!r}")
+        nnz = {et: [1.0] * K for et, K in edge_types.items()}
+        sh = RelationShard.split(edge_types, n_nodes, nnz, rank, world_size, allreduce, allgather, row_split_min=1)
+        if form == "seg":
+            if any(K % world_size for K in edge_types.values()):
+                raise ValueError("every group must hold world_size relation sets")
+            sh.chunks = {et: K // world_size for et, K in edge_types.items()}
+            sh.seg_rows = True
+        else:
+            sh.chunks = dict(edge_types)
+            sh.fused_rows = True
+        sh.scheme = "one relation set per GPU"
+        return sh
 
     def local_csr(self, csr: Dict[EdgeType, Sequence]) -> Dict[EdgeType, list]:
         """The graph's per-group relation lists with the relations of other ranks replaced by

@@ -229,6 +229,23 @@ def merge_chunks(csrs: Sequence[HostCSR], slabs: Sequence[int], chunk: int, n_sl
     return MergedCSR(rowptr.astype(np.int32), vcol, val, n_r, n_c, n_chunks, chunk, n_slabs * n_c)
 
 
+def chunk_segments(csrs: Sequence[HostCSR], m: MergedCSR) -> np.ndarray:
+    """Segment starts of merge_chunks' layout (dg_spmm_seg_f32): int32 [n_chunks·n_rows·chunk],
+    entry (c·n_rows + r)·chunk + t = the first nonzero of relation c·chunk + t in row r's range
+    of chunk c (relations run one after another inside the range; relation slots past the last
+    relation are empty segments at the range's end)."""
+    n_r, ch, nc = m.n_rows, m.chunk, m.n_chunks
+    seg = np.empty((nc, n_r, ch), np.int64)
+    start = m.rowptr[:-1].astype(np.int64).reshape(nc, n_r).copy()
+    for t in range(ch):
+        seg[:, :, t] = start
+        for c in range(nc):
+            k = c * ch + t
+            if k < len(csrs):
+                start[c] += np.diff(csrs[k].rowptr.astype(np.int64))
+    return seg.reshape(-1).astype(np.int32)
+
+
 def merge_windows(csrs: Sequence[HostCSR], slabs: Sequence[int], n_windows: int, n_slabs: int) -> MergedCSR:
     """The chunk-merged layout with COLUMN-WINDOW chunks: chunk w holds, for every row, the
     nonzeros of every relation whose column lies in window w (columns split into n_windows

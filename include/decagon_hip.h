@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (26); bumped whenever a struct layout or a signature changes. */
+/* ABI version (27); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -118,6 +118,49 @@ int dg_spmm_groups_lds_f32(const dg_rel_group* groups /* HOST array */, int32_t 
 int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                     int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx, float* y,
                     int64_t ldy, int32_t d, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Relation-segment SpMM (partial mode; one wave per (row, relation)), optionally with the
+ * next layer's projection reassociated into it — the sharded config-S form (one relation set
+ * per GPU, every node type row-split), where a rank's short row block would leave
+ * most CUs idle at one workgroup per row.  Over dg_rel_group's chunk-merged CSR with `chunk`
+ * relations per chunk (relation k = c*chunk + t), for every chunk c and row r:
+ *
+ *   w == NULL:  out[c][r][:]  = sum_{t} sum_{p in seg(c,r,t)} val[p] * X[vcol[p]][:]
+ *   w != NULL:  out[c][r][:]  = sum_{t} ( sum_{p in seg(c,r,t)} val[p] * H[vcol[p] - s*n_cols][:] ) · W[s]
+ *               (s = slab[k] or k; H = x, [n_cols][x_ld]; W a [K][64][32] stack)
+ *
+ * The second form is layer 2 as sum_k (A_k·H1_j)·W2_k instead of sum_k A_k·(H1_j·W2_k)
+ * (layers.py:113-114): the shared H1_j is gathered and only this rank's rows are projected.
+ * seg[(c*n_rows + r)*chunk + t] is the first nonzero of relation t of chunk c in row r inside
+ * [rowptr[c*n_rows + r], rowptr[c*n_rows + r + 1]); a segment ends where the next one starts
+ * (the last one at the range's end).  Relations run in t order within a range (merge_chunks).
+ * Requirements: 1 <= chunk <= 16, (n_chunks - 1)*chunk < n_rels <= n_chunks*chunk;
+ * w == NULL: d_in == d_out in {32, 64}; w != NULL (every group): d_in == 64, d_out == 32;
+ * x, out, w and x_ld 16-byte aligned; x_rows * x_ld < 2^31 with 0 <= vcol < x_rows.
+ * Replaces: tf.sparse_tensor_dense_matmul + tf.add_n (layers.py:90-92, :114-116) over a
+ * chunk's relations, and tf.matmul(x, weights_k) (layers.py:113).
+ * -------------------------------------------------------------------------------------- */
+typedef struct dg_seg_group {
+    const int32_t* rowptr;      /* device, [n_chunks*n_rows + 1]                          */
+    const int32_t* seg;         /* device, [n_chunks*n_rows*chunk] segment starts         */
+    const int32_t* vcol;        /* device, [nnz]                                          */
+    const float* val;           /* device, [nnz]                                          */
+    const int32_t* slab;        /* device, [n_rels] slab of local relation k, or NULL     */
+    const float* x;             /* device: stacked X (w == NULL) or H [n_cols][x_ld]      */
+    const float* w;             /* device, [K][64][32] weight stack, or NULL              */
+    float* out;                 /* device, [n_chunks][n_rows][d_out]                      */
+    int64_t x_ld;
+    int32_t n_rows;
+    int32_t n_cols;
+    int32_t n_chunks;
+    int32_t chunk;
+    int32_t n_rels;
+    int32_t x_rows;             /* bound on vcol (K*n_cols for the stacked forms)         */
+} dg_seg_group;
+
+int dg_spmm_seg_f32(const dg_seg_group* groups /* HOST array */, int32_t n_groups, int32_t d_in,
+                    int32_t d_out, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Fused GCN layer (T3 + T4 + T5 + T6, optionally T7 of the next layer, in one launch) for

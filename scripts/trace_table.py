@@ -4,7 +4,7 @@ import csv
 import glob
 import sys
 
-f = glob.glob(sys.argv[1] + "/t/**/*kernel_trace.csv", recursive=True)[0]
+f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
 d = collections.defaultdict(list)
 for r in csv.DictReader(open(f)):
     n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:56]

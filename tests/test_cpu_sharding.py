@@ -43,9 +43,23 @@ def test_relation_shard_lpt_partitions_every_relation():
         assert sorted(seen[k]) == list(range(v))
 
 
-def test_relation_shard_blocks():
-    s = RelationShard.blocks({(0, 0): 2, (1, 1): 6}, 2, 4)
-    assert s.local == {(0, 0): [4, 5], (1, 1): [12, 13, 14, 15, 16, 17]}
+def test_weak_sets_shard():
+    et, n = {(0, 0): 8, (0, 1): 4, (1, 0): 4, (1, 1): 24}, {0: 500, 1: 400}
+    seen = {0: [], 1: []}
+    for r in range(4):
+        s = RelationShard.weak_sets(et, n, r, 4, form="seg")
+        assert s.seg_rows and not s.fused_rows
+        assert s.chunks == {(0, 0): 2, (0, 1): 1, (1, 0): 1, (1, 1): 6}  # one chunk per relation set
+        assert s.local == {k: list(range(v)) for k, v in et.items()}    # every relation, on a row block
+        for t in (0, 1):
+            a, b, blk = s.row_block[t]
+            assert blk == -(-n[t] // 4)
+            seen[t] += list(range(a, b))
+    assert seen == {0: list(range(500)), 1: list(range(400))}
+    f = RelationShard.weak_sets(et, n, 1, 4, form="fused")
+    assert f.fused_rows and f.chunks == et
+    with pytest.raises(ValueError):
+        RelationShard.weak_sets({(0, 0): 3}, {0: 10}, 0, 2, form="seg")
 
 
 def _free_port():

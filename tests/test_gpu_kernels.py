@@ -110,6 +110,53 @@ def test_spmm_groups_chunks_and_slabs(K, chunk, d):
         assert rel_err(s.out.cpu().numpy(), w) <= 1e-5
 
 
+@pytest.mark.parametrize("chunk", [1, 3, 6, 16])
+@pytest.mark.parametrize("form", [(32, 32), (64, 64), (64, 32)])
+def test_spmm_seg_chunks_and_reassociated_projection(K, chunk, form):
+    """dg_spmm_seg_f32 (one wave per (row, relation)): chunk partials of the chunk-merged layout
+    with relations in arbitrary slabs, two groups (one with a short last chunk) in one launch;
+    with a weight stack (d_in 64 → d_out 32) the reassociated layer 2, Σ_k (Â_k·H)·W[slab_k]
+    (layers.py:113-114 with the sum regrouped), against the float64 products."""
+    from decagon_amd.sparse import chunk_segments, coo_to_csr, merge_chunks, sparse_to_tuple
+
+    d_in, d_out = form
+    proj = d_in != d_out
+    rng = np.random.default_rng(chunk * 1000 + d_in + d_out)
+    wants, specs = [], []
+    for (n_r, n_c, nrel, dens) in ((57, 90, 2 * chunk, 0.05), (40, 33, chunk + max(1, chunk // 2), 0.3)):
+        mats = [_rand_csr(rng, n_r, n_c, dens, empty_rows=0.2) for _ in range(nrel)]
+        mats[0] = sp.csr_matrix((n_r, n_c))  # an empty relation
+        total = nrel + 3
+        slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
+        hs = [coo_to_csr(*sparse_to_tuple(x)) for x in mats]
+        m = merge_chunks(hs, slabs, chunk, total)
+        seg = chunk_segments(hs, m)
+        nch = m.n_chunks
+        out = torch.full((nch, n_r, d_out), float("nan"), device="cuda")
+        want = np.zeros((nch, n_r, d_out))
+        if proj:
+            H = rng.standard_normal((n_c, 64)).astype(np.float32)
+            W = (0.2 * rng.standard_normal((total, 64, 32))).astype(np.float32)
+            x, w = torch.from_numpy(H).cuda(), torch.from_numpy(W).cuda()
+            for k, a in enumerate(mats):
+                want[k // chunk] += (a @ H.astype(np.float64)) @ W[slabs[k]].astype(np.float64)
+        else:
+            X = rng.standard_normal((total * n_c, d_in)).astype(np.float32)
+            x, w = torch.from_numpy(X).cuda(), None
+            for k, a in enumerate(mats):
+                want[k // chunk] += a @ X[slabs[k] * n_c:(slabs[k] + 1) * n_c].astype(np.float64)
+        specs.append(K.SegSpec(torch.from_numpy(m.rowptr).cuda(), torch.from_numpy(seg).cuda(),
+                               torch.from_numpy(m.vcol).cuda(), torch.from_numpy(m.val).cuda(), x, out, n_r, n_c,
+                               nch, chunk, nrel, d_in, total * n_c, vcol_max=int(m.vcol.max()), w=w,
+                               slab=torch.from_numpy(slabs).cuda(), slab_max=int(slabs.max())))
+        wants.append(want)
+    K.PreparedSeg(specs, d_in, d_out)()
+    for s, w in zip(specs, wants):
+        got = s.out.cpu().numpy()
+        assert rel_err(got, w) <= 1e-5
+        assert np.all(got[:, np.all(w == 0, axis=(0, 2))] == 0)  # rows without nonzeros: exact zeros
+
+
 @pytest.mark.parametrize("d", [12, 64])
 def test_spmm_shared_pattern(K, d):
     """DG_GROUP_SHARED_PATTERN: one CSR (X_j's) for every chunk, chunk k over its own slab

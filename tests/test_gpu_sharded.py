@@ -43,7 +43,7 @@ def _graph(kind, world=1):
 
     if kind == "S":
         return synthetic.load_S()
-    if kind == "S-rows":
+    if kind in ("S-rows", "S-rows-fused"):
         return synthetic.replicate_sets(synthetic.load_S(), world)
     if kind == "P-small":
         return synthetic.make_P(seed=3, n_proteins=1500, n_drugs=150, n_side_effects=60, ppi_edges=12000,
@@ -57,12 +57,9 @@ def _shard(kind, g, rank, world):
     nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
     if kind == "S":
         return RelationShard.lpt(g.edge_types, nnz, rank, world, torch_allreduce())
-    if kind == "S-rows":
-        sh = RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
-                                 row_split_min=1)
-        sh.chunks = dict(g.edge_types)
-        sh.fused_rows = True
-        return sh
+    if kind in ("S-rows", "S-rows-fused"):
+        return RelationShard.weak_sets(g.edge_types, g.n_nodes, rank, world, torch_allreduce(), torch_allgather(),
+                                       form="fused" if kind == "S-rows-fused" else "seg")
     return RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
                                row_split_min=1000)
 
@@ -75,13 +72,14 @@ def _rank(rank, world, kind, h2=32):
     shard = _shard(kind, g, rank, world)
     w1, w2 = _weights(g, 5, h2=h2)
     dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local, row_block=shard.row_block,
-                     chunk=shard.chunks)
+                     chunk=shard.chunks, segments=shard.seg_rows)
     plan = ForwardPlan(dg, {0: None, 1: None},
                        LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
                        LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, h2,
                        shard=shard)
     info = {"row_split": sorted(shard.row_block), "staged": dg.groups[(1, 1)].staged,
-            "local": {et: len(v) for et, v in shard.local.items()}, "fused": sorted(plan.fused)}
+            "local": {et: len(v) for et, v in shard.local.items()}, "fused": sorted(plan.fused),
+            "seg": plan.seg_mode, "gemms": len(plan._gemm2)}
     plan.run()
     torch.cuda.synchronize()
 
@@ -139,8 +137,10 @@ def _check(kind, world, h2=32):
     h1, emb = _oracle(kind, g, h2)
     for r in range(world):
         info, eager, graphed = got[r]
-        if kind == "S-rows":
-            assert info["row_split"] == [0, 1] and info["fused"] == [0, 1], info  # fused row blocks
+        if kind == "S-rows":  # row blocks in dg_spmm_seg_f32, layer 2 reassociated: no projection GEMM
+            assert info["row_split"] == [0, 1] and info["seg"] and not info["fused"] and info["gemms"] == 0, info
+        elif kind == "S-rows-fused":
+            assert info["row_split"] == [0, 1] and info["fused"] == [0, 1] and not info["seg"], info
         elif kind != "S":
             assert info["row_split"] == [0], info          # proteins row-split
             # drug×drug in the LDS-staged kernel whenever the rank holds enough of them (P-small
@@ -167,9 +167,17 @@ def test_sharded_S_forward_matches_oracle():
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_weak_scaling_S_row_split_matches_oracle(world):
-    """bench.py's config S at N GPUs: N relation sets, every node type row-split and finished
-    in the fused kernel over all N sets' relations, blocks all-gathered."""
+    """bench.py's config S at N GPUs: N relation sets, every node type row-split; each rank's
+    block in dg_spmm_seg_f32 (one chunk per relation set) + the epilogue, layer 2 reassociated
+    as Σ_k (Â_k·H1)·W2_k, blocks all-gathered."""
     _check("S-rows", world)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_weak_scaling_S_fused_form_matches_oracle(world):
+    """The same partition in the fused kernel (one workgroup per row, projection GEMM on every
+    rank) — RelationShard.weak_sets(form="fused"), DG_S_ROWS_FORM=fused."""
+    _check("S-rows-fused", world)
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
