@@ -622,8 +622,10 @@ class ForwardPlan:
                     grp.layout, grp.rel_map, xs.get(et), part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
                     slab_max=int(grp.rel_ids.max()), proj=sp))
             elif self.seg_mode:
-                segs.append(self._seg_spec(et, *seg_w[et], out=part) if et in (seg_w or {})
-                            else self._seg_spec(et, xs[et], part))
+                if et in (seg_w or {}):  # layer 2 reassociated: H1_j and W2's stack
+                    segs.append(self._seg_spec(et, seg_w[et][0], part, seg_w[et][1]))
+                else:
+                    segs.append(self._seg_spec(et, xs[et], part))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
         if segs:
