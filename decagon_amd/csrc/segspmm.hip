@@ -17,8 +17,8 @@
 //
 // Per wave (row r, relation t of chunk c):
 //   [W: issue the 8 float4 loads of this lane's W2 slice, before the pairs]
-//   pairs of the segment (one coalesced load of ≤ 64), 8 gathers in flight per lane
-//   (LP lanes per gathered row, 64/LP nonzeros per step), a shuffle butterfly → y = Â_k[r]·X
+//   pairs of the segment (one coalesced load of ≤ 64, the next 64 prefetched), the batch's 64
+//   gathers in flight at once (LP lanes per gathered row), a shuffle butterfly → y = Â_k[r]·X
 //   [W: y through the wave's LDS slot to the matvec layout (lane: output float4 l&7, input
 //    slice 8(l>>3) .. +8), 32 fmaf, a butterfly over the 8 slices → z = y·W_k]
 // then the chunk's waves add their rows in relation order (LDS, one barrier) and the first
@@ -42,7 +42,7 @@ struct SegGroupK {
     int32_t n_chunks;
     int32_t chunk;
     int32_t n_rels;
-    int32_t rpb;         // rows per workgroup: 16 / chunk
+    int32_t rpb;         // rows per workgroup: NW / chunk
     int32_t row_blocks;
     int32_t block_begin;
     int32_t n_blocks;
@@ -54,62 +54,69 @@ struct SegArgs {
     int32_t pad;
 };
 
-constexpr int kSegUnroll = 8;  // gathers in flight per lane
-
 // y = Σ_{p in [beg, end)} val[p] · X[vcol[p]] (X row v at xb + v·x_ld), folded: every lane
-// holds float4 (lane % LP) of the row.
+// holds float4 (lane % LP) of the row.  A batch of 64 pairs is one coalesced load (the next
+// batch's is issued before this one's gathers) and its 64 gathers are all in flight at once:
+// LP per lane, 64/LP nonzeros side by side.
 template <int LP>
 __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, const float* __restrict__ val,
                                              const float* xb, int x_ld, int beg, int end) {
     constexpr int G = dg::kWave / LP;
+    constexpr int U = LP;  // U·G = 64: one batch per round trip
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const float* xq = xb + (lane % LP) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int vc = 0;
+    float vv = 0.f;
+    if (beg + lane < end) {
+        vc = vcol[beg + lane];
+        vv = val[beg + lane];
+    }
 #pragma unroll 1
     for (int base = beg; base < end; base += 64) {
         const int n = min(64, end - base);
-        int vc = 0;
-        float vv = 0.f;
-        if (lane < n) {
-            vc = vcol[base + lane];
-            vv = val[base + lane];
-        }
         const int eoff = vc * x_ld;
-#pragma unroll 1
-        for (int s0 = 0; s0 < n; s0 += kSegUnroll * G) {
-            int o[kSegUnroll];
-            float w[kSegUnroll];
-#pragma unroll
-            for (int u = 0; u < kSegUnroll; ++u) {
-                const int src = (s0 + u * G + sub) & 63;
-                o[u] = __shfl(eoff, src);
-                w[u] = __shfl(vv, src);
-            }
-            float4 xv[kSegUnroll];
-#pragma unroll
-            for (int u = 0; u < kSegUnroll; ++u) {
-                const bool ok = s0 + u * G + sub < n;
-                xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-                if (!ok) w[u] = 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < kSegUnroll; ++u) dg::fma4(acc, w[u], xv[u]);
+        const float v = vv;
+        vc = 0;
+        vv = 0.f;
+        if (base + 64 + lane < end) {
+            vc = vcol[base + 64 + lane];
+            vv = val[base + 64 + lane];
         }
+        int o[U];
+        float w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int src = u * G + sub;
+            o[u] = __shfl(eoff, src);
+            w[u] = __shfl(v, src);
+        }
+        float4 xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = u * G + sub < n;
+            xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!ok) w[u] = 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
     }
 #pragma unroll
     for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
     return acc;
 }
 
-// PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.
-template <int LP, bool PROJ>
-__global__ __launch_bounds__(1024) void spmm_seg_kernel(const SegArgs a) {
+// PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.  NW waves per
+// workgroup: 8 (256 VGPRs per lane: a batch's 16 gathers + W's slice without spills) unless a
+// chunk holds more than 8 relations.
+template <int LP, bool PROJ, int NW>
+__global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;  // float4s of an output row
-    __shared__ float4 ybuf[16][16];
-    __shared__ float4 zbuf[16][DOUT4];
+    __shared__ float4 ybuf[NW][16];
+    __shared__ float4 zbuf[NW][DOUT4];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (segment bounds: scalar loads)
     int gi = 0;
 #pragma unroll 1
     while (gi + 1 < a.n_groups && (int)blockIdx.x >= a.g[gi + 1].block_begin) ++gi;
@@ -186,6 +193,9 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     SegArgs args{};
     int64_t blocks = 0;
     int ng = 0;
+    int nw = 8;
+    for (int i = 0; i < n_groups; ++i)
+        if (groups[i].chunk > 8) nw = 16;
     for (int i = 0; i < n_groups; ++i) {
         const dg_seg_group& s = groups[i];
         if (s.n_rows < 0 || s.n_chunks < 1 || s.chunk < 1 || s.chunk > 16 || s.n_rels < 0 || s.n_cols < 0 ||
@@ -215,7 +225,7 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
         k.n_chunks = s.n_chunks;
         k.chunk = s.chunk;
         k.n_rels = s.n_rels;
-        k.rpb = 16 / s.chunk;
+        k.rpb = nw / s.chunk;
         k.row_blocks = dg::ceil_div(s.n_rows, k.rpb);
         const int64_t items = (int64_t)s.n_chunks * k.row_blocks;
         k.n_blocks = static_cast<int32_t>(8 * ((items + 7) / 8));
@@ -226,12 +236,19 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     args.n_groups = ng;
     if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    dim3 grid(static_cast<unsigned>(blocks)), block(1024);
-    if (proj)
-        hipLaunchKernelGGL((spmm_seg_kernel<16, true>), grid, block, 0, st, args);
-    else if (d_in == 64)
-        hipLaunchKernelGGL((spmm_seg_kernel<16, false>), grid, block, 0, st, args);
-    else
-        hipLaunchKernelGGL((spmm_seg_kernel<8, false>), grid, block, 0, st, args);
+    dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);
+#define DG_SEG_LAUNCH(NW)                                                                 \
+    if (proj)                                                                             \
+        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW>), grid, block, 0, st, args);    \
+    else if (d_in == 64)                                                                  \
+        hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW>), grid, block, 0, st, args);   \
+    else                                                                                  \
+        hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW>), grid, block, 0, st, args);
+    if (nw == 8) {
+        DG_SEG_LAUNCH(8)
+    } else {
+        DG_SEG_LAUNCH(16)
+    }
+#undef DG_SEG_LAUNCH
     return dg::launch_status();
 }
