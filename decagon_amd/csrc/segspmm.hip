@@ -25,6 +25,13 @@
 // wave of the row writes out[c][r].  Fixed order, no atomics: bitwise reproducible.
 #include "common.h"
 
+#ifndef DG_SEG_U
+#define DG_SEG_U 0  // gathers in flight per lane and batch: 0 = LP (a batch of 64 in one round trip)
+#endif
+#ifndef DG_SEG_MIN_NW
+#define DG_SEG_MIN_NW 8  // waves per workgroup (16 when a chunk holds more than 8 relations)
+#endif
+
 namespace {
 
 struct SegGroupK {
@@ -62,7 +69,7 @@ template <int LP>
 __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, const float* __restrict__ val,
                                              const float* xb, int x_ld, int beg, int end) {
     constexpr int G = dg::kWave / LP;
-    constexpr int U = LP;  // U·G = 64: one batch per round trip
+    constexpr int U = DG_SEG_U ? DG_SEG_U : LP;  // U·G = 64: one batch per round trip
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const float* xq = xb + (lane % LP) * 4;
@@ -84,23 +91,26 @@ __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, c
             vc = vcol[base + 64 + lane];
             vv = val[base + 64 + lane];
         }
-        int o[U];
-        float w[U];
+#pragma unroll 1
+        for (int s0 = 0; s0 < n; s0 += U * G) {
+            int o[U];
+            float w[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int src = u * G + sub;
-            o[u] = __shfl(eoff, src);
-            w[u] = __shfl(v, src);
+            for (int u = 0; u < U; ++u) {
+                const int src = (s0 + u * G + sub) & 63;
+                o[u] = __shfl(eoff, src);
+                w[u] = __shfl(v, src);
+            }
+            float4 xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool ok = s0 + u * G + sub < n;
+                xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (!ok) w[u] = 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
         }
-        float4 xv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = u * G + sub < n;
-            xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-            if (!ok) w[u] = 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
     }
 #pragma unroll
     for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
@@ -116,7 +126,11 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
     const int lane = threadIdx.x & 63;
+#ifdef DG_SEG_VECTOR_BOUNDS
+    const int wave = threadIdx.x >> 6;
+#else
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (segment bounds: scalar loads)
+#endif
     int gi = 0;
 #pragma unroll 1
     while (gi + 1 < a.n_groups && (int)blockIdx.x >= a.g[gi + 1].block_begin) ++gi;
@@ -193,7 +207,7 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     SegArgs args{};
     int64_t blocks = 0;
     int ng = 0;
-    int nw = 8;
+    int nw = DG_SEG_MIN_NW;
     for (int i = 0; i < n_groups; ++i)
         if (groups[i].chunk > 8) nw = 16;
     for (int i = 0; i < n_groups; ++i) {

@@ -1,15 +1,19 @@
-# A/B of variant builds on the GPU box: for each decagon_amd/lib/var_<name>.so (built on the
-# CPU container with `python -m decagon_amd._build <name> DEFINE...`) and the default library,
-# run the same bench command REPS times and print one summary line per run.
-# Usage: bash scripts/ab.sh <tag> "<bench args>" <name>... ; env REPS (default 2)
+# A/B timing on the GPU box: the same bench command with the default library and each variant,
+# REPS rounds (default 2), one summary line per run (scripts/bench_summary.py).
+# A variant is NAME — decagon_amd/lib/var_NAME.so, built on the CPU container with
+# `python -m decagon_amd._build NAME FLAG[=VALUE]...` — or VAR=value, an environment setting (knobs
+# such as DG_S_ROWS_FORM, DG_PROJ_BLOCKS, DG_WPG) with the default library.
+# Usage: bash scripts/ab.sh <tag> "<bench args>" VARIANT...
 set -o pipefail
 tag=$1; shift
 args=$1; shift
 out=gpurun_out/ab_$tag; mkdir -p $out
 for rep in $(seq 1 ${REPS:-2}); do
   for v in base "$@"; do
-    lib=""; [ $v = base ] || lib=$PWD/decagon_amd/lib/var_$v.so
-    DG_LIB=$lib timeout -k 10 300 python bench.py $args > $out/${v}_$rep.json 2> $out/${v}_$rep.err || exit $?
-    python scripts/bench_summary.py $v $out/${v}_$rep.json
+    lib=""; envs=""
+    case $v in base) ;; *=*) envs=$v;; *) lib=$PWD/decagon_amd/lib/var_$v.so;; esac
+    name=$(echo "$v" | tr -c 'A-Za-z0-9_.-' '_')
+    env DG_LIB=$lib $envs timeout -k 10 300 python bench.py $args > $out/${name}_$rep.json 2> $out/${name}_$rep.err || exit $?
+    python scripts/bench_summary.py "$v" $out/${name}_$rep.json
   done
 done

@@ -13,6 +13,10 @@ def line(tag, d):
         out.append(f"kernel {rf['kernel_ms'] * 1e3:.2f} us frac {rf.get('frac', 0):.4f}")
     if "spmm_layer2_ms" in d:
         out.append(f"L2 {d['spmm_layer2_ms'] * 1e3:.2f} us")
+    if "max_rank_ms_per_step" in d:  # bench.py --simulate-world
+        out.append(f"max rank step {d['max_rank_ms_per_step'] * 1e3:.2f} us")
+        r = max(d["ranks"], key=lambda x: x["ms_per_step"])
+        out.append(f"its layer-1 / layer-2 SpMM {r['layer1_spmm_ms'] * 1e3:.2f} / {r['layer2_spmm_ms'] * 1e3:.2f} us")
     return " | ".join(out)
 
 
