@@ -26,10 +26,10 @@
 #include "common.h"
 
 #ifndef DG_SEG_U
-#define DG_SEG_U 0  // gathers in flight per lane and batch: 0 = LP (a batch of 64 in one round trip)
+#define DG_SEG_U 8  // gathers in flight per lane (0: LP — a batch of 64 in one round trip)
 #endif
 #ifndef DG_SEG_MIN_NW
-#define DG_SEG_MIN_NW 8  // waves per workgroup (16 when a chunk holds more than 8 relations)
+#define DG_SEG_MIN_NW 1  // waves per workgroup, at least (else: the launch's largest chunk)
 #endif
 
 namespace {
@@ -58,7 +58,7 @@ struct SegGroupK {
 struct SegArgs {
     SegGroupK g[DG_MAX_GROUPS];
     int32_t n_groups;
-    int32_t pad;
+    int32_t nw;  // waves per workgroup
 };
 
 // y = Σ_{p in [beg, end)} val[p] · X[vcol[p]] (X row v at xb + v·x_ld), folded: every lane
@@ -117,9 +117,9 @@ __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, c
     return acc;
 }
 
-// PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.  NW waves per
-// workgroup: 8 (256 VGPRs per lane: a batch's 16 gathers + W's slice without spills) unless a
-// chunk holds more than 8 relations.
+// PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.  a.nw waves per
+// workgroup (the launch's largest chunk, so a chunk-6 group wastes no wave slot; rows per
+// workgroup nw / chunk), at most NW.
 template <int LP, bool PROJ, int NW>
 __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;  // float4s of an output row
@@ -209,7 +209,9 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     int ng = 0;
     int nw = DG_SEG_MIN_NW;
     for (int i = 0; i < n_groups; ++i)
-        if (groups[i].chunk > 8) nw = 16;
+        if (groups[i].chunk > nw && groups[i].n_rows > 0 && groups[i].n_rels > 0) nw = groups[i].chunk;
+    if (nw > 16) return DG_EINVAL;
+    args.nw = nw;
     for (int i = 0; i < n_groups; ++i) {
         const dg_seg_group& s = groups[i];
         if (s.n_rows < 0 || s.n_chunks < 1 || s.chunk < 1 || s.chunk > 16 || s.n_rels < 0 || s.n_cols < 0 ||
@@ -250,7 +252,7 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     args.n_groups = ng;
     if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);
+    dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);  // (launch bounds: 8 or 16 waves)
 #define DG_SEG_LAUNCH(NW)                                                                 \
     if (proj)                                                                             \
         hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW>), grid, block, 0, st, args);    \
@@ -258,7 +260,7 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
         hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW>), grid, block, 0, st, args);   \
     else                                                                                  \
         hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW>), grid, block, 0, st, args);
-    if (nw == 8) {
+    if (nw <= 8) {
         DG_SEG_LAUNCH(8)
     } else {
         DG_SEG_LAUNCH(16)
