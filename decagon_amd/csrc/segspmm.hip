@@ -28,6 +28,9 @@
 #ifndef DG_SEG_U
 #define DG_SEG_U 8  // gathers in flight per lane (0: LP — a batch of 64 in one round trip)
 #endif
+#ifndef DG_SEG_UP
+#define DG_SEG_UP 4  // the same for the reassociated form (its W slice holds 32 VGPRs):
+#endif              // measured at S N = 8 rank 0: 8 → 4 took layer 2 from 8.0 to 6.7 µs
 #ifndef DG_SEG_MIN_NW
 #define DG_SEG_MIN_NW 1  // waves per workgroup, at least (else: the launch's largest chunk)
 #endif
@@ -65,11 +68,11 @@ struct SegArgs {
 // holds float4 (lane % LP) of the row.  A batch of 64 pairs is one coalesced load (the next
 // batch's is issued before this one's gathers) and its 64 gathers are all in flight at once:
 // LP per lane, 64/LP nonzeros side by side.
-template <int LP>
+template <int LP, int UU>
 __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, const float* __restrict__ val,
                                              const float* xb, int x_ld, int beg, int end) {
     constexpr int G = dg::kWave / LP;
-    constexpr int U = DG_SEG_U ? DG_SEG_U : LP;  // U·G = 64: one batch per round trip
+    constexpr int U = UU ? UU : LP;  // (U·G = 64: one batch per round trip)
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const float* xq = xb + (lane % LP) * 4;
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
             for (int i = 0; i < 8; ++i) wv[i] = *reinterpret_cast<const float4*>(W + i * 32);
             // H is shared by the relations: vcol = s·n_cols + col addresses row col
             const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;
-            const float4 y = seg_gather<16>(g.vcol, g.val, xb, g.x_ld, beg, end);
+            const float4 y = seg_gather<16, DG_SEG_UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
             if (lane < 16) ybuf[wave][lane] = y;
             __builtin_amdgcn_wave_barrier();
             const int ms = lane >> 3;
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
             dg::add4(z, dg::shfl_xor4(z, 32));
             res = z;
         } else {
-            res = seg_gather<LP>(g.vcol, g.val, g.x, g.x_ld, beg, end);
+            res = seg_gather<LP, DG_SEG_U>(g.vcol, g.val, g.x, g.x_ld, beg, end);
         }
     }
     if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
