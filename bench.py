@@ -156,8 +156,7 @@ def make_plan(args, graph, shard, device, keep_sums=False, dropout=None):
     chunk = args.chunk if shard is None or shard.chunks is None else shard.chunks
     dg = DeviceGraph(graph.edge_types, csr, device, None if shard is None else shard.local,
                      chunk=chunk, target_waves=args.target_waves,
-                     row_block=None if shard is None else shard.row_block,
-                     segments=shard is not None and shard.seg_rows)
+                     row_block=None if shard is None else shard.row_block)
     rng = np.random.default_rng(1234)
     n = graph.n_nodes
     w1 = LayerWeights({et: torch.from_numpy(glorot_stack(rng, K, n[et[1]], H1)).to(device)
@@ -261,7 +260,8 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
 
 
 KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm_groups_kernel<{lp}>",
-                "PreparedStaged": "spmm_staged_kernel"}
+                "PreparedStaged": "spmm_staged_kernel", "PreparedFusedSeg": "gcn_fused_seg_kernel<{lp}, false",
+                "PreparedSeg": "spmm_seg_kernel<{lp}, false"}
 
 
 def pmc_traffic(config, launch, d, layer=1):

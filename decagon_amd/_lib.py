@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 27
+ABI_VERSION = 28
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -163,6 +163,8 @@ SIGNATURES = {
     "dg_spmm_groups_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_groups_lds_f32": (c_int32, [POINTER(DgRelGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_seg_f32": (c_int32, [POINTER(DgSegGroup), c_int32, c_int32, c_int32, c_void_p]),
+    "dg_gcn_fused_seg_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32,
+                                       c_int32, c_void_p]),
     "dg_spmm_csr_f32": (
         c_int32,
         [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32,

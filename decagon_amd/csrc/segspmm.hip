@@ -120,6 +120,48 @@ __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, c
     return acc;
 }
 
+// One wave's share: relation t (local relation k) of chunk c in row r — its segment's sum
+// y = Σ val·X[vcol] and, with PROJ, z = y·W[slab(k)] (ybuf: the wave's 16-float4 LDS slot).
+// Returns the wave's row in the output layout (lanes < DOUT4 hold float4 lane of it).
+template <int LP, bool PROJ>
+__device__ __forceinline__ float4 seg_wave(const SegGroupK& g, int c, int r, int t, int k, float4* ybuf) {
+    const int lane = threadIdx.x & 63;
+    const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
+    const int beg = g.seg[si];
+    const int end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
+    if constexpr (PROJ) {
+        const int s = g.slab ? g.slab[k] : k;
+        // this lane's W_s slice: rows 8(l>>3) .. +8, columns 4(l&7) .. +4
+        const float* W = g.w + (int64_t)s * (64 * 32) + (lane >> 3) * (8 * 32) + (lane & 7) * 4;
+        float4 wv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wv[i] = *reinterpret_cast<const float4*>(W + i * 32);
+        // H is shared by the relations: vcol = s·n_cols + col addresses row col
+        const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;
+        const float4 y = seg_gather<16, DG_SEG_UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
+        if (lane < 16) ybuf[lane] = y;
+        __builtin_amdgcn_wave_barrier();
+        const int ms = lane >> 3;
+        const float4 ya = ybuf[2 * ms];
+        const float4 yb = ybuf[2 * ms + 1];
+        float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        dg::fma4(z, ya.x, wv[0]);
+        dg::fma4(z, ya.y, wv[1]);
+        dg::fma4(z, ya.z, wv[2]);
+        dg::fma4(z, ya.w, wv[3]);
+        dg::fma4(z, yb.x, wv[4]);
+        dg::fma4(z, yb.y, wv[5]);
+        dg::fma4(z, yb.z, wv[6]);
+        dg::fma4(z, yb.w, wv[7]);
+        dg::add4(z, dg::shfl_xor4(z, 8));
+        dg::add4(z, dg::shfl_xor4(z, 16));
+        dg::add4(z, dg::shfl_xor4(z, 32));
+        return z;
+    } else {
+        return seg_gather<LP, DG_SEG_U>(g.vcol, g.val, g.x, g.x_ld, beg, end);
+    }
+}
+
 // PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.  a.nw waves per
 // workgroup (the launch's largest chunk, so a chunk-6 group wastes no wave slot; rows per
 // workgroup nw / chunk), at most NW.
@@ -151,42 +193,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     const bool row_ok = slot < g.rpb && r < g.n_rows;
     const int k = c * g.chunk + t;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row_ok && k < g.n_rels) {  // wave-uniform
-        const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
-        const int beg = g.seg[si];
-        const int end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
-        if constexpr (PROJ) {
-            const int s = g.slab ? g.slab[k] : k;
-            // this lane's W_s slice: rows 8(l>>3) .. +8, columns 4(l&7) .. +4
-            const float* W = g.w + (int64_t)s * (64 * 32) + (lane >> 3) * (8 * 32) + (lane & 7) * 4;
-            float4 wv[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) wv[i] = *reinterpret_cast<const float4*>(W + i * 32);
-            // H is shared by the relations: vcol = s·n_cols + col addresses row col
-            const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;
-            const float4 y = seg_gather<16, DG_SEG_UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
-            if (lane < 16) ybuf[wave][lane] = y;
-            __builtin_amdgcn_wave_barrier();
-            const int ms = lane >> 3;
-            const float4 ya = ybuf[wave][2 * ms];
-            const float4 yb = ybuf[wave][2 * ms + 1];
-            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            dg::fma4(z, ya.x, wv[0]);
-            dg::fma4(z, ya.y, wv[1]);
-            dg::fma4(z, ya.z, wv[2]);
-            dg::fma4(z, ya.w, wv[3]);
-            dg::fma4(z, yb.x, wv[4]);
-            dg::fma4(z, yb.y, wv[5]);
-            dg::fma4(z, yb.z, wv[6]);
-            dg::fma4(z, yb.w, wv[7]);
-            dg::add4(z, dg::shfl_xor4(z, 8));
-            dg::add4(z, dg::shfl_xor4(z, 16));
-            dg::add4(z, dg::shfl_xor4(z, 32));
-            res = z;
-        } else {
-            res = seg_gather<LP, DG_SEG_U>(g.vcol, g.val, g.x, g.x_ld, beg, end);
-        }
-    }
+    if (row_ok && k < g.n_rels) res = seg_wave<LP, PROJ>(g, c, r, t, k, ybuf[wave]);  // wave-uniform
     if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
     __syncthreads();
     if (row_ok && t == 0 && lane < DOUT4) {
@@ -196,6 +203,119 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     }
 }
 
+// The fused form (dg_gcn_fused_seg_f32): one workgroup per output row of a target node type
+// i, one wave per (group, relation) — every group one chunk — then, in LDS, each group's
+// relations summed in order and L2-normalised (layers.py:93 / :117) by one wave, the groups
+// summed in order and relu'd (model.py:75) by wave 0, which writes the row.  With PROJ this is
+// layer 2 reassociated, so layer 1 needs no projection epilogue and no GEMM runs.
+struct FsTargetK {
+    float* out;
+    int32_t n_rows;
+    int32_t g_begin;
+    int32_t g_count;
+    int32_t relu;
+    int32_t block_begin;
+    int32_t pad;
+};
+
+struct FsArgs {
+    SegGroupK g[DG_MAX_GROUPS];
+    FsTargetK t[DG_MAX_GROUPS];
+    int32_t n_targets;
+    int32_t nw;
+};
+
+template <int LP, bool PROJ, int NW>
+__global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) {
+    constexpr int DOUT4 = PROJ ? 8 : LP;
+    __shared__ float4 ybuf[NW][16];
+    __shared__ float4 zbuf[NW][DOUT4];
+    __shared__ float4 nbuf[DG_MAX_GROUPS][DOUT4];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int ti = 0;
+#pragma unroll 1
+    while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
+    const FsTargetK& T = a.t[ti];
+    const int r = blockIdx.x - T.block_begin;
+    // wave -> (group gl, relation t): the target's groups' relations back to back
+    int gl = 0, base = 0;
+#pragma unroll 1
+    while (gl < T.g_count && wave >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
+    float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gl < T.g_count) res = seg_wave<LP, PROJ>(a.g[T.g_begin + gl], 0, r, wave - base, wave - base, ybuf[wave]);
+    if (lane < DOUT4) zbuf[wave][lane] = res;
+    __syncthreads();
+    if (wave < T.g_count) {
+        int gb = 0;
+#pragma unroll 1
+        for (int u = 0; u < wave; ++u) gb += a.g[T.g_begin + u].n_rels;
+        const int K = a.g[T.g_begin + wave].n_rels;
+        const int q = lane % DOUT4;
+        float4 s = zbuf[gb][q];
+#pragma unroll 1
+        for (int u = 1; u < K; ++u) dg::add4(s, zbuf[gb + u][q]);
+        // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
+        float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
+#pragma unroll
+        for (int m = 1; m < DOUT4; m <<= 1) ss += __shfl_xor(ss, m);
+        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+        if (lane < DOUT4) nbuf[wave][lane] = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+    }
+    __syncthreads();
+    if (wave == 0 && lane < DOUT4) {
+        float4 tot = nbuf[0][lane];
+        for (int u = 1; u < T.g_count; ++u) dg::add4(tot, nbuf[u][lane]);
+        if (T.relu) {
+            tot.x = fmaxf(tot.x, 0.f);
+            tot.y = fmaxf(tot.y, 0.f);
+            tot.z = fmaxf(tot.z, 0.f);
+            tot.w = fmaxf(tot.w, 0.f);
+        }
+        *reinterpret_cast<float4*>(T.out + (int64_t)r * (4 * DOUT4) + 4 * lane) = tot;
+    }
+}
+
+}  // namespace
+
+namespace {
+// Validate one dg_seg_group and copy it into the kernel form (skip: nothing to compute).
+int convert_seg(const dg_seg_group& s, bool proj, int d_in, SegGroupK& k, bool& skip) {
+    if (s.n_rows < 0 || s.n_chunks < 1 || s.chunk < 1 || s.chunk > 16 || s.n_rels < 0 || s.n_cols < 0 ||
+        s.x_rows < 0)
+        return DG_EINVAL;
+    if ((int64_t)s.n_chunks * s.chunk < s.n_rels || (int64_t)(s.n_chunks - 1) * s.chunk >= s.n_rels)
+        return DG_EINVAL;  // every chunk holds at least one relation
+    if ((s.w != nullptr) != proj) return DG_EINVAL;  // a weight stack exactly when d_in != d_out
+    skip = s.n_rows == 0 || s.n_rels == 0;
+    if (skip) return DG_OK;
+    if (!s.rowptr || !s.seg || !s.x) return DG_EINVAL;
+    if (!dg::aligned16(s.x) || (s.x_ld & 3)) return DG_EALIGN;
+    if (proj && !dg::aligned16(s.w)) return DG_EALIGN;
+    if (s.x_ld < d_in) return DG_EINVAL;
+    if ((int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;  // 32-bit gather offsets
+    k = SegGroupK{};
+    k.rowptr = s.rowptr;
+    k.seg = s.seg;
+    k.vcol = s.vcol;
+    k.val = s.val;
+    k.slab = s.slab;
+    k.x = s.x;
+    k.w = s.w;
+    k.out = s.out;
+    k.x_ld = static_cast<int32_t>(s.x_ld);
+    k.n_rows = s.n_rows;
+    k.n_cols = s.n_cols;
+    k.n_chunks = s.n_chunks;
+    k.chunk = s.chunk;
+    k.n_rels = s.n_rels;
+    return DG_OK;
+}
+
+int seg_shape(int32_t d_in, int32_t d_out, bool& proj) {
+    proj = d_in == 64 && d_out == 32;
+    return proj || (d_in == d_out && (d_in == 32 || d_in == 64)) ? DG_OK : DG_EINVAL;
+}
 }  // namespace
 
 extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out,
@@ -203,10 +323,7 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     if (n_groups < 0 || (n_groups > 0 && groups == nullptr)) return DG_EINVAL;
     if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
     bool proj = false;
-    if (d_in == 64 && d_out == 32)
-        proj = true;
-    else if (!(d_in == d_out && (d_in == 32 || d_in == 64)))
-        return DG_EINVAL;
+    if (seg_shape(d_in, d_out, proj) != DG_OK) return DG_EINVAL;
     SegArgs args{};
     int64_t blocks = 0;
     int ng = 0;
@@ -217,33 +334,13 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     args.nw = nw;
     for (int i = 0; i < n_groups; ++i) {
         const dg_seg_group& s = groups[i];
-        if (s.n_rows < 0 || s.n_chunks < 1 || s.chunk < 1 || s.chunk > 16 || s.n_rels < 0 || s.n_cols < 0 ||
-            s.x_rows < 0)
-            return DG_EINVAL;
-        if ((int64_t)s.n_chunks * s.chunk < s.n_rels || (int64_t)(s.n_chunks - 1) * s.chunk >= s.n_rels)
-            return DG_EINVAL;  // every chunk holds at least one relation
-        if ((s.w != nullptr) != proj) return DG_EINVAL;  // a weight stack exactly when d_in != d_out
-        if (s.n_rows == 0 || s.n_rels == 0) continue;
-        if (!s.rowptr || !s.seg || !s.x || !s.out) return DG_EINVAL;
-        if (!dg::aligned16(s.x) || !dg::aligned16(s.out) || (s.x_ld & 3)) return DG_EALIGN;
-        if (proj && !dg::aligned16(s.w)) return DG_EALIGN;
-        if (s.x_ld < d_in) return DG_EINVAL;
-        if ((int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;  // 32-bit gather offsets
+        bool skip = false;
+        const int rc = convert_seg(s, proj, d_in, args.g[ng], skip);
+        if (rc != DG_OK) return rc;
+        if (skip) continue;
         SegGroupK& k = args.g[ng++];
-        k.rowptr = s.rowptr;
-        k.seg = s.seg;
-        k.vcol = s.vcol;
-        k.val = s.val;
-        k.slab = s.slab;
-        k.x = s.x;
-        k.w = s.w;
-        k.out = s.out;
-        k.x_ld = static_cast<int32_t>(s.x_ld);
-        k.n_rows = s.n_rows;
-        k.n_cols = s.n_cols;
-        k.n_chunks = s.n_chunks;
-        k.chunk = s.chunk;
-        k.n_rels = s.n_rels;
+        if (!s.out) return DG_EINVAL;
+        if (!dg::aligned16(s.out)) return DG_EALIGN;
         k.rpb = nw / s.chunk;
         k.row_blocks = dg::ceil_div(s.n_rows, k.rpb);
         const int64_t items = (int64_t)s.n_chunks * k.row_blocks;
@@ -269,5 +366,64 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
         DG_SEG_LAUNCH(16)
     }
 #undef DG_SEG_LAUNCH
+    return dg::launch_status();
+}
+
+extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets,
+                                    int32_t n_targets, int32_t d_in, int32_t d_out, void* stream) {
+    if (n_groups < 1 || !groups || n_targets < 1 || !targets) return DG_EINVAL;
+    if (n_groups > DG_MAX_GROUPS || n_targets > DG_MAX_GROUPS) return DG_ETOOMANY;
+    bool proj = false;
+    if (seg_shape(d_in, d_out, proj) != DG_OK) return DG_EINVAL;
+    FsArgs a{};
+    for (int i = 0; i < n_groups; ++i) {
+        bool skip = false;
+        const int rc = convert_seg(groups[i], proj, d_in, a.g[i], skip);
+        if (rc != DG_OK) return rc;
+        // one chunk holding every relation of the group, at least one relation
+        if (groups[i].n_chunks != 1 || groups[i].chunk != groups[i].n_rels || groups[i].n_rels < 1) return DG_EINVAL;
+    }
+    int64_t blocks = 0;
+    int nw = 1;
+    for (int t = 0; t < n_targets; ++t) {
+        const dg_fused_target& s = targets[t];
+        if (!s.out || !dg::aligned16(s.out) || s.n_rows < 0 || s.g_count < 1 || s.g_begin < 0 ||
+            s.g_begin + s.g_count > n_groups || (s.flags & ~DG_EPI_RELU))
+            return DG_EINVAL;
+        int waves = 0;
+        for (int g = s.g_begin; g < s.g_begin + s.g_count; ++g) {
+            if (groups[g].n_rows != s.n_rows) return DG_EINVAL;
+            waves += groups[g].n_rels;
+        }
+        if (waves > 16) return DG_EINVAL;  // one wave per relation of the row
+        nw = waves > nw ? waves : nw;
+        FsTargetK& k = a.t[t];
+        k.out = s.out;
+        k.n_rows = s.n_rows;
+        k.g_begin = s.g_begin;
+        k.g_count = s.g_count;
+        k.relu = (s.flags & DG_EPI_RELU) ? 1 : 0;
+        k.block_begin = static_cast<int32_t>(blocks);
+        blocks += s.n_rows;
+    }
+    if (blocks > 0x7fffffff) return DG_EINVAL;
+    a.n_targets = n_targets;
+    a.nw = nw;
+    if (blocks == 0) return DG_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);
+#define DG_FS_LAUNCH(NW)                                                                      \
+    if (proj)                                                                                 \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW>), grid, block, 0, st, a);      \
+    else if (d_in == 64)                                                                      \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW>), grid, block, 0, st, a);     \
+    else                                                                                      \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW>), grid, block, 0, st, a);
+    if (nw <= 8) {
+        DG_FS_LAUNCH(8)
+    } else {
+        DG_FS_LAUNCH(16)
+    }
+#undef DG_FS_LAUNCH
     return dg::launch_status();
 }

@@ -73,6 +73,9 @@ FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
 CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "0") != "0"
 # layer 2 of staged groups makes its slabs H1_j·W2_k on the MFMA inside the SpMM kernel
 STAGED_PROJ = os.environ.get("DG_STAGED_PROJ", "1") != "0"
+# one-GPU plans whose node types all fit dg_gcn_fused_seg_f32 (config S) use it, layer 2
+# reassociated; DG_FUSED_SEG=0 keeps dg_gcn_fused_f32 with the projection epilogue + P
+FUSED_SEG = os.environ.get("DG_FUSED_SEG", "1") != "0"
 STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 
 
@@ -206,7 +209,7 @@ class DeviceGraph:
     def __init__(self, edge_types: Dict[EdgeType, int], adj: Dict[EdgeType, Sequence[Optional[HostCSR]]],
                  device: torch.device, local: Optional[Dict[EdgeType, Sequence[int]]] = None,
                  chunk=None, target_waves: int = 32768, d_policy: int = 64,
-                 row_block: Optional[Dict[int, Tuple[int, int, int]]] = None, segments: bool = False):
+                 row_block: Optional[Dict[int, Tuple[int, int, int]]] = None, segments: bool = True):
         """segments: also upload each chunk-merged group's segment starts (sparse.chunk_segments)
         for dg_spmm_seg_f32 — groups of at most 16 relations per chunk."""
         self.edge_types = dict(edge_types)
@@ -427,8 +430,17 @@ class ForwardPlan:
         self.staged_proj = {et for et in self.edge_types
                             if dgraph.groups[et].staged and dgraph.groups[et].n_rels and h1 == 64
                             and self.drop_state is None and STAGED_PROJ}
+        # one GPU (config S): every node type finished by dg_gcn_fused_seg_f32 — one workgroup
+        # per row, one wave per relation — with layer 2 reassociated (no projection in layer 1,
+        # no GEMM), when every group is one chunk of <= 16 relations per row in total
+        self.fused_seg = (FUSED_SEG and not self.flat_mode and not self.row_block and self.drop_state is None
+                          and h1 == 64 and h2 == 32
+                          and all(g.seg is not None and g.n_chunks == 1 and g.chunk == g.n_rels >= 1
+                                  and not g.staged for g in dgraph.groups.values())
+                          and all(sum(dgraph.groups[et].n_rels for et in ets) <= 16
+                                  for ets in self.targets.values()))
         self.seg_proj = {et for et in self.edge_types
-                         if self.seg_mode and dgraph.groups[et].n_rels and h1 == 64 and h2 == 32}
+                         if (self.seg_mode or self.fused_seg) and dgraph.groups[et].n_rels and h1 == 64 and h2 == 32}
         self.proj: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
@@ -445,7 +457,7 @@ class ForwardPlan:
         self.side_stream = (torch.cuda.Stream(dev) if dev.type == "cuda" and CONCURRENT_LAUNCHES else None)
 
         # ---- layer 1 (+ the layer-2 projections of rows it finishes) ----
-        self.fused = self._fused_targets()
+        self.fused = list(self.targets) if self.fused_seg else self._fused_targets()
         rels_from: Dict[int, int] = {}
         for et in self.edge_types:
             rels_from[et[1]] = rels_from.get(et[1], 0) + dgraph.groups[et].n_rels
@@ -454,6 +466,7 @@ class ForwardPlan:
         finished = (set(self.targets) - set(self.row_block)) if self.flat_mode else set(self.fused)
         proj_fused = [et for et in self.edge_types
                       if dgraph.groups[et].n_rels and et[1] in finished and et not in self.staged_proj
+                      and et not in self.seg_proj
                       and rels_from[et[1]] <= self.FUSED_PROJ_MAX_RELS and self.drop_state is None]
         if len(proj_fused) > DG_MAX_GROUPS:
             proj_fused = []
@@ -533,7 +546,7 @@ class ForwardPlan:
         return kernels.RelGroupSpec(grp.rowptr, grp.vcol, grp.val, x, out, grp.n_rows, grp.n_chunks, d,
                                     grp.K * grp.n_cols, vcol_max=grp.vcol_max)
 
-    def _seg_spec(self, et, x: torch.Tensor, out, w=None) -> kernels.SegSpec:
+    def _seg_spec(self, et, x: torch.Tensor, out=None, w=None) -> kernels.SegSpec:
         grp = self.g.groups[et]
         return kernels.SegSpec(grp.rowptr, grp.seg, grp.vcol, grp.val, x, out, grp.n_rows, grp.n_cols, grp.n_chunks,
                                grp.chunk, grp.n_rels, x.stride(-2),
@@ -550,7 +563,14 @@ class ForwardPlan:
         launches: List[Callable[[], None]] = []
         fused_t = self.fused
         gathers = []
-        if fused_t:
+        if self.fused_seg:
+            seg_w = seg_w or {}
+            tgts = [(outs[i], n[i], [self._seg_spec(et, seg_w[et][0], None, seg_w[et][1]) if et in seg_w
+                                     else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu)
+                    for i in fused_t]
+            launches.append(kernels.PreparedFusedSeg(tgts, self.h1 if seg_w else d, d))
+            self.launch_groups[id(launches[-1])] = [et for i in fused_t for et in self.targets[i]]
+        elif fused_t:
             # waves per group: small launches (latency-bound) split the densest row group's
             # batches of 64 over up to two waves; big launches have parallelism to spare
             avg = max(g.groups[et].nnz / max(1, g.groups[et].n_rows) for i in fused_t for et in self.targets[i])
@@ -757,7 +777,8 @@ class ForwardPlan:
     @property
     def spmm_launches(self):
         """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""
-        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged, kernels.PreparedSeg)
+        kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged, kernels.PreparedSeg,
+                 kernels.PreparedFusedSeg)
         pick = lambda L: [l for l in L.launches if isinstance(l, kinds)]
         return pick(self._layer1), pick(self._layer2)
 
@@ -789,7 +810,7 @@ class ForwardPlan:
         L = self._layer1 if layer == 1 else self._layer2
         d = self.h1 if layer == 1 else self.h2
         ets = self.launch_groups.get(id(launch), [])
-        fused = isinstance(launch, kernels.PreparedFused)
+        fused = isinstance(launch, (kernels.PreparedFused, kernels.PreparedFusedSeg))
         tot = sum(self.group_bytes(et, d, fused, layer) for et in ets)
         if fused:
             tot += sum(4 * d * self._out_rows(i) for i in L.fused_targets)

@@ -189,7 +189,7 @@ class SegSpec:
     vcol: torch.Tensor            # int32 [nnz]
     val: torch.Tensor             # float32 [nnz]
     x: torch.Tensor               # float32: stacked X (no w) or H [n_cols, x_ld]
-    out: torch.Tensor             # float32 [n_chunks, n_rows, d_out]
+    out: Optional[torch.Tensor]   # float32 [n_chunks, n_rows, d_out] (None in the fused form)
     n_rows: int
     n_cols: int
     n_chunks: int
@@ -202,12 +202,13 @@ class SegSpec:
     slab: Optional[torch.Tensor] = None   # int32 [n_rels] (None: relation k is slab k)
     slab_max: int = -1
 
-    def validate(self, d_in: int, d_out: int) -> None:
+    def validate(self, d_in: int, d_out: int, need_out: bool = True) -> None:
         for t, what in ((self.rowptr, "rowptr"), (self.seg, "seg"), (self.vcol, "vcol")):
             _dev(t, torch.int32, what)
         _dev(self.val, torch.float32, "val")
         _dev(self.x, torch.float32, "x")
-        _dev(self.out, torch.float32, "out")
+        if need_out:
+            _dev(self.out, torch.float32, "out")
         if not 1 <= self.chunk <= 16:
             raise ValueError("chunk must be in [1, 16]")
         if not (self.n_chunks - 1) * self.chunk < self.n_rels <= self.n_chunks * self.chunk:
@@ -224,7 +225,7 @@ class SegSpec:
             raise ValueError("x_ld must be >= d_in and a multiple of 4")
         if self.x_rows * self.x_ld >= 2**31:
             raise ValueError("dense operand too large for 32-bit gather offsets")
-        if self.out.numel() < self.n_chunks * self.n_rows * d_out:
+        if need_out and self.out.numel() < self.n_chunks * self.n_rows * d_out:
             raise ValueError("out too small for [n_chunks, n_rows, d_out]")
         if self.w is None:
             if self.n_rows and self.x_rows and self.x.numel() < (self.x_rows - 1) * self.x_ld + d_in:
@@ -246,32 +247,70 @@ class SegSpec:
             raise ValueError("n_rels > K")
 
 
+def _seg_array(specs: Sequence[SegSpec], d_in: int, d_out: int, need_out: bool):
+    if len(specs) > _lib.DG_MAX_GROUPS:
+        raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups per launch")
+    if len({s.w is None for s in specs}) > 1:
+        raise ValueError("every group of a launch has a weight stack, or none")
+    arr = (_lib.DgSegGroup * max(1, len(specs)))()
+    for i, s in enumerate(specs):
+        s.validate(d_in, d_out, need_out)
+        g = arr[i]
+        g.rowptr, g.seg = s.rowptr.data_ptr(), s.seg.data_ptr()
+        g.vcol = s.vcol.data_ptr() if s.vcol.numel() else None
+        g.val = s.val.data_ptr() if s.val.numel() else None
+        g.slab = s.slab.data_ptr() if s.slab is not None else None
+        g.x = s.x.data_ptr()
+        g.out = s.out.data_ptr() if s.out is not None else None
+        g.w = s.w.data_ptr() if s.w is not None else None
+        g.x_ld, g.n_rows, g.n_cols, g.n_chunks = s.x_ld, s.n_rows, s.n_cols, s.n_chunks
+        g.chunk, g.n_rels, g.x_rows = s.chunk, s.n_rels, s.x_rows
+    return arr
+
+
 class PreparedSeg:
     """A fixed dg_spmm_seg_f32 launch (every group with w, or none)."""
 
     def __init__(self, specs: Sequence[SegSpec], d_in: int, d_out: int):
-        if len(specs) > _lib.DG_MAX_GROUPS:
-            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} groups per launch")
-        if len({s.w is None for s in specs}) > 1:
-            raise ValueError("every group of a launch has a weight stack, or none")
-        arr = (_lib.DgSegGroup * max(1, len(specs)))()
-        for i, s in enumerate(specs):
-            s.validate(d_in, d_out)
-            g = arr[i]
-            g.rowptr, g.seg = s.rowptr.data_ptr(), s.seg.data_ptr()
-            g.vcol = s.vcol.data_ptr() if s.vcol.numel() else None
-            g.val = s.val.data_ptr() if s.val.numel() else None
-            g.slab = s.slab.data_ptr() if s.slab is not None else None
-            g.x, g.out = s.x.data_ptr(), s.out.data_ptr()
-            g.w = s.w.data_ptr() if s.w is not None else None
-            g.x_ld, g.n_rows, g.n_cols, g.n_chunks = s.x_ld, s.n_rows, s.n_cols, s.n_chunks
-            g.chunk, g.n_rels, g.x_rows = s.chunk, s.n_rels, s.x_rows
+        arr = _seg_array(specs, d_in, d_out, True)
         self.specs = list(specs)
         self._arr, self._n, self.d_in, self.d_out = arr, len(specs), d_in, d_out
         self._fn = _lib.load().dg_spmm_seg_f32
 
     def __call__(self, stream=None) -> None:
         check(self._fn(self._arr, self._n, self.d_in, self.d_out, _stream_ptr(stream)), "dg_spmm_seg_f32")
+
+
+class PreparedFusedSeg:
+    """A fixed dg_gcn_fused_seg_f32 launch: targets = [(out tensor, n_rows, [SegSpec], relu)],
+    every group one chunk holding all its relations (chunk == n_rels), at most 16 relations per
+    target; with weight stacks (d_in 64 → d_out 32) the reassociated layer 2."""
+
+    def __init__(self, targets, d_in: int, d_out: int):
+        specs, tarr = [], (DgFusedTarget * len(targets))()
+        for t, (out, n_rows, gspecs, relu) in enumerate(targets):
+            _dev(out, torch.float32, "out")
+            if out.numel() < n_rows * d_out:
+                raise ValueError("fused output too small")
+            if sum(s.n_rels for s in gspecs) > 16:
+                raise ValueError("at most 16 relations per target row")
+            tarr[t].out, tarr[t].n_rows = out.data_ptr(), n_rows
+            tarr[t].g_begin, tarr[t].g_count = len(specs), len(gspecs)
+            tarr[t].flags = _lib.DG_EPI_RELU if relu else 0
+            for s in gspecs:
+                if s.n_rows != n_rows or s.n_chunks != 1 or s.chunk != s.n_rels or s.n_rels < 1:
+                    raise ValueError("fused seg groups: target rows, one chunk of all relations")
+                specs.append(s)
+        if len(targets) > _lib.DG_MAX_GROUPS:
+            raise ValueError(f"at most {_lib.DG_MAX_GROUPS} targets per launch")
+        self._garr = _seg_array(specs, d_in, d_out, False)
+        self._keep = (specs, [t[0] for t in targets])
+        self._tarr, self._ng, self._nt, self.d_in, self.d_out = tarr, len(specs), len(targets), d_in, d_out
+        self._fn = _lib.load().dg_gcn_fused_seg_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._fn(self._garr, self._ng, self._tarr, self._nt, self.d_in, self.d_out, _stream_ptr(stream)),
+              "dg_gcn_fused_seg_f32")
 
 
 @dataclass

@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (27); bumped whenever a struct layout or a signature changes. */
+/* ABI version (28); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -120,6 +120,45 @@ int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                     int64_t ldy, int32_t d, void* stream);
 
 /* --------------------------------------------------------------------------------------
+ * Fused GCN layer (T3 + T4 + T5 + T6, optionally T7 of the next layer, in one launch) for
+ * node types whose groups each fit one chunk: for every target t (a node type i), r < n_rows,
+ *
+ *     out_t[r] = act( sum_{g in [g_begin, g_begin+g_count)} l2norm( sum_k A_g,k[r]·X_g,k ) )
+ *
+ * act = relu if flags & DG_EPI_RELU.  Every group must have n_chunks == 1; `out` is ignored.
+ * One workgroup per output row, `waves_per_group` waves per group sharing the row's nonzeros
+ * (g_count * waves_per_group <= 16).
+ * Projection epilogue: for each dg_proj p with p.target == t,
+ *     p.out[rel(kk)][r][c] = sum_k out_t[r][k] * p.w[rel(kk)][k][c]   kk < p.n_rels, c < d_out
+ * (rel(kk) = p.rel_map[kk] or kk; p.w is a [K][d][d_out] stack, p.out [K][n_rows][d_out])
+ * — the next layer's H_j·W_k (layers.py:113) for the rows just produced.
+ * Replaces the per-relation SpMM + add_n + l2_normalize of layers.py:85-94 / 109-118 and the
+ * sum over edge types (+ relu) of model.py:74-75 / 85-88.
+ * -------------------------------------------------------------------------------------- */
+typedef struct dg_fused_target {
+    float* out;                 /* device, [n_rows][d] */
+    int32_t n_rows;
+    int32_t g_begin;
+    int32_t g_count;
+    int32_t flags;              /* 0 or DG_EPI_RELU */
+} dg_fused_target;
+
+typedef struct dg_proj {
+    const float* w;             /* device, [K][d][d_out] weight stack        */
+    const int32_t* rel_map;     /* device, [n_rels] or NULL                  */
+    float* out;                 /* device, [K][n_rows of target][d_out]      */
+    int32_t n_rels;
+    int32_t target;             /* index into the targets array              */
+    int32_t d_out;
+    int32_t reserved;
+} dg_proj;
+
+int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
+                     const dg_fused_target* targets /* HOST */, int32_t n_targets,
+                     const dg_proj* projs /* HOST, may be NULL */, int32_t n_projs,
+                     int32_t waves_per_group, int32_t d, void* stream);
+
+/* --------------------------------------------------------------------------------------
  * Relation-segment SpMM (partial mode; one wave per (row, relation)), optionally with the
  * next layer's projection reassociated into it — the sharded config-S form (one relation set
  * per GPU, every node type row-split), where a rank's short row block would leave
@@ -162,44 +201,21 @@ typedef struct dg_seg_group {
 int dg_spmm_seg_f32(const dg_seg_group* groups /* HOST array */, int32_t n_groups, int32_t d_in,
                     int32_t d_out, void* stream);
 
-/* --------------------------------------------------------------------------------------
- * Fused GCN layer (T3 + T4 + T5 + T6, optionally T7 of the next layer, in one launch) for
- * node types whose groups each fit one chunk: for every target t (a node type i), r < n_rows,
+/* The fused form: a whole layer for node types whose groups each fit one chunk
+ * (n_chunks == 1, chunk == n_rels >= 1) with at most 16 relations per target row in total.
+ * For every target t (dg_fused_target: out [n_rows][d_out], groups [g_begin, g_begin + g_count),
+ * flags 0 or DG_EPI_RELU; groups[i].out unused) and row r < n_rows:
  *
- *     out_t[r] = act( sum_{g in [g_begin, g_begin+g_count)} l2norm( sum_k A_g,k[r]·X_g,k ) )
+ *   out_t[r] = act( sum_g l2norm( sum_{t < n_rels_g} seg-sum_g(r, t) ) )
  *
- * act = relu if flags & DG_EPI_RELU.  Every group must have n_chunks == 1; `out` is ignored.
- * One workgroup per output row, `waves_per_group` waves per group sharing the row's nonzeros
- * (g_count * waves_per_group <= 16).
- * Projection epilogue: for each dg_proj p with p.target == t,
- *     p.out[rel(kk)][r][c] = sum_k out_t[r][k] * p.w[rel(kk)][k][c]   kk < p.n_rels, c < d_out
- * (rel(kk) = p.rel_map[kk] or kk; p.w is a [K][d][d_out] stack, p.out [K][n_rows][d_out])
- * — the next layer's H_j·W_k (layers.py:113) for the rows just produced.
- * Replaces the per-relation SpMM + add_n + l2_normalize of layers.py:85-94 / 109-118 and the
- * sum over edge types (+ relu) of model.py:74-75 / 85-88.
- * -------------------------------------------------------------------------------------- */
-typedef struct dg_fused_target {
-    float* out;                 /* device, [n_rows][d] */
-    int32_t n_rows;
-    int32_t g_begin;
-    int32_t g_count;
-    int32_t flags;              /* 0 or DG_EPI_RELU */
-} dg_fused_target;
-
-typedef struct dg_proj {
-    const float* w;             /* device, [K][d][d_out] weight stack        */
-    const int32_t* rel_map;     /* device, [n_rels] or NULL                  */
-    float* out;                 /* device, [K][n_rows of target][d_out]      */
-    int32_t n_rels;
-    int32_t target;             /* index into the targets array              */
-    int32_t d_out;
-    int32_t reserved;
-} dg_proj;
-
-int dg_gcn_fused_f32(const dg_rel_group* groups /* HOST */, int32_t n_groups,
-                     const dg_fused_target* targets /* HOST */, int32_t n_targets,
-                     const dg_proj* projs /* HOST, may be NULL */, int32_t n_projs,
-                     int32_t waves_per_group, int32_t d, void* stream);
+ * with seg-sum as dg_spmm_seg_f32's (projected by W[slab] when the groups carry w).  One
+ * workgroup per row, one wave per (group, relation); relations and groups summed in order.
+ * With w this is layer 2 (layers.py:109-118) reassociated, Σ_k (Â_k·H1_j)·W2_k, so layer 1
+ * needs no projection of its rows.  Replaces layers.py:85-94 / 109-118 and model.py:74-75,
+ * 85-88 for such node types. */
+int dg_gcn_fused_seg_f32(const dg_seg_group* groups /* HOST */, int32_t n_groups,
+                         const dg_fused_target* targets /* HOST */, int32_t n_targets, int32_t d_in,
+                         int32_t d_out, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * LDS-staged relation SpMM for groups of many relations over a narrow column space

@@ -157,6 +157,58 @@ def test_spmm_seg_chunks_and_reassociated_projection(K, chunk, form):
         assert np.all(got[:, np.all(w == 0, axis=(0, 2))] == 0)  # rows without nonzeros: exact zeros
 
 
+@pytest.mark.parametrize("form", [(32, 32, True), (64, 64, True), (64, 32, False)])
+def test_gcn_fused_seg_layer(K, form):
+    """dg_gcn_fused_seg_f32: two node types, each with two groups of one chunk holding all their
+    relations (one with an empty relation, rows without nonzeros), finished in one launch —
+    act(Σ_g l2norm(Σ_k Â_k·X_k)) (layers.py:85-94, model.py:74-75), and with weight stacks the
+    reassociated layer 2, Σ_g l2norm(Σ_k (Â_k·H_j)·W[slab_k]) (layers.py:109-118, model.py:85-88)."""
+    from decagon_amd.sparse import chunk_segments, coo_to_csr, merge_chunks, sparse_to_tuple
+
+    d_in, d_out, relu = form
+    proj = d_in != d_out
+    rng = np.random.default_rng(d_in * 7 + d_out)
+    n = {0: 61, 1: 45}
+    ets = {(0, 0): 3, (0, 1): 2, (1, 0): 1, (1, 1): 6}
+    H = {j: rng.standard_normal((n[j], 64)).astype(np.float32) for j in n}
+    outs, targets, want = {}, [], {}
+    for i in (0, 1):
+        specs, tot = [], np.zeros((n[i], d_out))
+        for (ti, j), nrel in ets.items():
+            if ti != i:
+                continue
+            mats = [_rand_csr(rng, n[i], n[j], 0.1, empty_rows=0.2) for _ in range(nrel)]
+            if nrel > 2:
+                mats[1] = sp.csr_matrix((n[i], n[j]))
+            total = nrel + 2
+            slabs = rng.permutation(total)[:nrel].astype(np.int32)
+            hs = [coo_to_csr(*sparse_to_tuple(x)) for x in mats]
+            m = merge_chunks(hs, slabs, nrel, total)
+            seg = torch.from_numpy(chunk_segments(hs, m)).cuda()
+            ssum = np.zeros((n[i], d_out))
+            if proj:
+                W = (0.2 * rng.standard_normal((total, 64, 32))).astype(np.float32)
+                x, w = torch.from_numpy(H[j]).cuda(), torch.from_numpy(W).cuda()
+                for k, a in enumerate(mats):
+                    ssum += (a @ H[j].astype(np.float64)) @ W[slabs[k]].astype(np.float64)
+            else:
+                X = rng.standard_normal((total * n[j], d_in)).astype(np.float32)
+                x, w = torch.from_numpy(X).cuda(), None
+                for k, a in enumerate(mats):
+                    ssum += a @ X[slabs[k] * n[j]:(slabs[k] + 1) * n[j]].astype(np.float64)
+            tot += ssum / np.sqrt(np.maximum((ssum ** 2).sum(1, keepdims=True), 1e-12))
+            specs.append(K.SegSpec(torch.from_numpy(m.rowptr).cuda(), seg, torch.from_numpy(m.vcol).cuda(),
+                                   torch.from_numpy(m.val).cuda(), x, None, n[i], n[j], 1, nrel, nrel,
+                                   x.stride(0), total * n[j], vcol_max=int(m.vcol.max()), w=w,
+                                   slab=torch.from_numpy(slabs).cuda(), slab_max=int(slabs.max())))
+        outs[i] = torch.full((n[i], d_out), float("nan"), device="cuda")
+        targets.append((outs[i], n[i], specs, relu))
+        want[i] = np.maximum(tot, 0) if relu else tot
+    K.PreparedFusedSeg(targets, d_in, d_out)()
+    for i in (0, 1):
+        assert rel_err(outs[i].cpu().numpy(), want[i]) <= 1e-5
+
+
 @pytest.mark.parametrize("d", [12, 64])
 def test_spmm_shared_pattern(K, d):
     """DG_GROUP_SHARED_PATTERN: one CSR (X_j's) for every chunk, chunk k over its own slab

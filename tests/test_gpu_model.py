@@ -58,7 +58,13 @@ def _setup(z, edge_order=None):
     return dg, ph, model, opt, feed
 
 
-def test_forward_matches_golden(golden_S):
+@pytest.mark.parametrize("fused_seg", [True, False])
+def test_forward_matches_golden(golden_S, monkeypatch, fused_seg):
+    """Config S's golden forward through the Session, in dg_gcn_fused_seg_f32 (layer 2
+    reassociated; the default) and in dg_gcn_fused_f32 with the projection epilogue."""
+    from decagon_amd import engine
+
+    monkeypatch.setattr(engine, "FUSED_SEG", fused_seg)
     z = golden_S
     dg, ph, model, opt, feed = _setup(z)
     sess = dg.Session()
