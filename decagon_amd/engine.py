@@ -814,7 +814,7 @@ class ForwardPlan:
         tot = sum(self.group_bytes(et, d, fused, layer) for et in ets)
         if fused:
             tot += sum(4 * d * self._out_rows(i) for i in L.fused_targets)
-            if layer == 1:
+            if layer == 1 and isinstance(launch, kernels.PreparedFused):
                 for pj in launch._keep[2]:
                     K, din, dout = pj.w.shape
                     tot += 4 * pj.n_rels * (din * dout + pj.out.shape[1] * dout)
