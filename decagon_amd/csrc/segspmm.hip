@@ -25,12 +25,23 @@
 // wave of the row writes out[c][r].  Fixed order, no atomics: bitwise reproducible.
 #include "common.h"
 
+// gathers in flight per lane (U: plain sums, UP: the reassociated form, whose W slice holds
+// 32 VGPRs), per kernel — measured at config S (rows 4-81 nonzeros per relation), the
+// occupancy they leave matters more than the round trips they save:
+//   spmm_seg (N = 8 rank share, ≈ 650 workgroups): U 8 / UP 4 → 27.1 µs a step (U 4 / UP 2 27.3,
+//   UP 8 28.4, U 16 32.7);  fused seg (N = 1, 900 workgroups): U 4 / UP 2 → 20.4 µs (8 / 4 21.4)
 #ifndef DG_SEG_U
-#define DG_SEG_U 8  // gathers in flight per lane (0: LP — a batch of 64 in one round trip)
+#define DG_SEG_U 8
 #endif
 #ifndef DG_SEG_UP
-#define DG_SEG_UP 4  // the same for the reassociated form (its W slice holds 32 VGPRs):
-#endif              // measured at S N = 8 rank 0: 8 → 4 took layer 2 from 8.0 to 6.7 µs
+#define DG_SEG_UP 4
+#endif
+#ifndef DG_FSEG_U
+#define DG_FSEG_U 4
+#endif
+#ifndef DG_FSEG_UP
+#define DG_FSEG_UP 2
+#endif
 #ifndef DG_SEG_MIN_NW
 #define DG_SEG_MIN_NW 1  // waves per workgroup, at least (else: the launch's largest chunk)
 #endif
@@ -64,50 +75,87 @@ struct SegArgs {
     int32_t nw;  // waves per workgroup
 };
 
+// Broadcast lane m of each 16-lane row to the row (DPP row_newbcast:m — VALU, no LDS).  m
+// must fold to a constant (every caller's loops are unrolled).
+template <int M>
+__device__ __forceinline__ int row_bcast(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + M, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ int row_bcast_rt(int v, int m) {
+    switch (m) {
+#define DG_RB(M) \
+    case M: return row_bcast<M>(v);
+        DG_RB(0) DG_RB(1) DG_RB(2) DG_RB(3) DG_RB(4) DG_RB(5) DG_RB(6) DG_RB(7)
+        DG_RB(8) DG_RB(9) DG_RB(10) DG_RB(11) DG_RB(12) DG_RB(13) DG_RB(14) DG_RB(15)
+#undef DG_RB
+        default: return 0;
+    }
+}
+
 // y = Σ_{p in [beg, end)} val[p] · X[vcol[p]] (X row v at xb + v·x_ld), folded: every lane
-// holds float4 (lane % LP) of the row.  A batch of 64 pairs is one coalesced load (the next
-// batch's is issued before this one's gathers) and its 64 gathers are all in flight at once:
-// LP per lane, 64/LP nonzeros side by side.
+// holds float4 (lane % LP) of the row (LP ∈ {8, 16}).  A batch of 64 pairs is one coalesced
+// load — permuted so that the pair a lane group needs at step m sits in its own 16-lane row,
+// lane m (LP 16) or lane 8·h + m (LP 8, the row's two groups h) — and handed to the groups by
+// DPP row broadcasts; UU gathers per lane in flight; the next batch's pairs are loaded before
+// this batch's gathers.
 template <int LP, int UU>
 __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, const float* __restrict__ val,
                                              const float* xb, int x_ld, int beg, int end) {
-    constexpr int G = dg::kWave / LP;
-    constexpr int U = UU ? UU : LP;  // (U·G = 64: one batch per round trip)
+    static_assert(LP == 16 || LP == 8, "seg_gather: 64- or 32-float rows");
+    constexpr int G = dg::kWave / LP;  // nonzeros side by side
+    constexpr int S = dg::kWave / G;   // steps per batch of 64
+    constexpr int U = UU ? UU : S;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const float* xq = xb + (lane % LP) * 4;
+    // lane l holds pair perm(l) of the batch (pair m·G + sub: lane 16·sub + m, or 16·(sub/2) + 8·(sub%2) + m)
+    const int perm = LP == 16 ? 4 * (lane & 15) + (lane >> 4)
+                              : 8 * (lane & 7) + 2 * (lane >> 4) + ((lane >> 3) & 1);
+    const bool odd = LP == 8 && ((lane >> 3) & 1);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int vc = 0;
     float vv = 0.f;
-    if (beg + lane < end) {
-        vc = vcol[beg + lane];
-        vv = val[beg + lane];
+    if (beg + perm < end) {
+        vc = vcol[beg + perm];
+        vv = val[beg + perm];
     }
 #pragma unroll 1
     for (int base = beg; base < end; base += 64) {
         const int n = min(64, end - base);
         const int eoff = vc * x_ld;
-        const float v = vv;
+        const int vbits = __float_as_int(vv);
         vc = 0;
         vv = 0.f;
-        if (base + 64 + lane < end) {
-            vc = vcol[base + 64 + lane];
-            vv = val[base + 64 + lane];
+        if (base + 64 + perm < end) {
+            vc = vcol[base + 64 + perm];
+            vv = val[base + 64 + perm];
         }
-#pragma unroll 1
-        for (int s0 = 0; s0 < n; s0 += U * G) {
+#pragma unroll
+        for (int it = 0; it < S / U; ++it) {
+            if (it * U * G >= n) break;  // wave-uniform
             int o[U];
             float w[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int src = (s0 + u * G + sub) & 63;
-                o[u] = __shfl(eoff, src);
-                w[u] = __shfl(v, src);
+                const int m = it * U + u;
+                int oe, we;
+                if constexpr (LP == 16) {
+                    oe = row_bcast_rt(eoff, m);
+                    we = row_bcast_rt(vbits, m);
+                } else {
+                    const int o0 = row_bcast_rt(eoff, m), o1 = row_bcast_rt(eoff, 8 + m);
+                    const int w0 = row_bcast_rt(vbits, m), w1 = row_bcast_rt(vbits, 8 + m);
+                    oe = odd ? o1 : o0;
+                    we = odd ? w1 : w0;
+                }
+                o[u] = oe;
+                w[u] = __int_as_float(we);
             }
             float4 xv[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const bool ok = s0 + u * G + sub < n;
+                const bool ok = (it * U + u) * G + sub < n;
                 xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
                 if (!ok) w[u] = 0.f;
             }
@@ -123,7 +171,7 @@ __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, c
 // One wave's share: relation t (local relation k) of chunk c in row r — its segment's sum
 // y = Σ val·X[vcol] and, with PROJ, z = y·W[slab(k)] (ybuf: the wave's 16-float4 LDS slot).
 // Returns the wave's row in the output layout (lanes < DOUT4 hold float4 lane of it).
-template <int LP, bool PROJ>
+template <int LP, bool PROJ, int U, int UP>
 __device__ __forceinline__ float4 seg_wave(const SegGroupK& g, int c, int r, int t, int k, float4* ybuf) {
     const int lane = threadIdx.x & 63;
     const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
@@ -138,7 +186,7 @@ __device__ __forceinline__ float4 seg_wave(const SegGroupK& g, int c, int r, int
         for (int i = 0; i < 8; ++i) wv[i] = *reinterpret_cast<const float4*>(W + i * 32);
         // H is shared by the relations: vcol = s·n_cols + col addresses row col
         const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;
-        const float4 y = seg_gather<16, DG_SEG_UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
+        const float4 y = seg_gather<16, UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
         if (lane < 16) ybuf[lane] = y;
         __builtin_amdgcn_wave_barrier();
         const int ms = lane >> 3;
@@ -158,7 +206,7 @@ __device__ __forceinline__ float4 seg_wave(const SegGroupK& g, int c, int r, int
         dg::add4(z, dg::shfl_xor4(z, 32));
         return z;
     } else {
-        return seg_gather<LP, DG_SEG_U>(g.vcol, g.val, g.x, g.x_ld, beg, end);
+        return seg_gather<LP, U>(g.vcol, g.val, g.x, g.x_ld, beg, end);
     }
 }
 
@@ -193,7 +241,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     const bool row_ok = slot < g.rpb && r < g.n_rows;
     const int k = c * g.chunk + t;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row_ok && k < g.n_rels) res = seg_wave<LP, PROJ>(g, c, r, t, k, ybuf[wave]);  // wave-uniform
+    if (row_ok && k < g.n_rels) res = seg_wave<LP, PROJ, DG_SEG_U, DG_SEG_UP>(g, c, r, t, k, ybuf[wave]);  // wave-uniform
     if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
     __syncthreads();
     if (row_ok && t == 0 && lane < DOUT4) {
@@ -243,7 +291,8 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 #pragma unroll 1
     while (gl < T.g_count && wave >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gl < T.g_count) res = seg_wave<LP, PROJ>(a.g[T.g_begin + gl], 0, r, wave - base, wave - base, ybuf[wave]);
+    if (gl < T.g_count) res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(a.g[T.g_begin + gl], 0, r, wave - base, wave - base,
+                                                                   ybuf[wave]);
     if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
     if (wave < T.g_count) {
