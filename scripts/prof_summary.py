@@ -168,6 +168,30 @@ def main(root):
         launch_table(os.path.join(root, f"{cfg}_trace"))
     lds_table(root)
     config_d(root)
+    rank_share(root)
+
+
+def rank_share(root):
+    """Rank 0's share of the 8-GPU step on one GPU (bench.py --simulate-world 8, the
+    collectives as no-ops): kernel-trace stats of configs S and P."""
+    for cfg in ("S8", "P8"):
+        st = stats(os.path.join(root, f"{cfg}_trace"))
+        if not st:
+            continue
+        print(f"## config {cfg[0]} at N = 8: rank 0's share on one GPU (--simulate-world 8 --simulate-rank 0)\n")
+        bj = os.path.join(root, f"{cfg}_bench.json")
+        if os.path.exists(bj):
+            try:
+                rec = json.loads(open(bj).read().strip().splitlines()[-1])
+                print(f"{rec['max_rank_ms_per_step']*1e3:.1f} us/step under the profiler\n")
+            except Exception:
+                pass
+        print("| kernel | calls | avg us | total % |")
+        print("|---|---|---|---|")
+        for r in st[:12]:
+            print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | "
+                  f"{float(r['Percentage']):.1f} |")
+        print()
 
 
 def lds_table(root):

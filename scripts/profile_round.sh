@@ -31,6 +31,13 @@ for cfg in S P; do
     python3 bench.py --train --config $cfg $steps > $out/train${cfg}_bench.json 2> $out/train${cfg}_trace.log
   echo "train $cfg trace done"
 done
+# rank 0's share of the 8-GPU step (collectives as no-ops), configs S and P
+for cfg in S P; do
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${cfg}8_trace -o run -- \
+    python3 bench.py --config $cfg --simulate-world 8 --simulate-rank 0 --steps 50 --warmup 5 \
+    > $out/${cfg}8_bench.json 2> $out/${cfg}8_trace.log
+  echo "$cfg N=8 rank 0 trace done"
+done
 # config 5 (bf16 DEDICOM scorer): kernel trace, then MFMA busy cycles against the GPU clock
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/D_trace -o run -- \
   python3 bench.py --config D --steps 50 --warmup 5 --no-cpu-baseline > $out/D_bench.json 2> $out/D_trace.log
