@@ -193,6 +193,7 @@ class DeviceGroup:
     out_chunk: int = 1             # staged: snake-bin size (a layer's output chunk is a multiple)
     layout: Optional["kernels.StagedDevice"] = None  # staged: the diagonal-major layout
     host: Optional[List[HostCSR]] = None  # the local relations (host CSR), device order
+    seg: Optional[torch.Tensor] = None    # dg_spmm_seg_f32's segment starts (sparse.chunk_segments)
 
     @property
     def n_rels(self) -> int:
