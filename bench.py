@@ -264,6 +264,11 @@ KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm
                 "PreparedSeg": "spmm_seg_kernel<{lp}, false"}
 
 
+def _kernel_label(launch, lp):
+    pat = KERNEL_NAMES.get(type(launch).__name__, "?").format(lp=lp)
+    return pat if pat.endswith(">") or pat == "spmm_staged_kernel" else pat + ", …>"
+
+
 def pmc_traffic(config, launch, d, layer=1):
     """HBM bytes per launch of `launch` from the newest committed PMC pass
     (profiles/rNN_traffic.json, written by scripts/prof_summary.py from rocprofv3 --pmc
@@ -408,7 +413,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "traffic_profiled_kernel_ms": traffic_ms,
-                     "kernel": KERNEL_NAMES.get(type(dom).__name__, "?").format(lp=lp) + " (layer 1)",
+                     "kernel": _kernel_label(dom, lp) + " (layer 1)",
                      "kernel_ms": k_ms, "algorithmic_bytes": k_bytes},
         "spmm_layer1": {"launches": [type(x).__name__ for x in l1], "ms": l1_ms,
                         "algorithmic_bytes": l1_bytes, "GB_s": l1_bytes / (l1_ms * 1e-3) / 1e9,
