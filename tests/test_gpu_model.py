@@ -276,8 +276,14 @@ def test_full_size_config_P_matches_oracle():
     h1, emb = orc.decagon_forward_csr(g.edge_types, csr, {et: w.astype(np.float64) for et, w in w1.items()},
                                       {et: w.astype(np.float64) for et, w in w2.items()})
     for t in (0, 1):
-        assert rel_err(plan.hidden1[t].cpu().numpy(), h1[t]) <= TOL
-        assert rel_err(plan.embeddings[t].cpu().numpy(), emb[t]) <= TOL
+        got_h1, got_e = plan.hidden1[t].cpu().numpy(), plan.embeddings[t].cpu().numpy()
+        assert rel_err(got_h1, h1[t]) <= TOL
+        assert rel_err(got_e, emb[t]) <= TOL
+        # SURVEY §8c's elementwise pass-rate: |y − y_ref| <= 1e-4·|y_ref| + 1e-6, every element
+        # (23 M-nonzero fp32 sums against float64: a few near-zero elements may miss the floor)
+        for got_, want_ in ((got_h1, h1[t]), (got_e, emb[t])):
+            ok = np.abs(got_ - want_) <= 1e-4 * np.abs(want_) + 1e-6
+            assert ok.mean() >= 0.9999, (t, ok.mean())
 
 
 def test_training_sums_mode_matches_oracle(monkeypatch):
