@@ -151,6 +151,10 @@ def _check(kind, world, h2=32):
             for t in (0, 1):
                 assert rel_err(form[0][t], h1[t]) <= TOL, (r, "hidden1", t)
                 assert rel_err(form[1][t], emb[t]) <= TOL, (r, "embeddings", t)
+        for t in (0, 1):  # SURVEY §8c's elementwise pass-rate, |y − y_ref| <= 1e-4·|y_ref| + 1e-6
+            for got_, want_ in ((eager[0][t], h1[t]), (eager[1][t], emb[t])):
+                ok = np.abs(got_ - want_) <= 1e-4 * np.abs(want_) + 1e-6
+                assert ok.mean() >= 0.9999, (r, t, ok.mean())
         for t in (0, 1):  # the graph-captured phases reproduce the eager forward bit for bit
             assert np.array_equal(eager[0][t], graphed[0][t]) and np.array_equal(eager[1][t], graphed[1][t])
     # every relation of a relation-sharded group is owned by exactly one rank; a row-split
