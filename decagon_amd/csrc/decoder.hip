@@ -54,10 +54,20 @@ __global__ __launch_bounds__(256) void decoder_score_kernel(const DecArgs a) {
 //   pos[b] = score(rows[b], cols[b]),  neg[b] = score(neg_row[b], cols[b]),
 //   loss   = sum_b relu(neg[b] - (pos[b] - margin))
 // One workgroup of two waves per 32 pairs (wave 0 the positive tile, wave 1 the negative
-// tile).  Each workgroup folds its 32 hinge terms, publishes the partial (a write-through sc1
-// store, drained) and takes a ticket; the last one reads every partial with sc1 loads
-// (cdna_hip_programming.md Guideline 16; no L2 write-back or invalidate), adds them in block
-// order and resets the ticket counter — fixed order, no float atomics, one launch.
+// tile).  Each workgroup folds its 32 hinge terms into a partial, and the partials meet in one
+// launch without float atomics:
+//  - PACKED (at most 255 workgroups): one returning 64-bit atomic add per workgroup on a word
+//    that holds the arrival count (bits 56-63), the count of partials outside the fixed-point
+//    range (48-55) and the sum of the others as fixed point, 2^-32 units (0-47: a partial below
+//    256 is < 2^40, 255 of them < 2^48).  Integer sums do not depend on the order, so the result
+//    is bitwise reproducible; the workgroup that sees count = grid − 1 has the whole sum in
+//    hand (no partial store, drain or read-back).  A partial ≥ 256 (or NaN / inf) is stored
+//    write-through, drained and counted in bits 48-55 instead; the last workgroup then adds those
+//    in block order (they are rare: the others' stores are never read).
+//  - otherwise: each workgroup publishes its partial (a write-through sc1 store, drained) and
+//    takes a ticket; the last one reads every partial with sc1 loads (cdna_hip_programming.md
+//    Guideline 16; no L2 write-back or invalidate) and adds them in block order.
+// The last workgroup resets what it used for the next launch.
 struct HingeArgs {
     DecTab t;
     const int32_t* rows;
@@ -70,6 +80,7 @@ struct HingeArgs {
     float* loss;        // [1]
     float* partial;     // [gridDim.x]
     uint32_t* ticket;   // zero before the first launch; the last block resets it
+    unsigned long long* word;  // PACKED: count | out-of-range count | fixed-point sum (zero between launches)
     uint64_t seed;
     uint64_t offset;
     int32_t range;
@@ -81,10 +92,12 @@ struct HingeArgs {
 #define DG_DEC_ABL 0  // timing ablations only (wrong results): 1 no ticket, 2 no draw, 4 no scores, 8 empty
 #endif
 
+template <bool PACKED>
 __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
     __shared__ float sc[2][32];
     __shared__ float red[128];
     __shared__ int last;
+    __shared__ unsigned long long total;
     if (DG_DEC_ABL & 8) return;
     const int lane = threadIdx.x & 63;
     const int side = threadIdx.x >> 6;  // 0: positives, 1: negatives
@@ -131,6 +144,19 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
         if (lane == 0 && (DG_DEC_ABL & 1)) {
             a.partial[blockIdx.x] = term;
             last = 0;
+        } else if (lane == 0 && PACKED) {
+            unsigned long long add = 1ull << 56;
+            if (term < 256.0f) {  // (false for NaN and inf too)
+                add += static_cast<unsigned long long>(static_cast<double>(term) * 4294967296.0);
+            } else {
+                __hip_atomic_store(a.partial + blockIdx.x, term, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                add += 1ull << 48;
+            }
+            const unsigned long long old =
+                __hip_atomic_fetch_add(a.word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = (old >> 56) == gridDim.x - 1 ? 1 : 0;
+            total = old + add;
         } else if (lane == 0) {
             // hand-off without L2 write-back / invalidate (MI355X_MICROARCH.md "Valid forms",
             // first row): the partial is stored write-through (sc1) and drained before the
@@ -143,6 +169,23 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
     }
     __syncthreads();
     if (!last) return;  // block-uniform
+    if constexpr (PACKED) {
+        if (threadIdx.x == 0) {
+            double s = static_cast<double>(total & ((1ull << 48) - 1)) * (1.0 / 4294967296.0);
+            if ((total >> 48) & 0xFF) {  // partials outside the fixed-point range, in block order
+                for (int k = 0; k < (int)gridDim.x; ++k) {
+                    const float v = __hip_atomic_load(a.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (v != 0.f) {
+                        s += static_cast<double>(v);
+                        __hip_atomic_store(a.partial + k, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+            a.loss[0] = static_cast<float>(s);
+            __hip_atomic_store(a.word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     float s = 0.f;
     for (int k = threadIdx.x; k < (int)gridDim.x; k += 128)
         s += __hip_atomic_load(a.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -153,7 +196,8 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
         if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
+    for (int k = threadIdx.x; k < (int)gridDim.x; k += 128) a.partial[k] = 0.f;  // (read above; the PACKED
+    if (threadIdx.x == 0) {                                                      //  form reads zeros there)
         a.loss[0] = red[0];
         atomicExch(a.ticket, 0u);
     }
@@ -318,6 +362,12 @@ extern "C" int dg_unigram_sample_slots(const uint32_t* alias_table, int32_t rang
     return dg::launch_status();
 }
 
+// DG_DEC_TICKET=1: the ticket hand-off at any size (A/B and tests of both forms)
+static bool getenv_ticket() {
+    static const bool t = [] { const char* e = getenv("DG_DEC_TICKET"); return e && e[0] == '1'; }();
+    return t;
+}
+
 extern "C" int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
                                     int64_t ld_col, const int32_t* rows, const int32_t* cols,
                                     const int32_t* neg_rows, const uint32_t* alias_table,
@@ -344,13 +394,18 @@ extern "C" int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, cons
     a.neg_rows_out = neg_rows_out;
     a.loss = loss;
     a.ticket = reinterpret_cast<uint32_t*>(workspace);
+    a.word = reinterpret_cast<unsigned long long*>(workspace) + 1;
     a.partial = reinterpret_cast<float*>(workspace) + 4;
     a.seed = seed;
     a.offset = offset;
     a.range = range;
     a.n = n;
     a.margin = margin;
-    hipLaunchKernelGGL(decoder_hinge_kernel, dim3(blocks), dim3(128), 0,
-                       reinterpret_cast<hipStream_t>(stream), a);
+    if (blocks <= 255 && !(DG_DEC_ABL & 1) && !getenv_ticket())
+        hipLaunchKernelGGL(decoder_hinge_kernel<true>, dim3(blocks), dim3(128), 0,
+                           reinterpret_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(decoder_hinge_kernel<false>, dim3(blocks), dim3(128), 0,
+                           reinterpret_cast<hipStream_t>(stream), a);
     return dg::launch_status();
 }

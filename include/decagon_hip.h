@@ -446,8 +446,10 @@ int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, cons
  *                if non-NULL;
  *   pos[b] = score(rows[b], cols[b]);  neg[b] = score(neg_row[b], cols[b])   (as above)
  *   loss[0] = sum_b relu(neg[b] - (pos[b] - margin))   (fixed block order)
- * workspace: device, 16-byte aligned, 16 + 4*ceil(n/32) bytes, its first word zero before
- * the first call (the kernel leaves it zero again).  n >= 1.
+ * workspace: device, 16-byte aligned, 16 + 4*ceil(n/32) bytes, all zero before the first
+ * call (the kernel leaves it so).  n >= 1.  The partial sums of the 32-pair blocks meet in one
+ * returning 64-bit integer atomic per block (fixed point, 2^-32 units; order-free, so bitwise
+ * reproducible) when there are at most 255 blocks, else through a ticket and block-order reads.
  * Replaces optimizer.py:37-57 (sampler, gathers, pos/neg scores) + :116-120 (hinge). */
 int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
                          int64_t ld_col, const int32_t* rows, const int32_t* cols,

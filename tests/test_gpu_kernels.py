@@ -537,13 +537,15 @@ def test_shape_checks_fail_before_launch(K):
                        vcol_max=int(cl.max())).validate(32)
 
 
-@pytest.mark.parametrize("n", [512, 100, 1300])
-def test_decoder_hinge_fused(K, n):
+@pytest.mark.parametrize("n,scale", [(512, 1), (100, 1), (1300, 1), (9000, 1), (512, 40), (9000, 40)])
+def test_decoder_hinge_fused(K, n, scale):
     """dg_decoder_hinge_f32: sampled negatives are exactly dg_unigram_sample's draws, both
-    score vectors match the oracle, the loss is the hinge of optimizer.py:116-120."""
-    rng = np.random.default_rng(n)
+    score vectors match the oracle, the loss is the hinge of optimizer.py:116-120 — through the
+    packed fixed-point atomic (≤ 255 blocks), with block partials ≥ 256 (scale 40: the
+    write-through fallback inside it), and through the ticket (9,000 pairs: 282 blocks)."""
+    rng = np.random.default_rng(n + scale)
     d, n_r, n_c = 32, 400, 300
-    U = rng.standard_normal((n_r, d)).astype(np.float32)
+    U = (scale * rng.standard_normal((n_r, d))).astype(np.float32)
     V = rng.standard_normal((n_c, d)).astype(np.float32)
     G = (rng.standard_normal((d, d)) / 6).astype(np.float32)
     l = rng.standard_normal(d).astype(np.float32)
@@ -569,6 +571,14 @@ def test_decoder_hinge_fused(K, n):
     assert rel_err(op.neg.cpu().numpy(), neg) <= 1e-5
     want = orc.hinge_loss(pos, neg, 0.1)
     assert abs(float(op.loss[0]) - want) <= 1e-4 * abs(want)
+    # the hand-off itself, on the device's own scores: the float64 sum within fp32 rounding,
+    # the same bits on every launch
+    own = orc.hinge_loss(op.pos.cpu().numpy().astype(np.float64), op.neg.cpu().numpy().astype(np.float64), 0.1)
+    first = float(op.loss[0])
+    assert abs(first - own) <= 1e-6 * abs(own)
+    for _ in range(2):
+        op()
+        assert float(op.loss[0]) == first
     # given negatives
     op2 = K.PreparedDecoderHinge(dv(U), dv(V), dv(rows), dv(cols), dv(G), dv(l), 0.1, neg_rows=dv(negs))
     op2()
