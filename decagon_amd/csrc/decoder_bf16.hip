@@ -30,6 +30,10 @@ typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+#ifndef DG_DEC_CS_THREADS
+#define DG_DEC_CS_THREADS 768  // column-shared paired kernel: threads per workgroup (one per CU)
+#endif
+
 struct Bf16DecArgs {
     const uint16_t* row_table;
     const uint16_t* col_table;
@@ -282,6 +286,114 @@ __global__ __launch_bounds__(512) void decoder_bf16_paired_kernel(const Bf16DecA
         }
     }
 }
+
+// Column-shared form of the paired layout: a positive (u_p, v) and its negative (u_n, v) share
+// v and D_k, so uᵀ·D_k·R·D_k·v = (u ∘ D_k)ᵀ · T with T = R·(D_k ∘ v) computed ONCE for both:
+//     T[i][p] = Σ_n R[i][n] · bf16(D_k[n] v_n)      on v_mfma_f32_32x32x16_bf16
+// (A = R rows from LDS, B = the pairs' scaled v rows, built once per tile), then
+//     pos[p] = Σ_i u_p[i] D_k[i] T[i][p],   neg[p] = Σ_i u_n[i] D_k[i] T[i][p]
+// in the epilogue (fp32; a product of two bf16 values is exact in fp32) — half the MFMAs of
+// the row-side form above, one accumulator chain, and 64 B-operand VGPRs instead of 128, so
+// more waves per SIMD hide the row gathers.  The A rows are permuted as above: lane half h
+// owns the 16 contiguous i = 32t + 16h + [0, 16) of column tile t (32-byte runs of u_p, u_n
+// and D_k).  The bf16 operand rounding sits on D_k∘v instead of u∘D_k: the scores agree with
+// the row-side kernels to bf16 operand rounding, not bitwise.
+template <int D, bool HAS_L, int THREADS>
+__global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const Bf16DecArgs a) {
+    constexpr int KS = D / 16;
+    constexpr int NT = D / 32;
+    constexpr int SL = D / 8;
+    extern __shared__ uint4 rs[];  // R: row i, slot q (n = 8q .. 8q+7) at rs[i*SL + (q ^ (i % SL))]
+    const int tid = threadIdx.x;
+    for (int e = tid; e < D * SL; e += THREADS) {
+        const int i = e / SL, q = e - i * SL;
+        rs[i * SL + (q ^ (i % SL))] = *reinterpret_cast<const uint4*>(a.R + (int64_t)i * D + 8 * q);
+    }
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int r = lane & 31;
+    const int h = lane >> 5;
+    const int nh = a.n_pairs;  // pairs per half
+    const int n_tiles = (nh + 31) / 32;
+    const int stride = gridDim.x * (THREADS / 64);
+    const uint4 ones = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
+#pragma unroll 1
+    for (int tile = blockIdx.x * (THREADS / 64) + wave; tile < n_tiles; tile += stride) {
+        const int p = tile * 32 + r;
+        const bool valid = p < nh;
+        const int prp = valid ? a.rows[p] : 0;
+        const int prn = valid ? a.rows[nh + p] : 0;
+        const int pc = valid ? a.cols[p] : 0;
+        const int pk = (valid && a.rel) ? a.rel[p] : 0;
+        const uint16_t* up = a.row_table + (int64_t)prp * a.ld_row;
+        const uint16_t* un = a.row_table + (int64_t)prn * a.ld_row;
+        const uint16_t* v = a.col_table + (int64_t)pc * a.ld_col;
+        const uint16_t* lk = HAS_L ? a.L + (int64_t)pk * D : nullptr;
+        // B operand: bf16(D_k ∘ v)[16s + 8h + j], s < KS
+        bf16x8 b[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const uint4 vv = *reinterpret_cast<const uint4*>(v + 16 * s + 8 * h);
+            const uint4 ll = HAS_L ? *reinterpret_cast<const uint4*>(lk + 16 * s + 8 * h) : ones;
+            const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w}, lw[4] = {ll.x, ll.y, ll.z, ll.w};
+            bf16v8 x;  // round-to-nearest-even by the cast (v_cvt_pk_bf16_f32)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                x[2 * j] = (__bf16)(bf_lo(vw[j]) * bf_lo(lw[j]));
+                x[2 * j + 1] = (__bf16)(bf_hi(vw[j]) * bf_hi(lw[j]));
+            }
+            b[s] = valid ? __builtin_bit_cast(bf16x8, x) : bf16x8{};
+        }
+        float partp = 0.f, partn = 0.f;
+#pragma unroll 1
+        for (int t = 0; t < NT; ++t) {
+            // lane half h owns i = 32t + 16h + [0, 16): register j of the accumulator.  The
+            // epilogue's row runs are issued before the MFMAs (their latency hides behind them).
+            const int ib0 = 32 * t + 16 * h;
+            uint4 ep[2], en[2], el[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                ep[k] = *reinterpret_cast<const uint4*>(up + ib0 + 8 * k);
+                en[k] = *reinterpret_cast<const uint4*>(un + ib0 + 8 * k);
+            }
+            // A row m = r holds C row m = (j&3) + 8(j>>2) + 4h' of register j, lane half h'
+            const int ia = 32 * t + 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
+            f32x16 acc = {};
+            uint4 wa = rs[ia * SL + (h ^ (ia % SL))];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                uint4 xa = wa;
+                if (s + 1 < KS) xa = rs[ia * SL + ((2 * (s + 1) + h) ^ (ia % SL))];
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa), b[s], acc, 0, 0, 0);
+                wa = xa;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) el[k] = HAS_L ? *reinterpret_cast<const uint4*>(lk + ib0 + 8 * k) : ones;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t pw[4] = {ep[k].x, ep[k].y, ep[k].z, ep[k].w},
+                               nw[4] = {en[k].x, en[k].y, en[k].z, en[k].w},
+                               lw[4] = {el[k].x, el[k].y, el[k].z, el[k].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float l0 = bf_lo(lw[j]), l1 = bf_hi(lw[j]);
+                    partp = fmaf(acc[8 * k + 2 * j], bf_lo(pw[j]) * l0, partp);
+                    partp = fmaf(acc[8 * k + 2 * j + 1], bf_hi(pw[j]) * l1, partp);
+                    partn = fmaf(acc[8 * k + 2 * j], bf_lo(nw[j]) * l0, partn);
+                    partn = fmaf(acc[8 * k + 2 * j + 1], bf_hi(nw[j]) * l1, partn);
+                }
+            }
+        }
+        partp += __shfl_xor(partp, 32);
+        partn += __shfl_xor(partn, 32);
+        if (h == 0 && valid) {
+            a.out[p] = partp;
+            a.out[nh + p] = partn;
+        }
+    }
+}
 }  // namespace
 
 extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
@@ -330,15 +442,28 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
     if (n_half == 0) return DG_OK;
     Bf16DecArgs a{row_table, col_table, G, l_table, row_idx, col_idx, rel_idx, out, ld_row, ld_col, n_half, d};
     const int n_tiles = (n_half + 31) / 32;
-    int blocks = (n_tiles + 7) / 8;
-    if (blocks > 256) blocks = 256;  // persistent: one Rᵀ-holding workgroup per CU
     const int lds = d * d * 2;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#ifdef DG_DEC_ROWSIDE  // A/B builds: the row-side paired kernel (two MFMA chains per tile)
+    constexpr int kThreads = 512;
     static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
     dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_paired_kernel<256, true>), 160 * 1024, configured_l);
     dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_paired_kernel<256, false>), 160 * 1024, configured_nl);
 #define DG_DEC_LAUNCH(DD, HL) \
-    hipLaunchKernelGGL((decoder_bf16_paired_kernel<DD, HL>), dim3(blocks), dim3(512), lds, st, a)
+    hipLaunchKernelGGL((decoder_bf16_paired_kernel<DD, HL>), dim3(blocks), dim3(kThreads), lds, st, a)
+#else
+    if (!dg::aligned16(G)) return DG_EALIGN;  // R rows are staged into LDS in 16-byte pieces
+    constexpr int kThreads = DG_DEC_CS_THREADS;
+    static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
+    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, true, kThreads>), 160 * 1024,
+                  configured_l);
+    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, false, kThreads>), 160 * 1024,
+                  configured_nl);
+#define DG_DEC_LAUNCH(DD, HL) \
+    hipLaunchKernelGGL((decoder_bf16_colshared_kernel<DD, HL, kThreads>), dim3(blocks), dim3(kThreads), lds, st, a)
+#endif
+    int blocks = (n_tiles + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks > 256) blocks = 256;  // persistent: one R-holding workgroup per CU
     const bool hl = l_table != nullptr;
     if (d == 256) {
         if (hl) DG_DEC_LAUNCH(256, true); else DG_DEC_LAUNCH(256, false);

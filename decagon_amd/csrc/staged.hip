@@ -65,11 +65,13 @@ struct StagedGroupK {
     int32_t n_blocks;
     int32_t pad;
     // PROJ form: the slab of relation k is H · W[slab(k)] (H [n_cols][64], W [K][64][d]),
-    // computed in the workgroup on the fp32 MFMA instead of read from x
+    // computed in the workgroup on the MFMA instead of read from x: fp32 (PROJ 1) or, with hs,
+    // three bf16 products (PROJ 2)
     const float* h;
     const float* w;
+    const uint16_t* hs;  // H split into bf16 hi | lo rows ([n_cols][hs_ld], hi at 0..63, lo at 64..127)
     int32_t h_ld;
-    int32_t pad2;
+    int32_t hs_ld;
 };
 
 struct StagedArgs {
@@ -121,8 +123,22 @@ __device__ __forceinline__ void fold_step(float4 (&part)[4], int gsz) {
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 
-template <bool PROJ>
+// x = hi + lo to ≈ 2^-17 relative: hi = bf16(x) (nearest even), lo = bf16(x - hi)
+__device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+    bf16v8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        h[j] = (__bf16)x[j];
+        l[j] = (__bf16)(x[j] - (float)h[j]);
+    }
+    hi = __builtin_bit_cast(bf16x8, h);
+    lo = __builtin_bit_cast(bf16x8, l);
+}
+
+template <int PROJ>
 __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedArgs a) {
     extern __shared__ float4 lds[];
     const int tid = threadIdx.x;
@@ -203,7 +219,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
             if (q < n5) glds16(xk, off * 4, dst + q0 * 16);
         }
     };
-    // PROJ: relation i's slab slice computed on the fp32 MFMA — slabᵀ[n][v] = Σ_k W[k][col0 + n]
+    // PROJ 1: relation i's slab slice computed on the fp32 MFMA — slabᵀ[n][v] = Σ_k W[k][col0 + n]
     // H[v][k] on v_mfma_f32_16x16x4_f32 (A = W slice: lane l holds W[16q + m][col0 + (l & 15)],
     // q = l >> 4, for MFMA m; B = Hᵀ: H[v][16q + m] for its tile's row v = 16t + (l & 15); the
     // contraction order k = 16q + m is free), so lane l ends with slab[v][col0 + 4q .. +3] —
@@ -215,6 +231,41 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         const float* w = g.w + ((int64_t)sl * 64 + 16 * pq) * d + min(col0 + pn, d - 1);
 #pragma unroll
         for (int m = 0; m < 16; ++m) wa[m] = w[m * d];
+    };
+    // PROJ 2: the same slab from three bf16 products on v_mfma_f32_16x16x32_bf16,
+    //     W·H ≈ W_hi·H_hi + W_hi·H_lo + W_lo·H_hi      (each operand x = x_hi + x_lo, |x_lo| ≤ 2^-9 |x|;
+    // the dropped W_lo·H_lo and the rounding of the lo parts leave ≈ 2^-17 relative per product)
+    // at 16 cycles per MFMA instead of 16 × 32 for the fp32 form.  Lane l holds A = W[32kh +
+    // 8pq + j][col0 + pn] (k-half kh, j < 8; split per relation) and B = H[v][32kh + 8pq + j] from
+    // hs (split once per layer by dg_split_bf16x2_f32); C lands as in PROJ 1.
+    auto load_w2 = [&](int i, float (&wa)[16]) {
+        const int sl = __builtin_amdgcn_readfirstlane(slb[i]);
+        const float* w = g.w + ((int64_t)sl * 64 + 8 * pq) * d + min(col0 + pn, d - 1);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wa[8 * kh + j] = w[(32 * kh + j) * d];
+    };
+    auto slab_make2 = [&](int i, const float (&wa)[16]) {
+        float4* buf = xs0 + (i & 1) * a.xs_f4;
+        bf16x8 whi[2], wlo[2];
+        split_bf16(*reinterpret_cast<const float(*)[8]>(&wa[0]), whi[0], wlo[0]);
+        split_bf16(*reinterpret_cast<const float(*)[8]>(&wa[8]), whi[1], wlo[1]);
+        const int n_tiles = (n_cols + 15) >> 4;
+#pragma unroll 1
+        for (int t = wave; t < n_tiles; t += kMaxThreads / 64) {
+            const int v = 16 * t + pn;
+            const uint4* hp = reinterpret_cast<const uint4*>(g.hs + (int64_t)min(v, n_cols - 1) * g.hs_ld + 8 * pq);
+            const uint4 bh0 = hp[0], bh1 = hp[4], bl0 = hp[8], bl1 = hp[12];
+            f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[0], __builtin_bit_cast(bf16x8, bl0), lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[0], __builtin_bit_cast(bf16x8, bh0), hi, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[1], __builtin_bit_cast(bf16x8, bl1), lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[1], __builtin_bit_cast(bf16x8, bh1), hi, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[0], __builtin_bit_cast(bf16x8, bh0), lo, 0, 0, 0);
+            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[1], __builtin_bit_cast(bf16x8, bh1), lo, 0, 0, 0);
+            if (v < n_cols) buf[v * 5 + pq] = make_float4(hi[0] + lo[0], hi[1] + lo[1], hi[2] + lo[2], hi[3] + lo[3]);
+        }
     };
     // one 16-row tile at a time (measured: two tiles with interleaved accumulators made the
     // layer-2 launch 10 us slower — their MFMAs then crowd the gathers of the SIMD's other waves)
@@ -280,7 +331,11 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     };
 
     float wa[16];  // PROJ: the W slice of the next slab to make
-    if constexpr (PROJ) {
+    if constexpr (PROJ == 2) {
+        load_w2(0, wa);
+        slab_make2(0, wa);
+        if (nk > 1) load_w2(1, wa);
+    } else if constexpr (PROJ == 1) {
         load_w(0, wa);
         slab_make(0, wa);
         if (nk > 1) load_w(1, wa);
@@ -312,7 +367,12 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         // relation i-1's sums (deferred past the barrier: they cover un's latency)
         if (prlw > 0) accumulate(part, pvi, __builtin_amdgcn_readfirstlane(pbig));
         DG_TICK(c_acc);
-        if constexpr (PROJ) {
+        if constexpr (PROJ == 2) {
+            if (i + 1 < nk) {  // the other buffer: last read by relation i-1
+                slab_make2(i + 1, wa);
+                if (i + 2 < nk) load_w2(i + 2, wa);
+            }
+        } else if constexpr (PROJ == 1) {
             if (i + 1 < nk) {  // the other buffer: last read by relation i-1
                 slab_make(i + 1, wa);
                 if (i + 2 < nk) load_w(i + 2, wa);
@@ -430,6 +490,11 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
             if (!pj.h || !pj.w || pj.din != 64 || pj.h_ld < 64) return DG_EINVAL;
             if (!dg::aligned16(pj.h) || (pj.h_ld & 3)) return DG_EALIGN;
             if ((int64_t)s.n_cols * pj.h_ld > 0x7fffffffLL) return DG_EINVAL;
+            if ((pj.hs != nullptr) != (projs[0].hs != nullptr)) return DG_EINVAL;  // one form per launch
+            if (pj.hs) {
+                if (pj.hs_ld < 128 || (pj.hs_ld & 7) || !dg::aligned16(pj.hs)) return DG_EALIGN;
+                if ((int64_t)s.n_cols * pj.hs_ld > 0x7fffffffLL) return DG_EINVAL;
+            }
         } else {
             if (!s.x) return DG_EINVAL;
             if (!dg::aligned16(s.x) || (s.x_ld & 3) || s.x_ld < d) return DG_EALIGN;
@@ -440,6 +505,8 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
             k.h = projs[i].h;
             k.w = projs[i].w;
             k.h_ld = static_cast<int32_t>(projs[i].h_ld);
+            k.hs = projs[i].hs;
+            k.hs_ld = static_cast<int32_t>(projs[i].hs_ld);
         }
         k.pairs = reinterpret_cast<const int2*>(s.pairs);
         k.jm = s.jm;
@@ -497,15 +564,20 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
     }
 #endif
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (projs) {
+    if (projs && projs[0].hs) {
         static std::atomic<uint64_t> configured{0};
-        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<true>), kLdsBytes, configured);
-        hipLaunchKernelGGL(spmm_staged_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<2>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<2>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+                           static_cast<int>(lds), st, a);
+    } else if (projs) {
+        static std::atomic<uint64_t> configured{0};
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<1>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<1>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
                            static_cast<int>(lds), st, a);
     } else {
         static std::atomic<uint64_t> configured{0};
-        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<false>), kLdsBytes, configured);
-        hipLaunchKernelGGL(spmm_staged_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<0>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<0>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
                            static_cast<int>(lds), st, a);
     }
     return dg::launch_status();
@@ -521,4 +593,33 @@ extern "C" int dg_spmm_staged_proj_f32(const dg_staged_group* groups, const dg_s
                                        int32_t n_groups, int32_t d, void* stream) {
     if (!projs) return DG_EINVAL;
     return staged_launch(groups, projs, n_groups, d, stream);
+}
+
+namespace {
+// out row r = [bf16 hi of x[r][0..cols) | bf16 lo of x[r][0..cols)], x = hi + lo (split_bf16)
+__global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restrict__ x, int64_t ld, int32_t rows,
+                                                           int32_t cols, uint16_t* __restrict__ out, int64_t out_ld) {
+    const int per = cols >> 3;  // 8-column pieces per row
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)rows * per) return;
+    const int r = (int)(e / per), c = (int)(e - (int64_t)r * per) * 8;
+    const float4* xp = reinterpret_cast<const float4*>(x + r * ld + c);
+    const float4 x0 = xp[0], x1 = xp[1];
+    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    bf16x8 hi, lo;
+    split_bf16(v, hi, lo);
+    *reinterpret_cast<bf16x8*>(out + r * out_ld + c) = hi;
+    *reinterpret_cast<bf16x8*>(out + r * out_ld + cols + c) = lo;
+}
+}  // namespace
+
+extern "C" int dg_split_bf16x2_f32(const float* x, int64_t ld, int32_t rows, int32_t cols, uint16_t* out,
+                                   int64_t out_ld, void* stream) {
+    if (!x || !out || rows < 0 || cols <= 0 || (cols & 7) || ld < cols || out_ld < 2 * cols) return DG_EINVAL;
+    if (!dg::aligned16(x) || !dg::aligned16(out) || (ld & 3) || (out_ld & 7)) return DG_EALIGN;
+    if (rows == 0) return DG_OK;
+    const int64_t n = (int64_t)rows * (cols >> 3);
+    hipLaunchKernelGGL(split_bf16x2_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), x, ld, rows, cols, out, out_ld);
+    return dg::launch_status();
 }

@@ -452,9 +452,10 @@ class StagedSpec:
     x_ld: int
     x_rows: int
     slab_max: int = -1            # host-known max(slab) (or n_rels-1 without slab), for checks
-    # (H [n_cols][64], W [K][64][d]): relation k's operand is H·W[slab(k)], made in the kernel
-    # (dg_spmm_staged_proj_f32); x / x_ld / x_rows are then unused
-    proj: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+    # (H [n_cols][64], W [K][64][d]) or (H, W, Hs): relation k's operand is H·W[slab(k)], made in
+    # the kernel (dg_spmm_staged_proj_f32) — from Hs = split_bf16x2(H) (int16 [n_cols][128]) on
+    # the bf16 MFMA when given, else on the fp32 MFMA; x / x_ld / x_rows are then unused
+    proj: Optional[Tuple[torch.Tensor, ...]] = None
 
     def validate(self, d: int) -> None:
         L = self.layout
@@ -479,7 +480,13 @@ class StagedSpec:
                 raise ValueError("slab shorter than n_rels")
         smax = self.slab_max if self.slab_max >= 0 else L.n_rels - 1
         if self.proj is not None:
-            h, w = self.proj
+            h, w = self.proj[:2]
+            hs = self.proj[2] if len(self.proj) > 2 else None
+            if hs is not None:
+                _dev(hs, torch.int16, "proj hs")
+                if hs.dim() != 2 or hs.shape[0] < L.n_cols or hs.shape[1] < 128 or hs.stride(1) != 1 \
+                        or hs.stride(0) % 8 or hs.data_ptr() % 16:
+                    raise ValueError("proj hs must be [n_cols][>=128] int16, rows 16-byte aligned")
             if not (isinstance(h, torch.Tensor) and h.is_cuda and h.dtype == torch.float32):
                 raise ValueError("proj h: float32 device tensor required (rows may be padded)")
             _dev(w, torch.float32, "proj w")
@@ -515,8 +522,13 @@ class PreparedStaged:
             g.slab = s.slab.data_ptr() if s.slab is not None else None
             g.x = s.x.data_ptr() if s.x is not None else None
             if proj:
-                h, w = s.proj
+                h, w = s.proj[:2]
                 parr[i].h, parr[i].w, parr[i].h_ld, parr[i].din = h.data_ptr(), w.data_ptr(), h.stride(0), 64
+                hs = s.proj[2] if len(s.proj) > 2 else None
+                if (hs is None) != (len(specs[0].proj) < 3 or specs[0].proj[2] is None):
+                    raise ValueError("a staged launch's projected groups all carry Hs or none")
+                if hs is not None:
+                    parr[i].hs, parr[i].hs_ld = hs.data_ptr(), hs.stride(0)
             g.out = s.out.data_ptr()
             g.x_ld = s.x_ld
             g.n_rows, g.n_cols, g.n_rels = L.n_rows, L.n_cols, L.n_rels
@@ -531,6 +543,24 @@ class PreparedStaged:
             check(self._fn(self._arr, self._parr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_proj_f32")
         else:
             check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_f32")
+
+
+def split_bf16x2(x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """dg_split_bf16x2_f32: out[r] = [bf16 hi of x[r] | bf16 lo of x[r]] (int16 bit patterns),
+    x = hi + lo to ≈ 2^-17 relative — the H operand of the staged kernel's bf16 slab form."""
+    if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2):
+        raise ValueError("x: 2-d float32 device tensor required")
+    rows, cols = x.shape
+    if cols % 8 or x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+        raise ValueError("x needs a multiple of 8 contiguous columns, rows 16-byte aligned")
+    if out is None:
+        out = torch.empty((rows, 2 * cols), dtype=torch.int16, device=x.device)
+    _dev(out, torch.int16, "out")
+    if out.dim() != 2 or out.shape[0] < rows or out.shape[1] < 2 * cols or out.stride(1) != 1 or out.stride(0) % 8:
+        raise ValueError("out must be [rows][>= 2·cols] int16, rows 16-byte aligned")
+    check(_lib.load().dg_split_bf16x2_f32(x.data_ptr(), x.stride(0), rows, cols, out.data_ptr(), out.stride(0),
+                                          _stream_ptr(stream)), "dg_split_bf16x2_f32")
+    return out
 
 
 def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:
@@ -807,8 +837,9 @@ def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: t
     """bf16 DEDICOM scores of pairs (rows[p], cols[p]) of relations rel[p] (dg_decoder_score_bf16):
     uᵀ·D_k·G·D_k·v with bf16 tables / G / diagonals and fp32 accumulation (config 5).
     paired: the caller promises pair p and pair p + n/2 share the column and the relation (a
-    positive and its negative); dg_decoder_score_bf16_paired scores them together, reading cols
-    and rel of the first half only."""
+    positive and its negative); dg_decoder_score_bf16_paired contracts the shared side once,
+    T = G·bf16(D_k∘v), and dots it with both rows (half the MFMA work; the bf16 operand rounding
+    sits on D_k∘v instead of u∘D_k), reading cols and rel of the first half only."""
     n = rows.numel()
     if paired and (n % 2 or cols.numel() != n or (rel is not None and rel.numel() != n)):
         raise ValueError("paired scoring needs an even number of pairs, cols / rel of the same length")

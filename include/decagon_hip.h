@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (28); bumped whenever a struct layout or a signature changes. */
+/* ABI version (29); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -274,10 +274,22 @@ typedef struct dg_staged_proj {
     int64_t h_ld;
     int32_t din;                /* 64                                                      */
     int32_t pad;
+    /* optional (all groups of a launch or none): H split by dg_split_bf16x2_f32, bf16 rows
+     * [n_cols][hs_ld] (hi at 0..63, lo at 64..127; hs_ld >= 128, a multiple of 8, 16-byte
+     * aligned).  The slab is then W_hi·H_hi + W_hi·H_lo + W_lo·H_hi on the bf16 MFMA (fp32
+     * accumulation; ≈ 2^-17 relative per product) instead of the exact fp32 MFMA form. */
+    const uint16_t* hs;
+    int64_t hs_ld;
 } dg_staged_proj;
 
 int dg_spmm_staged_proj_f32(const dg_staged_group* groups /* HOST */, const dg_staged_proj* projs /* HOST */,
                             int32_t n_groups, int32_t d, void* stream);
+
+/* out[r][0..cols) = bf16(x[r][c]) (nearest even), out[r][cols..2 cols) = bf16(x[r][c] - hi):
+ * the operand split of dg_spmm_staged_proj_f32's bf16 form (x = hi + lo to ≈ 2^-17 relative).
+ * cols % 8 == 0; x rows 16-byte aligned (ld % 4 == 0), out_ld >= 2 cols, out_ld % 8 == 0. */
+int dg_split_bf16x2_f32(const float* x, int64_t ld, int32_t rows, int32_t cols, uint16_t* out,
+                        int64_t out_ld, void* stream);
 
 /* Host-only layout helper: one relation's pair block of the staged layout.  Its lanes
  * (virtual rows; n_lanes = 64 x waves) are given as a CSR over lanes (HOST arrays: lrowptr
@@ -415,26 +427,14 @@ int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint1
                           const int32_t* rel_idx, int32_t n_pairs, const uint16_t* G,
                           const uint16_t* l_table, int32_t d, float* out, void* stream);
 
-/* Config 5's slot scorer: every DEDICOM relation slot's positive batch and its sampled
- * negatives in one launch.  For local slot s (global id slot0 + s) and i < batch:
- *     neg_rows[s*batch + i] = draw (slot0+s)*batch + i of slot (slot0+s)'s alias table
- *                             (alias_table + (slot0+s)*alias_stride entries; stride 0: one
- *                             shared table) — the draws of dg_unigram_sample;
- *     out[s*batch + i]              = score(pos_rows[s*batch + i], pos_cols[s*batch + i])
- *     out[n_slots*batch + s*batch + i] = score(neg_rows[s*batch + i], pos_cols[s*batch + i])
- * with score(u, v) = sum_n ( sum_k u_k * bf16(D_k[k] * R[k][n]) ) * D_k[n] * v_n (fp32 after
- * the bf16 operand), D_k = D[slot0 + s].  Rt is Rᵀ (Rt[n][k] = R[k][n]), bf16 [d][d]; tables and
- * D are bf16 rows.  Per slot the product E·(D_k∘R) is computed once for every row of the row
- * table (32-row tiles on the bf16 MFMA) and each pair is a dot with it.  d == 256,
- * n_rows <= 1024, n_cols <= 65535, batch <= 512, 1 <= range <= n_rows.
- * Replaces optimizer.py:38-47 (fixed_unigram_candidate_sampler, per relation's degrees) and
- * :51-57 / :63-85 (batch_predict pos / neg, G = R, L = D_k: model.py:130-134). */
 /* The same scores for config 5's layout: pairs p < n_half and p + n_half (a positive and its
- * negative, optimizer.py:37-57) share the column and the relation, so col_idx / rel_idx are read
- * for the first half only (row_idx, out hold 2*n_half entries).  One wave scores both pairs of
- * a batch entry: every Rᵀ fragment it reads from LDS feeds two MFMAs, and the shared v and D_k
- * rows are loaded once.  Same bf16 operands and k order as dg_decoder_score_bf16; the epilogue
- * sums the n's in another fixed order (fp32 rounding apart, the same scores). */
+ * negative, optimizer.py:37-57 — the negative replaces the row) share the column and the
+ * relation, so col_idx / rel_idx are read for the first half only (row_idx, out hold 2*n_half
+ * entries).  The shared side is contracted once: T = G·bf16(l_k ∘ v) on the bf16 MFMA (fp32
+ * accumulation), then out[p] = sum_i u_p[i] l_k[i] T[i] and out[p + n_half] = sum_i u_n[i] l_k[i] T[i]
+ * in fp32 — half the MFMA work of scoring the two pairs apart.  The bf16 operand rounding sits
+ * on l_k∘v instead of u∘l_k, so the scores agree with dg_decoder_score_bf16 to bf16 operand
+ * rounding.  G must be 16-byte aligned. */
 int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
                                  int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
                                  const int32_t* rel_idx, int32_t n_half, const uint16_t* G,

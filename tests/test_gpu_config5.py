@@ -4,7 +4,7 @@ d = 256 bf16 DEDICOM decoder, then the hinge loss (decagon_amd.scorer.SlotScorer
 bench.py runs it) — against a float64 restatement of the reference's scores
 (decagon/deep/optimizer.py:51-57, 63-85 with G = R, L = D_k: model.py:130-134) and hinge
 (optimizer.py:116-120) over EVERY pair, with the same bf16 operand rounding as the kernel
-(inputs rounded to bf16; u∘D_k rounded to bf16 as the MFMA's operand; fp32 accumulation).
+(inputs rounded to bf16; D_k∘v rounded to bf16 as the MFMA's operand; fp32 accumulation).
 
 The negatives are read back from the device: each slot's are exactly the restated alias draws
 of THAT slot's degree^0.75 table (fixed_unigram_candidate_sampler over degrees[i][k],
@@ -36,8 +36,8 @@ def _scorer(device, slots=None, allreduce=None):
 
 
 def _restated_scores(c5, rows, cols):
-    """float64 uᵀ·D_k·R·D_k·v on the bf16-rounded inputs, u∘D_k rounded to bf16 (the MFMA
-    operand); pairs slot-major, B per slot."""
+    """float64 (u∘D_k)ᵀ·R·(D_k∘v) on the bf16-rounded inputs, D_k∘v rounded to bf16 (the MFMA
+    operand of the column-shared paired kernel); pairs slot-major, B per slot."""
     bf = torch.bfloat16
     E = torch.from_numpy(c5.E).to(bf).float().numpy()
     R = torch.from_numpy(c5.R).to(bf).double().numpy()
@@ -47,9 +47,9 @@ def _restated_scores(c5, rows, cols):
     step = 1 << 16
     for s in range(0, len(rows), step):
         r, c, k = rows[s:s + step], cols[s:s + step], rel[s:s + step]
-        a = torch.from_numpy(E[r] * D[k]).to(bf).double().numpy()          # the MFMA operand
-        b = D[k].astype(np.float64) * E[c].astype(np.float64)
-        out[s:s + step] = np.einsum("pn,pn->p", a @ R, b)
+        a = D[k].astype(np.float64) * E[r].astype(np.float64)
+        b = torch.from_numpy(D[k] * E[c]).to(bf).double().numpy()          # the MFMA operand
+        out[s:s + step] = np.einsum("pn,pn->p", a, b @ R.T)
     return out
 
 
