@@ -491,9 +491,13 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
         el = float(t[0])
     reps = args.kernel_reps if steps >= 50 else 20
     k_ms = time_kernel(sc.score, reps, stream)
-    flop_pair = 2 * d * d + 4 * d
+    # flops the column-shared paired kernel issues per (positive, negative) pair: T = R·(D_k∘v)
+    # on the MFMA (2d²) once for both, the B operand (d) and two dots with u∘D_k (2·3d) on the
+    # VALU — against 2·(2d² + 4d) when each pair is contracted on its own
+    flop_pp = 2 * d * d + 7 * d
     n = 2 * sc.n
-    tflops = n * flop_pair / (k_ms * 1e-3) / 1e12
+    tflops = sc.n * flop_pp / (k_ms * 1e-3) / 1e12
+    mfma_tflops = sc.n * 2 * d * d / (k_ms * 1e-3) / 1e12
     return {
         "metric": "DEDICOM scored pairs/sec (config 5: d=256 bf16, all 1,928 drug-drug slots)",
         "value": 2 * slots * B * steps / el,
@@ -513,8 +517,9 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
         "loss": float(sc.loss[0]),
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / BF16_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "decoder_bf16_paired_kernel<256, true>", "kernel_ms": k_ms,
-                     "algorithmic_flops": n * flop_pair},
+                     "kernel": "decoder_bf16_colshared_kernel<256, true, 768>", "kernel_ms": k_ms,
+                     "algorithmic_flops": sc.n * flop_pp, "mfma_tflops": mfma_tflops,
+                     "per_pair_form_tflops": n * (2 * d * d + 4 * d) / (k_ms * 1e-3) / 1e12},
     }
 
 

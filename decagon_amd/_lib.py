@@ -92,7 +92,7 @@ class DgSegGroup(ctypes.Structure):
 
 
 class DgStagedProj(ctypes.Structure):
-    _fields_ = [("h", c_void_p), ("w", c_void_p), ("h_ld", c_int64), ("din", c_int32), ("pad", c_int32),
+    _fields_ = [("h", c_void_p), ("w", c_void_p), ("h_ld", c_int64), ("din", c_int32), ("hs_parts", c_int32),
                 ("hs", c_void_p), ("hs_ld", c_int64)]
 
 
@@ -195,7 +195,7 @@ SIGNATURES = {
     "dg_dropout_advance": (c_int32, [c_void_p, c_void_p]),
     "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_staged_proj_f32": (c_int32, [POINTER(DgStagedGroup), POINTER(DgStagedProj), c_int32, c_int32, c_void_p]),
-    "dg_split_bf16x2_f32": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int64, c_void_p]),
+    "dg_split_bf16x_f32": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_int64, c_void_p]),
     "dg_staged_block": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),

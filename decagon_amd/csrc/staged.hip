@@ -69,7 +69,7 @@ struct StagedGroupK {
     // three bf16 products (PROJ 2)
     const float* h;
     const float* w;
-    const uint16_t* hs;  // H split into bf16 hi | lo rows ([n_cols][hs_ld], hi at 0..63, lo at 64..127)
+    const uint16_t* hs;  // H split into bf16 parts: rows [n_cols][hs_ld], part q at 64q .. 64q + 63
     int32_t h_ld;
     int32_t hs_ld;
 };
@@ -126,16 +126,24 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 
-// x = hi + lo to ≈ 2^-17 relative: hi = bf16(x) (nearest even), lo = bf16(x - hi)
-__device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
-    bf16v8 h, l;
+// x split into NS bf16 parts, each the nearest-even bf16 of what the previous ones leave:
+// NS = 2: x = p0 + p1 to ≈ 2^-17 relative; NS = 3: x = p0 + p1 + p2 exactly for normal fp32
+// values (8 + 8 + 8 significant bits cover the 24 of the fp32 mantissa)
+template <int NS>
+__device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8 (&part)[NS]) {
+    float r[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        h[j] = (__bf16)x[j];
-        l[j] = (__bf16)(x[j] - (float)h[j]);
+    for (int j = 0; j < 8; ++j) r[j] = x[j];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        bf16v8 b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            b[j] = (__bf16)r[j];
+            r[j] -= (float)b[j];
+        }
+        part[q] = __builtin_bit_cast(bf16x8, b);
     }
-    hi = __builtin_bit_cast(bf16x8, h);
-    lo = __builtin_bit_cast(bf16x8, l);
 }
 
 template <int PROJ>
@@ -232,12 +240,14 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
 #pragma unroll
         for (int m = 0; m < 16; ++m) wa[m] = w[m * d];
     };
-    // PROJ 2: the same slab from three bf16 products on v_mfma_f32_16x16x32_bf16,
-    //     W·H ≈ W_hi·H_hi + W_hi·H_lo + W_lo·H_hi      (each operand x = x_hi + x_lo, |x_lo| ≤ 2^-9 |x|;
-    // the dropped W_lo·H_lo and the rounding of the lo parts leave ≈ 2^-17 relative per product)
-    // at 16 cycles per MFMA instead of 16 × 32 for the fp32 form.  Lane l holds A = W[32kh +
-    // 8pq + j][col0 + pn] (k-half kh, j < 8; split per relation) and B = H[v][32kh + 8pq + j] from
-    // hs (split once per layer by dg_split_bf16x2_f32); C lands as in PROJ 1.
+    // PROJ 2 / 3: the same slab from bf16 products on v_mfma_f32_16x16x32_bf16 with each
+    // operand split into NS = PROJ bf16 parts (x = x0 + x1 [+ x2], |x_q| ≤ 2^-8q |x|):
+    //   NS = 2:  W·H ≈ W0·H0 + W0·H1 + W1·H0                 (≈ 2^-17 relative per product)
+    //   NS = 3:  W·H ≈ W0·H0 + (W0·H1 + W1·H0) + (W0·H2 + W1·H1 + W2·H0)   (dropped terms ≤ 2^-24:
+    //            fp32-grade; the fp32 form's 16 × 32 MFMA cycles per tile become 12 × 16)
+    // Lane l holds A = W[32kh + 8pq + j][col0 + pn] (k-half kh, j < 8; split per relation) and B =
+    // H[v][32kh + 8pq + j] from hs (split once per layer by dg_split_bf16x_f32); the partial
+    // products are summed smallest first; C lands as in PROJ 1.
     auto load_w2 = [&](int i, float (&wa)[16]) {
         const int sl = __builtin_amdgcn_readfirstlane(slb[i]);
         const float* w = g.w + ((int64_t)sl * 64 + 8 * pq) * d + min(col0 + pn, d - 1);
@@ -247,24 +257,35 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
             for (int j = 0; j < 8; ++j) wa[8 * kh + j] = w[(32 * kh + j) * d];
     };
     auto slab_make2 = [&](int i, const float (&wa)[16]) {
+        constexpr int NS = PROJ >= 2 ? PROJ : 2;
         float4* buf = xs0 + (i & 1) * a.xs_f4;
-        bf16x8 whi[2], wlo[2];
-        split_bf16(*reinterpret_cast<const float(*)[8]>(&wa[0]), whi[0], wlo[0]);
-        split_bf16(*reinterpret_cast<const float(*)[8]>(&wa[8]), whi[1], wlo[1]);
+        bf16x8 w0[NS], w1[NS];  // k-half 0 / 1 parts
+        split_bf16<NS>(*reinterpret_cast<const float(*)[8]>(&wa[0]), w0);
+        split_bf16<NS>(*reinterpret_cast<const float(*)[8]>(&wa[8]), w1);
         const int n_tiles = (n_cols + 15) >> 4;
 #pragma unroll 1
         for (int t = wave; t < n_tiles; t += kMaxThreads / 64) {
             const int v = 16 * t + pn;
             const uint4* hp = reinterpret_cast<const uint4*>(g.hs + (int64_t)min(v, n_cols - 1) * g.hs_ld + 8 * pq);
-            const uint4 bh0 = hp[0], bh1 = hp[4], bl0 = hp[8], bl1 = hp[12];
-            f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
-            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[0], __builtin_bit_cast(bf16x8, bl0), lo, 0, 0, 0);
-            hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[0], __builtin_bit_cast(bf16x8, bh0), hi, 0, 0, 0);
-            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[1], __builtin_bit_cast(bf16x8, bl1), lo, 0, 0, 0);
-            hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[1], __builtin_bit_cast(bf16x8, bh1), hi, 0, 0, 0);
-            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[0], __builtin_bit_cast(bf16x8, bh0), lo, 0, 0, 0);
-            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[1], __builtin_bit_cast(bf16x8, bh1), lo, 0, 0, 0);
-            if (v < n_cols) buf[v * 5 + pq] = make_float4(hi[0] + lo[0], hi[1] + lo[1], hi[2] + lo[2], hi[3] + lo[3]);
+            f32x4 acc[NS];  // acc[o]: the products of order o (parts a + b = o)
+#pragma unroll
+            for (int o = 0; o < NS; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh) {  // one k-half's H parts live at a time: hp[8q + 4kh]
+                bf16x8 hq[NS];
+#pragma unroll
+                for (int q = 0; q < NS; ++q) hq[q] = __builtin_bit_cast(bf16x8, hp[8 * q + 4 * kh]);
+                const bf16x8* wq = kh ? w1 : w0;
+#pragma unroll
+                for (int o = NS - 1; o >= 0; --o)
+#pragma unroll
+                    for (int q = 0; q <= o; ++q)
+                        acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[q], hq[o - q], acc[o], 0, 0, 0);
+            }
+            f32x4 sum = acc[NS - 1];
+#pragma unroll
+            for (int o = NS - 2; o >= 0; --o) sum += acc[o];
+            if (v < n_cols) buf[v * 5 + pq] = make_float4(sum[0], sum[1], sum[2], sum[3]);
         }
     };
     // one 16-row tile at a time (measured: two tiles with interleaved accumulators made the
@@ -331,7 +352,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     };
 
     float wa[16];  // PROJ: the W slice of the next slab to make
-    if constexpr (PROJ == 2) {
+    if constexpr (PROJ >= 2) {
         load_w2(0, wa);
         slab_make2(0, wa);
         if (nk > 1) load_w2(1, wa);
@@ -367,7 +388,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         // relation i-1's sums (deferred past the barrier: they cover un's latency)
         if (prlw > 0) accumulate(part, pvi, __builtin_amdgcn_readfirstlane(pbig));
         DG_TICK(c_acc);
-        if constexpr (PROJ == 2) {
+        if constexpr (PROJ >= 2) {
             if (i + 1 < nk) {  // the other buffer: last read by relation i-1
                 slab_make2(i + 1, wa);
                 if (i + 2 < nk) load_w2(i + 2, wa);
@@ -492,7 +513,8 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
             if ((int64_t)s.n_cols * pj.h_ld > 0x7fffffffLL) return DG_EINVAL;
             if ((pj.hs != nullptr) != (projs[0].hs != nullptr)) return DG_EINVAL;  // one form per launch
             if (pj.hs) {
-                if (pj.hs_ld < 128 || (pj.hs_ld & 7) || !dg::aligned16(pj.hs)) return DG_EALIGN;
+                if (pj.hs_parts != projs[0].hs_parts || pj.hs_parts < 2 || pj.hs_parts > 3) return DG_EINVAL;
+                if (pj.hs_ld < 64 * pj.hs_parts || (pj.hs_ld & 7) || !dg::aligned16(pj.hs)) return DG_EALIGN;
                 if ((int64_t)s.n_cols * pj.hs_ld > 0x7fffffffLL) return DG_EINVAL;
             }
         } else {
@@ -564,7 +586,12 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
     }
 #endif
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (projs && projs[0].hs) {
+    if (projs && projs[0].hs && projs[0].hs_parts == 3) {
+        static std::atomic<uint64_t> configured{0};
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<3>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<3>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+                           static_cast<int>(lds), st, a);
+    } else if (projs && projs[0].hs) {
         static std::atomic<uint64_t> configured{0};
         dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<2>), kLdsBytes, configured);
         hipLaunchKernelGGL(spmm_staged_kernel<2>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
@@ -596,9 +623,10 @@ extern "C" int dg_spmm_staged_proj_f32(const dg_staged_group* groups, const dg_s
 }
 
 namespace {
-// out row r = [bf16 hi of x[r][0..cols) | bf16 lo of x[r][0..cols)], x = hi + lo (split_bf16)
-__global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restrict__ x, int64_t ld, int32_t rows,
-                                                           int32_t cols, uint16_t* __restrict__ out, int64_t out_ld) {
+// out row r = [part 0 of x[r][0..cols) | part 1 | ...] (split_bf16<NS>)
+template <int NS>
+__global__ __launch_bounds__(256) void split_bf16x_kernel(const float* __restrict__ x, int64_t ld, int32_t rows,
+                                                          int32_t cols, uint16_t* __restrict__ out, int64_t out_ld) {
     const int per = cols >> 3;  // 8-column pieces per row
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)rows * per) return;
@@ -606,20 +634,26 @@ __global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restri
     const float4* xp = reinterpret_cast<const float4*>(x + r * ld + c);
     const float4 x0 = xp[0], x1 = xp[1];
     const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-    bf16x8 hi, lo;
-    split_bf16(v, hi, lo);
-    *reinterpret_cast<bf16x8*>(out + r * out_ld + c) = hi;
-    *reinterpret_cast<bf16x8*>(out + r * out_ld + cols + c) = lo;
+    bf16x8 part[NS];
+    split_bf16<NS>(v, part);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) *reinterpret_cast<bf16x8*>(out + r * out_ld + q * cols + c) = part[q];
 }
 }  // namespace
 
-extern "C" int dg_split_bf16x2_f32(const float* x, int64_t ld, int32_t rows, int32_t cols, uint16_t* out,
-                                   int64_t out_ld, void* stream) {
-    if (!x || !out || rows < 0 || cols <= 0 || (cols & 7) || ld < cols || out_ld < 2 * cols) return DG_EINVAL;
+extern "C" int dg_split_bf16x_f32(const float* x, int64_t ld, int32_t rows, int32_t cols, int32_t parts,
+                                  uint16_t* out, int64_t out_ld, void* stream) {
+    if (!x || !out || rows < 0 || cols <= 0 || (cols & 7) || ld < cols || parts < 2 || parts > 3 ||
+        out_ld < (int64_t)parts * cols)
+        return DG_EINVAL;
     if (!dg::aligned16(x) || !dg::aligned16(out) || (ld & 3) || (out_ld & 7)) return DG_EALIGN;
     if (rows == 0) return DG_OK;
     const int64_t n = (int64_t)rows * (cols >> 3);
-    hipLaunchKernelGGL(split_bf16x2_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), x, ld, rows, cols, out, out_ld);
+    const dim3 grid(static_cast<unsigned>((n + 255) / 256));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (parts == 3)
+        hipLaunchKernelGGL(split_bf16x_kernel<3>, grid, dim3(256), 0, st, x, ld, rows, cols, out, out_ld);
+    else
+        hipLaunchKernelGGL(split_bf16x_kernel<2>, grid, dim3(256), 0, st, x, ld, rows, cols, out, out_ld);
     return dg::launch_status();
 }

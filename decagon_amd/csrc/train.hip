@@ -281,21 +281,30 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     const float alpha = a.state ? a.state[2] : a.alpha;
     const int64_t f0 = (int64_t)(b - s.block_begin) * kAdamF4PerBlock;
     const int64_t nf4 = s.n >> 2;
+    // every load of the block's four float4 rounds first (clamped indices, no branch: 16
+    // loads in flight per lane), then the updates and the predicated stores
+    if (nf4 > 0) {
+        float4 p[4], m[4], v[4], g[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int64_t f = f0 + u * 256 + threadIdx.x;
-        if (f < nf4) {
-            float4 p = reinterpret_cast<float4*>(s.p)[f];
-            float4 m = reinterpret_cast<float4*>(s.m)[f];
-            float4 v = reinterpret_cast<float4*>(s.v)[f];
-            const float4 g = s.g ? reinterpret_cast<const float4*>(s.g)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-            adam1(p.x, g.x, m.x, v.x, alpha, a);
-            adam1(p.y, g.y, m.y, v.y, alpha, a);
-            adam1(p.z, g.z, m.z, v.z, alpha, a);
-            adam1(p.w, g.w, m.w, v.w, alpha, a);
-            reinterpret_cast<float4*>(s.p)[f] = p;
-            reinterpret_cast<float4*>(s.m)[f] = m;
-            reinterpret_cast<float4*>(s.v)[f] = v;
+        for (int u = 0; u < 4; ++u) {
+            const int64_t f = min(f0 + u * 256 + threadIdx.x, nf4 - 1);
+            p[u] = reinterpret_cast<const float4*>(s.p)[f];
+            m[u] = reinterpret_cast<const float4*>(s.m)[f];
+            v[u] = reinterpret_cast<const float4*>(s.v)[f];
+            g[u] = s.g ? reinterpret_cast<const float4*>(s.g)[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t f = f0 + u * 256 + threadIdx.x;
+            adam1(p[u].x, g[u].x, m[u].x, v[u].x, alpha, a);
+            adam1(p[u].y, g[u].y, m[u].y, v[u].y, alpha, a);
+            adam1(p[u].z, g[u].z, m[u].z, v[u].z, alpha, a);
+            adam1(p[u].w, g[u].w, m[u].w, v[u].w, alpha, a);
+            if (f < nf4) {
+                reinterpret_cast<float4*>(s.p)[f] = p[u];
+                reinterpret_cast<float4*>(s.m)[f] = m[u];
+                reinterpret_cast<float4*>(s.v)[f] = v[u];
+            }
         }
     }
     // the tail (n % 4 elements) by the segment's last block
