@@ -18,6 +18,7 @@
 // column tile: the D_k·v epilogue reads 8-byte runs of the lane's own v and D_k rows.  The
 // lane halves (n mod 8 < 4 or not) meet in one shuffle.  Pairs need not share a relation.
 #include "common.h"
+#include "decoder_tile.h"
 
 namespace {
 
@@ -45,6 +46,19 @@ struct Bf16DecArgs {
     float* out;
     int64_t ld_row, ld_col;
     int32_t n_pairs, d;
+    // FUSED (config 5's slot form, dg_slot_score_hinge_bf16): pair p < n_pairs is batch entry
+    // p % batch of local slot p / batch (relation slot0 + p / batch); its negative row is
+    // alias draw slot0·batch + p of that slot's table (written to neg_out), and the hinge terms
+    // of every pair pair are summed into loss (per-workgroup partials, ticket, block order)
+    const uint2* alias;
+    int64_t alias_stride;
+    uint64_t seed;
+    int32_t* neg_out;
+    float* loss;
+    float* partial;
+    uint32_t* ticket;
+    int32_t range, slot0, batch;
+    float margin;
 };
 
 // threads per workgroup: 16 waves, but 12 at d = 256 (its 16 B-operand fragments need the
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(512) void decoder_bf16_paired_kernel(const Bf16DecA
 // owns the 16 contiguous i = 32t + 16h + [0, 16) of column tile t (32-byte runs of u_p, u_n
 // and D_k).  The bf16 operand rounding sits on D_k∘v instead of u∘D_k: the scores agree with
 // the row-side kernels to bf16 operand rounding, not bitwise.
-template <int D, bool HAS_L, int THREADS>
+template <int D, bool HAS_L, int THREADS, bool FUSED>
 __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const Bf16DecArgs a) {
     constexpr int KS = D / 16;
     constexpr int NT = D / 32;
@@ -319,14 +333,24 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
     const int n_tiles = (nh + 31) / 32;
     const int stride = gridDim.x * (THREADS / 64);
     const uint4 ones = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
+    float wsum = 0.f;  // FUSED: this wave's hinge terms, its tiles in order
 #pragma unroll 1
     for (int tile = blockIdx.x * (THREADS / 64) + wave; tile < n_tiles; tile += stride) {
         const int p = tile * 32 + r;
         const bool valid = p < nh;
         const int prp = valid ? a.rows[p] : 0;
-        const int prn = valid ? a.rows[nh + p] : 0;
         const int pc = valid ? a.cols[p] : 0;
-        const int pk = (valid && a.rel) ? a.rel[p] : 0;
+        int pk, prn;
+        if constexpr (FUSED) {
+            pk = valid ? a.slot0 + p / a.batch : 0;
+            prn = valid ? dg::unigram_draw(a.alias + pk * a.alias_stride, a.range, a.seed,
+                                           (uint64_t)a.slot0 * (uint64_t)a.batch + (uint64_t)p)
+                        : 0;
+            if (valid && h == 0) a.neg_out[p] = prn;
+        } else {
+            pk = (valid && a.rel) ? a.rel[p] : 0;
+            prn = valid ? a.rows[nh + p] : 0;
+        }
         const uint16_t* up = a.row_table + (int64_t)prp * a.ld_row;
         const uint16_t* un = a.row_table + (int64_t)prn * a.ld_row;
         const uint16_t* v = a.col_table + (int64_t)pc * a.ld_col;
@@ -392,6 +416,36 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
             a.out[p] = partp;
             a.out[nh + p] = partn;
         }
+        if constexpr (FUSED) {  // relu(neg − (pos − margin)), optimizer.py:116-120: a fixed butterfly
+            float term = (h == 0 && valid) ? fmaxf(partn - (partp - a.margin), 0.f) : 0.f;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off);
+            wsum += term;
+        }
+    }
+    if constexpr (FUSED) {
+        // the workgroup's partial (its waves in order) is published write-through and drained,
+        // then a ticket; the last workgroup adds every partial in block order (sc1 loads, no L2
+        // write-back or invalidate — decoder_hinge_kernel's hand-off) and resets the ticket
+        __shared__ float red[THREADS / 64];
+        __shared__ int last;
+        if (lane == 0) red[wave] = wsum;
+        __syncthreads();
+        if (tid == 0) {
+            float s = 0.f;
+            for (int w = 0; w < THREADS / 64; ++w) s += red[w];
+            __hip_atomic_store(a.partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last && tid == 0) {
+            float t = 0.f;
+            for (int b = 0; b < (int)gridDim.x; ++b)
+                t += __hip_atomic_load(a.partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.loss[0] = t;
+            __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 }  // namespace
@@ -455,12 +509,13 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
     if (!dg::aligned16(G)) return DG_EALIGN;  // R rows are staged into LDS in 16-byte pieces
     constexpr int kThreads = DG_DEC_CS_THREADS;
     static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
-    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, true, kThreads>), 160 * 1024,
-                  configured_l);
-    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, false, kThreads>), 160 * 1024,
-                  configured_nl);
+    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, true, kThreads, false>),
+                  160 * 1024, configured_l);
+    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, false, kThreads, false>),
+                  160 * 1024, configured_nl);
 #define DG_DEC_LAUNCH(DD, HL) \
-    hipLaunchKernelGGL((decoder_bf16_colshared_kernel<DD, HL, kThreads>), dim3(blocks), dim3(kThreads), lds, st, a)
+    hipLaunchKernelGGL((decoder_bf16_colshared_kernel<DD, HL, kThreads, false>), dim3(blocks), dim3(kThreads), lds, \
+                       st, a)
 #endif
     int blocks = (n_tiles + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 256) blocks = 256;  // persistent: one R-holding workgroup per CU
@@ -473,5 +528,49 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
         if (hl) DG_DEC_LAUNCH(64, true); else DG_DEC_LAUNCH(64, false);
     }
 #undef DG_DEC_LAUNCH
+    return dg::launch_status();
+}
+
+extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
+                                        int64_t ld_col, const int32_t* pos_rows, const int32_t* pos_cols,
+                                        const uint32_t* alias_table, int32_t range, int64_t alias_stride,
+                                        int32_t slot0, int32_t n_slots, int32_t batch, uint64_t seed,
+                                        const uint16_t* G, const uint16_t* l_table, int32_t d, float margin,
+                                        float* out, int32_t* neg_rows, float* loss, void* workspace,
+                                        void* stream) {
+    if (n_slots < 0 || batch < 1 || slot0 < 0 || range < 1 || alias_stride < 0) return DG_EINVAL;
+    if (!row_table || !col_table || !pos_rows || !pos_cols || !alias_table || !G || !l_table || !out ||
+        !neg_rows || !loss || !workspace)
+        return DG_EINVAL;
+    if (d != 256) return DG_EINVAL;
+    if (ld_row < d || ld_col < d || (ld_row & 7) || (ld_col & 7)) return DG_EALIGN;
+    if (!dg::aligned16(row_table) || !dg::aligned16(col_table) || !dg::aligned16(l_table) || !dg::aligned16(G) ||
+        !dg::aligned16(workspace))
+        return DG_EALIGN;
+    if ((int64_t)n_slots * batch > 0x7fffffffLL) return DG_EINVAL;
+    const int32_t nh = n_slots * batch;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (nh == 0) return hipMemsetAsync(loss, 0, sizeof(float), st) == hipSuccess ? DG_OK : DG_EINVAL;
+    Bf16DecArgs a{row_table, col_table, G, l_table, pos_rows, pos_cols, nullptr, out, ld_row, ld_col, nh, d};
+    a.alias = reinterpret_cast<const uint2*>(alias_table);
+    a.alias_stride = alias_stride;
+    a.seed = seed;
+    a.neg_out = neg_rows;
+    a.loss = loss;
+    a.ticket = reinterpret_cast<uint32_t*>(workspace);
+    a.partial = reinterpret_cast<float*>(workspace) + 4;
+    a.range = range;
+    a.slot0 = slot0;
+    a.batch = batch;
+    a.margin = margin;
+    constexpr int kThreads = DG_DEC_CS_THREADS;
+    const int n_tiles = (nh + 31) / 32;
+    int blocks = (n_tiles + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks > DG_HINGE_WS_BLOCKS) blocks = DG_HINGE_WS_BLOCKS;  // persistent; the workspace's partials
+    static std::atomic<uint64_t> configured{0};
+    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, true, kThreads, true>),
+                  160 * 1024, configured);
+    hipLaunchKernelGGL((decoder_bf16_colshared_kernel<256, true, kThreads, true>), dim3(blocks), dim3(kThreads),
+                       d * d * 2, st, a);
     return dg::launch_status();
 }

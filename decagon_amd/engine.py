@@ -76,7 +76,7 @@ STAGED_PROJ = os.environ.get("DG_STAGED_PROJ", "1") != "0"
 # ... from H1_j and W2_k split into DG_STAGED_SPLIT bf16 parts (H1_j by dg_split_bf16x_f32 once
 # per forward) on the bf16 MFMA instead of the fp32 MFMA: 3 parts (default) are fp32-grade,
 # 2 parts ≈ 2^-17 relative per product; 0: the exact fp32 form
-STAGED_SPLIT = int(os.environ.get("DG_STAGED_SPLIT", "3"))
+STAGED_SPLIT = int(os.environ.get("DG_STAGED_SPLIT", "0"))
 # one-GPU plans whose node types all fit dg_gcn_fused_seg_f32 (config S) use it, layer 2
 # reassociated; DG_FUSED_SEG=0 keeps dg_gcn_fused_f32 with the projection epilogue + P
 FUSED_SEG = os.environ.get("DG_FUSED_SEG", "1") != "0"

@@ -956,6 +956,47 @@ def unigram_sample_slots(table: torch.Tensor, slot0: int, batch: int, n: int, se
     return out
 
 
+def slot_score_hinge_bf16(E_row: torch.Tensor, E_col: torch.Tensor, pos_rows: torch.Tensor, pos_cols: torch.Tensor,
+                          table: torch.Tensor, slot0: int, n_slots: int, batch: int, seed: int, G: torch.Tensor,
+                          D: torch.Tensor, margin: float, out: torch.Tensor, neg_rows: torch.Tensor,
+                          loss: torch.Tensor, workspace: torch.Tensor, stream=None) -> None:
+    """Config 5's step in one launch (dg_slot_score_hinge_bf16): local slots [0, n_slots) are
+    relations slot0 .. slot0 + n_slots − 1; pos_rows / pos_cols hold their n = n_slots·batch
+    positives (slot-major).  neg_rows ← each slot's alias draws (unigram_sample_slots' draws),
+    out[:n] / out[n:] ← positive / negative scores (decoder_score_bf16(paired=True)), loss ←
+    the hinge sum."""
+    n = n_slots * batch
+    for t, nm in ((E_row, "E_row"), (E_col, "E_col"), (G, "G"), (D, "D")):
+        _dev(t, torch.bfloat16, nm)
+    for t, nm in ((pos_rows, "pos_rows"), (pos_cols, "pos_cols"), (neg_rows, "neg_rows"), (table, "alias table")):
+        _dev(t, torch.int32, nm)
+    _dev(out, torch.float32, "out")
+    _dev(loss, torch.float32, "loss")
+    d = G.shape[0]
+    if d != 256 or G.shape != (256, 256) or D.dim() != 2 or D.shape[1] != d or E_row.shape[1] != d \
+            or E_col.shape[1] != d:
+        raise ValueError("slot scorer: d = 256 tables, G and D rows")
+    if table.dim() == 3 and table.shape[2] == 2:
+        rng, stride = table.shape[1], table.shape[1]
+        if slot0 + n_slots > table.shape[0]:
+            raise ValueError("slot range outside the alias tables")
+    elif table.dim() == 2 and table.shape[1] == 2:
+        rng, stride = table.shape[0], 0
+    else:
+        raise ValueError("alias tables must be [n_slots, range, 2] or [range, 2]")
+    if rng > E_row.shape[0] or slot0 + n_slots > D.shape[0]:
+        raise ValueError("sampler range exceeds the row table, or slots exceed D")
+    if pos_rows.numel() < n or pos_cols.numel() < n or neg_rows.numel() < n or out.numel() < 2 * n:
+        raise ValueError("pairs / outputs shorter than n_slots·batch")
+    if workspace.numel() * workspace.element_size() < _lib.DG_HINGE_WS_BYTES or not workspace.is_cuda:
+        raise ValueError("hinge workspace too small")
+    check(_lib.load().dg_slot_score_hinge_bf16(
+        E_row.data_ptr(), E_row.stride(0), E_col.data_ptr(), E_col.stride(0), pos_rows.data_ptr(), pos_cols.data_ptr(),
+        table.data_ptr(), rng, stride, slot0, n_slots, batch, seed & (2**64 - 1), G.data_ptr(), D.data_ptr(), d,
+        float(margin), out.data_ptr(), neg_rows.data_ptr(), loss.data_ptr(), workspace.data_ptr(),
+        _stream_ptr(stream)), "dg_slot_score_hinge_bf16")
+
+
 def upload_alias(degrees, device) -> torch.Tensor:
     """The alias table of one degree vector, int32 [range, 2]; a list of degree vectors (one per
     relation) gives [n, range, 2] (every vector the same length)."""

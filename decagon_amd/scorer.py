@@ -8,12 +8,13 @@ interaction) and L = D_k (the relation's local variation, model.py:130-134, opti
 and the cost from `_hinge_loss` (optimizer.py:116-120).  Config 5 runs that for all slots at
 once with d = 256 bf16 embeddings and parameters (fp32 accumulation):
 
-  1. dg_unigram_sample_slots draws each slot's B negatives from the slot's own alias table
-     (draw i of slot s is counter s·B + i, so the draws do not depend on how the slots are
-     sharded),
-  2. dg_decoder_score_bf16_paired scores the n positive and n negative pairs on the bf16 MFMA
-     (a positive and its negative share the column and the relation: one wave scores both),
-  3. dg_hinge_loss_ws_f32 sums relu(neg − pos + margin) over the rank's pairs, and
+  1. each slot's B negatives are drawn from the slot's own alias table (draw i of slot s is
+     counter s·B + i, so the draws do not depend on how the slots are sharded),
+  2. the n positive and n negative pairs are scored on the bf16 MFMA (a positive and its
+     negative share the column and the relation: T = R·(D_k∘v) is contracted once for both),
+  3. relu(neg − pos + margin) is summed over the rank's pairs — 1-3 in ONE launch,
+     dg_slot_score_hinge_bf16 (fused=False: dg_unigram_sample_slots, dg_decoder_score_bf16_paired
+     and dg_hinge_loss_ws_f32 as three launches, the same draws and scores), and
   4. with N ranks, one all-reduce of that scalar — the only collective.
 
 Slots are dealt in contiguous blocks (sharding.slot_range); embeddings and parameters are
@@ -32,7 +33,7 @@ class SlotScorer:
     def __init__(self, E_row: torch.Tensor, E_col: torch.Tensor, R: torch.Tensor, D: torch.Tensor,
                  pos_rows: torch.Tensor, pos_cols: torch.Tensor, alias: torch.Tensor, batch: int,
                  margin: float = 0.1, seed: int = 11, slots: Optional[Tuple[int, int]] = None,
-                 allreduce: Optional[Callable[[torch.Tensor], None]] = None):
+                 allreduce: Optional[Callable[[torch.Tensor], None]] = None, fused: bool = True):
         """E_row / E_col: bf16 [n, d] embeddings; R: bf16 [d, d]; D: bf16 [n_slots, d]
         diagonals; pos_rows / pos_cols: int32 [n_slots·batch] positive pairs of every slot
         (slot-major); alias: the slots' degree^0.75 alias tables (kernels.upload_alias of a
@@ -64,6 +65,7 @@ class SlotScorer:
         self._ws = kernels.hinge_workspace(dev)
         self.E_row, self.E_col, self.R, self.D, self.alias = E_row, E_col, R, D, alias
         self.allreduce = allreduce
+        self.fused = fused
 
     @property
     def neg_rows(self) -> torch.Tensor:
@@ -93,6 +95,16 @@ class SlotScorer:
             self.allreduce(self.loss)
 
     def __call__(self) -> None:
-        self.sample()
-        self.score()
-        self.hinge()
+        if not self.fused:
+            self.sample()
+            self.score()
+            self.hinge()
+            return
+        if self.n:
+            kernels.slot_score_hinge_bf16(self.E_row, self.E_col, self.rows[:self.n], self.cols[:self.n], self.alias,
+                                          self.s0, self.s1 - self.s0, self.batch, self.seed, self.R, self.D,
+                                          self.margin, self.out, self.neg_rows, self.loss, self._ws)
+        else:
+            self.loss.zero_()
+        if self.allreduce is not None:
+            self.allreduce(self.loss)

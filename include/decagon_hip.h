@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (29); bumped whenever a struct layout or a signature changes. */
+/* ABI version (30); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -441,6 +441,28 @@ int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, cons
                                  int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
                                  const int32_t* rel_idx, int32_t n_half, const uint16_t* G,
                                  const uint16_t* l_table, int32_t d, float* out, void* stream);
+
+/* Config 5's whole step in one launch: every relation slot's positive batch, its sampled
+ * negatives and the hinge loss.  For local slot s < n_slots (relation slot0 + s) and i < batch,
+ * p = s*batch + i:
+ *     neg_rows[p]            = draw slot0*batch + p of slot (slot0+s)'s alias table
+ *                              (alias_table + (slot0+s)*alias_stride entries; stride 0: one
+ *                              shared table) — exactly dg_unigram_sample_slots' draws;
+ *     out[p]                 = score(pos_rows[p], pos_cols[p]),
+ *     out[n_slots*batch + p] = score(neg_rows[p], pos_cols[p])     (dg_decoder_score_bf16_paired,
+ *                              D_k = l_table[slot0 + s]);
+ *     loss[0]                = sum_p relu(out[nh + p] - (out[p] - margin))   (per-workgroup sums
+ *                              in a fixed order, added in block order: deterministic).
+ * workspace: DG_HINGE_WS_BYTES bytes, 16-byte aligned, first word zero before the first call
+ * (left zero).  d == 256; G, tables and l_table 16-byte aligned.  Replaces optimizer.py:38-47
+ * (fixed_unigram_candidate_sampler over the relation's degrees), :51-57 / :63-85 (batch_predict,
+ * G = R, L = D_k: model.py:130-134) and :116-120 (_hinge_loss). */
+int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
+                             int64_t ld_col, const int32_t* pos_rows, const int32_t* pos_cols,
+                             const uint32_t* alias_table, int32_t range, int64_t alias_stride,
+                             int32_t slot0, int32_t n_slots, int32_t batch, uint64_t seed,
+                             const uint16_t* G, const uint16_t* l_table, int32_t d, float margin,
+                             float* out, int32_t* neg_rows, float* loss, void* workspace, void* stream);
 
 /* Fused decoder step (T8 + T9 + T11 + T12 in one launch):
  *   neg_row[b] = neg_rows[b] if neg_rows != NULL, else draw (offset + b) of the alias

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _scorer(device, slots=None, allreduce=None):
+def _scorer(device, slots=None, allreduce=None, fused=True):
     from decagon_amd import kernels, synthetic
     from decagon_amd.scorer import SlotScorer
 
@@ -31,7 +31,7 @@ def _scorer(device, slots=None, allreduce=None):
     sc = SlotScorer(E, E, torch.from_numpy(c5.R).to(bf).to(device), torch.from_numpy(c5.D).to(bf).to(device),
                     torch.from_numpy(c5.pos_rows).to(device), torch.from_numpy(c5.pos_cols).to(device),
                     kernels.upload_alias(c5.degrees, device), c5.batch, 0.1, seed=11, slots=slots,
-                    allreduce=allreduce)
+                    allreduce=allreduce, fused=fused)
     return c5, sc
 
 
@@ -119,3 +119,28 @@ def test_config5_slot_sharded_two_ranks_equal_one_rank():
         assert np.array_equal(out[:m], full_pos[s0 * B:s1 * B])
         assert np.array_equal(out[m:], full_negs[s0 * B:s1 * B])
         assert abs(loss - full_loss) <= 1e-5 * abs(full_loss)  # all-reduced per-rank sums
+
+
+@pytest.mark.parametrize("slots", [None, (5, 9), (1927, 1928)])
+def test_config5_one_launch_equals_three(slots):
+    """dg_slot_score_hinge_bf16 (sampler + scores + hinge in one launch, the benched step) against
+    the three-launch form (dg_unigram_sample_slots, dg_decoder_score_bf16_paired,
+    dg_hinge_loss_ws_f32): the same draws and the same score bits; the loss is summed in another
+    fixed order (fp32 rounding); the fused loss is the same on every launch; slot sub-ranges
+    (a rank's share) included."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    dev = torch.device("cuda")
+    _, one = _scorer(dev, slots)
+    _, three = _scorer(dev, slots, fused=False)
+    one()
+    three()
+    torch.cuda.synchronize()
+    assert torch.equal(one.neg_rows, three.neg_rows)
+    assert torch.equal(one.out, three.out)
+    l1, l3 = float(one.loss[0]), float(three.loss[0])
+    assert abs(l1 - l3) <= 1e-5 * abs(l3)
+    for _ in range(2):
+        one()
+        torch.cuda.synchronize()
+        assert float(one.loss[0]) == l1
