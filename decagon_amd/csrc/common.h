@@ -31,7 +31,10 @@ inline void lds_optin(const void* fn, int bytes, std::atomic<uint64_t>& done) {
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     const uint64_t bit = 1ull << (dev & 63);
     if (done.load(std::memory_order_acquire) & bit) return;
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
+        (void)hipGetLastError();  // not sticky: the launch after it reports its own status
+        return;                   // (and a launch that needs the opt-in fails loudly)
+    }
     done.fetch_or(bit, std::memory_order_acq_rel);
 }
 

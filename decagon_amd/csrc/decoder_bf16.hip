@@ -567,9 +567,11 @@ extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_ro
     const int n_tiles = (nh + 31) / 32;
     int blocks = (n_tiles + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > DG_HINGE_WS_BLOCKS) blocks = DG_HINGE_WS_BLOCKS;  // persistent; the workspace's partials
+    // the opt-in is the dynamic R buffer exactly: the kernel's static LDS (the hinge partials)
+    // comes on top of it, and static + dynamic must stay within the CU's 160 KB
     static std::atomic<uint64_t> configured{0};
     dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, true, kThreads, true>),
-                  160 * 1024, configured);
+                  d * d * 2, configured);
     hipLaunchKernelGGL((decoder_bf16_colshared_kernel<256, true, kThreads, true>), dim3(blocks), dim3(kThreads),
                        d * d * 2, st, a);
     return dg::launch_status();
