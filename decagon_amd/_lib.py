@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 30
+ABI_VERSION = 31
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -92,8 +92,7 @@ class DgSegGroup(ctypes.Structure):
 
 
 class DgStagedProj(ctypes.Structure):
-    _fields_ = [("h", c_void_p), ("w", c_void_p), ("h_ld", c_int64), ("din", c_int32), ("hs_parts", c_int32),
-                ("hs", c_void_p), ("hs_ld", c_int64)]
+    _fields_ = [("h", c_void_p), ("w", c_void_p), ("h_ld", c_int64), ("din", c_int32), ("pad", c_int32)]
 
 
 class DgProj(ctypes.Structure):
@@ -195,7 +194,6 @@ SIGNATURES = {
     "dg_dropout_advance": (c_int32, [c_void_p, c_void_p]),
     "dg_spmm_staged_f32": (c_int32, [POINTER(DgStagedGroup), c_int32, c_int32, c_void_p]),
     "dg_spmm_staged_proj_f32": (c_int32, [POINTER(DgStagedGroup), POINTER(DgStagedProj), c_int32, c_int32, c_void_p]),
-    "dg_split_bf16x_f32": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_int64, c_void_p]),
     "dg_staged_block": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),

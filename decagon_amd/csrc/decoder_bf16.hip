@@ -334,22 +334,42 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
     const int stride = gridDim.x * (THREADS / 64);
     const uint4 ones = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
     float wsum = 0.f;  // FUSED: this wave's hinge terms, its tiles in order
+    // a tile's indices (rows, column, relation; FUSED: the negative's alias entry) are loaded one
+    // tile ahead, so a tile's row gathers do not wait behind its index loads
+    struct Idx {
+        int prp, pc, pk, prn, j;
+        float u;
+        uint2 e;
+    };
+    auto fetch = [&](int tl, Idx& x) {
+        const int p = tl * 32 + r;
+        const bool ok = tl < n_tiles && p < nh;
+        x.prp = ok ? a.rows[p] : 0;
+        x.pc = ok ? a.cols[p] : 0;
+        if constexpr (FUSED) {
+            x.pk = ok ? a.slot0 + p / a.batch : 0;
+            dg::unigram_pick(a.range, a.seed, (uint64_t)a.slot0 * (uint64_t)a.batch + (uint64_t)p, x.j, x.u);
+            x.e = ok ? a.alias[x.pk * a.alias_stride + x.j] : make_uint2(0u, 0u);
+        } else {
+            x.pk = (ok && a.rel) ? a.rel[p] : 0;
+            x.prn = ok ? a.rows[nh + p] : 0;
+        }
+    };
+    Idx nxt;
+    fetch(blockIdx.x * (THREADS / 64) + wave, nxt);
 #pragma unroll 1
     for (int tile = blockIdx.x * (THREADS / 64) + wave; tile < n_tiles; tile += stride) {
         const int p = tile * 32 + r;
         const bool valid = p < nh;
-        const int prp = valid ? a.rows[p] : 0;
-        const int pc = valid ? a.cols[p] : 0;
-        int pk, prn;
+        const Idx cur = nxt;
+        fetch(tile + stride, nxt);
+        const int prp = cur.prp, pc = cur.pc, pk = cur.pk;
+        int prn;
         if constexpr (FUSED) {
-            pk = valid ? a.slot0 + p / a.batch : 0;
-            prn = valid ? dg::unigram_draw(a.alias + pk * a.alias_stride, a.range, a.seed,
-                                           (uint64_t)a.slot0 * (uint64_t)a.batch + (uint64_t)p)
-                        : 0;
+            prn = valid ? dg::unigram_take(cur.j, cur.u, cur.e) : 0;
             if (valid && h == 0) a.neg_out[p] = prn;
         } else {
-            pk = (valid && a.rel) ? a.rel[p] : 0;
-            prn = valid ? a.rows[nh + p] : 0;
+            prn = cur.prn;
         }
         const uint16_t* up = a.row_table + (int64_t)prp * a.ld_row;
         const uint16_t* un = a.row_table + (int64_t)prn * a.ld_row;

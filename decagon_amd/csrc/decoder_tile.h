@@ -22,13 +22,22 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 // {acceptance probability (float bits), alias index}.  One 64-bit hash gives the column j
 // (high 32 bits, scaled by range) and the 24-bit acceptance uniform (low bits): one 8-byte
 // load per draw, no search.
+// The counter-based part of draw idx: alias slot j and its uniform u (no memory access).
+__device__ __forceinline__ void unigram_pick(int range, uint64_t seed, uint64_t idx, int& j, float& u) {
+    const uint64_t h = splitmix64(seed ^ splitmix64(idx));
+    j = (int)(((h >> 32) * (uint64_t)range) >> 32);
+    u = (float)(h & 0xFFFFFFu) * (1.0f / 16777216.0f);
+}
+
+// Draw idx given its slot's table entry e = table[j].
+__device__ __forceinline__ int unigram_take(int j, float u, uint2 e) { return u < __uint_as_float(e.x) ? j : (int)e.y; }
+
 __device__ __forceinline__ int unigram_draw(const uint2* table, int range, uint64_t seed,
                                             uint64_t idx) {
-    const uint64_t h = splitmix64(seed ^ splitmix64(idx));
-    const int j = (int)(((h >> 32) * (uint64_t)range) >> 32);
-    const float u = (float)(h & 0xFFFFFFu) * (1.0f / 16777216.0f);
-    const uint2 e = table[j];
-    return u < __uint_as_float(e.x) ? j : (int)e.y;
+    int j;
+    float u;
+    unigram_pick(range, seed, idx, j, u);
+    return unigram_take(j, u, table[j]);
 }
 
 struct DecTab {

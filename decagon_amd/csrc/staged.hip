@@ -65,13 +65,11 @@ struct StagedGroupK {
     int32_t n_blocks;
     int32_t pad;
     // PROJ form: the slab of relation k is H · W[slab(k)] (H [n_cols][64], W [K][64][d]),
-    // computed in the workgroup on the MFMA instead of read from x: fp32 (PROJ 1) or, with hs,
-    // three bf16 products (PROJ 2)
+    // computed in the workgroup on the fp32 MFMA instead of read from x
     const float* h;
     const float* w;
-    const uint16_t* hs;  // H split into bf16 parts: rows [n_cols][hs_ld], part q at 64q .. 64q + 63
     int32_t h_ld;
-    int32_t hs_ld;
+    int32_t pad2;
 };
 
 struct StagedArgs {
@@ -123,30 +121,8 @@ __device__ __forceinline__ void fold_step(float4 (&part)[4], int gsz) {
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 
-// x split into NS bf16 parts, each the nearest-even bf16 of what the previous ones leave:
-// NS = 2: x = p0 + p1 to ≈ 2^-17 relative; NS = 3: x = p0 + p1 + p2 exactly for normal fp32
-// values (8 + 8 + 8 significant bits cover the 24 of the fp32 mantissa)
-template <int NS>
-__device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8 (&part)[NS]) {
-    float r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = x[j];
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        bf16v8 b;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            b[j] = (__bf16)r[j];
-            r[j] -= (float)b[j];
-        }
-        part[q] = __builtin_bit_cast(bf16x8, b);
-    }
-}
-
-template <int PROJ>
+template <bool PROJ>
 __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedArgs a) {
     extern __shared__ float4 lds[];
     const int tid = threadIdx.x;
@@ -227,7 +203,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
             if (q < n5) glds16(xk, off * 4, dst + q0 * 16);
         }
     };
-    // PROJ 1: relation i's slab slice computed on the fp32 MFMA — slabᵀ[n][v] = Σ_k W[k][col0 + n]
+    // PROJ: relation i's slab slice computed on the fp32 MFMA — slabᵀ[n][v] = Σ_k W[k][col0 + n]
     // H[v][k] on v_mfma_f32_16x16x4_f32 (A = W slice: lane l holds W[16q + m][col0 + (l & 15)],
     // q = l >> 4, for MFMA m; B = Hᵀ: H[v][16q + m] for its tile's row v = 16t + (l & 15); the
     // contraction order k = 16q + m is free), so lane l ends with slab[v][col0 + 4q .. +3] —
@@ -239,54 +215,6 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         const float* w = g.w + ((int64_t)sl * 64 + 16 * pq) * d + min(col0 + pn, d - 1);
 #pragma unroll
         for (int m = 0; m < 16; ++m) wa[m] = w[m * d];
-    };
-    // PROJ 2 / 3: the same slab from bf16 products on v_mfma_f32_16x16x32_bf16 with each
-    // operand split into NS = PROJ bf16 parts (x = x0 + x1 [+ x2], |x_q| ≤ 2^-8q |x|):
-    //   NS = 2:  W·H ≈ W0·H0 + W0·H1 + W1·H0                 (≈ 2^-17 relative per product)
-    //   NS = 3:  W·H ≈ W0·H0 + (W0·H1 + W1·H0) + (W0·H2 + W1·H1 + W2·H0)   (dropped terms ≤ 2^-24:
-    //            fp32-grade; the fp32 form's 16 × 32 MFMA cycles per tile become 12 × 16)
-    // Lane l holds A = W[32kh + 8pq + j][col0 + pn] (k-half kh, j < 8; split per relation) and B =
-    // H[v][32kh + 8pq + j] from hs (split once per layer by dg_split_bf16x_f32); the partial
-    // products are summed smallest first; C lands as in PROJ 1.
-    auto load_w2 = [&](int i, float (&wa)[16]) {
-        const int sl = __builtin_amdgcn_readfirstlane(slb[i]);
-        const float* w = g.w + ((int64_t)sl * 64 + 8 * pq) * d + min(col0 + pn, d - 1);
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) wa[8 * kh + j] = w[(32 * kh + j) * d];
-    };
-    auto slab_make2 = [&](int i, const float (&wa)[16]) {
-        constexpr int NS = PROJ >= 2 ? PROJ : 2;
-        float4* buf = xs0 + (i & 1) * a.xs_f4;
-        bf16x8 w0[NS], w1[NS];  // k-half 0 / 1 parts
-        split_bf16<NS>(*reinterpret_cast<const float(*)[8]>(&wa[0]), w0);
-        split_bf16<NS>(*reinterpret_cast<const float(*)[8]>(&wa[8]), w1);
-        const int n_tiles = (n_cols + 15) >> 4;
-#pragma unroll 1
-        for (int t = wave; t < n_tiles; t += kMaxThreads / 64) {
-            const int v = 16 * t + pn;
-            const uint4* hp = reinterpret_cast<const uint4*>(g.hs + (int64_t)min(v, n_cols - 1) * g.hs_ld + 8 * pq);
-            f32x4 acc[NS];  // acc[o]: the products of order o (parts a + b = o)
-#pragma unroll
-            for (int o = 0; o < NS; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int kh = 0; kh < 2; ++kh) {  // one k-half's H parts live at a time: hp[8q + 4kh]
-                bf16x8 hq[NS];
-#pragma unroll
-                for (int q = 0; q < NS; ++q) hq[q] = __builtin_bit_cast(bf16x8, hp[8 * q + 4 * kh]);
-                const bf16x8* wq = kh ? w1 : w0;
-#pragma unroll
-                for (int o = NS - 1; o >= 0; --o)
-#pragma unroll
-                    for (int q = 0; q <= o; ++q)
-                        acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[q], hq[o - q], acc[o], 0, 0, 0);
-            }
-            f32x4 sum = acc[NS - 1];
-#pragma unroll
-            for (int o = NS - 2; o >= 0; --o) sum += acc[o];
-            if (v < n_cols) buf[v * 5 + pq] = make_float4(sum[0], sum[1], sum[2], sum[3]);
-        }
     };
     // one 16-row tile at a time (measured: two tiles with interleaved accumulators made the
     // layer-2 launch 10 us slower — their MFMAs then crowd the gathers of the SIMD's other waves)
@@ -352,11 +280,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     };
 
     float wa[16];  // PROJ: the W slice of the next slab to make
-    if constexpr (PROJ >= 2) {
-        load_w2(0, wa);
-        slab_make2(0, wa);
-        if (nk > 1) load_w2(1, wa);
-    } else if constexpr (PROJ == 1) {
+    if constexpr (PROJ) {
         load_w(0, wa);
         slab_make(0, wa);
         if (nk > 1) load_w(1, wa);
@@ -388,12 +312,7 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         // relation i-1's sums (deferred past the barrier: they cover un's latency)
         if (prlw > 0) accumulate(part, pvi, __builtin_amdgcn_readfirstlane(pbig));
         DG_TICK(c_acc);
-        if constexpr (PROJ >= 2) {
-            if (i + 1 < nk) {  // the other buffer: last read by relation i-1
-                slab_make2(i + 1, wa);
-                if (i + 2 < nk) load_w2(i + 2, wa);
-            }
-        } else if constexpr (PROJ == 1) {
+        if constexpr (PROJ) {
             if (i + 1 < nk) {  // the other buffer: last read by relation i-1
                 slab_make(i + 1, wa);
                 if (i + 2 < nk) load_w(i + 2, wa);
@@ -511,12 +430,6 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
             if (!pj.h || !pj.w || pj.din != 64 || pj.h_ld < 64) return DG_EINVAL;
             if (!dg::aligned16(pj.h) || (pj.h_ld & 3)) return DG_EALIGN;
             if ((int64_t)s.n_cols * pj.h_ld > 0x7fffffffLL) return DG_EINVAL;
-            if ((pj.hs != nullptr) != (projs[0].hs != nullptr)) return DG_EINVAL;  // one form per launch
-            if (pj.hs) {
-                if (pj.hs_parts != projs[0].hs_parts || pj.hs_parts < 2 || pj.hs_parts > 3) return DG_EINVAL;
-                if (pj.hs_ld < 64 * pj.hs_parts || (pj.hs_ld & 7) || !dg::aligned16(pj.hs)) return DG_EALIGN;
-                if ((int64_t)s.n_cols * pj.hs_ld > 0x7fffffffLL) return DG_EINVAL;
-            }
         } else {
             if (!s.x) return DG_EINVAL;
             if (!dg::aligned16(s.x) || (s.x_ld & 3) || s.x_ld < d) return DG_EALIGN;
@@ -527,8 +440,6 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
             k.h = projs[i].h;
             k.w = projs[i].w;
             k.h_ld = static_cast<int32_t>(projs[i].h_ld);
-            k.hs = projs[i].hs;
-            k.hs_ld = static_cast<int32_t>(projs[i].hs_ld);
         }
         k.pairs = reinterpret_cast<const int2*>(s.pairs);
         k.jm = s.jm;
@@ -586,25 +497,15 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
     }
 #endif
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (projs && projs[0].hs && projs[0].hs_parts == 3) {
+    if (projs) {
         static std::atomic<uint64_t> configured{0};
-        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<3>), kLdsBytes, configured);
-        hipLaunchKernelGGL(spmm_staged_kernel<3>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
-                           static_cast<int>(lds), st, a);
-    } else if (projs && projs[0].hs) {
-        static std::atomic<uint64_t> configured{0};
-        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<2>), kLdsBytes, configured);
-        hipLaunchKernelGGL(spmm_staged_kernel<2>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
-                           static_cast<int>(lds), st, a);
-    } else if (projs) {
-        static std::atomic<uint64_t> configured{0};
-        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<1>), kLdsBytes, configured);
-        hipLaunchKernelGGL(spmm_staged_kernel<1>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<true>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
                            static_cast<int>(lds), st, a);
     } else {
         static std::atomic<uint64_t> configured{0};
-        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<0>), kLdsBytes, configured);
-        hipLaunchKernelGGL(spmm_staged_kernel<0>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
+        dg::lds_optin(reinterpret_cast<const void*>(&spmm_staged_kernel<false>), kLdsBytes, configured);
+        hipLaunchKernelGGL(spmm_staged_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(threads),
                            static_cast<int>(lds), st, a);
     }
     return dg::launch_status();
@@ -620,40 +521,4 @@ extern "C" int dg_spmm_staged_proj_f32(const dg_staged_group* groups, const dg_s
                                        int32_t n_groups, int32_t d, void* stream) {
     if (!projs) return DG_EINVAL;
     return staged_launch(groups, projs, n_groups, d, stream);
-}
-
-namespace {
-// out row r = [part 0 of x[r][0..cols) | part 1 | ...] (split_bf16<NS>)
-template <int NS>
-__global__ __launch_bounds__(256) void split_bf16x_kernel(const float* __restrict__ x, int64_t ld, int32_t rows,
-                                                          int32_t cols, uint16_t* __restrict__ out, int64_t out_ld) {
-    const int per = cols >> 3;  // 8-column pieces per row
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= (int64_t)rows * per) return;
-    const int r = (int)(e / per), c = (int)(e - (int64_t)r * per) * 8;
-    const float4* xp = reinterpret_cast<const float4*>(x + r * ld + c);
-    const float4 x0 = xp[0], x1 = xp[1];
-    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-    bf16x8 part[NS];
-    split_bf16<NS>(v, part);
-#pragma unroll
-    for (int q = 0; q < NS; ++q) *reinterpret_cast<bf16x8*>(out + r * out_ld + q * cols + c) = part[q];
-}
-}  // namespace
-
-extern "C" int dg_split_bf16x_f32(const float* x, int64_t ld, int32_t rows, int32_t cols, int32_t parts,
-                                  uint16_t* out, int64_t out_ld, void* stream) {
-    if (!x || !out || rows < 0 || cols <= 0 || (cols & 7) || ld < cols || parts < 2 || parts > 3 ||
-        out_ld < (int64_t)parts * cols)
-        return DG_EINVAL;
-    if (!dg::aligned16(x) || !dg::aligned16(out) || (ld & 3) || (out_ld & 7)) return DG_EALIGN;
-    if (rows == 0) return DG_OK;
-    const int64_t n = (int64_t)rows * (cols >> 3);
-    const dim3 grid(static_cast<unsigned>((n + 255) / 256));
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (parts == 3)
-        hipLaunchKernelGGL(split_bf16x_kernel<3>, grid, dim3(256), 0, st, x, ld, rows, cols, out, out_ld);
-    else
-        hipLaunchKernelGGL(split_bf16x_kernel<2>, grid, dim3(256), 0, st, x, ld, rows, cols, out, out_ld);
-    return dg::launch_status();
 }

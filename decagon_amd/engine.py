@@ -73,10 +73,6 @@ FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
 CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "0") != "0"
 # layer 2 of staged groups makes its slabs H1_j·W2_k on the MFMA inside the SpMM kernel
 STAGED_PROJ = os.environ.get("DG_STAGED_PROJ", "1") != "0"
-# ... from H1_j and W2_k split into DG_SLAB_SPLIT bf16 parts (H1_j by dg_split_bf16x_f32 once
-# per forward) on the bf16 MFMA instead of the fp32 MFMA: 3 parts (default) are fp32-grade,
-# 2 parts ≈ 2^-17 relative per product; 0: the exact fp32 form
-SLAB_SPLIT = int(os.environ.get("DG_SLAB_SPLIT", "0"))
 # one-GPU plans whose node types all fit dg_gcn_fused_seg_f32 (config S) use it, layer 2
 # reassociated; DG_FUSED_SEG=0 keeps dg_gcn_fused_f32 with the projection epilogue + P
 FUSED_SEG = os.environ.get("DG_FUSED_SEG", "1") != "0"
@@ -517,19 +513,10 @@ class ForwardPlan:
                 self.hidden1[j], (0, h1, 1), W, (h1 * h2, h2, 1), self.proj[et], (n[j] * h2, h2, 1),
                 n[j], h2, h1, grp.n_rels, b_map=grp.rel_map, b_batches=W.shape[0],
                 b_map_max=int(grp.rel_ids.max()) if grp.rel_map is not None else None))
-        # the staged groups' H1_j as bf16 hi / lo rows (their slabs on the bf16 MFMA)
-        self.h1_split: Dict[int, torch.Tensor] = {}
-        splits = []
-        if SLAB_SPLIT in (2, 3):
-            for j in sorted({et[1] for et in self.staged_proj}):
-                self.h1_split[j] = torch.empty((n[j], SLAB_SPLIT * h1), dtype=torch.int16, device=dev)
-                splits.append(lambda j=j: kernels.split_bf16x(self.hidden1[j], SLAB_SPLIT, self.h1_split[j]))
-        self._gemm2 = splits + drops + [kernels.PreparedGemmMulti(gemms[s:s + DG_MAX_GROUPS])
-                                        for s in range(0, len(gemms), DG_MAX_GROUPS)]
+        self._gemm2 = drops + [kernels.PreparedGemmMulti(gemms[s:s + DG_MAX_GROUPS])
+                               for s in range(0, len(gemms), DG_MAX_GROUPS)]
         self._layer2 = self._build_layer(self.proj, h2, False, f32,
                                          staged_proj={et: (self.hidden1[et[1]], w2.stacks[et])
-                                                      + ((self.h1_split[et[1]], SLAB_SPLIT)
-                                                         if et[1] in self.h1_split else ())
                                                       for et in self.staged_proj},
                                          seg_w={et: (self.hidden1[et[1]], w2.stacks[et]) for et in self.seg_proj})
 

@@ -452,11 +452,9 @@ class StagedSpec:
     x_ld: int
     x_rows: int
     slab_max: int = -1            # host-known max(slab) (or n_rels-1 without slab), for checks
-    # (H [n_cols][64], W [K][64][d]) or (H, W, Hs, parts): relation k's operand is H·W[slab(k)],
-    # made in the kernel (dg_spmm_staged_proj_f32) — from Hs = split_bf16x(H, parts) (int16
-    # [n_cols][64·parts]) on the bf16 MFMA when given, else on the fp32 MFMA; x / x_ld / x_rows
-    # are then unused
-    proj: Optional[Tuple[torch.Tensor, ...]] = None
+    # (H [n_cols][64], W [K][64][d]): relation k's operand is H·W[slab(k)], made in the kernel
+    # (dg_spmm_staged_proj_f32); x / x_ld / x_rows are then unused
+    proj: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
     def validate(self, d: int) -> None:
         L = self.layout
@@ -481,16 +479,7 @@ class StagedSpec:
                 raise ValueError("slab shorter than n_rels")
         smax = self.slab_max if self.slab_max >= 0 else L.n_rels - 1
         if self.proj is not None:
-            h, w = self.proj[:2]
-            hs = self.proj[2] if len(self.proj) > 2 else None
-            if hs is not None:
-                parts = self.proj[3]
-                if parts not in (2, 3):
-                    raise ValueError("proj hs: 2 or 3 bf16 parts")
-                _dev(hs, torch.int16, "proj hs")
-                if hs.dim() != 2 or hs.shape[0] < L.n_cols or hs.shape[1] < 64 * parts or hs.stride(1) != 1 \
-                        or hs.stride(0) % 8 or hs.data_ptr() % 16:
-                    raise ValueError("proj hs must be [n_cols][>= 64·parts] int16, rows 16-byte aligned")
+            h, w = self.proj
             if not (isinstance(h, torch.Tensor) and h.is_cuda and h.dtype == torch.float32):
                 raise ValueError("proj h: float32 device tensor required (rows may be padded)")
             _dev(w, torch.float32, "proj w")
@@ -526,13 +515,8 @@ class PreparedStaged:
             g.slab = s.slab.data_ptr() if s.slab is not None else None
             g.x = s.x.data_ptr() if s.x is not None else None
             if proj:
-                h, w = s.proj[:2]
+                h, w = s.proj
                 parr[i].h, parr[i].w, parr[i].h_ld, parr[i].din = h.data_ptr(), w.data_ptr(), h.stride(0), 64
-                hs = s.proj[2] if len(s.proj) > 2 else None
-                if (hs is None) != (len(specs[0].proj) < 3 or specs[0].proj[2] is None):
-                    raise ValueError("a staged launch's projected groups all carry Hs or none")
-                if hs is not None:
-                    parr[i].hs, parr[i].hs_ld, parr[i].hs_parts = hs.data_ptr(), hs.stride(0), s.proj[3]
             g.out = s.out.data_ptr()
             g.x_ld = s.x_ld
             g.n_rows, g.n_cols, g.n_rels = L.n_rows, L.n_cols, L.n_rels
@@ -547,27 +531,6 @@ class PreparedStaged:
             check(self._fn(self._arr, self._parr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_proj_f32")
         else:
             check(self._fn(self._arr, self._n, self.d, _stream_ptr(stream)), "dg_spmm_staged_f32")
-
-
-def split_bf16x(x: torch.Tensor, parts: int = 3, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-    """dg_split_bf16x_f32: out[r] = [part 0 of x[r] | part 1 | ...] (int16 bit patterns), each part
-    the nearest-even bf16 of what the previous ones leave — the H operand of the staged kernel's
-    bf16 slab forms (2 parts: ≈ 2^-17 relative; 3 parts: exact for normal values)."""
-    if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2):
-        raise ValueError("x: 2-d float32 device tensor required")
-    if parts not in (2, 3):
-        raise ValueError("parts: 2 or 3")
-    rows, cols = x.shape
-    if cols % 8 or x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
-        raise ValueError("x needs a multiple of 8 contiguous columns, rows 16-byte aligned")
-    if out is None:
-        out = torch.empty((rows, parts * cols), dtype=torch.int16, device=x.device)
-    _dev(out, torch.int16, "out")
-    if out.dim() != 2 or out.shape[0] < rows or out.shape[1] < parts * cols or out.stride(0) % 8:
-        raise ValueError("out must be [rows][>= parts·cols] int16, rows 16-byte aligned")
-    check(_lib.load().dg_split_bf16x_f32(x.data_ptr(), x.stride(0), rows, cols, parts, out.data_ptr(),
-                                         out.stride(0), _stream_ptr(stream)), "dg_split_bf16x_f32")
-    return out
 
 
 def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:

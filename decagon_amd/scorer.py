@@ -22,6 +22,7 @@ replicated (645 × 256 bf16 = 330 KB; the slots' alias tables 1,928 × 645 × 8 
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional, Tuple
 
 import torch
@@ -33,7 +34,7 @@ class SlotScorer:
     def __init__(self, E_row: torch.Tensor, E_col: torch.Tensor, R: torch.Tensor, D: torch.Tensor,
                  pos_rows: torch.Tensor, pos_cols: torch.Tensor, alias: torch.Tensor, batch: int,
                  margin: float = 0.1, seed: int = 11, slots: Optional[Tuple[int, int]] = None,
-                 allreduce: Optional[Callable[[torch.Tensor], None]] = None, fused: bool = True):
+                 allreduce: Optional[Callable[[torch.Tensor], None]] = None, fused: Optional[bool] = None):
         """E_row / E_col: bf16 [n, d] embeddings; R: bf16 [d, d]; D: bf16 [n_slots, d]
         diagonals; pos_rows / pos_cols: int32 [n_slots·batch] positive pairs of every slot
         (slot-major); alias: the slots' degree^0.75 alias tables (kernels.upload_alias of a
@@ -65,7 +66,8 @@ class SlotScorer:
         self._ws = kernels.hinge_workspace(dev)
         self.E_row, self.E_col, self.R, self.D, self.alias = E_row, E_col, R, D, alias
         self.allreduce = allreduce
-        self.fused = fused
+        # (DG_C5_FUSED=0: the three-launch form by default — A/B runs)
+        self.fused = (os.environ.get("DG_C5_FUSED", "1") != "0") if fused is None else fused
 
     @property
     def neg_rows(self) -> torch.Tensor:

@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (30); bumped whenever a struct layout or a signature changes. */
+/* ABI version (31); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -273,25 +273,12 @@ typedef struct dg_staged_proj {
     const float* w;             /* device, [K][din][d]                                     */
     int64_t h_ld;
     int32_t din;                /* 64                                                      */
-    int32_t hs_parts;           /* with hs: 2 or 3 (the same for every group of a launch)  */
-    /* optional (all groups of a launch or none): H split by dg_split_bf16x_f32 into hs_parts
-     * bf16 parts, rows [n_cols][hs_ld] (part q at 64q .. 64q + 63; hs_ld >= 64 hs_parts, a
-     * multiple of 8, 16-byte aligned).  The slab is then made from the parts' products on the
-     * bf16 MFMA (fp32 accumulation): 3 products at 2 parts (≈ 2^-17 relative), 6 at 3 parts
-     * (fp32-grade: the dropped terms are ≤ 2^-24) — instead of the fp32 MFMA form. */
-    const uint16_t* hs;
-    int64_t hs_ld;
+    int32_t pad;
 } dg_staged_proj;
 
 int dg_spmm_staged_proj_f32(const dg_staged_group* groups /* HOST */, const dg_staged_proj* projs /* HOST */,
                             int32_t n_groups, int32_t d, void* stream);
 
-/* x split into `parts` (2 or 3) bf16 parts, each the nearest-even bf16 of what the previous
- * ones leave: out[r][q*cols + c] = part q of x[r][c] — the H operand of dg_spmm_staged_proj_f32's
- * bf16 forms (2 parts: x = p0 + p1 to ≈ 2^-17 relative; 3 parts: exact for normal values).
- * cols % 8 == 0; x rows 16-byte aligned (ld % 4 == 0), out_ld >= parts·cols, out_ld % 8 == 0. */
-int dg_split_bf16x_f32(const float* x, int64_t ld, int32_t rows, int32_t cols, int32_t parts,
-                       uint16_t* out, int64_t out_ld, void* stream);
 
 /* Host-only layout helper: one relation's pair block of the staged layout.  Its lanes
  * (virtual rows; n_lanes = 64 x waves) are given as a CSR over lanes (HOST arrays: lrowptr

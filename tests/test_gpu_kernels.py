@@ -621,29 +621,6 @@ def test_spmm_staged(K, d, n_rows, n_cols, density, out_chunk):
     assert torch.equal(out, out2)
 
 
-@pytest.mark.parametrize("parts", [2, 3])
-def test_split_bf16x(K, parts):
-    """dg_split_bf16x_f32: part q = bf16(x − parts before it) (nearest even), bit for bit
-    against torch's bf16 rounding; 2 parts within 2^-16 relative, 3 parts exact; a padded
-    leading dimension on both sides."""
-    rng = np.random.default_rng(3)
-    xp = torch.from_numpy((rng.standard_normal((77, 72)) * 10.0 ** rng.integers(-3, 4, (77, 72))).astype(np.float32))
-    x = xp.cuda()[:, :64]
-    out = torch.zeros((77, 64 * parts + 8), dtype=torch.int16, device="cuda")
-    K.split_bf16x(x, parts, out)
-    got = out.cpu()
-    r = xp[:, :64].clone()
-    tot = torch.zeros_like(r, dtype=torch.float64)
-    for q in range(parts):
-        b = r.to(torch.bfloat16)
-        assert torch.equal(got[:, 64 * q:64 * q + 64], b.view(torch.int16)), q
-        r = r - b.float()
-        tot += b.double()
-    assert not got[:, 64 * parts:].any()
-    err = (tot - xp[:, :64].double()).abs() / xp[:, :64].double().abs()
-    assert float(err.max()) <= (0.0 if parts == 3 else 2.0 ** -16)
-
-
 @pytest.mark.parametrize("d", [32, 64, 40])
 @pytest.mark.parametrize("n_rows,n_cols,density,out_chunk", [
     (150, 137, 0.03, 5),     # a partial last 16-row projection tile, empty rows
@@ -651,12 +628,9 @@ def test_split_bf16x(K, parts):
     (645, 645, 0.3, 3),      # config P's shape: 41 tiles over 16 waves
     (64, 880, 0.01, 23),     # 55 tiles (up to 4 per wave)
 ])
-@pytest.mark.parametrize("parts", [0, 2, 3])
-def test_spmm_staged_projected(K, d, n_rows, n_cols, density, out_chunk, parts):
+def test_spmm_staged_projected(K, d, n_rows, n_cols, density, out_chunk):
     """dg_spmm_staged_proj_f32: relation k's operand H·W[slab(k)] made on the MFMA inside the
-    kernel — exact fp32 MFMA (parts 0), or bf16 products of H and W split into 2 parts (≈ 2^-17
-    relative per product: tolerance 2e-5) or 3 parts (fp32-grade: 1e-5) by dg_split_bf16x_f32 —
-    against the float64 Σ_k A_k·(H·W_slab(k)); H with a padded leading dimension."""
+    kernel, against the float64 Σ_k A_k·(H·W_slab(k)); H with a padded leading dimension."""
     from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, staged_layout
 
     rng = np.random.default_rng(7 * d + n_rows + n_cols)
@@ -672,8 +646,6 @@ def test_spmm_staged_projected(K, d, n_rows, n_cols, density, out_chunk, parts):
     n_out = -(-nrel // out_chunk)
     out = torch.zeros((n_out, n_rows, d), device="cuda")
     proj = (h, torch.from_numpy(W).cuda())
-    if parts:
-        proj += (K.split_bf16x(h, parts), parts)
     spec = K.StagedSpec(dev, torch.from_numpy(slabs).cuda(), None, out, out_chunk, d, 0,
                         slab_max=int(slabs.max()), proj=proj)
     K.PreparedStaged([spec], d)()
@@ -681,7 +653,7 @@ def test_spmm_staged_projected(K, d, n_rows, n_cols, density, out_chunk, parts):
     want = np.zeros((n_out, n_rows, d))
     for k, x in enumerate(mats):
         want[k // out_chunk] += x @ (H @ W[slabs[k]].astype(np.float64))
-    assert rel_err(out.cpu().numpy(), want) <= (2e-5 if parts == 2 else 1e-5)
+    assert rel_err(out.cpu().numpy(), want) <= 1e-5
     out2 = torch.zeros_like(out)
     spec.out = out2
     K.PreparedStaged([spec], d)()
