@@ -356,9 +356,13 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
         }
     };
     Idx nxt;
-    fetch(blockIdx.x * (THREADS / 64) + wave, nxt);
+    // tile order: round-major, then wave, then workgroup (tile = k·stride + wave·grid + block),
+    // so the last, partial round's tiles land one per workgroup on as many CUs as there are
+    // tiles — not all on the first few workgroups, where 12 waves would share each CU's MFMA
+    const int first = wave * (int)gridDim.x + (int)blockIdx.x;
+    fetch(first, nxt);
 #pragma unroll 1
-    for (int tile = blockIdx.x * (THREADS / 64) + wave; tile < n_tiles; tile += stride) {
+    for (int tile = first; tile < n_tiles; tile += stride) {
         const int p = tile * 32 + r;
         const bool valid = p < nh;
         const Idx cur = nxt;
