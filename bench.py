@@ -61,10 +61,13 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
                     help="config S: omit the P / D blocks of the default line")
-    ap.add_argument("--p-steps", type=int, default=20, help="timed steps of the P block")
-    ap.add_argument("--d-steps", type=int, default=20, help="timed steps of the D block")
+    ap.add_argument("--p-steps", type=int, default=100, help="timed steps of the P block")
+    ap.add_argument("--d-steps", type=int, default=100, help="timed steps of the D block")
     ap.add_argument("--kernel-reps", type=int, default=200)
-    ap.add_argument("--graph-steps", type=int, default=10,
+    # (each hipGraph replay boundary costs ≈ 5-20 µs of host launch + GPU ramp, measured by
+    # scripts/steps_sweep.sh: config S 20.8 µs a step at 20 steps in graphs of 10, 19.2 at 200
+    # in graphs of 50; so whole runs of up to 50 steps are one graph)
+    ap.add_argument("--graph-steps", type=int, default=50,
                     help="steps captured back to back in one hipGraph (the largest divisor of "
                          "--steps not above it is used)")
     ap.add_argument("--target-waves", type=int, default=32768)

@@ -318,9 +318,9 @@ struct FsTargetK {
     int32_t g_count;
     int32_t relu;
     int32_t block_begin;
-    int32_t waves;  // one per relation of the target's groups
+    int32_t waves;  // waves per row: one per relation (items <= 16), else the workgroup's 16
     int32_t rpb;    // rows per workgroup: nw / waves (at most kFsMaxRpb)
-    int32_t pad;
+    int32_t items;  // (group, relation) items of a row: the relations of every group, every chunk
 };
 
 struct FsArgs {
@@ -336,11 +336,14 @@ constexpr int kFsMaxRpb = 1;  // A/B: one row per workgroup
 constexpr int kFsMaxRpb = 4;
 #endif
 
+// groups per target in the looped form's per-wave accumulators (config S: 2)
+constexpr int kFsLoopGroups = 4;
+
 template <int LP, bool PROJ, int NW>
 __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;
     __shared__ float4 ybuf[NW][16];
-    __shared__ float4 zbuf[NW][DOUT4];
+    __shared__ float4 zbuf[NW][kFsLoopGroups][DOUT4];
     __shared__ float4 nbuf[kFsMaxRpb][DG_MAX_GROUPS][DOUT4];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -349,30 +352,47 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
     while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
     const FsTargetK& T = a.t[ti];
     const int r0 = (blockIdx.x - T.block_begin) * T.rpb;
-    // wave -> (row slot, group gl, relation t): each slot's groups' relations back to back
+    // wave -> (row slot, items wi, wi + waves, ...): item i is relation k of group gl (the
+    // slot's groups' relations back to back; k = c·chunk + t: chunk c, relation t).  With at
+    // most 16 items a row (config S on one GPU) every wave owns one item; a row block of N
+    // relation sets (config S's N-GPU rank share) has the workgroup's 16 waves loop, each
+    // summing its items per group in item order
     const int slot = wave / T.waves;
     const int wi = wave - slot * T.waves;
     const int r = r0 + slot;
-    int gl = 0, base = 0;
+    float4 acc[kFsLoopGroups];
+#pragma unroll
+    for (int q = 0; q < kFsLoopGroups; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (slot < T.rpb && r < T.n_rows) {
 #pragma unroll 1
-    while (gl < T.g_count && wi >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
-    float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (slot < T.rpb && r < T.n_rows && gl < T.g_count)
-        res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(a.g[T.g_begin + gl], 0, r, wi - base, wi - base,
-                                                         ybuf[wave]);
-    if (lane < DOUT4) zbuf[wave][lane] = res;
+        for (int i = wi; i < T.items; i += T.waves) {
+            int gl = 0, base = 0;
+#pragma unroll 1
+            while (gl + 1 < T.g_count && i >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
+            const SegGroupK& g = a.g[T.g_begin + gl];
+            const int k = i - base;
+            const int c = k / g.chunk;
+            const float4 res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(g, c, r, k - c * g.chunk, k, ybuf[wave]);
+#pragma unroll
+            for (int q = 0; q < kFsLoopGroups; ++q)
+                if (q == gl) dg::add4(acc[q], res);
+        }
+    }
+    if (lane < DOUT4) {
+#pragma unroll
+        for (int q = 0; q < kFsLoopGroups; ++q) zbuf[wave][q][lane] = acc[q];
+    }
     __syncthreads();
-    // one wave per (row slot, group): its relations summed in order, L2-normalised
+    // one wave per (row slot, group): the slot's waves' sums of that group in wave order —
+    // item order, since a group's items are consecutive (one item per wave: exactly the
+    // relation order; the other groups' waves add exact zeros) — then L2-normalised
     if (wave < T.rpb * T.g_count) {
         const int s2 = wave / T.g_count, gg = wave - s2 * T.g_count;
-        int gb = s2 * T.waves;
-#pragma unroll 1
-        for (int u = 0; u < gg; ++u) gb += a.g[T.g_begin + u].n_rels;
-        const int K = a.g[T.g_begin + gg].n_rels;
+        const int gb = s2 * T.waves;
         const int q = lane % DOUT4;
-        float4 sum = zbuf[gb][q];
+        float4 sum = zbuf[gb][gg][q];
 #pragma unroll 1
-        for (int u = 1; u < K; ++u) dg::add4(sum, zbuf[gb + u][q]);
+        for (int u = 1; u < T.waves; ++u) dg::add4(sum, zbuf[gb + u][gg][q]);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
         float ss = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
 #pragma unroll
@@ -498,8 +518,7 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
         bool skip = false;
         const int rc = convert_seg(groups[i], proj, d_in, a.g[i], skip);
         if (rc != DG_OK) return rc;
-        // one chunk holding every relation of the group, at least one relation
-        if (groups[i].n_chunks != 1 || groups[i].chunk != groups[i].n_rels || groups[i].n_rels < 1) return DG_EINVAL;
+        if (groups[i].n_rels < 1 || groups[i].n_rows < 1) return DG_EINVAL;  // (convert_seg checked the chunks)
     }
     int64_t blocks = 0;
     int nw = 1;
@@ -508,12 +527,14 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
         if (!s.out || !dg::aligned16(s.out) || s.n_rows < 0 || s.g_count < 1 || s.g_begin < 0 ||
             s.g_begin + s.g_count > n_groups || (s.flags & ~DG_EPI_RELU))
             return DG_EINVAL;
-        int waves = 0;
+        int items = 0;
         for (int g = s.g_begin; g < s.g_begin + s.g_count; ++g) {
             if (groups[g].n_rows != s.n_rows) return DG_EINVAL;
-            waves += groups[g].n_rels;
+            items += groups[g].n_rels;
         }
-        if (waves > 16) return DG_EINVAL;  // one wave per relation of the row
+        // one wave per item (<= 16 a row), else 16 looping waves (at most kFsLoopGroups groups)
+        if (items > 16 && s.g_count > kFsLoopGroups) return DG_EINVAL;
+        const int waves = items > 16 ? 16 : items;
         nw = waves > nw ? waves : nw;
         FsTargetK& k = a.t[t];
         k.out = s.out;
@@ -522,6 +543,7 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
         k.g_count = s.g_count;
         k.relu = (s.flags & DG_EPI_RELU) ? 1 : 0;
         k.waves = waves;
+        k.items = items;
     }
     // rows per workgroup: a target with fewer relations per row than the widest one fills the
     // workgroup's waves with more rows

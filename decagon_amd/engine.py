@@ -76,6 +76,10 @@ STAGED_PROJ = os.environ.get("DG_STAGED_PROJ", "1") != "0"
 # one-GPU plans whose node types all fit dg_gcn_fused_seg_f32 (config S) use it, layer 2
 # reassociated; DG_FUSED_SEG=0 keeps dg_gcn_fused_f32 with the projection epilogue + P
 FUSED_SEG = os.environ.get("DG_FUSED_SEG", "1") != "0"
+# config S's N-GPU rank share (seg mode): each row of the rank's block finished by one
+# dg_gcn_fused_seg_f32 workgroup whose 16 waves loop over the row's N relation sets
+# (DG_SEG_FUSED=0: dg_spmm_seg_f32 partials + the epilogue launch)
+SEG_FUSED = os.environ.get("DG_SEG_FUSED", "1") != "0"
 STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 
 
@@ -564,6 +568,23 @@ class ForwardPlan:
         launches: List[Callable[[], None]] = []
         fused_t = self.fused
         gathers = []
+        if self.seg_mode and SEG_FUSED:
+            # every node type row-split: one launch finishes this rank's row block of each
+            # (its workgroups' waves loop over the N relation sets), then the all-gathers
+            seg_w = seg_w or {}
+            tgts = []
+            for i in self.targets:
+                a, b, blk = self.row_block[i]
+                pad = self._pad[i, 1 if relu else 2]
+                r0 = self.shard.rank * blk
+                gathers.append((pad, pad[r0:r0 + blk]))
+                tgts.append((pad[r0:r0 + (b - a)], b - a,
+                             [self._seg_spec(et, seg_w[et][0], None, seg_w[et][1]) if et in seg_w
+                              else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu))
+            launches.append(kernels.PreparedFusedSeg(tgts, self.h1 if seg_w else d, d))
+            self.launch_groups[id(launches[-1])] = [et for i in self.targets for et in self.targets[i]]
+            return _Layer(launches, None, False, self.allreduce, [], [], {}, self.side_stream, None, (), gathers,
+                          self.allgather)
         if self.fused_seg:
             seg_w = seg_w or {}
             tgts = [(outs[i], n[i], [self._seg_spec(et, seg_w[et][0], None, seg_w[et][1]) if et in seg_w

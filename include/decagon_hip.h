@@ -201,15 +201,18 @@ typedef struct dg_seg_group {
 int dg_spmm_seg_f32(const dg_seg_group* groups /* HOST array */, int32_t n_groups, int32_t d_in,
                     int32_t d_out, void* stream);
 
-/* The fused form: a whole layer for node types whose groups each fit one chunk
- * (n_chunks == 1, chunk == n_rels >= 1) with at most 16 relations per target row in total.
+/* The fused form: a whole layer for the target node types, every output row finished in one
+ * workgroup.  Groups are chunk-merged as for dg_spmm_seg_f32 (any n_chunks; n_rels >= 1).
  * For every target t (dg_fused_target: out [n_rows][d_out], groups [g_begin, g_begin + g_count),
  * flags 0 or DG_EPI_RELU; groups[i].out unused) and row r < n_rows:
  *
  *   out_t[r] = act( sum_g l2norm( sum_{t < n_rels_g} seg-sum_g(r, t) ) )
  *
- * with seg-sum as dg_spmm_seg_f32's (projected by W[slab] when the groups carry w).  One
- * workgroup per row, one wave per (group, relation); relations and groups summed in order.
+ * with seg-sum as dg_spmm_seg_f32's over relation t = c*chunk + t' of the group (projected by
+ * W[slab] when the groups carry w).  One workgroup per row: one wave per (group, relation) when
+ * a row has at most 16 relations in total, else (at most 4 groups a target) 16 waves each
+ * summing every 16th relation of the row per group, then the 16 sums in wave order; groups
+ * summed in order.
  * With w this is layer 2 (layers.py:109-118) reassociated, Σ_k (Â_k·H1_j)·W2_k, so layer 1
  * needs no projection of its rows.  Replaces layers.py:85-94 / 109-118 and model.py:74-75,
  * 85-88 for such node types. */
