@@ -184,131 +184,16 @@ __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf
 }
 
 
-// Paired form (config 5's layout: pair p < n_half and pair p + n_half — a positive and its
-// negative — share the column and the relation, optimizer.py:37-57): one wave scores the 32
-// positives and the 32 negatives of one batch tile together.  Every Rᵀ fragment read from LDS
-// feeds two MFMAs (the LDS traffic per MFMA halves), and each lane loads the shared v and D_k
-// rows once for both pairs.  One column tile of 32 at a time (the positive and negative
-// accumulators are the two independent chains); A rows permuted so that lane half h owns the
-// 16 contiguous n = 32t + 16h + [0, 16), read as 32-byte runs of v and D_k.  Each pair's
-// arithmetic is exactly the unpaired kernel's: the same bf16 operands, k order and epilogue order.
-// 512 threads (two waves per SIMD: both pairs' B operands stay in registers).
-template <int D, bool HAS_L>
-__global__ __launch_bounds__(512) void decoder_bf16_paired_kernel(const Bf16DecArgs a) {
-    constexpr int kThreads = 512;
-    constexpr int KS = D / 16;
-    constexpr int NT = D / 32;
-    constexpr int SL = D / 8;
-    extern __shared__ uint4 rt[];
-    const int tid = threadIdx.x;
-    for (int e = tid; e < D * SL; e += kThreads) {
-        const int n = e / SL, q = e - n * SL;
-        uint16_t v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = a.R[(int64_t)(8 * q + j) * D + n];
-        uint4 w;
-        w.x = v[0] | (uint32_t)v[1] << 16;
-        w.y = v[2] | (uint32_t)v[3] << 16;
-        w.z = v[4] | (uint32_t)v[5] << 16;
-        w.w = v[6] | (uint32_t)v[7] << 16;
-        rt[n * SL + (q ^ (n % SL))] = w;
-    }
-    __syncthreads();
-
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int r = lane & 31;
-    const int h = lane >> 5;
-    const int nh = a.n_pairs;  // pairs per half
-    const int n_tiles = (nh + 31) / 32;
-    const int stride = gridDim.x * (kThreads / 64);
-#pragma unroll 1
-    for (int tile = blockIdx.x * (kThreads / 64) + wave; tile < n_tiles; tile += stride) {
-        const int p = tile * 32 + r;
-        const bool valid = p < nh;
-        const int prp = valid ? a.rows[p] : 0;
-        const int prn = valid ? a.rows[nh + p] : 0;
-        const int pc = valid ? a.cols[p] : 0;
-        const int pk = (valid && a.rel) ? a.rel[p] : 0;
-        const uint16_t* up = a.row_table + (int64_t)prp * a.ld_row;
-        const uint16_t* un = a.row_table + (int64_t)prn * a.ld_row;
-        const uint16_t* v = a.col_table + (int64_t)pc * a.ld_col;
-        const uint16_t* lk = HAS_L ? a.L + (int64_t)pk * D : nullptr;
-        bf16x8 bp[KS], bn[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const uint4 u1 = *reinterpret_cast<const uint4*>(up + 16 * s + 8 * h);
-            const uint4 u2 = *reinterpret_cast<const uint4*>(un + 16 * s + 8 * h);
-            uint4 ll = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
-            if (HAS_L) ll = *reinterpret_cast<const uint4*>(lk + 16 * s + 8 * h);
-            const uint32_t w1[4] = {u1.x, u1.y, u1.z, u1.w}, w2[4] = {u2.x, u2.y, u2.z, u2.w},
-                           lw[4] = {ll.x, ll.y, ll.z, ll.w};
-            bf16v8 x1, x2;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                x1[2 * j] = (__bf16)(bf_lo(w1[j]) * bf_lo(lw[j]));
-                x1[2 * j + 1] = (__bf16)(bf_hi(w1[j]) * bf_hi(lw[j]));
-                x2[2 * j] = (__bf16)(bf_lo(w2[j]) * bf_lo(lw[j]));
-                x2[2 * j + 1] = (__bf16)(bf_hi(w2[j]) * bf_hi(lw[j]));
-            }
-            bp[s] = valid ? __builtin_bit_cast(bf16x8, x1) : bf16x8{};
-            bn[s] = valid ? __builtin_bit_cast(bf16x8, x2) : bf16x8{};
-        }
-        float partp = 0.f, partn = 0.f;
-#pragma unroll 1
-        for (int t = 0; t < NT; ++t) {
-            // lane half h owns n = 32t + 16h + [0, 16): register j of the accumulator
-            const int nb0 = 32 * t + 16 * h;
-            uint4 ev[2], el[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) ev[i] = *reinterpret_cast<const uint4*>(v + nb0 + 8 * i);
-            // A row m = r holds C row m = (j&3) + 8(j>>2) + 4h' of register j, lane half h'
-            const int na = 32 * t + 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
-            f32x16 accp = {}, accn = {};
-            uint4 wa = rt[na * SL + (h ^ (na % SL))];
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                uint4 xa = wa;
-                if (s + 1 < KS) xa = rt[na * SL + ((2 * (s + 1) + h) ^ (na % SL))];
-                accp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa), bp[s], accp, 0, 0, 0);
-                accn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa), bn[s], accn, 0, 0, 0);
-                wa = xa;
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-                el[i] = HAS_L ? *reinterpret_cast<const uint4*>(lk + nb0 + 8 * i)
-                              : make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const uint32_t vw[4] = {ev[i].x, ev[i].y, ev[i].z, ev[i].w},
-                               lw[4] = {el[i].x, el[i].y, el[i].z, el[i].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float c0 = bf_lo(lw[j]) * bf_lo(vw[j]), c1 = bf_hi(lw[j]) * bf_hi(vw[j]);
-                    partp = fmaf(accp[8 * i + 2 * j], c0, partp);
-                    partp = fmaf(accp[8 * i + 2 * j + 1], c1, partp);
-                    partn = fmaf(accn[8 * i + 2 * j], c0, partn);
-                    partn = fmaf(accn[8 * i + 2 * j + 1], c1, partn);
-                }
-            }
-        }
-        partp += __shfl_xor(partp, 32);
-        partn += __shfl_xor(partn, 32);
-        if (h == 0 && valid) {
-            a.out[p] = partp;
-            a.out[nh + p] = partn;
-        }
-    }
-}
-
-// Column-shared form of the paired layout: a positive (u_p, v) and its negative (u_n, v) share
+// Paired layout (config 5): a positive (u_p, v) and its negative (u_n, v) share
 // v and D_k, so uᵀ·D_k·R·D_k·v = (u ∘ D_k)ᵀ · T with T = R·(D_k ∘ v) computed ONCE for both:
 //     T[i][p] = Σ_n R[i][n] · bf16(D_k[n] v_n)      on v_mfma_f32_32x32x16_bf16
 // (A = R rows from LDS, B = the pairs' scaled v rows, built once per tile), then
 //     pos[p] = Σ_i u_p[i] D_k[i] T[i][p],   neg[p] = Σ_i u_n[i] D_k[i] T[i][p]
 // in the epilogue (fp32; a product of two bf16 values is exact in fp32) — half the MFMAs of
-// the row-side form above, one accumulator chain, and 64 B-operand VGPRs instead of 128, so
-// more waves per SIMD hide the row gathers.  The A rows are permuted as above: lane half h
+// contracting each pair's row side on its own (round 3's first half: one wave scored the
+// positive and negative tiles with two MFMA chains, 128 B-operand VGPRs, 2 waves per SIMD:
+// 311.7 µs against 221.7 µs for this form), one accumulator chain, and 64 B-operand VGPRs,
+// so 3 waves per SIMD hide the row gathers.  The A rows are permuted as above: lane half h
 // owns the 16 contiguous i = 32t + 16h + [0, 16) of column tile t (32-byte runs of u_p, u_n
 // and D_k).  The bf16 operand rounding sits on D_k∘v instead of u∘D_k: the scores agree with
 // the row-side kernels to bf16 operand rounding, not bitwise.
@@ -522,14 +407,6 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
     const int n_tiles = (n_half + 31) / 32;
     const int lds = d * d * 2;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#ifdef DG_DEC_ROWSIDE  // A/B builds: the row-side paired kernel (two MFMA chains per tile)
-    constexpr int kThreads = 512;
-    static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
-    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_paired_kernel<256, true>), 160 * 1024, configured_l);
-    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_paired_kernel<256, false>), 160 * 1024, configured_nl);
-#define DG_DEC_LAUNCH(DD, HL) \
-    hipLaunchKernelGGL((decoder_bf16_paired_kernel<DD, HL>), dim3(blocks), dim3(kThreads), lds, st, a)
-#else
     if (!dg::aligned16(G)) return DG_EALIGN;  // R rows are staged into LDS in 16-byte pieces
     constexpr int kThreads = DG_DEC_CS_THREADS;
     static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
@@ -540,7 +417,6 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
 #define DG_DEC_LAUNCH(DD, HL) \
     hipLaunchKernelGGL((decoder_bf16_colshared_kernel<DD, HL, kThreads, false>), dim3(blocks), dim3(kThreads), lds, \
                        st, a)
-#endif
     int blocks = (n_tiles + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > 256) blocks = 256;  // persistent: one R-holding workgroup per CU
     const bool hl = l_table != nullptr;
