@@ -392,9 +392,12 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 #pragma unroll 1
         while (gl < T.g_count && wi >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
         float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row_ok && gl < T.g_count)
-            res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(a.g[T.g_begin + gl], 0, r, wi - base, wi - base,
-                                                             ybuf[wave]);
+        if (row_ok && gl < T.g_count) {
+            const SegGroupK& g = a.g[T.g_begin + gl];
+            const int k = wi - base;
+            const int c = k / g.chunk;  // (several chunks: a rank's row block of N <= 2 relation sets)
+            res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(g, c, r, k - c * g.chunk, k, ybuf[wave]);
+        }
         if (lane < DOUT4) zbuf[wave][0][lane] = res;
     }
     __syncthreads();

@@ -77,9 +77,13 @@ STAGED_PROJ = os.environ.get("DG_STAGED_PROJ", "1") != "0"
 # reassociated; DG_FUSED_SEG=0 keeps dg_gcn_fused_f32 with the projection epilogue + P
 FUSED_SEG = os.environ.get("DG_FUSED_SEG", "1") != "0"
 # config S's N-GPU rank share (seg mode): each row of the rank's block finished by one
-# dg_gcn_fused_seg_f32 workgroup whose 16 waves loop over the row's N relation sets
-# (DG_SEG_FUSED=0: dg_spmm_seg_f32 partials + the epilogue launch)
+# dg_gcn_fused_seg_f32 workgroup, one wave per relation of the row's N relation sets
+# (DG_SEG_FUSED=0, or more relations a row: dg_spmm_seg_f32 partials + the epilogue launch)
 SEG_FUSED = os.environ.get("DG_SEG_FUSED", "1") != "0"
+# ... when a row has at most this many relations (one wave each).  Rank shares measured
+# (bench.py --simulate-world N, max over ranks): N = 2 18.7 µs fused against 27.8 seg + epilogue;
+# N = 4 (28 relations a drug row, 16 looping waves) 25.2 against 25.1; N = 8 35.6 against 25.6
+SEG_FUSED_MAX_ITEMS = int(os.environ.get("DG_SEG_FUSED_MAX", "16"))
 STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 
 
@@ -568,7 +572,8 @@ class ForwardPlan:
         launches: List[Callable[[], None]] = []
         fused_t = self.fused
         gathers = []
-        if self.seg_mode and SEG_FUSED:
+        if self.seg_mode and SEG_FUSED and all(sum(g.groups[et].n_rels for et in ets) <= SEG_FUSED_MAX_ITEMS
+                                               for ets in self.targets.values()):
             # every node type row-split: one launch finishes this rank's row block of each
             # (its workgroups' waves loop over the N relation sets), then the all-gathers
             seg_w = seg_w or {}
