@@ -318,9 +318,9 @@ struct FsTargetK {
     int32_t g_count;
     int32_t relu;
     int32_t block_begin;
-    int32_t waves;  // waves per row: one per relation (items <= 16), else the workgroup's 16
+    int32_t waves;  // waves per row: one per relation of the target's groups (<= 16)
     int32_t rpb;    // rows per workgroup: nw / waves (at most kFsMaxRpb)
-    int32_t items;  // (group, relation) items of a row: the relations of every group, every chunk
+    int32_t pad;
 };
 
 struct FsArgs {
@@ -336,15 +336,11 @@ constexpr int kFsMaxRpb = 1;  // A/B: one row per workgroup
 constexpr int kFsMaxRpb = 4;
 #endif
 
-// groups per target in the looped form's per-wave accumulators (config S: 2)
-constexpr int kFsLoopGroups = 4;
-
-template <int LP, bool PROJ, int NW, bool LOOP>
+template <int LP, bool PROJ, int NW>
 __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;
-    constexpr int KG = LOOP ? kFsLoopGroups : 1;  // per-wave group sums kept
     __shared__ float4 ybuf[NW][16];
-    __shared__ float4 zbuf[NW][KG][DOUT4];
+    __shared__ float4 zbuf[NW][DOUT4];
     __shared__ float4 nbuf[kFsMaxRpb][DG_MAX_GROUPS][DOUT4];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -353,75 +349,35 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
     while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
     const FsTargetK& T = a.t[ti];
     const int r0 = (blockIdx.x - T.block_begin) * T.rpb;
-    // wave -> (row slot, item wi): item i is relation k of group gl (the slot's groups'
-    // relations back to back; k = c·chunk + t: chunk c, relation t).  With at most 16 items a
-    // row (config S on one GPU) every wave owns one item; a row block of N relation sets
-    // (LOOP: config S's N-GPU rank share) has the workgroup's 16 waves loop over items wi,
-    // wi + 16, ..., each summing its items per group in item order (registers for 4 groups:
-    // the one-item form keeps its lower register count and occupancy)
+    // wave -> (row slot, group gl, relation k of the group): each slot's groups' relations back
+    // to back; k = c·chunk + t (chunk c, relation t: a rank's row block of several relation
+    // sets keeps one chunk per set)
     const int slot = wave / T.waves;
     const int wi = wave - slot * T.waves;
     const int r = r0 + slot;
-    const bool row_ok = slot < T.rpb && r < T.n_rows;
-    if constexpr (LOOP) {
-        float4 acc[KG];
-#pragma unroll
-        for (int q = 0; q < KG; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row_ok) {
+    int gl = 0, base = 0;
 #pragma unroll 1
-            for (int i = wi; i < T.items; i += T.waves) {
-                int gl = 0, base = 0;
-#pragma unroll 1
-                while (gl + 1 < T.g_count && i >= base + a.g[T.g_begin + gl].n_rels)
-                    base += a.g[T.g_begin + gl++].n_rels;
-                const SegGroupK& g = a.g[T.g_begin + gl];
-                const int k = i - base;
-                const int c = k / g.chunk;
-                const float4 res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(g, c, r, k - c * g.chunk, k, ybuf[wave]);
-#pragma unroll
-                for (int q = 0; q < KG; ++q)
-                    if (q == gl) dg::add4(acc[q], res);
-            }
-        }
-        if (lane < DOUT4) {
-#pragma unroll
-            for (int q = 0; q < KG; ++q) zbuf[wave][q][lane] = acc[q];
-        }
-    } else {
-        int gl = 0, base = 0;
-#pragma unroll 1
-        while (gl < T.g_count && wi >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
-        float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row_ok && gl < T.g_count) {
-            const SegGroupK& g = a.g[T.g_begin + gl];
-            const int k = wi - base;
-            const int c = k / g.chunk;  // (several chunks: a rank's row block of N <= 2 relation sets)
-            res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(g, c, r, k - c * g.chunk, k, ybuf[wave]);
-        }
-        if (lane < DOUT4) zbuf[wave][0][lane] = res;
+    while (gl < T.g_count && wi >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
+    float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (slot < T.rpb && r < T.n_rows && gl < T.g_count) {
+        const SegGroupK& g = a.g[T.g_begin + gl];
+        const int k = wi - base;
+        const int c = k / g.chunk;
+        res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(g, c, r, k - c * g.chunk, k, ybuf[wave]);
     }
+    if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
-    // one wave per (row slot, group): the group's sums in order (LOOP: the slot's 16 waves' sums
-    // in wave order, i.e. item order; else the group's own waves, i.e. relation order), then
-    // L2-normalised
+    // one wave per (row slot, group): its relations summed in order, L2-normalised
     if (wave < T.rpb * T.g_count) {
         const int s2 = wave / T.g_count, gg = wave - s2 * T.g_count;
+        int gb = s2 * T.waves;
+#pragma unroll 1
+        for (int u = 0; u < gg; ++u) gb += a.g[T.g_begin + u].n_rels;
+        const int K = a.g[T.g_begin + gg].n_rels;
         const int q = lane % DOUT4;
-        float4 sum;
-        if constexpr (LOOP) {
-            const int gb = s2 * T.waves;
-            sum = zbuf[gb][gg][q];
+        float4 sum = zbuf[gb][q];
 #pragma unroll 1
-            for (int u = 1; u < T.waves; ++u) dg::add4(sum, zbuf[gb + u][gg][q]);
-        } else {
-            int gb = s2 * T.waves;
-#pragma unroll 1
-            for (int u = 0; u < gg; ++u) gb += a.g[T.g_begin + u].n_rels;
-            const int K = a.g[T.g_begin + gg].n_rels;
-            sum = zbuf[gb][0][q];
-#pragma unroll 1
-            for (int u = 1; u < K; ++u) dg::add4(sum, zbuf[gb + u][0][q]);
-        }
+        for (int u = 1; u < K; ++u) dg::add4(sum, zbuf[gb + u][q]);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
         float ss = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
 #pragma unroll
@@ -551,7 +507,6 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
     }
     int64_t blocks = 0;
     int nw = 1;
-    bool loop = false;  // some target has more than 16 items a row: every target runs the looped form
     for (int t = 0; t < n_targets; ++t) {
         const dg_fused_target& s = targets[t];
         if (!s.out || !dg::aligned16(s.out) || s.n_rows < 0 || s.g_count < 1 || s.g_begin < 0 ||
@@ -562,11 +517,9 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
             if (groups[g].n_rows != s.n_rows) return DG_EINVAL;
             items += groups[g].n_rels;
         }
-        // one wave per item (<= 16 a row), else 16 looping waves (at most kFsLoopGroups groups)
-        if (items > 16 && s.g_count > kFsLoopGroups) return DG_EINVAL;
-        const int waves = items > 16 ? 16 : items;
+        if (items > 16) return DG_EINVAL;  // one wave per relation of the row
+        const int waves = items;
         nw = waves > nw ? waves : nw;
-        loop = loop || items > 16;
         FsTargetK& k = a.t[t];
         k.out = s.out;
         k.n_rows = s.n_rows;
@@ -574,7 +527,6 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
         k.g_count = s.g_count;
         k.relu = (s.flags & DG_EPI_RELU) ? 1 : 0;
         k.waves = waves;
-        k.items = items;
     }
     // rows per workgroup: a target with fewer relations per row than the widest one fills the
     // workgroup's waves with more rows
@@ -590,19 +542,17 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
     if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);
-#define DG_FS_LAUNCH(NW, LOOP)                                                                     \
-    if (proj)                                                                                      \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, LOOP>), grid, block, 0, st, a);     \
-    else if (d_in == 64)                                                                           \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW, LOOP>), grid, block, 0, st, a);    \
-    else                                                                                           \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW, LOOP>), grid, block, 0, st, a);
-    if (loop) {
-        DG_FS_LAUNCH(16, true)
-    } else if (nw <= 8) {
-        DG_FS_LAUNCH(8, false)
+#define DG_FS_LAUNCH(NW)                                                                      \
+    if (proj)                                                                                 \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW>), grid, block, 0, st, a);      \
+    else if (d_in == 64)                                                                      \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW>), grid, block, 0, st, a);     \
+    else                                                                                      \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW>), grid, block, 0, st, a);
+    if (nw <= 8) {
+        DG_FS_LAUNCH(8)
     } else {
-        DG_FS_LAUNCH(16, false)
+        DG_FS_LAUNCH(16)
     }
 #undef DG_FS_LAUNCH
     return dg::launch_status();

@@ -80,10 +80,10 @@ FUSED_SEG = os.environ.get("DG_FUSED_SEG", "1") != "0"
 # dg_gcn_fused_seg_f32 workgroup, one wave per relation of the row's N relation sets
 # (DG_SEG_FUSED=0, or more relations a row: dg_spmm_seg_f32 partials + the epilogue launch)
 SEG_FUSED = os.environ.get("DG_SEG_FUSED", "1") != "0"
-# ... when a row has at most this many relations (one wave each).  Rank shares measured
-# (bench.py --simulate-world N, max over ranks): N = 2 18.7 µs fused against 27.8 seg + epilogue;
-# N = 4 (28 relations a drug row, 16 looping waves) 25.2 against 25.1; N = 8 35.6 against 25.6
-SEG_FUSED_MAX_ITEMS = int(os.environ.get("DG_SEG_FUSED_MAX", "16"))
+# ... when a row has at most 16 relations (one wave each: N <= 2 for config S).  A form whose 16
+# waves looped over more relations measured 25.2 µs a rank share at N = 4 (seg + epilogue 25.1)
+# and 35.6 at N = 8 (25.6), so it was not kept
+SEG_FUSED_MAX_ITEMS = 16
 STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 
 

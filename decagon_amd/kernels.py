@@ -283,9 +283,8 @@ class PreparedSeg:
 
 class PreparedFusedSeg:
     """A fixed dg_gcn_fused_seg_f32 launch: targets = [(out tensor, n_rows, [SegSpec], relu)],
-    each output row finished by one workgroup — one wave per relation when a row has at most 16,
-    else 16 looping waves (at most 4 groups a target); with weight stacks (d_in 64 → d_out 32)
-    the reassociated layer 2."""
+    each output row finished by one workgroup, one wave per relation (at most 16 a row; groups
+    chunk-merged, any chunks); with weight stacks (d_in 64 → d_out 32) the reassociated layer 2."""
 
     def __init__(self, targets, d_in: int, d_out: int):
         specs, tarr = [], (DgFusedTarget * len(targets))()
@@ -293,8 +292,8 @@ class PreparedFusedSeg:
             _dev(out, torch.float32, "out")
             if out.numel() < n_rows * d_out:
                 raise ValueError("fused output too small")
-            if sum(s.n_rels for s in gspecs) > 16 and len(gspecs) > 4:
-                raise ValueError("more than 16 relations per target row: at most 4 groups")
+            if sum(s.n_rels for s in gspecs) > 16:
+                raise ValueError("at most 16 relations per target row")
             tarr[t].out, tarr[t].n_rows = out.data_ptr(), n_rows
             tarr[t].g_begin, tarr[t].g_count = len(specs), len(gspecs)
             tarr[t].flags = _lib.DG_EPI_RELU if relu else 0

@@ -209,10 +209,8 @@ int dg_spmm_seg_f32(const dg_seg_group* groups /* HOST array */, int32_t n_group
  *   out_t[r] = act( sum_g l2norm( sum_{t < n_rels_g} seg-sum_g(r, t) ) )
  *
  * with seg-sum as dg_spmm_seg_f32's over relation t = c*chunk + t' of the group (projected by
- * W[slab] when the groups carry w).  One workgroup per row: one wave per (group, relation) when
- * a row has at most 16 relations in total, else (at most 4 groups a target) 16 waves each
- * summing every 16th relation of the row per group, then the 16 sums in wave order; groups
- * summed in order.
+ * W[slab] when the groups carry w), at most 16 relations a target row in total.  One
+ * workgroup per row, one wave per (group, relation); relations and groups summed in order.
  * With w this is layer 2 (layers.py:109-118) reassociated, Σ_k (Â_k·H1_j)·W2_k, so layer 1
  * needs no projection of its rows.  Replaces layers.py:85-94 / 109-118 and model.py:74-75,
  * 85-88 for such node types. */
