@@ -141,15 +141,18 @@ class TorchForward(_Forward):
             return h1, self._layer(lambda et, k: h1[et[1]] @ self.w2[et][k], False)
 
 
-def _time(fwd, seconds: float):
+def _time(fwd, seconds: float, min_reps: int = 50, max_seconds: float = 30.0):
+    """Per-forward wall times: at least `seconds` and at least `min_reps` forwards (BASELINE.md:
+    the median of >= 50 runs), unless `max_seconds` run out first."""
     fwd.run()  # warm-up (allocator, thread pool)
-    reps, t0 = 0, time.perf_counter()
+    times, t0 = [], time.perf_counter()
     while True:
+        t = time.perf_counter()
         fwd.run()
-        reps += 1
+        times.append(time.perf_counter() - t)
         el = time.perf_counter() - t0
-        if el >= seconds or (reps >= 2 and el * (reps + 1) / reps > seconds * 1.5):
-            return reps, el
+        if (el >= seconds and len(times) >= min_reps) or el >= max_seconds:
+            return times, el
 
 
 def measure(graph, h1: int, h2: int, seconds: float = 10.0, seed: int = 1234) -> dict:
@@ -162,20 +165,20 @@ def measure(graph, h1: int, h2: int, seconds: float = 10.0, seed: int = 1234) ->
     torch.set_num_threads(threads)
     try:
         tf = TorchForward(graph, h1, h2, seed)
-        reps_t, el_t = _time(tf, seconds)
+        times_t, el_t = _time(tf, seconds)
     finally:
         torch.set_num_threads(prev)
     sf = ScipyForward(graph, h1, h2, seed)
-    reps_s, el_s = _time(sf, seconds)
+    times_s, el_s = _time(sf, seconds)
     edges = 2 * sf.nnz
     model = cpu_model()
+    med_t, med_s = float(np.median(times_t)), float(np.median(times_s))
     return {
-        "value": edges * reps_t / el_t, "unit": "edges/s", "cores": threads, "kind": "port",
+        "value": edges / med_t, "unit": "edges/s", "cores": threads, "kind": "port",
         "cpu_model": model, "threads_rule": why,
-        "sample": (f"{reps_t} full 2-layer forwards of config {graph.name} ({sf.nnz} nnz/layer) in {el_t:.1f} s, "
-                   f"torch-CPU fp32 CSR, {threads} threads on {model}"),
-        "ms_per_forward": el_t * 1e3 / reps_t,
-        "scipy_1thread": {"value": edges * reps_s / el_s, "unit": "edges/s", "cores": 1,
-                          "ms_per_forward": el_s * 1e3 / reps_s,
-                          "sample": f"{reps_s} forwards in {el_s:.1f} s, scipy.sparse CSR fp32, 1 thread"},
+        "sample": (f"median of {len(times_t)} full 2-layer forwards of config {graph.name} ({sf.nnz} nnz/layer, "
+                   f"{el_t:.1f} s), torch-CPU fp32 CSR, {threads} threads on {model}"),
+        "ms_per_forward": med_t * 1e3, "ms_per_forward_mean": el_t * 1e3 / len(times_t),
+        "scipy_1thread": {"value": edges / med_s, "unit": "edges/s", "cores": 1, "ms_per_forward": med_s * 1e3,
+                          "sample": f"median of {len(times_s)} forwards ({el_s:.1f} s), scipy.sparse CSR fp32, 1 thread"},
     }
