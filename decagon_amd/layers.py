@@ -134,14 +134,35 @@ def _glorot_stack(k: int, d_in: int, d_out: int) -> torch.Tensor:
     return torch.from_numpy(arr).to(runtime.param_device())
 
 
+def _dropout(ctx, layer, tag: int):
+    """(keep, device state, tag) for a layer called on its own with dropout > 0, else None: the
+    counter-based masks of dropout.h from the layer's own state {seed, step} in the session,
+    advanced once per run, so every run draws new masks (TF's RNG stream itself is not
+    reproducible; the distribution is: kept with probability keep, scaled by 1/keep)."""
+    v = ctx.value(layer.dropout) if isinstance(layer.dropout, Node) else layer.dropout
+    rate = float(v)
+    if rate == 0.0:
+        return None
+    if not 0.0 < rate < 1.0:
+        raise ValueError(f"dropout rate {rate} outside [0, 1)")
+    key = ("layer_dropout_state", id(layer))
+    cache = ctx.session.caches
+    if key not in cache:
+        cache[key] = torch.tensor([layer.dropout_seed, 0], dtype=torch.int64, device=ctx.session.device)
+    state = cache[key]
+    kernels.dropout_advance(state)
+    return 1.0 - rate, state, tag
+
+
 def _check_dropout(ctx, dropout) -> None:
     v = ctx.value(dropout) if isinstance(dropout, Node) else dropout
     if float(v) != 0.0:
-        raise NotImplementedError(
-            "dropout > 0 is the training path (SURVEY §8f); the forward parity path runs at 0")
+        raise NotImplementedError("a decoder's _call with dropout > 0 (dead code in the reference, SURVEY §0.4)")
 
 
 class _GraphConvBase(MultiLayer):
+    dropout_seed = 20180702  # the standalone layer's dropout masks (a model's start at 20180701)
+
     def _make_weights(self, d_in: int, d_out: int) -> None:
         self.weights_stack = _glorot_stack(self.num_types, d_in, d_out)
         scope = self._scope()
@@ -177,10 +198,10 @@ class GraphConvolutionSparseMulti(_GraphConvBase):
             raise NotImplementedError("sigmoid activation inside a GCN layer is not on the HIP path")
 
         def fn(ctx):
-            _check_dropout(ctx, self.dropout)
+            drop = _dropout(ctx, self, 1 << 16)
             grp = self._adj_group(ctx, kind == "relu")
             feat = runtime.feature_csr(ctx, inputs)
-            return runtime.gcn_layer(grp, self.weights_stack, feat, self.output_dim, kind == "relu")
+            return runtime.gcn_layer(grp, self.weights_stack, feat, self.output_dim, kind == "relu", drop)
 
         return Node(f"{self.name}/out", fn)
 
@@ -204,11 +225,11 @@ class GraphConvolutionMulti(_GraphConvBase):
             raise NotImplementedError("sigmoid activation inside a GCN layer is not on the HIP path")
 
         def fn(ctx):
-            _check_dropout(ctx, self.dropout)
+            drop = _dropout(ctx, self, 2 << 16)
             grp = self._adj_group(ctx, kind == "relu")
             h = ctx.value(inputs)
             h = runtime.as_device_f32(h)
-            return runtime.gcn_layer_dense(grp, self.weights_stack, h, self.output_dim, kind == "relu")
+            return runtime.gcn_layer_dense(grp, self.weights_stack, h, self.output_dim, kind == "relu", drop)
 
         return Node(f"{self.name}/out", fn)
 

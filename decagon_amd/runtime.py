@@ -260,34 +260,56 @@ def _conv(grp: DeviceGroup, x: torch.Tensor, d_out: int, per_rel_relu: bool) -> 
 
 
 def gcn_layer(grp: DeviceGroup, W: torch.Tensor, feat: Optional[HostCSR], d_out: int,
-              per_rel_relu: bool) -> torch.Tensor:
-    """GraphConvolutionSparseMulti._call (layers.py:85-94) for one edge type."""
+              per_rel_relu: bool, drop=None) -> torch.Tensor:
+    """GraphConvolutionSparseMulti._call (layers.py:85-94) for one edge type.  drop = (keep,
+    device state {seed, step}, tag): dropout_sparse (layers.py:23-31, :88) drawn per relation —
+    identity features: a row mask on each W_k; sparse features: a mask on X_j's values inside
+    the shared-pattern SpMM (the ForwardPlan's masks, dropout.h)."""
     K, F, _ = W.shape
+    dev = W.device
     if feat is None:
         if F != grp.n_cols:
             raise ValueError("identity features need one weight row per node")
         x = W
+        if drop is not None:
+            keep, state, tag = drop
+            x = torch.empty_like(W)
+            kernels.dropout_rows(W, x, state, tag, keep)
     else:
-        from .sparse import merge_chunks
-
-        fm = merge_chunks([feat] * K, np.arange(K), 1, K)
-        dev = W.device
         x = torch.empty((K, feat.shape[0], d_out), device=dev, dtype=torch.float32)
-        kernels.spmm_groups([kernels.RelGroupSpec(
-            torch.from_numpy(fm.rowptr).to(dev), torch.from_numpy(fm.vcol).to(dev),
-            torch.from_numpy(fm.val).to(dev), W, x, feat.shape[0], K, d_out, K * F,
-            vcol_max=int(fm.vcol.max()) if fm.nnz else -1)], d_out)
+        if drop is not None:
+            keep, state, tag = drop
+            spec = kernels.RelGroupSpec(torch.from_numpy(feat.rowptr).to(dev), torch.from_numpy(feat.col).to(dev),
+                                        torch.from_numpy(feat.val).to(dev), W, x, feat.shape[0], K, d_out, F,
+                                        vcol_max=int(feat.col.max()) if feat.nnz else -1, shared=True,
+                                        drop=(state, tag, keep))
+        else:
+            from .sparse import merge_chunks
+
+            fm = merge_chunks([feat] * K, np.arange(K), 1, K)
+            spec = kernels.RelGroupSpec(torch.from_numpy(fm.rowptr).to(dev), torch.from_numpy(fm.vcol).to(dev),
+                                        torch.from_numpy(fm.val).to(dev), W, x, feat.shape[0], K, d_out, K * F,
+                                        vcol_max=int(fm.vcol.max()) if fm.nnz else -1)
+        kernels.spmm_groups([spec], d_out)
     return _conv(grp, x, d_out, per_rel_relu)
 
 
 def gcn_layer_dense(grp: DeviceGroup, W: torch.Tensor, h: torch.Tensor, d_out: int,
-                    per_rel_relu: bool) -> torch.Tensor:
-    """GraphConvolutionMulti._call (layers.py:109-118) for one edge type."""
+                    per_rel_relu: bool, drop=None) -> torch.Tensor:
+    """GraphConvolutionMulti._call (layers.py:109-118) for one edge type.  drop = (keep, device
+    state, tag): tf.nn.dropout of the inputs drawn per relation (layers.py:112) — an element mask
+    M_k on H for each relation, then H∘M_k/keep · W_k."""
     K, d_in, _ = W.shape
     if h.shape != (grp.n_cols, d_in):
         raise ValueError(f"inputs shape {tuple(h.shape)} != ({grp.n_cols}, {d_in})")
     P = torch.empty((K, grp.n_cols, d_out), device=h.device, dtype=torch.float32)
-    kernels.PreparedGemm(h, (0, d_in, 1), W, (d_in * d_out, d_out, 1), P, (grp.n_cols * d_out, d_out, 1),
+    a, a_stride = h, 0
+    if drop is not None:
+        keep, state, tag = drop
+        a = torch.empty((K, grp.n_cols, d_in), device=h.device, dtype=torch.float32)
+        kernels.dropout_elems(h.contiguous(), a, state, tag, keep)
+        a_stride = grp.n_cols * d_in
+    kernels.PreparedGemm(a, (a_stride, d_in, 1), W, (d_in * d_out, d_out, 1), P, (grp.n_cols * d_out, d_out, 1),
                          grp.n_cols, d_out, d_in, K)()
     return _conv(grp, P, d_out, per_rel_relu)
 

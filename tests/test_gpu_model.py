@@ -325,3 +325,55 @@ def test_training_sums_mode_matches_oracle(monkeypatch):
         s2 = sum(orc.sparse_dense_matmul(g.adj[et][k], h1[j] @ w2[et][k].astype(np.float64)) for k in range(K))
         assert rel_err(plan._layer1.views[et].view(n[i], 64).cpu().numpy(), s1) <= TOL
         assert rel_err(plan._layer2.views[et].view(n[i], 32).cpu().numpy(), s2) <= TOL
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_standalone_layer_dropout_matches_oracle(golden_S, dense):
+    """A layer called on its own with dropout > 0 (layers.py:88 dropout_sparse on the identity
+    features, :112 tf.nn.dropout of the dense inputs), drawn per relation with the device's
+    counter-based masks: each run against the float64 layer on the SAME masks, regenerated by
+    oracle.dropout_scale from the layer's state {seed, step}; two runs draw different masks."""
+    import decagon_amd as dg
+    from decagon_amd.layers import _GraphConvBase
+    from oracle import decagon_oracle as orc
+
+    z = golden_S
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    keep = 0.75
+    ph = dg.construct_placeholders({(1, 1): 6})
+    adj = {(1, 1): [ph["adj_mats_1,1,%d" % k] for k in range(6)]}
+    feed = {ph["adj_mats_1,1,%d" % k]: (z[f"adj_1_1_{k}_coords"], z[f"adj_1_1_{k}_values"], (400, 400))
+            for k in range(6)}
+    A = [(z[f"adj_1_1_{k}_coords"], z[f"adj_1_1_{k}_values"], (400, 400)) for k in range(6)]
+    if dense:
+        rng = np.random.default_rng(5)
+        H = rng.standard_normal((400, 64)).astype(np.float32)
+        W = [rng.uniform(-0.2, 0.2, (64, 32)).astype(np.float32) for _ in range(6)]
+        lay = dg.GraphConvolutionMulti(64, 32, adj, dropout=1 - keep, edge_type=(1, 1), num_types=6)
+        x = dg.placeholder(np.float32, name="h_in")
+        feed[x] = H
+        tag, n_mask = 2 << 16, 6 * 400 * 64
+    else:
+        W = [z[f"w1_1_1_{k}"] for k in range(6)]
+        lay = dg.GraphConvolutionSparseMulti({1: 400}, 64, adj, {1: 400}, dropout=1 - keep, edge_type=(1, 1),
+                                             num_types=6)
+        x = ph["feat_1"]
+        feed[x] = (np.stack([np.arange(400)] * 2, 1), np.ones(400), (400, 400))
+        tag, n_mask = 1 << 16, 6 * 400
+    for k in range(6):
+        lay.vars["weights_%d" % k].load(W[k])
+    node = lay(x)
+    sess = dg.Session()
+    runs = [sess.run(node, feed) for _ in range(2)]
+    for step, got in enumerate(runs, start=1):
+        m = orc.dropout_scale(_GraphConvBase.dropout_seed, step, tag, n_mask, keep).astype(np.float64)
+        outs = []
+        for k in range(6):
+            if dense:
+                xk = (H.astype(np.float64) * m.reshape(6, 400, 64)[k]) @ W[k].astype(np.float64)
+            else:
+                xk = m.reshape(6, 400)[k][:, None] * W[k].astype(np.float64)
+            outs.append(np.maximum(orc.sparse_dense_matmul(A[k], xk), 0))
+        assert rel_err(got, orc.l2_normalize_rows(np.sum(outs, 0))) <= TOL, step
+    assert not np.allclose(runs[0], runs[1])
