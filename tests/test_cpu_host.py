@@ -365,32 +365,3 @@ def test_global_variables_are_scoped_to_their_graph():
     init_a._fn(_Ctx())
     assert all(not np.array_equal(va[k], v.eval()) for k, v in a.layers1[0, 0].vars.items())
     assert all(np.array_equal(vb[k], v.eval()) for k, v in b.layers1[0, 0].vars.items())
-
-
-def test_slot_columns_cover_every_pair_once():
-    """kernels.slot_columns (config 5's column entries): every pair of every slot in exactly one
-    entry of its own slot's tiles, an entry's pairs all of its column, at most two, two-pair
-    entries before one-pair ones, tiles of 32 padded with empty entries."""
-    from decagon_amd import kernels
-
-    rng = np.random.default_rng(3)
-    n_slots, batch = 5, 37
-    cols = rng.integers(0, 9, n_slots * batch)
-    ec, ep, ts = kernels.slot_columns(cols, n_slots, batch)
-    assert ec.shape == (32 * len(ts),) and ep.shape == (32 * len(ts), 2)
-    seen = np.zeros(n_slots * batch, int)
-    for t, s in enumerate(ts):
-        ent_c, ent_p = ec[32 * t:32 * t + 32], ep[32 * t:32 * t + 32]
-        two = ent_p[:, 1] >= 0
-        for c, (p0, p1) in zip(ent_c, ent_p):
-            if c < 0:
-                assert p0 < 0 and p1 < 0
-                continue
-            for p in (p0, p1):
-                if p >= 0:
-                    assert p // batch == s and cols[p] == c
-                    seen[p] += 1
-        if t == 0 or ts[t - 1] != s:  # a slot's first tile: two-pair entries lead
-            k = int(two.sum())
-            assert two[:k].all()
-    assert (seen == 1).all()
