@@ -493,18 +493,17 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
     reps = args.kernel_reps if steps >= 50 else 20
-    # the step's one launch (sampler + scores + hinge: dg_slot_score_hinge_cols_bf16), alone
-    k_ms = time_kernel(sc.launch, reps, stream)
-    # flops issued: T = R·(D_k∘v) on the MFMA (2d²) once per scored column — per (positive,
-    # negative) pair in the per-pair form, per column entry of a tile (padding included) in the
-    # column-entry form — the B operand (d) per column and two dots with u∘D_k (2·3d) per pair
-    # on the VALU; the per-pair form of every pair apart would be 2·(2d² + 4d)
-    n_col = sc.tile_slot.numel() * 32 if sc.cols_form else sc.n
-    mfma_flops = n_col * 2 * d * d
-    flops = mfma_flops + n_col * d + sc.n * 6 * d
+    # the step's one launch (sampler + scores + hinge: dg_slot_score_hinge_bf16), alone
+    k_ms = time_kernel(lambda: kernels.slot_score_hinge_bf16(
+        sc.E_row, sc.E_col, sc.rows[:sc.n], sc.cols[:sc.n], sc.alias, sc.s0, sc.s1 - sc.s0, sc.batch, sc.seed, sc.R,
+        sc.D, sc.margin, sc.out, sc.neg_rows, sc.loss, sc._ws), reps, stream)
+    # flops the column-shared paired kernel issues per (positive, negative) pair: T = R·(D_k∘v)
+    # on the MFMA (2d²) once for both, the B operand (d) and two dots with u∘D_k (2·3d) on the
+    # VALU — against 2·(2d² + 4d) when each pair is contracted on its own
+    flop_pp = 2 * d * d + 7 * d
     n = 2 * sc.n
-    tflops = flops / (k_ms * 1e-3) / 1e12
-    mfma_tflops = mfma_flops / (k_ms * 1e-3) / 1e12
+    tflops = sc.n * flop_pp / (k_ms * 1e-3) / 1e12
+    mfma_tflops = sc.n * 2 * d * d / (k_ms * 1e-3) / 1e12
     return {
         "metric": "DEDICOM scored pairs/sec (config 5: d=256 bf16, all 1,928 drug-drug slots)",
         "value": 2 * slots * B * steps / el,
@@ -524,11 +523,9 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
         "loss": float(sc.loss[0]),
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / BF16_PEAK_TFLOPS, "traffic": None,
-                     "kernel": ("decoder_bf16_slotcols_kernel<512> (sampler + scores + hinge, column entries)"
-                                if sc.cols_form else
-                                "decoder_bf16_colshared_kernel<256, true, 768, true> (sampler + scores + hinge)"),
+                     "kernel": "decoder_bf16_colshared_kernel<256, true, 768, true> (sampler + scores + hinge)",
                      "kernel_ms": k_ms,
-                     "algorithmic_flops": flops, "mfma_tflops": mfma_tflops, "scored_columns": n_col,
+                     "algorithmic_flops": sc.n * flop_pp, "mfma_tflops": mfma_tflops,
                      "per_pair_form_tflops": n * (2 * d * d + 4 * d) / (k_ms * 1e-3) / 1e12},
     }
 

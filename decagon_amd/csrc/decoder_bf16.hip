@@ -34,9 +34,6 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 #ifndef DG_DEC_CS_THREADS
 #define DG_DEC_CS_THREADS 768  // column-shared paired kernel: threads per workgroup (one per CU)
 #endif
-#ifndef DG_DEC_COLS_THREADS
-#define DG_DEC_COLS_THREADS 512  // column-entry form (two pairs a lane: 3 waves per SIMD would spill)
-#endif
 
 struct Bf16DecArgs {
     const uint16_t* row_table;
@@ -62,13 +59,6 @@ struct Bf16DecArgs {
     uint32_t* ticket;
     int32_t range, slot0, batch;
     float margin;
-    // column-entry form (dg_slot_score_hinge_cols_bf16): tile t holds 32 entries of local slot
-    // tile_slot[t]; entry e scores column ent_col[e] (-1: empty) for the pairs ent_pair[e]
-    // (up to 2 positives of that column, -1: none)
-    const int32_t* ent_col;
-    const int2* ent_pair;
-    const int32_t* tile_slot;
-    int32_t n_ctiles;
 };
 
 // threads per workgroup: 16 waves, but 12 at d = 256 (its 16 B-operand fragments need the
@@ -367,175 +357,6 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
         }
     }
 }
-
-// Column-entry form of the fused slot step: a slot's positives that share a column share T =
-// R·bf16(D_k∘v) as well (a slot's 512 positives touch ≈ 340 distinct columns at config 5), so
-// each lane owns one COLUMN and up to two of its pairs (the host groups a slot's pairs by
-// column, two to an entry; entries with two pairs first, so a tile's lanes mostly agree).
-// Every pair's arithmetic is exactly the per-pair kernel's (same T column, same epilogue order):
-// the scores and draws are bit-identical to decoder_bf16_colshared_kernel<.., FUSED>; the tiles
-// — and with them the MFMAs and the v gathers — drop by the column sharing (30,848 → 23,402).
-template <int THREADS>
-__global__ __launch_bounds__(THREADS) void decoder_bf16_slotcols_kernel(const Bf16DecArgs a) {
-    constexpr int D = 256;
-    constexpr int KS = D / 16;
-    constexpr int NT = D / 32;
-    constexpr int SL = D / 8;
-    extern __shared__ uint4 rs[];
-    const int tid = threadIdx.x;
-    for (int e = tid; e < D * SL; e += THREADS) {
-        const int i = e / SL, q = e - i * SL;
-        rs[i * SL + (q ^ (i % SL))] = *reinterpret_cast<const uint4*>(a.R + (int64_t)i * D + 8 * q);
-    }
-    __syncthreads();
-
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int r = lane & 31;
-    const int h = lane >> 5;
-    const int nh = a.n_pairs;
-    const int stride = gridDim.x * (THREADS / 64);
-    float wsum = 0.f;
-    const int first = wave * (int)gridDim.x + (int)blockIdx.x;  // round-major (see above)
-#pragma unroll 1
-    for (int tile = first; tile < a.n_ctiles; tile += stride) {
-        const int ent = tile * 32 + r;
-        const int pk = a.slot0 + a.tile_slot[tile];
-        const int col = a.ent_col[ent];
-        const int2 pp = a.ent_pair[ent];
-        const bool ok0 = pp.x >= 0, ok1 = pp.y >= 0;
-        const uint64_t c0 = (uint64_t)a.slot0 * (uint64_t)a.batch;
-        const uint2* tab = a.alias + pk * a.alias_stride;
-        int prn0 = 0, prn1 = 0;
-        if (ok0) prn0 = dg::unigram_draw(tab, a.range, a.seed, c0 + (uint64_t)pp.x);
-        if (ok1) prn1 = dg::unigram_draw(tab, a.range, a.seed, c0 + (uint64_t)pp.y);
-        if (h == 0) {
-            if (ok0) a.neg_out[pp.x] = prn0;
-            if (ok1) a.neg_out[pp.y] = prn1;
-        }
-        const int prp0 = ok0 ? a.rows[pp.x] : 0, prp1 = ok1 ? a.rows[pp.y] : 0;
-        const uint16_t* v = a.col_table + (int64_t)(col < 0 ? 0 : col) * a.ld_col;
-        const uint16_t* lk = a.L + (int64_t)pk * D;
-        bf16x8 b[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const uint4 vv = *reinterpret_cast<const uint4*>(v + 16 * s + 8 * h);
-            const uint4 ll = *reinterpret_cast<const uint4*>(lk + 16 * s + 8 * h);
-            const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w}, lw[4] = {ll.x, ll.y, ll.z, ll.w};
-            bf16v8 x;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                x[2 * j] = (__bf16)(bf_lo(vw[j]) * bf_lo(lw[j]));
-                x[2 * j + 1] = (__bf16)(bf_hi(vw[j]) * bf_hi(lw[j]));
-            }
-            b[s] = col >= 0 ? __builtin_bit_cast(bf16x8, x) : bf16x8{};
-        }
-        float pp0 = 0.f, pn0 = 0.f, pp1 = 0.f, pn1 = 0.f;
-        asm volatile("" ::: "memory");  // the B operand's loads stay ahead of the epilogue's pointers
-#pragma unroll 1
-        for (int t = 0; t < NT; ++t) {
-            const int ib0 = 32 * t + 16 * h;
-            // row pointers made here, not kept across the B operand (register pressure)
-            const uint16_t* up0 = a.row_table + (int64_t)prp0 * a.ld_row;
-            const uint16_t* un0 = a.row_table + (int64_t)prn0 * a.ld_row;
-            const uint16_t* up1 = a.row_table + (int64_t)prp1 * a.ld_row;
-            const uint16_t* un1 = a.row_table + (int64_t)prn1 * a.ld_row;
-            // pair 0's rows before the MFMAs; pair 1's after pair 0's epilogue, in the same
-            // registers (both at once spill)
-            uint4 e0[2], f0[2], el[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                e0[k] = *reinterpret_cast<const uint4*>(up0 + ib0 + 8 * k);
-                f0[k] = *reinterpret_cast<const uint4*>(un0 + ib0 + 8 * k);
-            }
-            const int ia = 32 * t + 16 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
-            f32x16 acc = {};
-            uint4 wa = rs[ia * SL + (h ^ (ia % SL))];
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                uint4 xa = wa;
-                if (s + 1 < KS) xa = rs[ia * SL + ((2 * (s + 1) + h) ^ (ia % SL))];
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa), b[s], acc, 0, 0, 0);
-                wa = xa;
-            }
-#pragma unroll
-            for (int k = 0; k < 2; ++k) el[k] = *reinterpret_cast<const uint4*>(lk + ib0 + 8 * k);
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t w0[4] = {e0[k].x, e0[k].y, e0[k].z, e0[k].w},
-                               n0[4] = {f0[k].x, f0[k].y, f0[k].z, f0[k].w},
-                               lw[4] = {el[k].x, el[k].y, el[k].z, el[k].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float l0 = bf_lo(lw[j]), l1 = bf_hi(lw[j]);
-                    pp0 = fmaf(acc[8 * k + 2 * j], bf_lo(w0[j]) * l0, pp0);
-                    pp0 = fmaf(acc[8 * k + 2 * j + 1], bf_hi(w0[j]) * l1, pp0);
-                    pn0 = fmaf(acc[8 * k + 2 * j], bf_lo(n0[j]) * l0, pn0);
-                    pn0 = fmaf(acc[8 * k + 2 * j + 1], bf_hi(n0[j]) * l1, pn0);
-                }
-            }
-            if (ok1) {
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    e0[k] = *reinterpret_cast<const uint4*>(up1 + ib0 + 8 * k);
-                    f0[k] = *reinterpret_cast<const uint4*>(un1 + ib0 + 8 * k);
-                }
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const uint32_t w1[4] = {e0[k].x, e0[k].y, e0[k].z, e0[k].w},
-                                   n1[4] = {f0[k].x, f0[k].y, f0[k].z, f0[k].w},
-                                   lw[4] = {el[k].x, el[k].y, el[k].z, el[k].w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float l0 = bf_lo(lw[j]), l1 = bf_hi(lw[j]);
-                        pp1 = fmaf(acc[8 * k + 2 * j], bf_lo(w1[j]) * l0, pp1);
-                        pp1 = fmaf(acc[8 * k + 2 * j + 1], bf_hi(w1[j]) * l1, pp1);
-                        pn1 = fmaf(acc[8 * k + 2 * j], bf_lo(n1[j]) * l0, pn1);
-                        pn1 = fmaf(acc[8 * k + 2 * j + 1], bf_hi(n1[j]) * l1, pn1);
-                    }
-                }
-            }
-        }
-        pp0 += __shfl_xor(pp0, 32);
-        pn0 += __shfl_xor(pn0, 32);
-        pp1 += __shfl_xor(pp1, 32);
-        pn1 += __shfl_xor(pn1, 32);
-        if (h == 0) {
-            if (ok0) {
-                a.out[pp.x] = pp0;
-                a.out[nh + pp.x] = pn0;
-            }
-            if (ok1) {
-                a.out[pp.y] = pp1;
-                a.out[nh + pp.y] = pn1;
-            }
-        }
-        float term = (h == 0 && ok0) ? fmaxf(pn0 - (pp0 - a.margin), 0.f) : 0.f;
-        term += (h == 0 && ok1) ? fmaxf(pn1 - (pp1 - a.margin), 0.f) : 0.f;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off);
-        wsum += term;
-    }
-    __shared__ float red[THREADS / 64];
-    __shared__ int last;
-    if (lane == 0) red[wave] = wsum;
-    __syncthreads();
-    if (tid == 0) {
-        float s = 0.f;
-        for (int w = 0; w < THREADS / 64; ++w) s += red[w];
-        __hip_atomic_store(a.partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last && tid == 0) {
-        float t = 0.f;
-        for (int b = 0; b < (int)gridDim.x; ++b)
-            t += __hip_atomic_load(a.partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a.loss[0] = t;
-        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
 }  // namespace
 
 extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
@@ -653,51 +474,5 @@ extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_ro
                   d * d * 2, configured);
     hipLaunchKernelGGL((decoder_bf16_colshared_kernel<256, true, kThreads, true>), dim3(blocks), dim3(kThreads),
                        d * d * 2, st, a);
-    return dg::launch_status();
-}
-
-extern "C" int dg_slot_score_hinge_cols_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
-                                             int64_t ld_col, const int32_t* pos_rows, const int32_t* ent_col,
-                                             const int32_t* ent_pair, const int32_t* tile_slot, int32_t n_ctiles,
-                                             const uint32_t* alias_table, int32_t range, int64_t alias_stride,
-                                             int32_t slot0, int32_t n_slots, int32_t batch, uint64_t seed,
-                                             const uint16_t* G, const uint16_t* l_table, int32_t d, float margin,
-                                             float* out, int32_t* neg_rows, float* loss, void* workspace,
-                                             void* stream) {
-    if (n_slots < 0 || batch < 1 || slot0 < 0 || range < 1 || alias_stride < 0 || n_ctiles < 0) return DG_EINVAL;
-    if (!row_table || !col_table || !pos_rows || !alias_table || !G || !l_table || !out || !neg_rows || !loss ||
-        !workspace || (n_ctiles > 0 && (!ent_col || !ent_pair || !tile_slot)))
-        return DG_EINVAL;
-    if (d != 256) return DG_EINVAL;
-    if (ld_row < d || ld_col < d || (ld_row & 7) || (ld_col & 7)) return DG_EALIGN;
-    if (!dg::aligned16(row_table) || !dg::aligned16(col_table) || !dg::aligned16(l_table) || !dg::aligned16(G) ||
-        !dg::aligned16(workspace) || (reinterpret_cast<uintptr_t>(ent_pair) & 7))
-        return DG_EALIGN;
-    if ((int64_t)n_slots * batch > 0x7fffffffLL || (int64_t)n_ctiles * 32 > 0x7fffffffLL) return DG_EINVAL;
-    const int32_t nh = n_slots * batch;
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (nh == 0 || n_ctiles == 0) return hipMemsetAsync(loss, 0, sizeof(float), st) == hipSuccess ? DG_OK : DG_EINVAL;
-    Bf16DecArgs a{row_table, col_table, G, l_table, pos_rows, nullptr, nullptr, out, ld_row, ld_col, nh, d};
-    a.alias = reinterpret_cast<const uint2*>(alias_table);
-    a.alias_stride = alias_stride;
-    a.seed = seed;
-    a.neg_out = neg_rows;
-    a.loss = loss;
-    a.ticket = reinterpret_cast<uint32_t*>(workspace);
-    a.partial = reinterpret_cast<float*>(workspace) + 4;
-    a.range = range;
-    a.slot0 = slot0;
-    a.batch = batch;
-    a.margin = margin;
-    a.ent_col = ent_col;
-    a.ent_pair = reinterpret_cast<const int2*>(ent_pair);
-    a.tile_slot = tile_slot;
-    a.n_ctiles = n_ctiles;
-    constexpr int kThreads = DG_DEC_COLS_THREADS;
-    int blocks = (n_ctiles + kThreads / 64 - 1) / (kThreads / 64);
-    if (blocks > DG_HINGE_WS_BLOCKS) blocks = DG_HINGE_WS_BLOCKS;
-    static std::atomic<uint64_t> configured{0};
-    dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_slotcols_kernel<kThreads>), d * d * 2, configured);
-    hipLaunchKernelGGL((decoder_bf16_slotcols_kernel<kThreads>), dim3(blocks), dim3(kThreads), d * d * 2, st, a);
     return dg::launch_status();
 }

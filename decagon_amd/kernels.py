@@ -960,83 +960,6 @@ def slot_score_hinge_bf16(E_row: torch.Tensor, E_col: torch.Tensor, pos_rows: to
         _stream_ptr(stream)), "dg_slot_score_hinge_bf16")
 
 
-def slot_columns(cols: np.ndarray, n_slots: int, batch: int, per_entry: int = 2):
-    """The column entries of dg_slot_score_hinge_cols_bf16 for local slots 0..n_slots-1 whose
-    positives' columns are cols (slot-major, n_slots·batch): per slot, its pairs grouped by
-    column, up to `per_entry` (2) pairs an entry, entries with two pairs first, padded to
-    tiles of 32.  Returns (ent_col int32 [T·32], ent_pair int32 [T·32, 2], tile_slot int32 [T])."""
-    if per_entry != 2:
-        raise ValueError("two pairs an entry")
-    cols = np.asarray(cols, np.int64).reshape(n_slots, batch)
-    ec, ep, ts = [], [], []
-    for s in range(n_slots):
-        order = np.argsort(cols[s], kind="stable")
-        sc = cols[s][order]
-        pairs = s * batch + order
-        uniq, start, cnt = np.unique(sc, return_index=True, return_counts=True)
-        col_e, p0_e, p1_e = [], [], []
-        for u, st, n in zip(uniq, start, cnt):
-            for q in range(0, int(n), 2):
-                col_e.append(int(u))
-                p0_e.append(int(pairs[st + q]))
-                p1_e.append(int(pairs[st + q + 1]) if q + 1 < n else -1)
-        col_e, p0_e, p1_e = np.asarray(col_e), np.asarray(p0_e), np.asarray(p1_e)
-        first = np.argsort(p1_e < 0, kind="stable")        # two-pair entries first
-        n_e = len(col_e)
-        n_pad = -(-n_e // 32) * 32
-        c = np.full(n_pad, -1, np.int32)
-        pp = np.full((n_pad, 2), -1, np.int32)
-        c[:n_e], pp[:n_e, 0], pp[:n_e, 1] = col_e[first], p0_e[first], p1_e[first]
-        ec.append(c)
-        ep.append(pp)
-        ts.append(np.full(n_pad // 32, s, np.int32))
-    return (np.concatenate(ec) if ec else np.zeros(0, np.int32),
-            np.concatenate(ep) if ep else np.zeros((0, 2), np.int32),
-            np.concatenate(ts) if ts else np.zeros(0, np.int32))
-
-
-def slot_score_hinge_cols_bf16(E_row: torch.Tensor, E_col: torch.Tensor, pos_rows: torch.Tensor,
-                               ent_col: torch.Tensor, ent_pair: torch.Tensor, tile_slot: torch.Tensor,
-                               table: torch.Tensor, slot0: int, n_slots: int, batch: int, seed: int, G: torch.Tensor,
-                               D: torch.Tensor, margin: float, out: torch.Tensor, neg_rows: torch.Tensor,
-                               loss: torch.Tensor, workspace: torch.Tensor, stream=None) -> None:
-    """slot_score_hinge_bf16 over column entries (slot_columns): the same draws and scores."""
-    n = n_slots * batch
-    for t, nm in ((E_row, "E_row"), (E_col, "E_col"), (G, "G"), (D, "D")):
-        _dev(t, torch.bfloat16, nm)
-    for t, nm in ((pos_rows, "pos_rows"), (neg_rows, "neg_rows"), (table, "alias table"), (ent_col, "ent_col"),
-                  (ent_pair, "ent_pair"), (tile_slot, "tile_slot")):
-        _dev(t, torch.int32, nm)
-    _dev(out, torch.float32, "out")
-    _dev(loss, torch.float32, "loss")
-    d = G.shape[0]
-    if d != 256 or G.shape != (256, 256) or D.dim() != 2 or D.shape[1] != d or E_row.shape[1] != d \
-            or E_col.shape[1] != d:
-        raise ValueError("slot scorer: d = 256 tables, G and D rows")
-    n_ct = tile_slot.numel()
-    if ent_col.numel() != 32 * n_ct or ent_pair.numel() != 64 * n_ct:
-        raise ValueError("column entries: 32 a tile, two pair slots an entry")
-    if table.dim() == 3 and table.shape[2] == 2:
-        rng, stride = table.shape[1], table.shape[1]
-        if slot0 + n_slots > table.shape[0]:
-            raise ValueError("slot range outside the alias tables")
-    elif table.dim() == 2 and table.shape[1] == 2:
-        rng, stride = table.shape[0], 0
-    else:
-        raise ValueError("alias tables must be [n_slots, range, 2] or [range, 2]")
-    if rng > E_row.shape[0] or slot0 + n_slots > D.shape[0]:
-        raise ValueError("sampler range exceeds the row table, or slots exceed D")
-    if pos_rows.numel() < n or neg_rows.numel() < n or out.numel() < 2 * n:
-        raise ValueError("pairs / outputs shorter than n_slots·batch")
-    if workspace.numel() * workspace.element_size() < _lib.DG_HINGE_WS_BYTES or not workspace.is_cuda:
-        raise ValueError("hinge workspace too small")
-    check(_lib.load().dg_slot_score_hinge_cols_bf16(
-        E_row.data_ptr(), E_row.stride(0), E_col.data_ptr(), E_col.stride(0), pos_rows.data_ptr(), ent_col.data_ptr(),
-        ent_pair.data_ptr(), tile_slot.data_ptr(), n_ct, table.data_ptr(), rng, stride, slot0, n_slots, batch,
-        seed & (2**64 - 1), G.data_ptr(), D.data_ptr(), d, float(margin), out.data_ptr(), neg_rows.data_ptr(),
-        loss.data_ptr(), workspace.data_ptr(), _stream_ptr(stream)), "dg_slot_score_hinge_cols_bf16")
-
-
 def upload_alias(degrees, device) -> torch.Tensor:
     """The alias table of one degree vector, int32 [range, 2]; a list of degree vectors (one per
     relation) gives [n, range, 2] (every vector the same length)."""

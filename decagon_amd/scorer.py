@@ -68,14 +68,6 @@ class SlotScorer:
         self.allreduce = allreduce
         # (DG_C5_FUSED=0: the three-launch form by default — A/B runs)
         self.fused = (os.environ.get("DG_C5_FUSED", "1") != "0") if fused is None else fused
-        # the fused launch over column entries (kernels.slot_columns: a slot's positives grouped
-        # by column, two to an entry — the positives are fixed, so the entries are built once)
-        self.cols_form = self.fused and n > 0 and os.environ.get("DG_C5_COLS", "1") != "0"
-        if self.cols_form:
-            ec, ep, ts = kernels.slot_columns(cols.cpu().numpy(), s1 - s0, batch)
-            self.ent_col = torch.from_numpy(ec).to(dev)
-            self.ent_pair = torch.from_numpy(ep).to(dev)
-            self.tile_slot = torch.from_numpy(ts).to(dev)
 
     @property
     def neg_rows(self) -> torch.Tensor:
@@ -110,20 +102,11 @@ class SlotScorer:
             self.score()
             self.hinge()
             return
-        self.launch()
-        if self.allreduce is not None:
-            self.allreduce(self.loss)
-
-    def launch(self) -> None:
-        """The fused form's one launch (sampler + scores + this rank's hinge sum)."""
-        if self.cols_form:
-            kernels.slot_score_hinge_cols_bf16(self.E_row, self.E_col, self.rows[:self.n], self.ent_col, self.ent_pair,
-                                               self.tile_slot, self.alias, self.s0, self.s1 - self.s0, self.batch,
-                                               self.seed, self.R, self.D, self.margin, self.out, self.neg_rows,
-                                               self.loss, self._ws)
-        elif self.n:
+        if self.n:
             kernels.slot_score_hinge_bf16(self.E_row, self.E_col, self.rows[:self.n], self.cols[:self.n], self.alias,
                                           self.s0, self.s1 - self.s0, self.batch, self.seed, self.R, self.D,
                                           self.margin, self.out, self.neg_rows, self.loss, self._ws)
         else:
             self.loss.zero_()
+        if self.allreduce is not None:
+            self.allreduce(self.loss)

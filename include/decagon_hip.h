@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (32); bumped whenever a struct layout or a signature changes. */
+/* ABI version (31); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -429,20 +429,6 @@ int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, cons
                                  int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
                                  const int32_t* rel_idx, int32_t n_half, const uint16_t* G,
                                  const uint16_t* l_table, int32_t d, float* out, void* stream);
-
-/* The same step with the positives grouped by column: a slot's pairs that share a column share
- * T = G·bf16(l_k∘v) too.  Tile t (< n_ctiles) holds 32 entries of local slot tile_slot[t]; entry e
- * scores column ent_col[e] (-1: empty) for pairs ent_pair[2e], ent_pair[2e+1] (-1: none) — every
- * pair p < n_slots*batch in exactly one entry of its slot.  pos_rows as above (pos_cols is
- * implied by the entries); draws, scores and outputs are those of dg_slot_score_hinge_bf16, bit
- * for bit (the loss is summed in another fixed order). */
-int dg_slot_score_hinge_cols_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
-                                  int64_t ld_col, const int32_t* pos_rows, const int32_t* ent_col,
-                                  const int32_t* ent_pair, const int32_t* tile_slot, int32_t n_ctiles,
-                                  const uint32_t* alias_table, int32_t range, int64_t alias_stride,
-                                  int32_t slot0, int32_t n_slots, int32_t batch, uint64_t seed,
-                                  const uint16_t* G, const uint16_t* l_table, int32_t d, float margin,
-                                  float* out, int32_t* neg_rows, float* loss, void* workspace, void* stream);
 
 /* Config 5's whole step in one launch: every relation slot's positive batch, its sampled
  * negatives and the hinge loss.  For local slot s < n_slots (relation slot0 + s) and i < batch,
