@@ -96,15 +96,14 @@ constexpr int kRowsPerBlock = 4 * kRowsPerWave;
 #define DG_GROUP_KUNROLL 4
 #endif
 #ifndef DG_GROUP_U4_BLOCKS
-#define DG_GROUP_U4_BLOCKS 0x7fffffff  // 2048: measured below, pending the parity run
+#define DG_GROUP_U4_BLOCKS 2048
 #endif
 // Partial-mode launches of at least this many workgroups (8 waves a SIMD) keep kGroupUnroll
 // gathers in flight instead of kUnroll: they are occupancy-bound and the shorter unroll holds
-// fewer VGPRs (config P forward 432 → 422 µs, training 1.70 → 1.68 ms); smaller launches keep
-// kUnroll (config S training: 4 costs 3-4 µs a step).  Same bits either way.
+// fewer VGPRs (config P forward 432-435 → 421-424 µs, training 1.70 → 1.68 ms; 2 no better,
+// 16 worse); smaller launches keep kUnroll (config S training: 4 costs 3-4 µs a step).  Same
+// bits either way.
 constexpr int kUnroll = DG_KUNROLL;  // gathers in flight per lane
-// partial mode keeps fewer in flight: its waves already overlap kRowsPerWave rows' loads
-// (config P, 100 steps: 8 → 4 −10 µs a forward step, 2 no better)
 constexpr int kGroupUnroll = DG_GROUP_KUNROLL;
 
 // The first batch of 64 (vcol, val) pairs of a range (batch wpart): lane l holds pair l.
