@@ -91,6 +91,11 @@ def parse(argv=None):
                     help="--simulate-world: time only this rank (default: every rank)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                     "gloo only to exercise the multi-rank path on a single-GPU box)")
+    ap.add_argument("--exchange", choices=["rccl", "peer", "peer-kernel"], default="rccl",
+                    help="N > 1 (and --simulate-world): the row-split blocks' all-gather over RCCL, or by peer "
+                         "stores over xGMI (peer.py) fused into the finishing launches (peer) or as a "
+                         "stand-alone launch (peer-kernel); the line's \"peer\" block times the peer form "
+                         "beside the RCCL default at N > 1 either way")
     return ap.parse_args(argv)
 
 
@@ -118,7 +123,17 @@ def collectives(backend):
     return torch_allreduce(), torch_allgather()
 
 
-def build_workload(config, rank, world, sharded, backend="nccl"):
+def peer_config(exchange, loopback=False):
+    """The RelationShard.peer of an --exchange choice (None: RCCL / the backend's all-gather)."""
+    if exchange == "rccl":
+        return None
+    from decagon_amd.peer import PeerConfig, dist_gather
+
+    mode = "fused" if exchange == "peer" else "kernel"
+    return PeerConfig(mode=mode, loopback=True) if loopback else PeerConfig(mode=mode, gather=dist_gather())
+
+
+def build_workload(config, rank, world, sharded, backend="nccl", exchange="rccl"):
     from decagon_amd import synthetic
     from decagon_amd.sharding import RelationShard
 
@@ -145,6 +160,8 @@ def build_workload(config, rank, world, sharded, backend="nccl"):
         scaling = "strong"
         workload = ("P: polypharmacy-shaped 19,085 proteins + 645 drugs, 964 side effects "
                     "(1,932 drug-drug matrices), 2 GCN layers d=64/32 + DEDICOM decoder B=512+512")
+    if shard is not None:
+        shard.peer = peer_config(exchange)
     return graph, shard, scaling, workload
 
 
@@ -322,9 +339,11 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
     kernel's roofline, the whole layer-1 SpMM.  Returns (record fields, graph)."""
     import torch
 
-    graph, shard, scaling, workload = build_workload(config, rank, world, sharded, args.backend)
+    graph, shard, scaling, workload = build_workload(config, rank, world, sharded, args.backend, args.exchange)
     plan, dg = make_plan(args, graph, shard, device)
     dec = Decoder(graph, plan, device, rank)
+    if sharded:
+        dist.barrier()  # (a peer exchange's first wait is bounded: start the ranks together)
 
     def step():
         plan.run()
@@ -426,8 +445,17 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
     }
     if sharded:
         rec["rank_ms_per_step"] = el * 1e3 / steps
+        if plan.peer is not None:
+            rec["peer_error_word"] = plan.peer.error()
         if args.backend == "nccl" and use_graph:
             rec["phases"] = phase_times(plan, dec, stream, dist, min(kernel_reps, 20))
+        if plan.xregion is not None and use_graph:
+            rec["peer_probe"] = peer_probe(plan, stream, dist, min(kernel_reps, 20), rank, world)
+        rec["_outputs"] = [{t: h.cpu().numpy() for t, h in plan.hidden1.items()},
+                           {t: e.cpu().numpy() for t, e in plan.embeddings.items()}]
+        if plan.peer is not None:
+            dist.barrier()
+            plan.peer.close()
     del plan, dec
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -459,6 +487,89 @@ def phase_times(plan, dec, stream, dist, reps):
     out["compute_total_us"] = sum(out["compute_us"])
     out["exchange_total_us"] = sum(out["exchange_us"])
     return out
+
+
+def peer_probe(plan, stream, dist, reps, rank, world):
+    """Each layer's row-split all-gather as ONE stand-alone peer-store exchange launch
+    (dg_peer_allgather, peer.py: IPC-mapped peer regions, write-through stores, bounded flag
+    waits), timed alone like the phases — so the driver's N-GPU run records what the peer
+    exchange costs on xGMI beside whatever exchange the step ran.  Never raises: an IPC or
+    timeout failure is reported in the block."""
+    import torch
+
+    from decagon_amd.peer import PeerConfig, PeerExchange, dist_gather
+
+    out = {"kernel": "peer_push_kernel (dg_peer_allgather)", "layers_us": [], "bytes_per_rank": []}
+    ex = plan.peer
+    own = ex is None
+    try:
+        if own:
+            ex = PeerExchange(plan.xregion, rank, world, PeerConfig(mode="kernel", gather=dist_gather()))
+            plan.peer = ex
+        fns = plan.peer_probe()
+        dist.barrier()
+        for fn in fns:
+            out["layers_us"].append(time_kernel(fn, reps, stream) * 1e3)
+        out["bytes_per_rank"] = [sum(4 * plan._pad[i, layer].shape[1] * plan.row_block[i][2]
+                                     for i in plan.row_block) for layer in (1, 2)]
+        out["error_word"] = ex.error()
+    except Exception as e:  # IPC refused / a peer failed: record it, keep the bench line
+        out["error"] = f"{type(e).__name__}: {e}"
+    t = torch.tensor(out["layers_us"] or [0.0], dtype=torch.float64, device=stream.device)
+    try:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if out["layers_us"]:
+            out["layers_us"] = t.tolist()
+    except Exception as e:
+        out["error"] = out.get("error", "") + f"; max-reduce: {e}"
+    if own and ex is not None:
+        plan.peer = None
+        try:
+            dist.barrier()
+            ex.close()
+        except Exception:
+            pass
+    return out
+
+
+def peer_step(args, rank, world, device, dist, steps, warmup, ref_outputs):
+    """config S's step with the all-gathers done by peer stores fused into the finishing
+    launches (--exchange peer), timed as the default step is — beside the RCCL default, which
+    stays `value` — and checked bit for bit against the RCCL step's outputs."""
+    import torch
+
+    rec = {"exchange": "peer (fused into the finishing launches)"}
+    try:
+        graph, shard, _, _ = build_workload("S", rank, world, True, args.backend, "peer")
+        plan, dg = make_plan(args, graph, shard, device)
+        dec = Decoder(graph, plan, device, rank)
+
+        def step():
+            plan.run()
+            dec()
+
+        stream = torch.cuda.Stream(device)
+        dist.barrier()
+        G = steps_per_graph(steps, args.graph_steps)
+        el = timed_steps(step, steps, warmup, G, stream, True, dist.barrier)
+        err = plan.peer.error()
+        same = all(np.array_equal(plan.hidden1[t].cpu().numpy(), ref_outputs[0][t]) and
+                   np.array_equal(plan.embeddings[t].cpu().numpy(), ref_outputs[1][t]) for t in plan.hidden1)
+        t = torch.tensor([el, float(2 * dg.total_nnz), 0.0 if (same and err == 0) else 1.0],
+                         dtype=torch.float64, device=device)
+        tm = t.clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        rec.update({"ms_per_step": float(tm[0]) * 1e3 / steps, "value": float(t[1]) * steps / float(tm[0]),
+                    "unit": "edges/s", "steps": steps, "steps_per_graph": G,
+                    "bitwise_equal_to_rccl_and_no_timeout_all_ranks": float(tm[2]) == 0.0, "error_word": err})
+        dist.barrier()
+        plan.peer.close()
+        del plan, dec
+        torch.cuda.synchronize()
+    except Exception as e:
+        rec["error"] = f"{type(e).__name__}: {e}"
+    return rec
 
 
 # ----------------------------------------------------------------------------- config 5
@@ -679,6 +790,9 @@ def main_simulate(args):
             shard = RelationShard.weak_sets(graph.edge_types, graph.n_nodes, r, N, _no_op_reduce, _no_op)
         else:
             shard = RelationShard.polypharmacy(graph, r, N, comm=False)
+        # --exchange peer / peer-kernel: the loopback rehearsal of the peer exchange — every
+        # "peer" copy local scratch, every flag raised by the rank itself (peer.py)
+        shard.peer = peer_config(args.exchange, loopback=True)
         plan, dg = make_plan(args, graph, shard, device)
         dec = Decoder(graph, plan, device, r)
 
@@ -693,6 +807,9 @@ def main_simulate(args):
         for L in (plan._layer1, plan._layer2):
             coll.append({"allreduce_bytes": 0 if L.flat is None else 4 * L.flat.numel(),
                          "allgather_bytes": sum(4 * o.numel() for o, _ in L.gathers)})
+        if plan.peer is not None:
+            phases["peer_error_word"] = plan.peer.error()
+            plan.peer.close()
         ranks.append({"rank": r, "ms_per_step": el * 1e3 / args.steps, "nnz_per_layer": dg.total_nnz,
                       "collectives_per_layer": coll, **phases})
         print(f"rank {r}/{N}: {ranks[-1]['ms_per_step'] * 1e3:.1f} us/step, {dg.total_nnz} nnz", file=sys.stderr,
@@ -700,7 +817,10 @@ def main_simulate(args):
         del plan, dec, dg
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-    rec = {"metric": f"config {args.config} sharded-step rehearsal on one GPU (collectives not run)", "world": N,
+    what = ("collectives not run" if args.exchange == "rccl" else
+            f"exchange {args.exchange} in loopback: the peer stores, arrivals, flags and polls run, "
+            "the xGMI wire latency does not")
+    rec = {"metric": f"config {args.config} sharded-step rehearsal on one GPU ({what})", "world": N,
            "steps": args.steps, "warmup": args.warmup, "steps_per_graph": G,
            "max_rank_ms_per_step": max(x["ms_per_step"] for x in ranks), "ranks": ranks}
     print(json.dumps(rec), file=JSON_OUT, flush=True)
@@ -740,6 +860,10 @@ def main():
 
     rec, graph = forward_bench(args, args.config, rank, world, sharded, device, dist, args.steps, args.warmup,
                                args.kernel_reps)
+    ref_outputs = rec.pop("_outputs", None)
+    if sharded and args.config == "S" and args.exchange == "rccl" and args.backend == "nccl":
+        # the peer-store form of the same step beside the RCCL default
+        rec["peer"] = peer_step(args, rank, world, device, dist, args.steps, args.warmup, ref_outputs)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(graph, args.cpu_seconds)
@@ -750,6 +874,7 @@ def main():
         # driver's own run
         p, pgraph = forward_bench(args, "P", rank, world, sharded, device, dist, args.p_steps, 3,
                                   min(args.kernel_reps, 20))
+        p.pop("_outputs", None)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             p["cpu_baseline"] = cpu_baseline(pgraph, args.cpu_seconds)
         del pgraph

@@ -22,13 +22,19 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 31
+ABI_VERSION = 32
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
 DG_GROUP_DROPOUT = 2
 DG_GROUP_DENSE_ROWS = 4  # dg_gcn_fused_f32 only: row r of the group's sum is x[r]
 DG_MAX_ADAM_SEGS = 32
+DG_PEER_MAX = 8  # peer exchange (decagon_hip.h)
+DG_PEER_SLOTS = 8
+DG_PEER_STATE_WORDS = 2 * DG_PEER_SLOTS + 1
+DG_PEER_ERROR_WORD = 2 * DG_PEER_SLOTS
+DG_IPC_HANDLE_BYTES = 64
+DG_EPI_PUSH = 1
 
 _ERRS = {DG_EINVAL: "DG_EINVAL", DG_EALIGN: "DG_EALIGN", DG_ETOOMANY: "DG_ETOOMANY"}
 
@@ -116,7 +122,21 @@ class DgEpiTarget(ctypes.Structure):
         ("reserved0", c_int32),
         ("out", c_void_p),
         ("n_rows", c_int32),
-        ("reserved", c_int32 * 3),
+        ("target_flags", c_int32),
+        ("reserved", c_int32 * 2),
+    ]
+
+
+class DgPeerXchg(ctypes.Structure):
+    _fields_ = [
+        ("delta", c_int64 * DG_PEER_MAX),
+        ("flags", c_void_p * DG_PEER_MAX),
+        ("state", c_void_p),
+        ("timeout_ticks", c_int64),
+        ("rank", c_int32),
+        ("world", c_int32),
+        ("slot", c_int32),
+        ("loopback", c_int32),
     ]
 
 
@@ -176,6 +196,17 @@ SIGNATURES = {
          c_int32, c_void_p],
     ),
     "dg_gcn_epilogue_multi_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, c_void_p]),
+    "dg_gcn_epilogue_peer_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, POINTER(DgPeerXchg),
+                                           c_void_p]),
+    "dg_gcn_fused_seg_peer_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32,
+                                            c_int32, POINTER(DgPeerXchg), c_void_p]),
+    "dg_peer_alloc": (c_int32, [c_int64, c_int32, POINTER(c_void_p)]),
+    "dg_peer_free": (c_int32, [c_void_p]),
+    "dg_ipc_get_handle": (c_int32, [c_void_p, c_void_p, POINTER(c_int64)]),
+    "dg_ipc_open": (c_int32, [c_void_p, POINTER(c_void_p)]),
+    "dg_ipc_close": (c_int32, [c_void_p]),
+    "dg_peer_allgather": (c_int32, [POINTER(DgPeerXchg), c_void_p, POINTER(c_int64), POINTER(c_int64), c_int32,
+                                    c_void_p]),
     "dg_gcn_epilogue_f32": (
         c_int32,
         [POINTER(DgEpiGroup), c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],

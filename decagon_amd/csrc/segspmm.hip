@@ -24,6 +24,7 @@
 // then the chunk's waves add their rows in relation order (LDS, one barrier) and the first
 // wave of the row writes out[c][r].  Fixed order, no atomics: bitwise reproducible.
 #include "common.h"
+#include "peer.h"
 
 // gathers in flight per lane (U: plain sums, UP: the reassociated form, whose W slice holds
 // 32 VGPRs), per kernel — measured at config S (rows 4-81 nonzeros per relation), the
@@ -106,6 +107,7 @@ __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, c
     constexpr int G = dg::kWave / LP;  // nonzeros side by side
     constexpr int S = dg::kWave / G;   // steps per batch of 64
     constexpr int U = UU ? UU : S;
+    static_assert(U >= 1 && U <= S && S % U == 0, "seg_gather: the unroll must divide the steps of a batch");
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const float* xq = xb + (lane % LP) * 4;
@@ -176,6 +178,7 @@ __device__ __forceinline__ float4 seg_gather_shfl(const int32_t* __restrict__ vc
                                              const float* xb, int x_ld, int beg, int end) {
     constexpr int G = dg::kWave / LP;
     constexpr int U = UU ? UU : LP;  // (U·G = 64: one batch per round trip)
+    static_assert(U >= 1 && U <= LP && LP % U == 0, "seg_gather_shfl: the unroll must divide the steps of a batch");
     const int lane = threadIdx.x & 63;
     const int sub = lane / LP;
     const float* xq = xb + (lane % LP) * 4;
@@ -328,6 +331,7 @@ struct FsArgs {
     FsTargetK t[DG_MAX_GROUPS];
     int32_t n_targets;
     int32_t nw;
+    dg::PeerK P;  // PEER: every finished row also goes to every peer's copy (peer.h)
 };
 
 #ifdef DG_FS_RPB1
@@ -336,7 +340,7 @@ constexpr int kFsMaxRpb = 1;  // A/B: one row per workgroup
 constexpr int kFsMaxRpb = 4;
 #endif
 
-template <int LP, bool PROJ, int NW>
+template <int LP, bool PROJ, int NW, bool PEER>
 __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;
     __shared__ float4 ybuf[NW][16];
@@ -395,8 +399,11 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
             tot.z = fmaxf(tot.z, 0.f);
             tot.w = fmaxf(tot.w, 0.f);
         }
-        *reinterpret_cast<float4*>(T.out + (int64_t)(r0 + wave) * (4 * DOUT4) + 4 * lane) = tot;
+        const int64_t o = (int64_t)(r0 + wave) * (4 * DOUT4) + 4 * lane;
+        *reinterpret_cast<float4*>(T.out + o) = tot;
+        if constexpr (PEER) dg::peer_store4(a.P, T.out, (uint32_t)T.n_rows * (16 * DOUT4), (uint32_t)o * 4, tot);
     }
+    if constexpr (PEER) dg::peer_arrive(a.P);  // the last workgroup raises the flags and waits
 }
 
 }  // namespace
@@ -492,8 +499,9 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     return dg::launch_status();
 }
 
-extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets,
-                                    int32_t n_targets, int32_t d_in, int32_t d_out, void* stream) {
+namespace {
+int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets, int32_t n_targets,
+                     int32_t d_in, int32_t d_out, const dg_peer_xchg* xchg, void* stream) {
     if (n_groups < 1 || !groups || n_targets < 1 || !targets) return DG_EINVAL;
     if (n_groups > DG_MAX_GROUPS || n_targets > DG_MAX_GROUPS) return DG_ETOOMANY;
     bool proj = false;
@@ -539,21 +547,47 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
     if (blocks > 0x7fffffff) return DG_EINVAL;
     a.n_targets = n_targets;
     a.nw = nw;
+    if (xchg) {
+        const int rc = dg::peer_convert(xchg, a.P);
+        if (rc != DG_OK) return rc;
+        for (int t = 0; t < n_targets; ++t)  // 32-bit buffer offsets into each peer's copy
+            if ((int64_t)targets[t].n_rows * d_out * 4 > 0x7fffffffLL) return DG_EINVAL;
+        if (blocks == 0) blocks = 1;  // no rows here: one workgroup still takes part in the exchange
+    }
     if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);
-#define DG_FS_LAUNCH(NW)                                                                      \
-    if (proj)                                                                                 \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW>), grid, block, 0, st, a);      \
-    else if (d_in == 64)                                                                      \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW>), grid, block, 0, st, a);     \
-    else                                                                                      \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW>), grid, block, 0, st, a);
-    if (nw <= 8) {
-        DG_FS_LAUNCH(8)
+#define DG_FS_LAUNCH(NW, PEER)                                                                    \
+    if (proj)                                                                                     \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER>), grid, block, 0, st, a);    \
+    else if (d_in == 64)                                                                          \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW, PEER>), grid, block, 0, st, a);   \
+    else                                                                                          \
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW, PEER>), grid, block, 0, st, a);
+    if (xchg) {
+        if (nw <= 8) {
+            DG_FS_LAUNCH(8, true)
+        } else {
+            DG_FS_LAUNCH(16, true)
+        }
+    } else if (nw <= 8) {
+        DG_FS_LAUNCH(8, false)
     } else {
-        DG_FS_LAUNCH(16)
+        DG_FS_LAUNCH(16, false)
     }
 #undef DG_FS_LAUNCH
     return dg::launch_status();
+}
+}  // namespace
+
+extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets,
+                                    int32_t n_targets, int32_t d_in, int32_t d_out, void* stream) {
+    return fused_seg_launch(groups, n_groups, targets, n_targets, d_in, d_out, nullptr, stream);
+}
+
+extern "C" int dg_gcn_fused_seg_peer_f32(const dg_seg_group* groups, int32_t n_groups,
+                                         const dg_fused_target* targets, int32_t n_targets, int32_t d_in,
+                                         int32_t d_out, const dg_peer_xchg* xchg, void* stream) {
+    if (!xchg) return DG_EINVAL;
+    return fused_seg_launch(groups, n_groups, targets, n_targets, d_in, d_out, xchg, stream);
 }

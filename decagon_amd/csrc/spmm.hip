@@ -25,6 +25,7 @@
 // the next layer's projection of the finished row.
 #include "common.h"
 #include "dropout.h"
+#include "peer.h"
 
 #ifndef DG_FUSED_ABL
 #define DG_FUSED_ABL 0  // timing ablations only (wrong results): 1 no gathers, 8 empty kernels
@@ -411,6 +412,8 @@ struct EpiTargetK {
     int32_t g_begin;      // its groups: g[g_begin .. g_begin + g_count)
     int32_t g_count;
     int32_t block_begin;  // its first workgroup
+    int32_t push;         // PEER launches: its rows also go to every peer's copy (DG_EPI_PUSH)
+    int32_t pad;
 };
 
 struct EpiArgs {
@@ -420,25 +423,16 @@ struct EpiArgs {
     int32_t d;
     int32_t flags;
     int32_t pad;
+    dg::PeerK P;  // PEER launches: the finished rows also go to every peer's copy (peer.h)
 };
 
 // One wave per output row: LP lanes cover the row's d floats (a float4 each) and the
 // wave's CG = 64/LP lane groups split the chunks (group cg sums chunks cg, cg+CG, ... with four
 // loads in flight), combined by an xor butterfly — every lane ends with the same bits, so the
 // result is deterministic; then the L2 norm over the row's LP lanes.
-template <int LP>
-__global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
-    constexpr int CG = dg::kWave / LP;  // chunk groups per wave
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int cg = lane / LP;
-    const int q = lane % LP;
-    int ti = 0;  // node type of this workgroup (several finish in one launch)
-#pragma unroll 1
-    while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
-    const EpiTargetK& t = a.t[ti];
-    const int r = ((int)blockIdx.x - t.block_begin) * 4 + wave;
-    if (r >= t.n_rows) return;  // wave-uniform; no barriers
+template <int LP, bool PEER>
+__device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK& t, int r, int cg, int q) {
+    constexpr int CG = dg::kWave / LP;
     const int d = a.d;
     const bool qok = q * 4 < d;
     const int64_t plane = (int64_t)t.n_rows * d;
@@ -487,7 +481,30 @@ __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
         dg::add4(tot, s);
     }
     if (a.flags & DG_EPI_RELU) tot = relu4(tot);
-    if (qok && cg == 0) *reinterpret_cast<float4*>(t.out + off) = tot;
+    if (qok && cg == 0) {
+        *reinterpret_cast<float4*>(t.out + off) = tot;
+        if constexpr (PEER)
+            if (t.push) dg::peer_store4(a.P, t.out, (uint32_t)(plane * 4), (uint32_t)(off * 4), tot);
+    }
+}
+
+// PEER: the rows are also stored into every peer's copy of the row-split output and the launch
+// ends with the peer-store exchange (peer.h: the last workgroup raises the flags and waits), so
+// every wave reaches the closing barrier.
+template <int LP, bool PEER>
+__global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
+    constexpr int CG = dg::kWave / LP;  // chunk groups per wave
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int cg = lane / LP;
+    const int q = lane % LP;
+    int ti = 0;  // node type of this workgroup (several finish in one launch)
+#pragma unroll 1
+    while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
+    const EpiTargetK& t = a.t[ti];
+    const int r = ((int)blockIdx.x - t.block_begin) * 4 + wave;
+    if (r < t.n_rows) epilogue_row<LP, PEER>(a, t, r, cg, q);  // wave-uniform
+    if constexpr (PEER) dg::peer_arrive(a.P);
 }
 
 // Partial mode over a SMALL shared operand (every nonzero of the launch gathers from one
@@ -619,7 +636,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 31; }
+extern "C" int32_t dg_abi_version(void) { return 32; }
 
 
 namespace {
@@ -807,8 +824,9 @@ extern "C" int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const 
     return dg_spmm_groups_f32(&g, 1, d, stream);
 }
 
-extern "C" int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets, int32_t n_targets, int32_t d,
-                                         int32_t flags, void* stream) {
+namespace {
+int epilogue_launch(const dg_epi_target* targets, int32_t n_targets, int32_t d, int32_t flags,
+                    const dg_peer_xchg* xchg, void* stream) {
     if (n_targets < 1 || targets == nullptr) return DG_EINVAL;
     if (n_targets > DG_EPI_MAX_TARGETS) return DG_ETOOMANY;
     if (d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
@@ -828,6 +846,8 @@ extern "C" int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets, int32_t n
         k.g_begin = ng;
         k.g_count = T.n_groups;
         k.block_begin = static_cast<int32_t>(blocks);
+        if (T.target_flags & ~DG_EPI_PUSH) return DG_EINVAL;
+        k.push = (xchg && (T.target_flags & DG_EPI_PUSH)) ? 1 : 0;
         for (int i = 0; i < T.n_groups; ++i) {
             if (!T.groups[i].partial || T.groups[i].n_chunks < 1) return DG_EINVAL;
             if (!dg::aligned16(T.groups[i].partial) || !dg::aligned16(T.groups[i].sum_out)) return DG_EALIGN;
@@ -838,17 +858,42 @@ extern "C" int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets, int32_t n
         }
         blocks += dg::ceil_div(T.n_rows, 4);  // one wave per row
     }
-    if (blocks == 0) return DG_OK;
+    if (blocks == 0) {
+        if (!xchg) return DG_OK;
+        blocks = 1;  // no rows here: one workgroup still takes part in the exchange
+    }
     if (blocks > 0x7fffffff) return DG_EINVAL;
     a.d = d;
     a.flags = flags;
     const int lp = dg::lanes_per_row(d);
     dim3 grid(static_cast<unsigned>(blocks)), block(256);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define DG_LAUNCH_EPI(L) hipLaunchKernelGGL(epilogue_kernel<L>, grid, block, 0, st, a)
-    DG_LP_SWITCH(lp, DG_LAUNCH_EPI)
+    if (xchg) {
+        const int rc = dg::peer_convert(xchg, a.P);
+        if (rc != DG_OK) return rc;
+        for (int ti = 0; ti < a.n_targets; ++ti)  // 32-bit buffer offsets into each peer's copy
+            if ((int64_t)a.t[ti].n_rows * d * 4 > 0x7fffffffLL) return DG_EINVAL;
+#define DG_LAUNCH_EPI(L) hipLaunchKernelGGL((epilogue_kernel<L, true>), grid, block, 0, st, a)
+        DG_LP_SWITCH(lp, DG_LAUNCH_EPI)
 #undef DG_LAUNCH_EPI
+    } else {
+#define DG_LAUNCH_EPI(L) hipLaunchKernelGGL((epilogue_kernel<L, false>), grid, block, 0, st, a)
+        DG_LP_SWITCH(lp, DG_LAUNCH_EPI)
+#undef DG_LAUNCH_EPI
+    }
     return dg::launch_status();
+}
+}  // namespace
+
+extern "C" int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets, int32_t n_targets, int32_t d,
+                                         int32_t flags, void* stream) {
+    return epilogue_launch(targets, n_targets, d, flags, nullptr, stream);
+}
+
+extern "C" int dg_gcn_epilogue_peer_f32(const dg_epi_target* targets, int32_t n_targets, int32_t d, int32_t flags,
+                                        const dg_peer_xchg* xchg, void* stream) {
+    if (!xchg) return DG_EINVAL;
+    return epilogue_launch(targets, n_targets, d, flags, xchg, stream);
 }
 
 extern "C" int dg_gcn_epilogue_f32(const dg_epi_group* groups, int32_t n_groups, float* out,
@@ -859,7 +904,7 @@ extern "C" int dg_gcn_epilogue_f32(const dg_epi_group* groups, int32_t n_groups,
     if (flags & ~(DG_EPI_L2NORM | DG_EPI_RELU | DG_EPI_CHUNK_RELU)) return DG_EINVAL;
     if (n_rows == 0) return DG_OK;
     if (!out || !dg::aligned16(out)) return out ? DG_EALIGN : DG_EINVAL;
-    const dg_epi_target t{groups, n_groups, 0, out, n_rows, {0, 0, 0}};
+    const dg_epi_target t{groups, n_groups, 0, out, n_rows, 0, {0, 0}};
     return dg_gcn_epilogue_multi_f32(&t, 1, d, flags, stream);
 }
 

@@ -324,8 +324,9 @@ class ForwardPlan:
         self.row_block = dict(dgraph.row_block)
         self.world = shard.world_size if shard is not None else 1
         self.allgather = shard.allgather if shard is not None else None
-        if self.row_block and (shard is None or self.allgather is None or shard.row_block != self.row_block):
-            raise ValueError("a row-split device graph needs its RelationShard (with an all-gather)")
+        if self.row_block and (shard is None or shard.row_block != self.row_block
+                               or (self.allgather is None and getattr(shard, "peer", None) is None)):
+            raise ValueError("a row-split device graph needs its RelationShard (with an all-gather or a peer exchange)")
         if shard is not None and allreduce is None:
             raise ValueError("a RelationShard needs its all-reduce")
         # dropout (training): (keep probability, device state {seed, step}); every forward
@@ -399,8 +400,9 @@ class ForwardPlan:
                         self._pre.append(lambda W=W, xd=xd, t=t: kernels.dropout_rows(W, xd, self.drop_state, t,
                                                                                       self.keep))
                     elif grp.n_rels:
-                        self._pre.append(lambda W=W, xd=xd, t=t, m=grp.rel_map, F=F: kernels.dropout_rows_map(
-                            W, xd, m, F, self.drop_state, t, self.keep, True, True))
+                        self._pre.append(lambda W=W, xd=xd, t=t, m=grp.rel_map, F=F, mx=int(grp.rel_ids.max()):
+                                         kernels.dropout_rows_map(W, xd, m, F, self.drop_state, t, self.keep, True,
+                                                                  True, rel_map_max=mx))
                     x1[et] = xd
                 continue
             if fj.shape[0] != n[j] or fj.shape[1] != F:
@@ -420,15 +422,33 @@ class ForwardPlan:
 
         # row-split node types: the full output rows live in a buffer padded to world × block
         # rows (this rank finishes its block in place, the all-gather fills the rest)
-        # (keyed by node type and layer: h1 == h2 must not share a buffer)
+        # (keyed by node type and layer: h1 == h2 must not share a buffer).  Every such buffer
+        # is carved from ONE exchange region with the same layout on every rank, which a peer
+        # exchange (peer.py) maps into every peer
         self._pad: Dict[Tuple[int, int], torch.Tensor] = {}
+        self.xregion: Optional[torch.Tensor] = None
+        self.peer = None
+        split_nodes = [i for i in self.targets if i in self.row_block]
+        if split_nodes:
+            layout, off = {}, 0
+            for layer, d in ((1, h1), (2, h2)):
+                for i in split_nodes:
+                    nb = self.world * self.row_block[i][2] * d
+                    layout[i, layer] = (off, nb, d)
+                    off += -(-nb // 64) * 64  # 256-byte aligned
+            self.xregion = torch.empty(max(off, 64), **f32)
+            for (i, layer), (o, nb, d) in layout.items():
+                self._pad[i, layer] = self.xregion[o:o + nb].view(-1, d)
+            pc = getattr(shard, "peer", None)
+            if pc is not None:
+                from .peer import PeerExchange
+
+                self.peer = PeerExchange(self.xregion, shard.rank, self.world, pc)
 
         def out_buf(i, d, layer):
             if i not in self.row_block:
                 return torch.empty((n[i], d), **f32)
-            pad = torch.empty((self.world * self.row_block[i][2], d), **f32)
-            self._pad[i, layer] = pad
-            return pad[:n[i]]
+            return self._pad[i, layer][:n[i]]
 
         self.hidden1 = {i: out_buf(i, h1, 1) for i in self.targets}
         self.embeddings = {i: out_buf(i, h2, 2) for i in self.targets}
@@ -510,8 +530,8 @@ class ForwardPlan:
                     drops.append(lambda j=j, hd=hd, t=t: kernels.dropout_elems(self.hidden1[j], hd, self.drop_state,
                                                                                t, self.keep))
                 else:
-                    drops.append(lambda j=j, hd=hd, t=t, m=smap: kernels.dropout_elems_map(
-                        self.hidden1[j], hd, m, self.drop_state, t, self.keep))
+                    drops.append(lambda j=j, hd=hd, t=t, m=smap, mx=int(sids.max()): kernels.dropout_elems_map(
+                        self.hidden1[j], hd, m, self.drop_state, t, self.keep, rel_map_max=mx))
                 gemms.append(kernels.PreparedGemm(
                     hd, (n[j] * h1, h1, 1), W, (h1 * h2, h2, 1), self.proj[et], (n[j] * h2, h2, 1),
                     n[j], h2, h1, grp.n_rels, b_map=smap, b_batches=W.shape[0],
@@ -586,10 +606,13 @@ class ForwardPlan:
                 tgts.append((pad[r0:r0 + (b - a)], b - a,
                              [self._seg_spec(et, seg_w[et][0], None, seg_w[et][1]) if et in seg_w
                               else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu))
-            launches.append(kernels.PreparedFusedSeg(tgts, self.h1 if seg_w else d, d))
+            fused_peer = self._peer_fused(relu)
+            launches.append(kernels.PreparedFusedSeg(tgts, self.h1 if seg_w else d, d, peer=fused_peer))
             self.launch_groups[id(launches[-1])] = [et for i in self.targets for et in self.targets[i]]
+            if fused_peer is not None:
+                gathers = []  # the launch itself ends with the exchange
             return _Layer(launches, None, False, self.allreduce, [], [], {}, self.side_stream, None, (), gathers,
-                          self.allgather)
+                          self.allgather, self._peer_gather_all(gathers, relu))
         if self.fused_seg:
             seg_w = seg_w or {}
             tgts = [(outs[i], n[i], [self._seg_spec(et, seg_w[et][0], None, seg_w[et][1]) if et in seg_w
@@ -691,6 +714,7 @@ class ForwardPlan:
             self.launch_groups[id(launches[-1])] = spmm_ets[s:s + DG_MAX_GROUPS]
         need_zero = send is flat and flat is not None and any(g.groups[et].n_rels == 0 for et in red)
         epis, local_epis = [], []
+        epi_peer = self._peer_fused(relu) if split_t else None
         if split_t:
             blocks = []
             for i in split_t:
@@ -705,7 +729,9 @@ class ForwardPlan:
                         views[et] = torch.empty((b - a) * d, **f32)
                         parts[n_] = (parts[n_][0], parts[n_][1], views[et])
                 blocks.append((parts, pad[r0:r0 + (b - a)], b - a))
-                gathers.append((pad, pad[r0:r0 + blk]))
+                if epi_peer is None:  # (else the epilogue launch itself ends with the exchange)
+                    gathers.append((pad, pad[r0:r0 + blk]))
+            n_push = len(blocks)
             # the relation-sharded node types' chunk reduces ride in the same launch: a target
             # whose groups write their pre-normalisation sums into the send buffer (its
             # finished rows go to a scratch buffer, unread) — one launch per layer instead of two
@@ -721,7 +747,8 @@ class ForwardPlan:
                         grp_parts.append((part, nc, sviews[et] if reduced else None))
                     blocks.append((grp_parts, torch.empty((n[i], d), **f32), n[i]))
                 reduces = []
-            local_epis.append(kernels.PreparedEpilogueMulti(blocks, d, flags))
+            local_epis.append(kernels.PreparedEpilogueMulti(
+                blocks, d, flags, peer=epi_peer, push=[t < n_push for t in range(len(blocks))]))
         launches += reduces
         if flat is not None:
             # sharded: the all-reduced group sums S_ij are finished by ONE fused launch whose
@@ -749,7 +776,39 @@ class ForwardPlan:
                 epis.append(kernels.PreparedEpilogueMulti(
                     [([partials[et] for et in self.targets[i]], outs[i], n[i]) for i in tl], d, flags))
         return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream, send,
-                      local_epis, gathers, self.allgather)
+                      local_epis, gathers, self.allgather, self._peer_gather_all(gathers, relu))
+
+    # ---- peer exchange (peer.py) ----
+    def _peer_fused(self, layer1: bool):
+        """(PeerExchange, slot) for a finishing launch that pushes its rows and exchanges, or None."""
+        if self.peer is None or self.peer.cfg.mode != "fused":
+            return None
+        from .peer import SLOT_FUSED
+
+        return self.peer, SLOT_FUSED + (0 if layer1 else 1)
+
+    def _peer_gather_all(self, gathers, layer1: bool):
+        """With a peer exchange, the layer's remaining all-gathers as ONE stand-alone
+        dg_peer_allgather launch (mode "kernel", or a finishing launch without a push form)."""
+        if self.peer is None or not gathers:
+            return None
+        from .peer import SLOT_KERNEL
+
+        return self.peer.allgather_fn([blk for _, blk in gathers], SLOT_KERNEL + (0 if layer1 else 1))
+
+    def peer_probe(self):
+        """bench.py: each layer's stand-alone peer exchange of this rank's blocks (slots
+        SLOT_PROBE + layer - 1), to time beside whatever exchange the plan runs."""
+        from .peer import SLOT_PROBE
+
+        out = []
+        for layer in (1, 2):
+            blks = [self._pad[i, layer][self.shard.rank * self.row_block[i][2]:
+                                        (self.shard.rank + 1) * self.row_block[i][2]]
+                    for i in self.targets if i in self.row_block]
+            if blks:
+                out.append(self.peer.allgather_fn(blks, SLOT_PROBE + layer - 1))
+        return out
 
     def _identity_spec(self, i: int, x: torch.Tensor, d: int) -> kernels.RelGroupSpec:
         """A group spec with no adjacency (DG_GROUP_DENSE_ROWS): the fused kernel reads the dense
@@ -883,7 +942,7 @@ class _Layer:
     """The prepared launches of one layer and how to run them."""
 
     def __init__(self, launches, flat, need_zero, allreduce, epilogues, fused_targets, views=None,
-                 side_stream=None, send=None, local_epilogues=(), gathers=(), allgather=None):
+                 side_stream=None, send=None, local_epilogues=(), gathers=(), allgather=None, gather_all=None):
         self.launches = launches
         self.side_stream = side_stream
         self.flat = flat
@@ -896,6 +955,7 @@ class _Layer:
         self.local_epilogues = list(local_epilogues)  # row-split blocks, finished before the exchange
         self.gathers = list(gathers)                  # (padded out, this rank's block) per node type
         self.allgather = allgather
+        self.gather_all = gather_all                  # all gathers in one peer-exchange launch
 
     @property
     def has_exchange(self) -> bool:
@@ -906,6 +966,9 @@ class _Layer:
         all-gather of the row-split blocks."""
         if self.flat is not None and self.allreduce is not None:
             self.allreduce(self.send, self.flat)
+        if self.gather_all is not None:
+            self.gather_all()
+            return
         for out, blk in self.gathers:
             self.allgather(out, blk)
 

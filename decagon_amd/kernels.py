@@ -286,7 +286,10 @@ class PreparedFusedSeg:
     each output row finished by one workgroup, one wave per relation (at most 16 a row; groups
     chunk-merged, any chunks); with weight stacks (d_in 64 → d_out 32) the reassociated layer 2."""
 
-    def __init__(self, targets, d_in: int, d_out: int):
+    def __init__(self, targets, d_in: int, d_out: int, peer=None):
+        """peer = (PeerExchange, slot): every target's `out` lies in the exchange region; the
+        launch also pushes the rows to every peer and ends with the exchange
+        (dg_gcn_fused_seg_peer_f32)."""
         specs, tarr = [], (DgFusedTarget * len(targets))()
         for t, (out, n_rows, gspecs, relu) in enumerate(targets):
             _dev(out, torch.float32, "out")
@@ -306,9 +309,22 @@ class PreparedFusedSeg:
         self._garr = _seg_array(specs, d_in, d_out, False)
         self._keep = (specs, [t[0] for t in targets])
         self._tarr, self._ng, self._nt, self.d_in, self.d_out = tarr, len(specs), len(targets), d_in, d_out
-        self._fn = _lib.load().dg_gcn_fused_seg_f32
+        self._xchg = None
+        if peer is not None:
+            ex, slot = peer
+            for out, *_ in targets:
+                ex.offset(out)  # raises unless inside the region
+            self._xchg = ctypes.byref(ex.xchg(slot))
+            self._keep = self._keep + (ex,)
+            self._fn = _lib.load().dg_gcn_fused_seg_peer_f32
+        else:
+            self._fn = _lib.load().dg_gcn_fused_seg_f32
 
     def __call__(self, stream=None) -> None:
+        if self._xchg is not None:
+            check(self._fn(self._garr, self._ng, self._tarr, self._nt, self.d_in, self.d_out, self._xchg,
+                           _stream_ptr(stream)), "dg_gcn_fused_seg_peer_f32")
+            return
         check(self._fn(self._garr, self._ng, self._tarr, self._nt, self.d_in, self.d_out, _stream_ptr(stream)),
               "dg_gcn_fused_seg_f32")
 
@@ -589,7 +605,10 @@ class PreparedEpilogueMulti:
     group's optional sum_out [n_rows, d] receives its pre-normalisation sum S_ij."""
 
     def __init__(self, targets: Sequence[Tuple[Sequence[Tuple[torch.Tensor, int]], torch.Tensor, int]], d: int,
-                 flags: int):
+                 flags: int, peer=None, push: Optional[Sequence[bool]] = None):
+        """peer = (PeerExchange, slot): the targets flagged in `push` (their `out` inside the
+        exchange region) also go to every peer, and the launch ends with the exchange
+        (dg_gcn_epilogue_peer_f32)."""
         if not targets or len(targets) > 8:
             raise ValueError("1..8 targets per launch")
         if sum(len(p) for p, _, _ in targets) > _lib.DG_MAX_GROUPS:
@@ -622,12 +641,24 @@ class PreparedEpilogueMulti:
             tarr[t].n_groups = len(partials)
             tarr[t].out = out.data_ptr()
             tarr[t].n_rows = n_rows
+            if peer is not None and (push is None or push[t]):
+                peer[0].offset(out)  # raises unless inside the region
+                tarr[t].target_flags = _lib.DG_EPI_PUSH
         self._tarr = tarr
         self._args = (len(targets), d, flags)
-        self._fn = _lib.load().dg_gcn_epilogue_multi_f32
+        self._xchg = None
+        if peer is not None:
+            self._xchg = ctypes.byref(peer[0].xchg(peer[1]))
+            self._keep.append(peer[0])
+            self._fn = _lib.load().dg_gcn_epilogue_peer_f32
+        else:
+            self._fn = _lib.load().dg_gcn_epilogue_multi_f32
 
     def __call__(self, stream=None) -> None:
         n, d, f = self._args
+        if self._xchg is not None:
+            check(self._fn(self._tarr, n, d, f, self._xchg, _stream_ptr(stream)), "dg_gcn_epilogue_peer_f32")
+            return
         check(self._fn(self._tarr, n, d, f, _stream_ptr(stream)), "dg_gcn_epilogue_multi_f32")
 
 
@@ -1191,21 +1222,33 @@ def dropout_elems(src: torch.Tensor, out: torch.Tensor, state: torch.Tensor, tag
                                            _stream_ptr(stream)), "dg_dropout_elems_f32")
 
 
+def _map_max(rel_map: torch.Tensor, rel_map_max: Optional[int]) -> int:
+    """max(rel_map): host-known (plans pass it, so a captured step never syncs) or read once."""
+    if not rel_map.numel():
+        return -1
+    return int(rel_map.max()) if rel_map_max is None else int(rel_map_max)
+
+
 def dropout_rows_map(inp: torch.Tensor, out: torch.Tensor, rel_map: torch.Tensor, rows_per_slab: int,
                      state: torch.Tensor, tag: int, keep: float, in_global: bool, out_global: bool,
-                     stream=None) -> None:
+                     stream=None, rel_map_max: Optional[int] = None) -> None:
     """Row masks of a relation shard: local slab b (rows_per_slab rows) is global relation
     rel_map[b] and takes its mask bits; in / out addressed at global slabs (in_global /
-    out_global) or local ones (dg_dropout_rows_map_f32)."""
+    out_global) or local ones (dg_dropout_rows_map_f32).  The mask bit of a row is its global
+    row index, 32-bit: (max(rel_map) + 1)·rows_per_slab must stay below 2^32, as the
+    unmapped dg_dropout_rows_f32 requires of its rows."""
     _dev(inp, torch.float32, "in")
     _dev(out, torch.float32, "out")
     _dev(rel_map, torch.int32, "rel_map")
     _drop_state(state)
     d = inp.shape[-1]
     n_map = rel_map.numel()
+    mx = _map_max(rel_map, rel_map_max)
+    if (mx + 1) * rows_per_slab >= 0xFFFFFFFF:
+        raise ValueError("dropout_rows_map: global row indices exceed the 32-bit mask counter")
     for t, glob in ((inp, in_global), (out, out_global)):
         slabs = t.numel() // (rows_per_slab * d) if rows_per_slab else 0
-        need = (int(rel_map.max()) + 1) if (glob and n_map) else n_map
+        need = (mx + 1) if (glob and n_map) else n_map
         if t.shape[-1] != d or slabs < need:
             raise ValueError("dropout_rows_map: operand too small for its slabs")
     check(_lib.load().dg_dropout_rows_map_f32(inp.data_ptr(), out.data_ptr(), rel_map.data_ptr(), n_map,
@@ -1215,9 +1258,11 @@ def dropout_rows_map(inp: torch.Tensor, out: torch.Tensor, rel_map: torch.Tensor
 
 
 def dropout_elems_map(src: torch.Tensor, out: torch.Tensor, rel_map: torch.Tensor, state: torch.Tensor, tag: int,
-                      keep: float, stream=None) -> None:
+                      keep: float, stream=None, rel_map_max: Optional[int] = None) -> None:
     """out[b] = src ∘ M_{rel_map[b]} / keep (src [n][d], out [K_local][n][d]): the per-relation
-    tf.nn.dropout masks of a relation shard (dg_dropout_elems_map_f32)."""
+    tf.nn.dropout masks of a relation shard (dg_dropout_elems_map_f32).  Mask elements are
+    rel_map[b]·n·d + r·d + f, 32-bit: (max(rel_map) + 1)·n·d must stay below 2^32, as the
+    unmapped dg_dropout_elems_f32 requires of its K·n·d."""
     _dev(src, torch.float32, "src")
     _dev(out, torch.float32, "out")
     _dev(rel_map, torch.int32, "rel_map")
@@ -1225,6 +1270,8 @@ def dropout_elems_map(src: torch.Tensor, out: torch.Tensor, rel_map: torch.Tenso
     K, n, d = out.shape
     if tuple(src.shape) != (n, d) or rel_map.numel() != K:
         raise ValueError("dropout_elems_map: shapes")
+    if (_map_max(rel_map, rel_map_max) + 1) * n * d >= 0xFFFFFFFF:
+        raise ValueError("dropout_elems_map: mask element indices exceed the 32-bit mask counter")
     check(_lib.load().dg_dropout_elems_map_f32(src.data_ptr(), out.data_ptr(), rel_map.data_ptr(), K, n, d,
                                                state.data_ptr(), tag, keep, _stream_ptr(stream)),
           "dg_dropout_elems_map_f32")

@@ -277,9 +277,10 @@ class DecagonOptimizer:
         params = [p for p, _ in pairs] + [model.edge_type2decoder[et].flat for et in ets]
         grads = [g for _, g in pairs] + [dec_grads[et] for et in ets]
         if not apply:
-            if tp.sharded:
-                raise NotImplementedError("grads_vars under sharding: each relation's gradient lives on its owner rank")
-            return self._grads_vars(model, tp, dec_grads)
+            # (sharded: every relation's gradient gathered from its owner rank, so every rank
+            # returns the whole model's (gradient, variable) list, as compute_gradients does)
+            gW1, gW2 = tp.full_grads()
+            return self._grads_vars(model, gW1, gW2, dec_grads)
         # the Adam slots belong to the variables (session-wide); the prepared launch, which holds
         # this plan's gradient buffers, lives on the TrainPlan, so evicting the plan frees both
         key = ("adam", id(self))
@@ -293,15 +294,16 @@ class DecagonOptimizer:
         st.apply(prep[1])
         return None
 
-    def _grads_vars(self, model, tp, dec_grads):
-        """[(gradient, variable value)] in model.vars order (layers 1, layers 2, decoders)."""
+    def _grads_vars(self, model, gW1, gW2, dec_grads):
+        """[(gradient, variable value)] in model.vars order (layers 1, layers 2, decoders);
+        gW1 / gW2: every relation's gradient stack (TrainPlan.full_grads)."""
         out = []
         for et, lay in model.layers1.items():
             for k in range(lay.num_types):
-                out.append((tp.gW1[et][k], lay.vars["weights_%d" % k].tensor))
+                out.append((gW1[et][k], lay.vars["weights_%d" % k].tensor))
         for et, lay in model.layers2.items():
             for k in range(lay.num_types):
-                out.append((tp.gW2[et][k], lay.vars["weights_%d" % k].tensor))
+                out.append((gW2[et][k], lay.vars["weights_%d" % k].tensor))
         for et, dec in model.edge_type2decoder.items():
             for var in dec.vars.values():
                 off = (var.tensor.data_ptr() - dec.flat.data_ptr()) // 4

@@ -1,0 +1,201 @@
+"""Peer-store exchange over xGMI: the sharded forward's all-gather of row-split blocks without
+RCCL (csrc/peer.h has the device protocol, include/decagon_hip.h the C ABI).
+
+Why: config S at N GPUs (weak scaling, sharding.RelationShard.weak_sets) exchanges two small
+row blocks per step (29 KB + 14 KB per rank at N = 8).  An RCCL all-gather of that size costs
+several µs of launch, handshake and per-hop latency; ≥ 6× at 8 GPUs leaves ≈ 2 µs for both
+(DESIGN.md §6).  Here every rank's finishing kernel stores its finished rows straight into
+every peer's copy of the output (IPC-mapped peer memory) and its last workgroup raises an
+arrival flag at every peer and waits — bounded — for theirs, so the exchange costs no launch
+of its own.
+
+    region   one device tensor per rank holding every row-split output of the plan, the same
+             layout on every rank (ForwardPlan carves the padded outputs from it); exported
+             with hipIpcGetMemHandle and opened by every peer
+    flags    one uncached block per rank ([DG_PEER_SLOTS][DG_PEER_MAX] words) that the peers
+             write and only its owner polls
+    state    this rank's per-slot {arrivals, epoch} and the error word (a torch int32 tensor)
+
+Modes (PeerConfig.mode): "fused" — the row-split layer's finishing launch pushes and
+exchanges (dg_gcn_epilogue_peer_f32 / dg_gcn_fused_seg_peer_f32), slots 0 and 1;
+"kernel" — the layer's exchange is one stand-alone dg_peer_allgather launch, slots 2 and 3.
+`loopback` is the one-GPU rehearsal: every "peer" copy is local scratch, and the last
+workgroup raises every rank's flag itself, so one process times a rank's share with the
+exchange's stores, arrivals, flags and polls in it (not the xGMI wire latency).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import DgPeerXchg, check
+
+TIMEOUT_S = 2.0          # a wait gives up (error word) after this long
+_TICKS_PER_S = 100e6     # s_memrealtime: 100 MHz
+
+SLOT_FUSED = 0           # + layer - 1
+SLOT_KERNEL = 2          # + layer - 1
+SLOT_PROBE = 4           # + layer - 1: bench.py's stand-alone exchange timing beside another mode
+
+
+@dataclass
+class PeerConfig:
+    """How a RelationShard's row-split blocks are exchanged when not over RCCL."""
+
+    mode: str = "fused"                                       # "fused" | "kernel"
+    gather: Optional[Callable[[object], List[object]]] = None  # all-gather of picklable objects
+    loopback: bool = False
+    timeout_s: float = TIMEOUT_S
+
+    def __post_init__(self):
+        if self.mode not in ("fused", "kernel"):
+            raise ValueError(f"unknown peer exchange mode {self.mode!r}")
+        if not self.loopback and self.gather is None:
+            raise ValueError("a peer exchange across processes needs an object all-gather")
+
+
+def dist_gather(group=None) -> Callable[[object], List[object]]:
+    """The object all-gather of torch.distributed's default (or given) group."""
+    import torch.distributed as dist
+
+    def _g(obj):
+        out = [None] * dist.get_world_size(group)
+        dist.all_gather_object(out, obj, group=group)
+        return out
+
+    return _g
+
+
+class PeerExchange:
+    """This rank's view of every rank's exchange region and flag block (collective: every
+    rank constructs it at the same point, with regions of the same size and layout)."""
+
+    def __init__(self, region: torch.Tensor, rank: int, world: int, cfg: PeerConfig):
+        if not region.is_cuda or not region.is_contiguous():
+            raise ValueError("the exchange region must be a contiguous device tensor")
+        if region.data_ptr() % 16:
+            raise ValueError("the exchange region must be 16-byte aligned")
+        if not 1 <= world <= _lib.DG_PEER_MAX or not 0 <= rank < world:
+            raise ValueError(f"peer exchange: rank {rank} of {world} (at most {_lib.DG_PEER_MAX} ranks)")
+        self.lib = _lib.load()
+        self.region, self.rank, self.world, self.cfg = region, rank, world, cfg
+        self.nbytes = region.numel() * region.element_size()
+        dev = region.device
+        self.state = torch.zeros(32, dtype=torch.int32, device=dev)
+        fp = ctypes.c_void_p()
+        check(self.lib.dg_peer_alloc(4 * _lib.DG_PEER_SLOTS * _lib.DG_PEER_MAX, 2, ctypes.byref(fp)), "dg_peer_alloc")
+        self._flags = fp.value
+        self._opened: List[int] = []
+        self._scratch: List[torch.Tensor] = []
+        base = region.data_ptr()
+        bases, flags = [0] * world, [0] * world
+        if cfg.loopback:
+            for p in range(world):
+                if p == rank:
+                    bases[p] = base
+                else:
+                    self._scratch.append(torch.empty_like(region))
+                    bases[p] = self._scratch[-1].data_ptr()
+                flags[p] = self._flags
+        else:
+            mine = (self._handle(base), self._handle(self._flags), self.nbytes)
+            got = cfg.gather(mine)
+            if len(got) != world:
+                raise RuntimeError(f"peer exchange: {len(got)} ranks answered, {world} expected")
+            for p, ((h, off), (hf, offf), nb) in enumerate(got):
+                if nb != self.nbytes:
+                    raise RuntimeError(f"peer exchange: rank {p}'s region is {nb} B, this rank's {self.nbytes} B")
+                if p == rank:
+                    bases[p], flags[p] = base, self._flags
+                    continue
+                bases[p] = self._open(h) + off
+                flags[p] = self._open(hf) + offf
+        self.bases, self.flags = bases, flags
+        self.delta = [b - base for b in bases]
+        if any(d % 16 for d in self.delta):
+            raise RuntimeError("peer exchange: a peer region is not 16-byte aligned")
+        self._descs = {}
+
+    # ---- IPC ----
+    def _handle(self, ptr: int) -> Tuple[bytes, int]:
+        h = (ctypes.c_char * _lib.DG_IPC_HANDLE_BYTES)()
+        off = ctypes.c_int64()
+        check(self.lib.dg_ipc_get_handle(ptr, h, ctypes.byref(off)), "dg_ipc_get_handle")
+        return bytes(h), int(off.value)
+
+    def _open(self, handle: bytes) -> int:
+        h = (ctypes.c_char * _lib.DG_IPC_HANDLE_BYTES).from_buffer_copy(handle)
+        p = ctypes.c_void_p()
+        check(self.lib.dg_ipc_open(h, ctypes.byref(p)), "dg_ipc_open (hipIpcOpenMemHandle)")
+        self._opened.append(p.value)
+        return p.value
+
+    # ---- descriptors ----
+    def xchg(self, slot: int) -> DgPeerXchg:
+        """The C descriptor of one exchange slot (kept alive by this object)."""
+        if not 0 <= slot < _lib.DG_PEER_SLOTS:
+            raise ValueError(f"slot {slot} out of range")
+        d = self._descs.get(slot)
+        if d is None:
+            d = DgPeerXchg()
+            for p in range(self.world):
+                d.delta[p] = self.delta[p]
+                d.flags[p] = self.flags[p]
+            d.state = self.state.data_ptr()
+            d.timeout_ticks = int(self.cfg.timeout_s * _TICKS_PER_S)
+            d.rank, d.world, d.slot, d.loopback = self.rank, self.world, slot, int(self.cfg.loopback)
+            self._descs[slot] = d
+        return d
+
+    def offset(self, t: torch.Tensor) -> int:
+        """Byte offset of a tensor (view) inside the region."""
+        off = t.data_ptr() - self.region.data_ptr()
+        if off < 0 or off + t.numel() * t.element_size() > self.nbytes:
+            raise ValueError("tensor is not inside the exchange region")
+        return off
+
+    def allgather_fn(self, blocks: Sequence[torch.Tensor], slot: int) -> Callable[[], None]:
+        """A prepared stand-alone exchange of this rank's blocks (views of the region)."""
+        n = len(blocks)
+        if not 1 <= n <= _lib.DG_MAX_GROUPS:
+            raise ValueError("1..8 blocks per exchange")
+        offs = (ctypes.c_int64 * n)(*[self.offset(b) for b in blocks])
+        sizes = (ctypes.c_int64 * n)(*[b.numel() * b.element_size() for b in blocks])
+        x = self.xchg(slot)
+        fn, reg = self.lib.dg_peer_allgather, self.region.data_ptr()
+        keep = (offs, sizes, x, list(blocks))
+
+        def run(stream=None):
+            _ = keep
+            s = torch.cuda.current_stream() if stream is None else stream
+            check(fn(ctypes.byref(x), reg, offs, sizes, n, s.cuda_stream), "dg_peer_allgather")
+
+        return run
+
+    # ---- status ----
+    def error(self) -> int:
+        """The error word (0: every wait so far completed); synchronises the device."""
+        torch.cuda.synchronize(self.region.device)
+        return int(self.state[_lib.DG_PEER_ERROR_WORD].item())
+
+    def check(self) -> None:
+        e = self.error()
+        if e:
+            raise RuntimeError(f"peer exchange timed out: slot {(e >> 8) & 0xff}, waiting for rank {e & 0xff} "
+                               f"(error word {e:#x})")
+
+    def close(self) -> None:
+        """Unmap the peers' regions and free the flag block (after the last exchange)."""
+        if self.region.is_cuda:
+            torch.cuda.synchronize(self.region.device)
+        for p in self._opened:
+            self.lib.dg_ipc_close(p)
+        self._opened = []
+        if self._flags:
+            self.lib.dg_peer_free(self._flags)
+            self._flags = 0
+        self._scratch = []

@@ -98,6 +98,10 @@ class RelationShard:
     # row-split node types in dg_spmm_seg_f32 + the epilogue, layer 2 reassociated (config S's
     # weak scaling at N GPUs; `chunks` then holds the relations per set)
     seg_rows: bool = False
+    # the row-split blocks exchanged by peer stores over xGMI instead of `allgather`
+    # (peer.PeerConfig: the finishing launch pushes its rows and ends with the exchange, or a
+    # stand-alone exchange launch); the all-reduce of relation-sharded sums stays `allreduce`
+    peer: Optional[object] = None
 
     @staticmethod
     def lpt(edge_types: Dict[EdgeType, int], rel_cost: Dict[EdgeType, Sequence[float]], rank: int,

@@ -220,8 +220,9 @@ class TrainPlan:
                     self._w1_drop.append(lambda g=self.gW1[et], tg=tg:
                                          kernels.dropout_rows(g, g, fwd.drop_state, tg, fwd.keep))
                 else:
-                    self._w1_drop.append(lambda g=self.gW1[et], tg=tg, m=idmap, F=F: kernels.dropout_rows_map(
-                        g, g, m, F, fwd.drop_state, tg, fwd.keep, False, False))
+                    self._w1_drop.append(lambda g=self.gW1[et], tg=tg, m=idmap, F=F, mx=int(ids.max()):
+                                         kernels.dropout_rows_map(g, g, m, F, fwd.drop_state, tg, fwd.keep, False,
+                                                                  False, rel_map_max=mx))
             runs[j].append((part, n_runs))
         chunked = lambda xs: [xs[s:s + DG_MAX_GROUPS] for s in range(0, len(xs), DG_MAX_GROUPS)]  # noqa: E731
         # Âᵀ·dS: operands small enough for LDS (the drug side) take the LDS-staged form
@@ -281,6 +282,44 @@ class TrainPlan:
             f()
         for gr in self._rowsplit_grads:  # row-split groups: Σ over the ranks' row blocks
             self.allreduce(gr)
+
+    def full_grads(self) -> Tuple[Dict[EdgeType, torch.Tensor], Dict[EdgeType, torch.Tensor]]:
+        """Every relation's W1 / W2 gradient as full [K, ...] stacks, on every rank — what
+        compute_gradients returns for the whole model (optimizer.py:114).  One GPU: the stacks
+        themselves.  Sharded: a relation-sharded group's relation k lives on its owner rank
+        only, so the local slices are placed at their global ids in zero stacks and the stacks
+        of every such group are summed over the ranks in ONE all-reduce (exactly one rank owns
+        each relation: the sum is a gather, bit-exact); a row-split group's stacks are already
+        complete and equal on every rank (all-reduced by the backward) and are copied."""
+        if not self.sharded:
+            return self.gW1, self.gW2
+        rb = self.fwd.row_block
+        shapes, sizes = [], []
+        for name, grads in (("w1", self.gW1), ("w2", self.gW2)):
+            for et in self.fwd.edge_types:
+                if et[0] in rb:
+                    continue
+                K = self.fwd.g.groups[et].K
+                shapes.append((name, et, (K,) + tuple(grads[et].shape[1:])))
+                sizes.append(int(np.prod(shapes[-1][2])))
+        dev = self.fwd.g.device
+        flat = torch.zeros(int(sum(sizes)), dtype=torch.float32, device=dev)
+        out = {"w1": {}, "w2": {}}
+        off = 0
+        for (name, et, shape), sz in zip(shapes, sizes):
+            full = flat[off:off + sz].view(shape)
+            off += sz
+            ids = self.local_ids[et]
+            if len(ids):
+                full[torch.from_numpy(ids).to(dev)] = (self.gW1 if name == "w1" else self.gW2)[et]
+            out[name][et] = full
+        if flat.numel():
+            self.allreduce(flat)
+        for name, grads in (("w1", self.gW1), ("w2", self.gW2)):
+            for et in self.fwd.edge_types:
+                if et[0] in rb:
+                    out[name][et] = grads[et].clone()
+        return out["w1"], out["w2"]
 
     def adam_pairs(self, w1: LayerWeights, w2: LayerWeights) -> List[Tuple[torch.Tensor, torch.Tensor]]:
         """(parameter, gradient) of every GCN weight this plan updates: whole stacks on one GPU;

@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (31); bumped whenever a struct layout or a signature changes. */
+/* ABI version (32); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -104,8 +104,6 @@ typedef struct dg_rel_group {
 int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
                        int32_t d, void* stream);
 
-/* Single relation, plain CSR: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
- * Replaces one tf.sparse_tensor_dense_matmul (layers.py:90).  ldy must equal d. */
 /* The same partial-mode product (out[c][r][:] = Σ val·X[vcol][:]) for groups whose whole
  * dense operand is small — x_rows <= 1137 rows (it is staged in LDS, 144 B per row per
  * 32-column slice): the backward's Âᵀ·dS_ij, where every relation of the group reads the
@@ -115,6 +113,8 @@ int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_gr
 int dg_spmm_groups_lds_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups, int32_t d,
                            void* stream);
 
+/* Single relation, plain CSR: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
+ * Replaces one tf.sparse_tensor_dense_matmul (layers.py:90).  ldy must equal d. */
 int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                     int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx, float* y,
                     int64_t ldy, int32_t d, void* stream);
@@ -332,11 +332,80 @@ typedef struct dg_epi_target {
     int32_t reserved0;
     float* out;                 /* device, [n_rows][d], 16-byte aligned                     */
     int32_t n_rows;
-    int32_t reserved[3];
+    int32_t target_flags;       /* 0, or DG_EPI_PUSH (dg_gcn_epilogue_peer_f32 only)        */
+    int32_t reserved[2];
 } dg_epi_target;
 
 int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets /* HOST array */, int32_t n_targets,
                               int32_t d, int32_t flags, void* stream);
+
+/* --------------------------------------------------------------------------------------
+ * Peer-store exchange over xGMI: the all-gather of the row-split blocks of the sharded
+ * forward (decagon_amd/sharding.py; one per layer, made necessary by the normalisation of
+ * the full per-(i,j) sum, layers.py:92-93), without RCCL.
+ *
+ * Every rank holds the row-split outputs of a layer in ONE exchange region of the same layout
+ * on every rank (its own rows block `rank`); each rank maps every peer's region (IPC) and
+ * stores its finished rows straight into them, write-through at system scope.  The launch's
+ * last workgroup then stores the slot's epoch into word [slot][rank] of every peer's flag
+ * block (uncached memory) and waits — bounded by timeout_ticks of the 100 MHz s_memrealtime
+ * clock — until every rank's epoch for the slot has arrived in its own block; the kernels
+ * that read the gathered rows start after that launch ends.  A wait that times out sets the
+ * error word state[DG_PEER_ERROR_WORD] (0x10000 | slot << 8 | source rank) and returns; once
+ * it is set, every later wait returns at once (the host checks the word and raises).
+ * state: this rank's device words, zeroed once: per slot {arrivals, epoch}, then the error word.
+ * A slot's launches must all use the same grid (the arrival count), and every rank must run
+ * the same sequence of exchanges per slot.
+ * Replaces: the RCCL/NCCL all-gather of the sharded step (the reference has no parallelism).
+ * -------------------------------------------------------------------------------------- */
+#define DG_PEER_MAX 8
+#define DG_PEER_SLOTS 8
+#define DG_PEER_STATE_WORDS (2 * DG_PEER_SLOTS + 1)
+#define DG_PEER_ERROR_WORD (2 * DG_PEER_SLOTS)
+#define DG_IPC_HANDLE_BYTES 64
+#define DG_EPI_PUSH 1           /* dg_epi_target.target_flags: push this target's rows          */
+
+typedef struct dg_peer_xchg {
+    int64_t delta[DG_PEER_MAX];   /* bytes from this rank's exchange region to rank p's region as
+                                     mapped in this process (delta[rank] = 0; 16-byte multiples) */
+    uint32_t* flags[DG_PEER_MAX]; /* rank p's flag block [DG_PEER_SLOTS][DG_PEER_MAX], mapped here */
+    uint32_t* state;              /* device, DG_PEER_STATE_WORDS words of THIS rank, zeroed once  */
+    int64_t timeout_ticks;        /* > 0: s_memrealtime ticks (100 MHz) a wait may spin           */
+    int32_t rank, world;          /* 1 <= world <= DG_PEER_MAX                                    */
+    int32_t slot;                 /* < DG_PEER_SLOTS                                              */
+    int32_t loopback;             /* 1: one-GPU rehearsal — every "peer" region is local scratch, */
+                                  /* flags[p] all this rank's block, and the last workgroup raises */
+                                  /* word [slot][p] for every p itself                             */
+} dg_peer_xchg;
+
+/* Device memory for the exchange: kind 0 = hipMalloc-like (coarse-grained), 1 = fine-grained,
+ * 2 = uncached (the flag blocks).  Zero-filled.  These two are the library's only allocating
+ * entry points; the memory is the caller's to free with dg_peer_free. */
+int dg_peer_alloc(int64_t bytes, int32_t kind, void** ptr /* HOST out */);
+int dg_peer_free(void* ptr);
+/* IPC: the handle (DG_IPC_HANDLE_BYTES, host) of the allocation holding ptr and ptr's byte
+ * offset in it; open / close a peer process's handle in this process. */
+int dg_ipc_get_handle(void* ptr, void* handle /* HOST out */, int64_t* offset /* HOST out */);
+int dg_ipc_open(const void* handle /* HOST */, void** ptr /* HOST out */);
+int dg_ipc_close(void* ptr);
+
+/* Stand-alone exchange: push bytes [offsets[s], offsets[s] + sizes[s]) of this rank's region
+ * (its blocks) into every peer's region at the same offsets, then raise / wait as above. */
+int dg_peer_allgather(const dg_peer_xchg* xchg /* HOST */, const void* region, const int64_t* offsets /* HOST */,
+                      const int64_t* sizes /* HOST */, int32_t n_seg, void* stream);
+
+/* dg_gcn_epilogue_multi_f32 that also pushes the rows of every target with DG_EPI_PUSH (its
+ * `out` inside the exchange region) to every peer and ends with the exchange: the finishing
+ * launch of a row-split layer and its all-gather in one kernel. */
+int dg_gcn_epilogue_peer_f32(const dg_epi_target* targets /* HOST array */, int32_t n_targets, int32_t d,
+                             int32_t flags, const dg_peer_xchg* xchg /* HOST */, void* stream);
+
+/* dg_gcn_fused_seg_f32 whose every target's `out` lies in the exchange region: the rows are
+ * also pushed to every peer and the launch ends with the exchange (config S at N = 2: a
+ * layer and its all-gather in one kernel). */
+int dg_gcn_fused_seg_peer_f32(const dg_seg_group* groups /* HOST */, int32_t n_groups,
+                              const dg_fused_target* targets /* HOST */, int32_t n_targets, int32_t d_in,
+                              int32_t d_out, const dg_peer_xchg* xchg /* HOST */, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Batched strided fp32 GEMM on the f32-input MFMA (v_mfma_f32_32x32x2_f32, exact fp32):
@@ -460,8 +529,10 @@ int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_row, const ui
  *   loss[0] = sum_b relu(neg[b] - (pos[b] - margin))   (fixed block order)
  * workspace: device, 16-byte aligned, 16 + 4*ceil(n/32) bytes, all zero before the first
  * call (the kernel leaves it so).  n >= 1.  The partial sums of the 32-pair blocks meet in one
- * returning 64-bit integer atomic per block (fixed point, 2^-32 units; order-free, so bitwise
- * reproducible) when there are at most 255 blocks, else through a ticket and block-order reads.
+ * returning 64-bit integer atomic per block (fixed point, each partial rounded to the nearest
+ * 2^-32: the loss is within 255·2^-33 ≈ 3e-8 absolute of the sum of the fp32 partials; integer
+ * adds are order-free, so bitwise reproducible) when there are at most 255 blocks, else
+ * through a ticket and block-order reads (the fp32 partials in block order).
  * Replaces optimizer.py:37-57 (sampler, gathers, pos/neg scores) + :116-120 (hinge). */
 int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
                          int64_t ld_col, const int32_t* rows, const int32_t* cols,

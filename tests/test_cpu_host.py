@@ -53,7 +53,7 @@ def test_is_identity():
 
 def _declared_symbols():
     hdr = (ROOT / "include" / "decagon_hip.h").read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|int32_t)\s+(dg_\w+)\s*\(", hdr, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t)\s+(dg_\w+)\s*\(", hdr, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -66,6 +66,27 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, f"{s} not bound in _lib.SIGNATURES"
     assert lib.dg_abi_version() == _lib.ABI_VERSION
+
+
+def test_integration_doc_matches_abi():
+    """INTEGRATION.md is the maintainer's binding guide: the ABI number it states and its
+    stub asserts, the stubs' argtypes, and its table's coverage of every declared entry point
+    must match the library (a stale doc fails here, not in a maintainer's first call)."""
+    from decagon_amd import _lib
+
+    doc = (ROOT / "INTEGRATION.md").read_text()
+    stated = {int(x) for x in re.findall(r"`dg_abi_version\(\)` returns (\d+)", doc)}
+    asserted = {int(x) for x in re.findall(r"dg_abi_version\(\) == (\d+)", doc)}
+    assert stated == {_lib.ABI_VERSION} and asserted == {_lib.ABI_VERSION}, (stated, asserted)
+    names = {"c_void_p": ctypes.c_void_p, "c_int32": ctypes.c_int32, "c_int64": ctypes.c_int64}
+    stubs = re.findall(r"_lib\.(dg_\w+)\.argtypes = \[([^\]]*)\]", doc, re.S)
+    assert len(stubs) >= 2
+    for fn, body in stubs:
+        got = [names[t.strip()] for t in body.replace("\n", " ").split(",") if t.strip()]
+        assert got == list(_lib.SIGNATURES[fn][1]), fn
+    table = set(re.findall(r"`(dg_\w+)`", doc))
+    missing = [s for s in _declared_symbols() if s not in table and s != "dg_abi_version"]
+    assert not missing, f"INTEGRATION.md's table does not list {missing}"
 
 
 def test_abi_rejects_bad_arguments_without_a_device():

@@ -574,6 +574,15 @@ def test_decoder_hinge_fused(K, n, scale):
     own = orc.hinge_loss(op.pos.cpu().numpy().astype(np.float64), op.neg.cpu().numpy().astype(np.float64), 0.1)
     first = float(op.loss[0])
     assert abs(first - own) <= 1e-6 * abs(own)
+    if n <= 255 * 32 and scale == 1:
+        # the packed form: each block partial rounded to the nearest 2^-32 (decoder.hip), so the
+        # sum of the fp32 block partials is met within 255·2^-33 absolute, without bias
+        pos_d, neg_d = op.pos.cpu().numpy(), op.neg.cpu().numpy()
+        parts = [np.float32(0)] * -(-n // 32)
+        for b in range(len(parts)):
+            t = np.maximum(neg_d[32 * b:32 * b + 32] - (pos_d[32 * b:32 * b + 32] - np.float32(0.1)), 0)
+            parts[b] = np.float64(t.astype(np.float32).sum(dtype=np.float32))
+        assert abs(first - sum(parts)) <= len(parts) * 2.0 ** -33 + 1e-6 * abs(own)
     for _ in range(2):
         op()
         assert float(op.loss[0]) == first

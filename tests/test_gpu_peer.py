@@ -1,0 +1,296 @@
+"""GPU: the peer-store exchange (peer.py, csrc/peer.h) — IPC-mapped peer memory, write-through
+stores at system scope, arrival flags with bounded waits — against RCCL-free expectations.
+
+The ranks are processes sharing the test box's one GPU (gloo for the host side): each maps
+every other rank's exchange region with hipIpcOpenMemHandle, which the one-GPU box allows
+across processes of the same device, so the protocol runs exactly as on 8 GPUs except that
+the stores reach the peer's memory without crossing xGMI.  Checked:
+
+  * the stand-alone exchange (dg_peer_allgather) fills every rank's region with every rank's
+    block, repeatedly (epochs advance, no flag is ever reset), at 2 / 4 / 8 ranks;
+  * config S's weak-scaling forward (bench.py at N GPUs: one relation set per rank, every node
+    type row-split) with its two all-gathers replaced by the peer exchange — fused into the
+    finishing launches (the N = 2 fused-seg form and the N >= 4 seg + epilogue form) and as
+    stand-alone launches — equals the float64 oracle (decagon/deep/layers.py:85-118,
+    model.py:64-88) within 1e-4 and the RCCL-free gloo form bit for bit, eager and replayed
+    from a hipGraph, at 2 / 4 / 8 ranks;
+  * the same for the scaled-down config P (proteins row-split; the drug sums still all-reduced);
+  * the one-process loopback rehearsal (bench.py --simulate-world --exchange peer) equals the
+    unsharded forward's rank block;
+  * a wait that cannot complete times out, sets the error word and later waits fail fast.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_err, run_ranks
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+TOL = 1e-4
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _allgather_rank(rank, world, rounds):
+    import torch.distributed as dist
+
+    from decagon_amd.peer import PeerConfig, PeerExchange, dist_gather
+
+    dev = torch.device("cuda", 0)
+    blk = 3000  # floats per rank's block (12 KB: the push kernel's partial workgroup path)
+    region = torch.full((world * blk + 64,), float("nan"), dtype=torch.float32, device=dev)
+    ex = PeerExchange(region, rank, world, PeerConfig(mode="kernel", gather=dist_gather()))
+    fn = ex.allgather_fn([region[rank * blk:(rank + 1) * blk]], 2)
+    seen = []
+    for it in range(rounds):
+        region[rank * blk:(rank + 1) * blk] = torch.arange(blk, device=dev, dtype=torch.float32) + 1e4 * rank + it
+        torch.cuda.synchronize()
+        dist.barrier()  # every rank's previous round is read before anyone pushes again
+        fn()
+        torch.cuda.synchronize()
+        got = region[:world * blk].view(world, blk).cpu().numpy()
+        seen.append(got)
+        dist.barrier()
+    err = ex.error()
+    state = ex.state.cpu().numpy().tolist()
+    ex.close()
+    return seen, err, state
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_peer_allgather_fills_every_region(world):
+    _need_gpu()
+    rounds = 3
+    got = run_ranks(_allgather_rank, world, (rounds,))
+    blk = 3000
+    for r in range(world):
+        seen, err, state = got[r]
+        assert err == 0, (r, hex(err))
+        assert state[2 * 2 + 1] == rounds and state[2 * 2] == 0, state  # slot 2: epoch, arrivals reset
+        for it in range(rounds):
+            want = np.arange(blk, dtype=np.float32)[None, :] + 1e4 * np.arange(world)[:, None] + it
+            assert np.array_equal(seen[it], want.astype(np.float32)), (r, it)
+
+
+def _graph(kind, world):
+    from decagon_amd import synthetic
+
+    if kind == "S":
+        return synthetic.replicate_sets(synthetic.load_S(), world)
+    return synthetic.make_P(seed=3, n_proteins=1500, n_drugs=150, n_side_effects=60, ppi_edges=12000,
+                            target_edges=1200)
+
+
+def _weights(g, seed=5):
+    rng = np.random.default_rng(seed)
+    n = g.n_nodes
+    w1 = {et: rng.uniform(-0.1, 0.1, (K, n[et[1]], 64)).astype(np.float32) for et, K in g.edge_types.items()}
+    w2 = {et: rng.uniform(-0.3, 0.3, (K, 64, 32)).astype(np.float32) for et, K in g.edge_types.items()}
+    return w1, w2
+
+
+def _shard(kind, g, rank, world, peer):
+    from decagon_amd.sharding import RelationShard, torch_allgather, torch_allreduce
+
+    if kind == "S":
+        sh = RelationShard.weak_sets(g.edge_types, g.n_nodes, rank, world, torch_allreduce(), torch_allgather())
+    else:
+        nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
+        sh = RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
+                                 row_split_min=1000)
+    sh.peer = peer
+    return sh
+
+
+def _plan(kind, g, rank, world, peer):
+    from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
+
+    dev = torch.device("cuda", 0)
+    shard = _shard(kind, g, rank, world, peer)
+    w1, w2 = _weights(g)
+    dg = DeviceGraph(g.edge_types, shard.local_csr(g.csr()), dev, shard.local, row_block=shard.row_block,
+                     chunk=shard.chunks, segments=shard.seg_rows)
+    return ForwardPlan(dg, {0: None, 1: None},
+                       LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
+                       LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, 32,
+                       shard=shard)
+
+
+def _grab(plan):
+    return ({t: plan.hidden1[t].cpu().numpy() for t in (0, 1)},
+            {t: plan.embeddings[t].cpu().numpy() for t in (0, 1)})
+
+
+def _forward_rank(rank, world, kind, mode):
+    import torch.distributed as dist
+
+    from decagon_amd.peer import PeerConfig, dist_gather
+
+    g = _graph(kind, world)
+    plan = _plan(kind, g, rank, world, PeerConfig(mode=mode, gather=dist_gather()))
+    info = {"seg": plan.seg_mode, "exchanges": sum(L.has_exchange for L in (plan._layer1, plan._layer2)),
+            "fused_kinds": sorted({type(l).__name__ for l in plan._layer1.launches}),
+            "gather_all": [L.gather_all is not None for L in (plan._layer1, plan._layer2)]}
+    outs = []
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        for it in range(2):  # two eager forwards: the epochs advance
+            dist.barrier()
+            plan.run()
+            stream.synchronize()
+            plan.peer.check()
+            dist.barrier()
+            outs.append(_grab(plan))
+            dist.barrier()
+        # replayed from hipGraphs: the whole forward twice in one graph when every exchange is
+        # a kernel (config S); otherwise (config P: the drug sums' gloo all-reduce) each phase
+        # between eager all-reduces captured, as test_gpu_sharded does
+        seq = []
+        phases = plan.phases()
+        if all(k == "compute" for k, _ in phases) or kind == "S":
+            cg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(cg, stream=stream):
+                plan.run()
+                plan.run()
+            seq.append(cg.replay)
+        else:
+            for k, fn in phases:
+                if k == "exchange":
+                    seq.append(fn)
+                    continue
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph, stream=stream):
+                    fn()
+                seq.append(gph.replay)
+        for buf in list(plan.hidden1.values()) + list(plan.embeddings.values()):
+            buf.fill_(float("nan"))
+        stream.synchronize()
+        dist.barrier()
+        for f in seq:
+            f()
+        stream.synchronize()
+        plan.peer.check()
+        dist.barrier()
+        outs.append(_grab(plan))
+        dist.barrier()
+    # the same partition over gloo all-gathers (the RCCL-free reference form of the exchange)
+    ref = _plan(kind, g, rank, world, None)
+    ref.run()
+    torch.cuda.synchronize()
+    base = _grab(ref)
+    state = plan.peer.state.cpu().numpy().tolist()
+    dist.barrier()
+    plan.peer.close()
+    return info, outs, base, state
+
+
+def _oracle(kind, g):
+    from oracle import decagon_oracle as orc
+
+    w1, w2 = _weights(g)
+    adj = {et: [(c, v.astype(np.float32).astype(np.float64), s) for c, v, s in mats] for et, mats in g.adj.items()}
+    n = g.n_nodes
+    feats = {t: (np.stack([np.arange(n[t])] * 2, 1), np.ones(n[t]), (n[t], n[t])) for t in n}
+    return orc.decagon_forward(g.edge_types, adj, feats,
+                               {et: [x.astype(np.float64) for x in w] for et, w in w1.items()},
+                               {et: [x.astype(np.float64) for x in w] for et, w in w2.items()})
+
+
+@pytest.mark.parametrize("kind,world,mode", [("S", 2, "fused"), ("S", 4, "fused"), ("S", 8, "fused"),
+                                             ("S", 2, "kernel"), ("S", 8, "kernel"), ("P", 2, "fused"),
+                                             ("P", 4, "kernel")])
+def test_peer_exchange_forward_matches_oracle(kind, world, mode):
+    _need_gpu()
+    got = run_ranks(_forward_rank, world, (kind, mode))
+    g = _graph(kind, world)
+    h1, emb = _oracle(kind, g)
+    for r in range(world):
+        info, outs, base, state = got[r]
+        assert state[16] == 0, (r, hex(state[16]))  # the error word
+        if mode == "fused" and kind == "S":
+            assert info["exchanges"] == 0, info     # the finishing launches exchange
+        if mode == "kernel":
+            assert all(info["gather_all"]), info
+        for form in outs:
+            for t in (0, 1):
+                assert rel_err(form[0][t], h1[t]) <= TOL, (r, "hidden1", t)
+                assert rel_err(form[1][t], emb[t]) <= TOL, (r, "embeddings", t)
+                # the exchange moves bytes: bit-identical to the gloo all-gather form
+                assert np.array_equal(form[0][t], base[0][t]) and np.array_equal(form[1][t], base[1][t]), (r, t)
+
+
+def test_peer_loopback_rehearsal_matches_rank_block():
+    """One process standing in for rank r of N (bench.py --simulate-world N --exchange peer):
+    the "peers" are local scratch copies and the last workgroup raises every flag itself; the
+    rank's own rows equal the unsharded forward's, the scratch copies hold them too."""
+    _need_gpu()
+    from decagon_amd.peer import PeerConfig
+    from decagon_amd.sharding import _no_op, _no_op_reduce
+
+    world = 8
+    g = _graph("S", world)
+    h1, emb = _oracle("S", g)
+    for rank in (0, world - 1):
+        from decagon_amd.sharding import RelationShard
+
+        sh = RelationShard.weak_sets(g.edge_types, g.n_nodes, rank, world, _no_op_reduce, _no_op)
+        sh.peer = PeerConfig(mode="fused", loopback=True)
+        from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
+
+        dev = torch.device("cuda", 0)
+        w1, w2 = _weights(g)
+        dg = DeviceGraph(g.edge_types, sh.local_csr(g.csr()), dev, sh.local, row_block=sh.row_block,
+                         chunk=sh.chunks, segments=sh.seg_rows)
+        plan = ForwardPlan(dg, {0: None, 1: None},
+                           LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
+                           LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, 32, shard=sh)
+        # the other ranks' hidden1 rows (which the loopback never receives) from the oracle, so
+        # this rank's layer 2 has its whole operand
+        for t in (0, 1):
+            plan.hidden1[t].copy_(torch.from_numpy(h1[t].astype(np.float32)))
+        for _ in range(3):
+            plan.run()
+        plan.peer.check()
+        for t in (0, 1):
+            a, b, blk = sh.row_block[t]
+            for got_, want in ((plan.hidden1[t], h1[t]), (plan.embeddings[t], emb[t])):
+                assert np.max(np.abs(got_[a:b].cpu().numpy() - want[a:b])) <= TOL * np.max(np.abs(want)), (rank, t)
+            for scratch in plan.peer._scratch:
+                # every "peer" copy holds this rank's block of layer 1 and layer 2
+                o1 = plan.peer.offset(plan._pad[t, 1]) // 4
+                assert torch.equal(scratch[o1 + a * 64:o1 + b * 64], plan.xregion[o1 + a * 64:o1 + b * 64])
+        plan.peer.close()
+
+
+def test_peer_wait_times_out_and_fails_fast():
+    """A rank whose peer never exchanges: the bounded wait sets the error word (slot, source
+    rank) within its timeout and a second exchange returns at once."""
+    _need_gpu()
+    import time
+
+    from decagon_amd import _lib
+    from decagon_amd.peer import PeerConfig, PeerExchange
+
+    dev = torch.device("cuda", 0)
+    region = torch.zeros(4096, dtype=torch.float32, device=dev)
+    # loopback with world 2 but the flag of "rank 1" never raised: a descriptor whose loopback
+    # bit is cleared raises only word [slot][rank]
+    ex = PeerExchange(region, 0, 2, PeerConfig(mode="kernel", loopback=True, timeout_s=0.2))
+    x = ex.xchg(3)
+    x.loopback = 0
+    fn = ex.allgather_fn([region[:1024]], 3)
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    err = ex.error()
+    assert err == 0x10000 | (3 << 8) | 1, hex(err)
+    assert 0.15 <= t1 - t0 <= 5.0, t1 - t0
+    fn()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t1 < 0.15  # fails fast once the error word is set
+    assert int(ex.state[_lib.DG_PEER_ERROR_WORD]) == err
+    ex.close()

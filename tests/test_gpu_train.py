@@ -45,6 +45,70 @@ def _batch_feed(z, ph, opt, feed, b):
     return f, e, rt, ct
 
 
+def _sharded_grads_vars_rank(rank, world, b, split):
+    """One rank of a sharded Session: `sess.shard` set, grads_vars fetched through the drop-in
+    surface (optimizer.py:114's compute_gradients) — every variable's gradient on every rank."""
+    from conftest import GOLDEN
+    from decagon_amd.sharding import RelationShard, torch_allgather, torch_allreduce
+
+    z = np.load(GOLDEN / "synthetic_S.npz", allow_pickle=False)
+    dg, ph, model, opt, feed = _setup(z)
+    f, e, rt, ct = _batch_feed(z, ph, opt, feed, b)
+    nnz = {et: [len(z[f"adj_{et[0]}_{et[1]}_{k}_values"]) for k in range(K)] for et, K in model.edge_types.items()}
+    n = {0: int(z["n_nodes"][0]), 1: int(z["n_nodes"][1])}
+    sess = dg.Session()
+    if split:  # the genes (500 rows) row-split, the drugs' relations LPT-sharded
+        sess.shard = RelationShard.split(model.edge_types, n, nnz, rank, world, torch_allreduce(), torch_allgather(),
+                                         row_split_min=450)
+    else:
+        sess.shard = RelationShard.lpt(model.edge_types, nnz, rank, world, torch_allreduce())
+    gv = sess.run(opt.grads_vars, feed_dict=f)
+    owned = {et: list(v) for et, v in sess.shard.local.items()}
+    return [(np.asarray(g), np.asarray(v)) for g, v in gv], owned, sorted(sess.shard.row_block)
+
+
+@pytest.mark.parametrize("b,split", [(0, False), (3, False), (1, True)])
+def test_sharded_grads_vars_match_oracle(golden_S, b, split):
+    """grads_vars on 2 gloo ranks sharing the GPU (relations LPT-sharded; or the genes
+    row-split): every rank returns EVERY variable's gradient — each relation's gathered from
+    its owner rank (TrainPlan.full_grads) — equal to the float64 oracle's TF gradients within
+    1e-4, and the ranks' lists are identical bit for bit."""
+    from conftest import run_ranks
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    z = golden_S
+    got = run_ranks(_sharded_grads_vars_rank, 2, (b, split))
+    dg, ph, model, opt, feed = _setup(z)
+    e, rt, ct = (int(v) for v in z[f"batch{b}_meta"])
+    w1, w2, dec, adj = _oracle_inputs(z, model, model.edge_types)
+    cost, ref = orc.train_grads(model.edge_types, adj, {0: None, 1: None}, w1, w2, model.decoders, dec, 32,
+                                z[f"batch{b}_edges"], z[f"batch{b}_neg"], e, rt, ct, 0.1)
+    want = []
+    for et, K in model.edge_types.items():
+        want += [ref["w1"][et][k] for k in range(K)]
+    for et, K in model.edge_types.items():
+        want += [ref["w2"][et][k] for k in range(K)]
+    for et in model.edge_types:
+        want += [ref["dec"][et][n] for n in model.edge_type2decoder[et].vars]
+    (gv0, owned0, rb0), (gv1, owned1, rb1) = got[0], got[1]
+    assert rb0 == ([0] if split else [])
+    if not split:  # the relations really are split between the ranks
+        assert all(sorted(owned0[et] + owned1[et]) == list(range(K)) for et, K in model.edge_types.items())
+        assert any(len(owned0[et]) < K for et, K in model.edge_types.items())
+    assert len(gv0) == len(gv1) == len(want)
+    nonzero = 0
+    for (g0, v0), (g1, v1), w in zip(gv0, gv1, want):
+        assert np.array_equal(g0, g1) and np.array_equal(v0, v1)
+        scale = np.max(np.abs(w))
+        if scale == 0:
+            assert np.max(np.abs(g0)) == 0.0
+        else:
+            nonzero += 1
+            assert np.max(np.abs(g0 - w)) <= TOL * scale, f"gradient off by {rel_err(g0, w):.2e}"
+    assert nonzero > 0
+
+
 @pytest.mark.parametrize("b", [0, 1, 2, 3])
 def test_grads_vars_match_oracle(golden_S, b):
     """Every variable's gradient (all four decoder kinds of config S appear across batches)."""
