@@ -81,6 +81,29 @@ __device__ __forceinline__ void peer_store4(const PeerK& P, const float* base, u
     }
 }
 
+// Wave-level bounded wait: lane s polls word [slot][s] of this rank's block (one round trip per
+// poll for every source) until all of [0, world) reached epoch; on timeout lane 0 sets the
+// error word (0x10000 | slot << 8 | the first late source).
+__device__ __forceinline__ void peer_poll(const PeerK& P, uint32_t epoch, int lane) {
+    const bool mine = lane < P.world;
+    const uint32_t* own = P.flags[P.rank] + P.slot * DG_PEER_MAX + lane;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+    for (;;) {
+        const uint32_t v = mine ? __hip_atomic_load(own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : epoch;
+        const uint64_t who = __ballot((int32_t)(v - epoch) < 0);
+        if (!who) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)P.timeout) {
+            if (lane == 0)
+                __hip_atomic_store(P.state + 2 * DG_PEER_SLOTS,
+                                   0x10000u | ((uint32_t)P.slot << 8) | ((uint32_t)__ffsll((long long)who) - 1u),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // Called by EVERY thread of EVERY workgroup of the launch after its peer stores: drain, meet,
 // count; wave 0 of the last workgroup raises this rank's flag at every peer (lane p stores to
 // peer p) and waits for theirs (lane s polls source s: one round trip per poll for all ranks),
@@ -96,7 +119,7 @@ __device__ __forceinline__ void peer_arrive(const PeerK& P) {
     old = __shfl(old, 0);
     if (old + 1u != gridDim.x) return;
     uint32_t* ep = P.state + 2 * P.slot + 1;
-    uint32_t* err = P.state + 2 * DG_PEER_SLOTS;
+    const uint32_t* err = P.state + 2 * DG_PEER_SLOTS;
     uint32_t epoch = 0, failed = 0;
     if (lane == 0) {
         __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch counts anew
@@ -110,28 +133,10 @@ __device__ __forceinline__ void peer_arrive(const PeerK& P) {
 #pragma unroll
     for (int p = 0; p < DG_PEER_MAX; ++p)
         if (lane == p) fp = P.flags[p];
-    const bool mine = lane < P.world;
-    if (mine)
+    if (lane < P.world)
         __hip_atomic_store(fp + P.slot * DG_PEER_MAX + (P.loopback ? lane : P.rank), epoch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-    if (!failed) {  // (a set error word: an earlier wait timed out; fail fast)
-        const uint32_t* own = P.flags[P.rank] + P.slot * DG_PEER_MAX + lane;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-#pragma unroll 1
-        for (;;) {
-            const uint32_t v = mine ? __hip_atomic_load(own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : epoch;
-            const bool late = (int32_t)(v - epoch) < 0;
-            const uint64_t who = __ballot(late);
-            if (!who) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)P.timeout) {
-                if (lane == 0)
-                    __hip_atomic_store(err, 0x10000u | ((uint32_t)P.slot << 8) | (uint32_t)__ffsll((long long)who) - 1u,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
+    if (!failed) peer_poll(P, epoch, lane);  // (a set error word: fail fast)
     if (lane == 0) __hip_atomic_store(ep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

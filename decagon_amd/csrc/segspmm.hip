@@ -43,6 +43,19 @@
 #ifndef DG_FSEG_UP
 #define DG_FSEG_UP 2
 #endif
+#ifndef DG_FSEG_UP_WL
+#define DG_FSEG_UP_WL 4  // the reassociated fused form with W in LDS (no 32-VGPR W slice per wave)
+#endif
+#ifndef DG_FSEG_WL
+#define DG_FSEG_WL 2     // the fused layer 2's W slabs: 0 in registers through the gathers (round 3),
+#endif                   // 1 staged in LDS per workgroup, 2 read after the gathers (config S layer 2
+                         // 7.35 / 9.45 / 6.87 us, step 19.66 / 21.88 / 19.36 us at 200 steps)
+#ifndef DG_SEG_UP_WL
+#define DG_SEG_UP_WL 4   // the reassociated seg form with the W slice read after the gathers
+#endif
+#ifndef DG_SEG_WL
+#define DG_SEG_WL 2      // spmm_seg_kernel's W slice: 0 in registers through the gathers, 2 read after
+#endif                   // them (config S's N = 8 rank share 31.0 -> 30.6 us, loopback exchange)
 #ifndef DG_SEG_MIN_NW
 #define DG_SEG_MIN_NW 1  // waves per workgroup, at least (else: the launch's largest chunk)
 #endif
@@ -268,10 +281,58 @@ __device__ __forceinline__ float4 seg_wave(const SegGroupK& g, int c, int r, int
     }
 }
 
+// The reassociated wave with its W_k slab in LDS (wl: 64 x 32 floats as 512 float4, row-major,
+// staged once per workgroup for every row slot that uses relation k) instead of 32 VGPRs of
+// W slice per wave held across the gathers: the registers go to gathers in flight (UP).
+// beg / end: the segment, loaded by the caller before the staging barrier.
+// wl == nullptr: the slab is read from global memory after the gathers (one more L2 round trip
+// at the end instead of 32 VGPRs held through them).
+// WL 0: the W slice loaded from global memory before the gathers (held through them), as
+// seg_wave; WL 1: from the workgroup's LDS copy after them; WL 2: from global after them.
+template <int UP, int WL>
+__device__ __forceinline__ float4 seg_wave_wl(const SegGroupK& g, int k, int beg, int end, float4* ybuf,
+                                              const float4* wl) {
+    const int lane = threadIdx.x & 63;
+    const int s = g.slab ? g.slab[k] : k;
+    const int ms = lane >> 3;
+    // rows 8·ms .. +8 of the slab, output float4 lane & 7
+    const float4* w = (WL == 1 ? wl : reinterpret_cast<const float4*>(g.w + (int64_t)s * (64 * 32))) + (8 * ms) * 8 +
+                      (lane & 7);
+    float4 wv[8];
+    if constexpr (WL == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wv[i] = w[8 * i];
+    }
+    const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;  // vcol = s·n_cols + col addresses row col
+    const float4 y = seg_gather_shfl<16, UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
+    if constexpr (WL != 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wv[i] = w[8 * i];
+    }
+    if (lane < 16) ybuf[lane] = y;
+    __builtin_amdgcn_wave_barrier();
+    const float4 ya = ybuf[2 * ms];
+    const float4 yb = ybuf[2 * ms + 1];
+    float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    dg::fma4(z, ya.x, wv[0]);
+    dg::fma4(z, ya.y, wv[1]);
+    dg::fma4(z, ya.z, wv[2]);
+    dg::fma4(z, ya.w, wv[3]);
+    dg::fma4(z, yb.x, wv[4]);
+    dg::fma4(z, yb.y, wv[5]);
+    dg::fma4(z, yb.z, wv[6]);
+    dg::fma4(z, yb.w, wv[7]);
+    dg::add4(z, dg::shfl_xor4(z, 8));
+    dg::add4(z, dg::shfl_xor4(z, 16));
+    dg::add4(z, dg::shfl_xor4(z, 32));
+    return z;
+}
+
 // PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.  a.nw waves per
 // workgroup (the launch's largest chunk, so a chunk-6 group wastes no wave slot; rows per
 // workgroup nw / chunk), at most NW.
-template <int LP, bool PROJ, int NW>
+// WL (PROJ only): seg_wave_wl's W-slice modes (0: seg_wave's, in registers through the gathers).
+template <int LP, bool PROJ, int NW, int WL = 0>
 __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;  // float4s of an output row
     __shared__ float4 ybuf[NW][16];
@@ -299,7 +360,18 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     const bool row_ok = slot < g.rpb && r < g.n_rows;
     const int k = c * g.chunk + t;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row_ok && k < g.n_rels) res = seg_wave<LP, PROJ, DG_SEG_U, DG_SEG_UP>(g, c, r, t, k, ybuf[wave]);  // wave-uniform
+    if constexpr (PROJ && WL != 0) {
+        const bool live = row_ok && k < g.n_rels;
+        int beg = 0, end = 0;
+        if (live) {
+            const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
+            beg = g.seg[si];
+            end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
+        }
+        if (live) res = seg_wave_wl<DG_SEG_UP_WL, 2>(g, k, beg, end, ybuf[wave], nullptr);
+    } else if (row_ok && k < g.n_rels) {
+        res = seg_wave<LP, PROJ, DG_SEG_U, DG_SEG_UP>(g, c, r, t, k, ybuf[wave]);  // wave-uniform
+    }
     if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
     __syncthreads();
     if (row_ok && t == 0 && lane < DOUT4) {
@@ -340,12 +412,17 @@ constexpr int kFsMaxRpb = 1;  // A/B: one row per workgroup
 constexpr int kFsMaxRpb = 4;
 #endif
 
-template <int LP, bool PROJ, int NW, bool PEER>
+// WL (PROJ only): the layer-2 W slab of each wave's relation not held in registers through the
+// gathers.  WL 1: every relation's slab staged in (dynamic) LDS once per workgroup by row slot
+// 0's waves — the segment bounds are loaded first, so the staging barrier costs no extra round
+// trip; WL 2: each wave reads its slab from global memory after its gathers.
+template <int LP, bool PROJ, int NW, bool PEER, int WL = 0>
 __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
     __shared__ float4 nbuf[kFsMaxRpb][DG_MAX_GROUPS][DOUT4];
+    extern __shared__ __attribute__((aligned(16))) float4 wdyn[];  // WL 1: [waves][512]
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int ti = 0;
@@ -363,7 +440,34 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 #pragma unroll 1
     while (gl < T.g_count && wi >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (slot < T.rpb && r < T.n_rows && gl < T.g_count) {
+    if constexpr (PROJ && WL != 0) {
+        const bool live = slot < T.rpb && r < T.n_rows && gl < T.g_count;
+        const int gi = T.g_begin + (gl < T.g_count ? gl : 0);
+        const int k = wi - base;
+        int beg = 0, end = 0;
+        if (live) {  // the segment bounds, issued before the staging loads
+            const SegGroupK& g = a.g[gi];
+            const int c = k / g.chunk, t = k - c * g.chunk;
+            const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
+            beg = g.seg[si];
+            end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
+        }
+        if constexpr (WL == 1) {
+            if (slot == 0 && wi < T.waves) {  // row slot 0's waves stage their relations' W slabs
+                const SegGroupK& g = a.g[gi];
+                const int sl = g.slab ? g.slab[k] : k;
+                const float4* W = reinterpret_cast<const float4*>(g.w + (int64_t)sl * (64 * 32));
+                float4 tmp[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) tmp[i] = W[lane + 64 * i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) wdyn[wi * 512 + lane + 64 * i] = tmp[i];
+            }
+            __syncthreads();
+        }
+        if (live)
+            res = seg_wave_wl<DG_FSEG_UP_WL, WL>(a.g[gi], k, beg, end, ybuf[wave], WL == 1 ? wdyn + wi * 512 : nullptr);
+    } else if (slot < T.rpb && r < T.n_rows && gl < T.g_count) {
         const SegGroupK& g = a.g[T.g_begin + gl];
         const int k = wi - base;
         const int c = k / g.chunk;
@@ -448,8 +552,35 @@ int seg_shape(int32_t d_in, int32_t d_out, bool& proj) {
 }
 }  // namespace
 
-extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out,
-                               void* stream) {
+namespace {
+// The launch dispatch of both kernels: runtime switches onto the instantiated template forms.
+template <int NW>
+void launch_seg(bool proj, int d_in, int wl, dim3 grid, dim3 block, hipStream_t st, const SegArgs& a) {
+    if (proj && wl != 0)
+        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW, 2>), grid, block, 0, st, a);
+    else if (proj)
+        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW>), grid, block, 0, st, a);
+    else if (d_in == 64)
+        hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW>), grid, block, 0, st, a);
+}
+
+template <int NW, bool PEER>
+void launch_fs(bool proj, int d_in, int wl, size_t lds, dim3 grid, dim3 block, hipStream_t st, const FsArgs& a) {
+    if (proj && wl == 1)
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER, 1>), grid, block, lds, st, a);
+    else if (proj && wl == 2)
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER, 2>), grid, block, 0, st, a);
+    else if (proj)
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER>), grid, block, 0, st, a);
+    else if (d_in == 64)
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW, PEER>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW, PEER>), grid, block, 0, st, a);
+}
+
+int seg_launch(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out, void* stream) {
     if (n_groups < 0 || (n_groups > 0 && groups == nullptr)) return DG_EINVAL;
     if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
     bool proj = false;
@@ -483,23 +614,13 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
     if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);  // (launch bounds: 8 or 16 waves)
-#define DG_SEG_LAUNCH(NW)                                                                 \
-    if (proj)                                                                             \
-        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW>), grid, block, 0, st, args);    \
-    else if (d_in == 64)                                                                  \
-        hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW>), grid, block, 0, st, args);   \
-    else                                                                                  \
-        hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW>), grid, block, 0, st, args);
-    if (nw <= 8) {
-        DG_SEG_LAUNCH(8)
-    } else {
-        DG_SEG_LAUNCH(16)
-    }
-#undef DG_SEG_LAUNCH
+    if (nw <= 8)
+        launch_seg<8>(proj, d_in, DG_SEG_WL, grid, block, st, args);
+    else
+        launch_seg<16>(proj, d_in, DG_SEG_WL, grid, block, st, args);
     return dg::launch_status();
 }
 
-namespace {
 int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets, int32_t n_targets,
                      int32_t d_in, int32_t d_out, const dg_peer_xchg* xchg, void* stream) {
     if (n_groups < 1 || !groups || n_targets < 1 || !targets) return DG_EINVAL;
@@ -557,28 +678,28 @@ int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fuse
     if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);
-#define DG_FS_LAUNCH(NW, PEER)                                                                    \
-    if (proj)                                                                                     \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER>), grid, block, 0, st, a);    \
-    else if (d_in == 64)                                                                          \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW, PEER>), grid, block, 0, st, a);   \
-    else                                                                                          \
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW, PEER>), grid, block, 0, st, a);
+    // WL 1: LDS for the widest target's slabs (8 KB a relation), at most 64 KB (8 relations a row;
+    // wider rows — config S's N = 2 form — read the slabs after the gathers instead, WL 2)
+    const int wl = !proj ? 0 : (DG_FSEG_WL == 1 && nw > 8 ? 2 : DG_FSEG_WL);
+    const size_t wl_lds = wl == 1 ? (size_t)nw * 512 * 16 : 0;
     if (xchg) {
-        if (nw <= 8) {
-            DG_FS_LAUNCH(8, true)
-        } else {
-            DG_FS_LAUNCH(16, true)
-        }
+        if (nw <= 8)
+            launch_fs<8, true>(proj, d_in, wl, wl_lds, grid, block, st, a);
+        else
+            launch_fs<16, true>(proj, d_in, wl, wl_lds, grid, block, st, a);
     } else if (nw <= 8) {
-        DG_FS_LAUNCH(8, false)
+        launch_fs<8, false>(proj, d_in, wl, wl_lds, grid, block, st, a);
     } else {
-        DG_FS_LAUNCH(16, false)
+        launch_fs<16, false>(proj, d_in, wl, wl_lds, grid, block, st, a);
     }
-#undef DG_FS_LAUNCH
     return dg::launch_status();
 }
 }  // namespace
+
+extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out,
+                               void* stream) {
+    return seg_launch(groups, n_groups, d_in, d_out, stream);
+}
 
 extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets,
                                     int32_t n_targets, int32_t d_in, int32_t d_out, void* stream) {

@@ -85,6 +85,10 @@ SEG_FUSED = os.environ.get("DG_SEG_FUSED", "1") != "0"
 # and 35.6 at N = 8 (25.6), so it was not kept
 SEG_FUSED_MAX_ITEMS = 16
 STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
+# sharded forward plans: layer 2 of the non-staged groups reassociated over the rank's own rows
+# and relations, Σ_k (Â_k·H1_j)·W2_k in dg_spmm_seg_f32, instead of every rank projecting all of
+# H1_j·W2_k (config P's PPI: 19,085 rows x 2 relations, 9.4 µs on every rank at N = 8)
+REASSOC_ROWS = os.environ.get("DG_REASSOC_ROWS", "1") != "0"
 
 
 def staged_out_chunk(grp, d: int) -> int:
@@ -202,6 +206,9 @@ class DeviceGroup:
     layout: Optional["kernels.StagedDevice"] = None  # staged: the diagonal-major layout
     host: Optional[List[HostCSR]] = None  # the local relations (host CSR), device order
     seg: Optional[torch.Tensor] = None    # dg_spmm_seg_f32's segment starts (sparse.chunk_segments)
+    # a windowed row-split group's second layout for the reassociated layer 2 (all its relations
+    # in one chunk, with segment starts): (rowptr, vcol, val, seg, chunk, n_chunks, vcol_max)
+    seg2: Optional[tuple] = None
 
     @property
     def n_rels(self) -> int:
@@ -282,6 +289,12 @@ class DeviceGraph:
             g.host = loc  # local relations in device order (the backward builds Âᵀ from them)
             if segments and loc and not staged and not windows and m.chunk <= 16:
                 g.seg = torch.from_numpy(chunk_segments(loc, m)).to(device)
+            elif windows and et[0] in self.row_block and len(loc) <= 16 and REASSOC_ROWS:
+                # (sharded: layer 2 of this group reassociated over the rank's rows, ForwardPlan)
+                m2 = merge_chunks(loc, ids, len(loc), K)
+                up = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
+                g.seg2 = (up(m2.rowptr), up(m2.vcol), up(m2.val), up(chunk_segments(loc, m2)), m2.chunk, m2.n_chunks,
+                          int(m2.vcol.max()) if m2.nnz else -1)
             if staged:
                 lay = staged_layout(loc, kernels.staged_block,
                                     lanes=int(os.environ.get("DG_STAGED_LANES", "1024")),
@@ -470,6 +483,13 @@ class ForwardPlan:
                                   for ets in self.targets.values()))
         self.seg_proj = {et for et in self.edge_types
                          if (self.seg_mode or self.fused_seg) and dgraph.groups[et].n_rels and h1 == 64 and h2 == 32}
+        # sharded forward plans: every other non-staged group's layer 2 reassociated as well, over
+        # the rank's own rows / relations (config P: PPI in its one-chunk layout, (0,1), (1,0)),
+        # so no rank runs a projection GEMM over all of H1 (REASSOC_ROWS)
+        self.seg_proj |= {et for et in self.edge_types
+                          if REASSOC_ROWS and shard is not None and not keep_sums and self.drop_state is None
+                          and h1 == 64 and h2 == 32 and dgraph.groups[et].n_rels and not dgraph.groups[et].staged
+                          and (dgraph.groups[et].seg is not None or dgraph.groups[et].seg2 is not None)}
         self.proj: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
@@ -577,10 +597,17 @@ class ForwardPlan:
 
     def _seg_spec(self, et, x: torch.Tensor, out=None, w=None) -> kernels.SegSpec:
         grp = self.g.groups[et]
-        return kernels.SegSpec(grp.rowptr, grp.seg, grp.vcol, grp.val, x, out, grp.n_rows, grp.n_cols, grp.n_chunks,
-                               grp.chunk, grp.n_rels, x.stride(-2),
-                               grp.K * grp.n_cols, vcol_max=grp.vcol_max, w=w, slab=grp.rel_map,
+        if grp.seg is None and grp.seg2 is not None:  # a windowed group's one-chunk layout
+            rp, vc, vv, sg, ch, nc, vmax = grp.seg2
+        else:
+            rp, vc, vv, sg, ch, nc, vmax = grp.rowptr, grp.vcol, grp.val, grp.seg, grp.chunk, grp.n_chunks, grp.vcol_max
+        return kernels.SegSpec(rp, sg, vc, vv, x, out, grp.n_rows, grp.n_cols, nc, ch, grp.n_rels, x.stride(-2),
+                               grp.K * grp.n_cols, vcol_max=vmax, w=w, slab=grp.rel_map,
                                slab_max=int(grp.rel_ids.max()) if grp.n_rels else -1)
+
+    def _seg_chunks(self, et) -> int:
+        grp = self.g.groups[et]
+        return grp.seg2[5] if (grp.seg is None and grp.seg2 is not None) else grp.n_chunks
 
     def _build_layer(self, xs: Dict[EdgeType, torch.Tensor], d, relu, f32, projs=(), staged_proj=None, seg_w=None):
         """Prepared launches of one layer: fused targets in one dg_gcn_fused_f32 launch; the
@@ -674,9 +701,12 @@ class ForwardPlan:
                 sviews[et] = send[off:off + sz]
                 off += sz
         partials, specs, staged, reduces, segs = {}, [], [], [], []
+        reassoc = set(seg_w or {}) if not self.seg_mode else set()  # layer 2 reassociated outside seg mode
         for et in rest:
             grp = g.groups[et]
             n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
+            if et in reassoc:
+                n_out = self._seg_chunks(et)
             if flat is not None and et in views and n_out == 1:
                 part = sviews[et]  # single chunk: the SpMM writes the group sum in place
             else:
@@ -691,7 +721,7 @@ class ForwardPlan:
                 staged.append(kernels.StagedSpec(
                     grp.layout, grp.rel_map, xs.get(et), part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
                     slab_max=int(grp.rel_ids.max()), proj=sp))
-            elif self.seg_mode:
+            elif self.seg_mode or et in reassoc:
                 if et in (seg_w or {}):  # layer 2 reassociated: H1_j and W2's stack
                     segs.append(self._seg_spec(et, seg_w[et][0], part, seg_w[et][1]))
                 else:
@@ -700,7 +730,8 @@ class ForwardPlan:
                 specs.append(self._spec(et, xs[et], part, d))
         if segs:
             d_in = self.h1 if seg_w else d
-            seg_ets = [et for et in rest if g.groups[et].n_rels]
+            seg_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged
+                       and (self.seg_mode or et in reassoc)]
             for s in range(0, len(segs), DG_MAX_GROUPS):
                 launches.append(kernels.PreparedSeg(segs[s:s + DG_MAX_GROUPS], d_in, d))
                 self.launch_groups[id(launches[-1])] = seg_ets[s:s + DG_MAX_GROUPS]
