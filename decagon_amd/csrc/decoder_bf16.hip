@@ -23,6 +23,7 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 
@@ -33,6 +34,15 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 
 #ifndef DG_DEC_CS_THREADS
 #define DG_DEC_CS_THREADS 768  // column-shared paired kernel: threads per workgroup (one per CU)
+#endif
+#ifndef DG_DEC_CS16
+#define DG_DEC_CS16 1          // config 5's fused step on the 16x16x32 form (0: the 32x32x16 one)
+#endif
+#ifndef DG_DEC_CS16_THREADS
+#define DG_DEC_CS16_THREADS 768
+#endif
+#ifndef DG_DEC_CS16_PIN
+#define DG_DEC_CS16_PIN 1
 #endif
 
 struct Bf16DecArgs {
@@ -357,6 +367,251 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
         }
     }
 }
+
+// Config 5's fused step on v_mfma_f32_16x16x32_bf16 (dg_slot_score_hinge_bf16; d = 256, every
+// 32-pair tile inside one relation slot).  Same arithmetic as the column-shared kernel above —
+// T = R·bf16(D_k∘v) once per (positive, negative) pair, pos / neg = (u∘D_k)ᵀ·T in fp32 — but
+// laid out for the load path, which bounds that kernel (PMC on the MI355X: TA busy 74 %, TD
+// 82 % of the kernel, MFMA 22 %, waves parked on memory 60 %): there a row load instruction
+// spans 32 pairs x 32 B, here 16 pairs x 64 B (the 16x16x32 B operand gives a pair's 4 lane
+// groups 8 consecutive k each), and D_k — one relation per tile — is read from LDS (one
+// coalesced 512-B load per tile) instead of by 32 of the 80 row loads.
+//   wave tile = 32 pairs as two 16-pair halves b (pair 16b + (lane & 15)); lane group g = lane >> 4
+//   B[b][s] = bf16(D_k ∘ v)[32s + 8g + j]                         (8 k-steps of 32, 64 VGPRs)
+//   M-tile t of T (16 rows): row m holds i(t, m) = 32(t>>1) + 8(m>>2) + 4(t&1) + (m&3), so the
+//   accumulator rows of lane group g over tiles 2q, 2q+1 are i = 32q + 8g + [0, 8) — one 16-B
+//   load of u_p, u_n and D_k each per two tiles, a pair's 4 lanes reading 64 contiguous bytes
+//   A = R rows i(t, m) from LDS (XOR-swizzled 16-B slots), each fragment feeding both halves.
+// FUSED = false: the paired scores alone (dg_decoder_score_bf16_paired's form: given negative
+// rows, a relation per pair, D_k — or identity — read per lane from global memory); the same
+// arithmetic in the same order, so the fused step and its three-launch decomposition agree bit
+// for bit.
+template <int THREADS, bool FUSED>
+__global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16DecArgs a) {
+    constexpr int D = 256;
+    constexpr int SL = D / 8;                 // 16-byte slots per R row
+    constexpr int WAVES = THREADS / 64;
+    extern __shared__ uint4 rs[];             // R: row i, slot q at rs[i*SL + (q ^ (i % SL))]; then D_k rows
+    const int tid = threadIdx.x;
+    for (int e = tid; e < D * SL; e += THREADS) {
+        const int i = e / SL, q = e - i * SL;
+        rs[i * SL + (q ^ (i % SL))] = *reinterpret_cast<const uint4*>(a.R + (int64_t)i * D + 8 * q);
+    }
+    __syncthreads();
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    uint4* dks = rs + D * SL + wave * (D / 8);  // this wave's tile's D_k row (512 B)
+    const int pl = lane & 15;                   // the lane's pair in each half
+    const int g = lane >> 4;                    // its k / row group
+    const int nh = a.n_pairs;
+    const int n_tiles = (nh + 31) / 32;
+    const int stride = gridDim.x * WAVES;
+    // (the host checks that both tables fit 32-bit byte offsets)
+    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.row_table), 0, 0x7fffffff, 0x00020000);
+    const auto crs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.col_table), 0, 0x7fffffff, 0x00020000);
+    float wsum = 0.f;
+    const uint4 ones = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);  // bf16 1.0
+    struct Idx {
+        int prp[2], pc[2], j[2];  // (non-FUSED: j = the given negative row)
+        float u[2];
+        uint2 e[2];               // (non-FUSED: e.x = the pair's relation)
+        uint2 dk;                 // FUSED: this lane's 8 bytes of the tile's D_k row
+    };
+    auto fetch = [&](int tl, Idx& x) {
+        const bool okt = tl < n_tiles;
+        const int pk = okt && FUSED ? a.slot0 + (tl * 32) / a.batch : a.slot0;  // (a tile never straddles slots)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int p = tl * 32 + 16 * b + pl;
+            const bool ok = okt && p < nh;
+            x.prp[b] = ok ? a.rows[p] : 0;
+            x.pc[b] = ok ? a.cols[p] : 0;
+            if constexpr (FUSED) {
+                dg::unigram_pick(a.range, a.seed, (uint64_t)a.slot0 * (uint64_t)a.batch + (uint64_t)p, x.j[b],
+                                 x.u[b]);
+                x.e[b] = ok ? a.alias[pk * a.alias_stride + x.j[b]] : make_uint2(0u, 0u);
+            } else {
+                x.j[b] = ok ? a.rows[nh + p] : 0;
+                x.e[b] = make_uint2((ok && a.rel) ? (uint32_t)a.rel[p] : 0u, 0u);
+            }
+        }
+        if constexpr (FUSED)
+            x.dk = okt ? *reinterpret_cast<const uint2*>(a.L + (int64_t)pk * D + 4 * lane) : make_uint2(0u, 0u);
+    };
+    Idx nxt;
+    const int first = wave * (int)gridDim.x + (int)blockIdx.x;  // round-major tile order (see above)
+    fetch(first, nxt);
+#pragma unroll 1
+    for (int tile = first; tile < n_tiles; tile += stride) {
+        const Idx cur = nxt;
+        fetch(tile + stride, nxt);
+        // D_k row of the tile, lane l: elements 4l .. 4l+3.  (The 8-byte store and the 16-byte
+        // reads are different types to the compiler — no assumed aliasing — so explicit compiler
+        // barriers keep the previous tile's reads before the store and this tile's after it; the
+        // LDS executes one wave's accesses in order.)
+        if constexpr (FUSED) {
+            asm volatile("" ::: "memory");
+            reinterpret_cast<uint2*>(dks)[lane] = cur.dk;
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        }
+        const uint16_t* lk[2];  // non-FUSED: each half's pairs' D_k rows (NULL: identity)
+        // rows through buffer loads from the uniform table bases: a 32-bit byte offset per row
+        // (1 VGPR) instead of a 64-bit address (2)
+        int up[2], un[2];
+        bool valid[2];
+        bf16x8 bq[2][8];
+        uint4 vv[2][8];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // every v load first (16 in flight), then the B operand
+            const int p = tile * 32 + 16 * b + pl;
+            valid[b] = p < nh;
+            int prn;
+            if constexpr (FUSED) {
+                prn = valid[b] ? dg::unigram_take(cur.j[b], cur.u[b], cur.e[b]) : 0;
+                if (valid[b] && g == 0) a.neg_out[p] = prn;
+            } else {
+                prn = cur.j[b];
+                lk[b] = a.L ? a.L + (int64_t)cur.e[b].x * D + 8 * g : nullptr;
+            }
+            up[b] = 2 * (cur.prp[b] * (int)a.ld_row + 8 * g);
+            un[b] = 2 * (prn * (int)a.ld_row + 8 * g);
+            const int vo = 2 * (cur.pc[b] * (int)a.ld_col + 8 * g);
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                vv[b][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(crs, vo + 64 * s, 0, 0));
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            uint4 llf = ones;
+            if constexpr (FUSED) llf = dks[4 * s + g];  // D_k[32s + 8g .. +8], shared by both halves
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                uint4 ll = llf;
+                if constexpr (!FUSED) ll = lk[b] ? *reinterpret_cast<const uint4*>(lk[b] + 32 * s) : ones;
+                const uint32_t lw[4] = {ll.x, ll.y, ll.z, ll.w};
+                const uint32_t vw[4] = {vv[b][s].x, vv[b][s].y, vv[b][s].z, vv[b][s].w};
+                bf16v8 x;  // round-to-nearest-even by the cast (v_cvt_pk_bf16_f32)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    x[2 * j] = (__bf16)(bf_lo(vw[j]) * bf_lo(lw[j]));
+                    x[2 * j + 1] = (__bf16)(bf_hi(vw[j]) * bf_hi(lw[j]));
+                }
+                bq[b][s] = valid[b] ? __builtin_bit_cast(bf16x8, x) : bf16x8{};
+            }
+        }
+        float pp[2] = {0.f, 0.f}, pn[2] = {0.f, 0.f};
+#pragma unroll 1
+        for (int q = 0; q < 8; ++q) {  // M-tiles 2q, 2q+1: rows i = 32q + 8g + [0, 8) of this lane group
+            uint4 ep[2], en[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                ep[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, up[b] + 64 * q, 0, 0));
+                en[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, un[b] + 64 * q, 0, 0));
+            }
+
+            f32x4 acc[2][2] = {};
+
+            // the row's swizzle key, opaque per iteration: its 16 slot offsets are q-invariant,
+            // and hoisted out of the loop they hold 16 VGPRs (spilled at 3 waves per SIMD)
+            int key = 8 * (pl >> 2) + (pl & 3);
+            asm volatile("" : "+v"(key));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // M-tile t = 2q + h: A row m = pl -> i(t, m)
+                const int ia = 32 * q + 4 * h + key;  // i % SL = 4h + key
+                const int kx = 4 * h + key;
+                uint4 wa = rs[ia * SL + (g ^ kx)];
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    uint4 xa = wa;
+                    if (s + 1 < 8) xa = rs[ia * SL + ((4 * (s + 1) + g) ^ kx)];
+                    acc[0][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa), bq[0][s],
+                                                                        acc[0][h], 0, 0, 0);
+                    acc[1][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa), bq[1][s],
+                                                                        acc[1][h], 0, 0, 0);
+                    wa = xa;
+#if DG_DEC_CS16_PIN
+                    __builtin_amdgcn_sched_barrier(0);  // one A fragment ahead, no deeper
+#endif
+                }
+                // (keeps the second tile's A reads from being hoisted above the first tile's
+                // MFMAs: 64 more live VGPRs, spilled at 3 waves per SIMD)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            uint4 elf = ones;
+            if constexpr (FUSED) elf = dks[4 * q + g];  // D_k[32q + 8g .. +8]
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                uint4 el = elf;
+                if constexpr (!FUSED) el = lk[b] ? *reinterpret_cast<const uint4*>(lk[b] + 32 * q) : ones;
+                const uint32_t lw[4] = {el.x, el.y, el.z, el.w};
+                const uint32_t pw[4] = {ep[b].x, ep[b].y, ep[b].z, ep[b].w};
+                const uint32_t nw[4] = {en[b].x, en[b].y, en[b].z, en[b].w};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {  // accumulator register r of tile 2q + h is row 32q + 8g + 4h + r
+#pragma unroll
+                    for (int r2 = 0; r2 < 2; ++r2) {  // elements 4h + 2r2, 4h + 2r2 + 1: word 2h + r2
+                        const float l0 = bf_lo(lw[2 * h + r2]), l1 = bf_hi(lw[2 * h + r2]);
+                        pp[b] = fmaf(acc[b][h][2 * r2], bf_lo(pw[2 * h + r2]) * l0, pp[b]);
+                        pp[b] = fmaf(acc[b][h][2 * r2 + 1], bf_hi(pw[2 * h + r2]) * l1, pp[b]);
+                        pn[b] = fmaf(acc[b][h][2 * r2], bf_lo(nw[2 * h + r2]) * l0, pn[b]);
+                        pn[b] = fmaf(acc[b][h][2 * r2 + 1], bf_hi(nw[2 * h + r2]) * l1, pn[b]);
+                    }
+                }
+                // Each half's sums pass through an opaque copy, so the compiler cannot pair
+                // the two halves' chains into v_pk_fma_f32 (as it does in the FUSED form
+                // without this).  With that pairing the MI355X returned a wrong low-half sum
+                // (pos of half 0) for ≈ 2 % of tiles, varying from run to run. Measured: 15-25
+                // of 640 tiles bad per run without the copy, none in 4 runs with it. The
+                // paired form's epilogue is not paired by the compiler (plain v_fmac_f32).
+                asm volatile("" : "+v"(pp[b]), "+v"(pn[b]));
+            }
+        }
+        float term = 0.f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // the pair's 4 lane groups, in a fixed butterfly
+            pp[b] += __shfl_xor(pp[b], 16);
+            pp[b] += __shfl_xor(pp[b], 32);
+            pn[b] += __shfl_xor(pn[b], 16);
+            pn[b] += __shfl_xor(pn[b], 32);
+            const int p = tile * 32 + 16 * b + pl;
+            if (g == 0 && valid[b]) {
+                a.out[p] = pp[b];
+                a.out[nh + p] = pn[b];
+            }
+            if (FUSED && g == 0 && valid[b]) term += fmaxf(pn[b] - (pp[b] - a.margin), 0.f);  // optimizer.py:116-120
+        }
+        if constexpr (FUSED) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off);
+            wsum += term;
+            asm volatile("" ::: "memory");    // (this tile's D_k reads stay before the next tile's store)
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if constexpr (!FUSED) return;
+    // the workgroup's partial (its waves in order), write-through + drained, then a ticket; the
+    // last workgroup adds every partial in block order (decoder_bf16_colshared_kernel's hand-off)
+    __shared__ float red[WAVES];
+    __shared__ int last;
+    if (lane == 0) red[wave] = wsum;
+    __syncthreads();
+    if (tid == 0) {
+        float t = 0.f;
+        for (int w = 0; w < WAVES; ++w) t += red[w];
+        __hip_atomic_store(a.partial + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && tid == 0) {
+        float t = 0.f;
+        for (int b = 0; b < (int)gridDim.x; ++b)
+            t += __hip_atomic_load(a.partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.loss[0] = t;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 }  // namespace
 
 extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
@@ -408,6 +663,18 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
     const int lds = d * d * 2;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (!dg::aligned16(G)) return DG_EALIGN;  // R rows are staged into LDS in 16-byte pieces
+    if (DG_DEC_CS16 && d == 256) {
+        // the 16x16x32 form (decoder_bf16_cs16_kernel, FUSED = false): bit-identical scores to
+        // dg_slot_score_hinge_bf16's; 32-bit byte offsets into the tables are required
+        constexpr int kT16 = DG_DEC_CS16_THREADS;
+        const int lds16 = d * d * 2 + (kT16 / 64) * d * 2;
+        int blocks16 = (n_tiles + kT16 / 64 - 1) / (kT16 / 64);
+        if (blocks16 > 256) blocks16 = 256;
+        static std::atomic<uint64_t> configured16p{0};
+        dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_cs16_kernel<kT16, false>), lds16, configured16p);
+        hipLaunchKernelGGL((decoder_bf16_cs16_kernel<kT16, false>), dim3(blocks16), dim3(kT16), lds16, st, a);
+        return dg::launch_status();
+    }
     constexpr int kThreads = DG_DEC_CS_THREADS;
     static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
     dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, true, kThreads, false>),
@@ -467,6 +734,19 @@ extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_ro
     const int n_tiles = (nh + 31) / 32;
     int blocks = (n_tiles + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > DG_HINGE_WS_BLOCKS) blocks = DG_HINGE_WS_BLOCKS;  // persistent; the workspace's partials
+    // the 16x16x32 form: every 32-pair tile inside one slot (one D_k), tables within 32-bit
+    // byte offsets (its row loads are buffer loads)
+    if (DG_DEC_CS16 && batch % 32 == 0 && (int64_t)range * ld_row * 2 < 0x7fffffffLL &&
+        (int64_t)range * ld_col * 2 < 0x7fffffffLL) {
+        constexpr int kT16 = DG_DEC_CS16_THREADS;
+        const int lds16 = d * d * 2 + (kT16 / 64) * d * 2;  // R + a D_k row per wave
+        int blocks16 = (n_tiles + kT16 / 64 - 1) / (kT16 / 64);
+        if (blocks16 > DG_HINGE_WS_BLOCKS) blocks16 = DG_HINGE_WS_BLOCKS;
+        static std::atomic<uint64_t> configured16{0};
+        dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_cs16_kernel<kT16, true>), lds16, configured16);
+        hipLaunchKernelGGL((decoder_bf16_cs16_kernel<kT16, true>), dim3(blocks16), dim3(kT16), lds16, st, a);
+        return dg::launch_status();
+    }
     // the opt-in is the dynamic R buffer exactly: the kernel's static LDS (the hinge partials)
     // comes on top of it, and static + dynamic must stay within the CU's 160 KB
     static std::atomic<uint64_t> configured{0};

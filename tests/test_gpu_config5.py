@@ -140,7 +140,8 @@ def test_config5_one_launch_equals_three(slots):
     assert torch.equal(one.out, three.out)
     l1, l3 = float(one.loss[0]), float(three.loss[0])
     assert abs(l1 - l3) <= 1e-5 * abs(l3)
-    for _ in range(2):
+    for _ in range(3):  # (a wrong sum that came and went once showed up in ≈ 2 % of tiles per launch)
         one()
         torch.cuda.synchronize()
         assert float(one.loss[0]) == l1
+        assert torch.equal(one.out, three.out)
