@@ -441,20 +441,25 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
     Idx nxt;
     const int first = wave * (int)gridDim.x + (int)blockIdx.x;  // round-major tile order (see above)
     fetch(first, nxt);
+    // D_k row of a tile, lane l: elements 4l .. 4l+3.  (The 8-byte store and the 16-byte reads
+    // are different types to the compiler — no assumed aliasing — so explicit compiler barriers
+    // keep a tile's reads before the next tile's store and after its own; the LDS executes one
+    // wave's accesses in order.)  The first tile's row is stored here, every later one at the
+    // end of the tile before it, where its load has long completed (the rows' waits in the q
+    // loop) — at the top of the tile the store would wait for the just-issued index loads.
+    auto put_dk = [&](const uint2 dk) {
+        if constexpr (FUSED) {
+            asm volatile("" ::: "memory");
+            reinterpret_cast<uint2*>(dks)[lane] = dk;
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+    put_dk(nxt.dk);
 #pragma unroll 1
     for (int tile = first; tile < n_tiles; tile += stride) {
         const Idx cur = nxt;
         fetch(tile + stride, nxt);
-        // D_k row of the tile, lane l: elements 4l .. 4l+3.  (The 8-byte store and the 16-byte
-        // reads are different types to the compiler — no assumed aliasing — so explicit compiler
-        // barriers keep the previous tile's reads before the store and this tile's after it; the
-        // LDS executes one wave's accesses in order.)
-        if constexpr (FUSED) {
-            asm volatile("" ::: "memory");
-            reinterpret_cast<uint2*>(dks)[lane] = cur.dk;
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-        }
         const uint16_t* lk[2];  // non-FUSED: each half's pairs' D_k rows (NULL: identity)
         // rows through buffer loads from the uniform table bases: a 32-bit byte offset per row
         // (1 VGPR) instead of a 64-bit address (2)
@@ -567,6 +572,7 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
                 asm volatile("" : "+v"(pp[b]), "+v"(pn[b]));
             }
         }
+        put_dk(nxt.dk);  // (after this tile's last D_k read)
         float term = 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {  // the pair's 4 lane groups, in a fixed butterfly
@@ -585,8 +591,6 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off);
             wsum += term;
-            asm volatile("" ::: "memory");    // (this tile's D_k reads stay before the next tile's store)
-            __builtin_amdgcn_wave_barrier();
         }
     }
     if constexpr (!FUSED) return;
