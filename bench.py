@@ -281,7 +281,7 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
 
 KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm_groups_kernel<{lp}>",
                 "PreparedStaged": "spmm_staged_kernel", "PreparedFusedSeg": "gcn_fused_seg_kernel<{lp}, false",
-                "PreparedSeg": "spmm_seg_kernel<{lp}, false"}
+                "PreparedSeg": "spmm_seg_kernel<{lp}, false", "PreparedSegFinish": "spmm_seg_kernel<{lp}, false"}
 
 
 def _kernel_label(launch, lp):
@@ -628,13 +628,13 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
         "data": "synthetic: per-slot relations (Zipf sizes, SURVEY §8d), positives = slot edges, negatives "
                 "device-sampled from each slot's own degree^0.75 table, random bf16 E / R / D_k",
         "config": {"workload": f"config 5: {slots} relation slots x ({B} pos + {B} neg) pairs, d={d}, "
-                               "DEDICOM uT.D_k.R.D_k.v on v_mfma_f32_32x32x16_bf16 + hinge loss",
+                               "DEDICOM uT.D_k.R.D_k.v on v_mfma_f32_16x16x32_bf16 + hinge loss",
                    "pairs_per_step": 2 * slots * B, "slots_this_rank": s1 - s0, "hipgraph": not args.no_graph,
                    "steps_per_graph": G},
         "loss": float(sc.loss[0]),
         "roofline": {"bound": "mfma", "achieved": tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / BF16_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "decoder_bf16_colshared_kernel<256, true, 768, true> (sampler + scores + hinge)",
+                     "kernel": "decoder_bf16_cs16_kernel<768, true> (sampler + scores + hinge)",
                      "kernel_ms": k_ms,
                      "algorithmic_flops": sc.n * flop_pp, "mfma_tflops": mfma_tflops,
                      "per_pair_form_tflops": n * (2 * d * d + 4 * d) / (k_ms * 1e-3) / 1e12},

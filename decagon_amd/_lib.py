@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 32
+ABI_VERSION = 33
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -109,6 +109,11 @@ class DgProj(ctypes.Structure):
 class DgFusedTarget(ctypes.Structure):
     _fields_ = [("out", c_void_p), ("n_rows", c_int32), ("g_begin", c_int32), ("g_count", c_int32),
                 ("flags", c_int32)]
+
+
+class DgSegFinish(ctypes.Structure):
+    _fields_ = [("out", c_void_p), ("n_rows", c_int32), ("g_begin", c_int32), ("g_count", c_int32),
+                ("target_flags", c_int32)]
 
 
 class DgEpiGroup(ctypes.Structure):
@@ -200,6 +205,8 @@ SIGNATURES = {
                                            c_void_p]),
     "dg_gcn_fused_seg_peer_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32,
                                             c_int32, POINTER(DgPeerXchg), c_void_p]),
+    "dg_spmm_seg_finish_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgSegFinish), c_int32, c_int32,
+                                         c_int32, c_int32, c_void_p, POINTER(DgPeerXchg), c_void_p]),
     "dg_peer_alloc": (c_int32, [c_int64, c_int32, POINTER(c_void_p)]),
     "dg_peer_free": (c_int32, [c_void_p]),
     "dg_ipc_get_handle": (c_int32, [c_void_p, c_void_p, POINTER(c_int64)]),

@@ -493,7 +493,6 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK&
 // every wave reaches the closing barrier.
 template <int LP, bool PEER>
 __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
-    constexpr int CG = dg::kWave / LP;  // chunk groups per wave
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int cg = lane / LP;
@@ -636,7 +635,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 32; }
+extern "C" int32_t dg_abi_version(void) { return 33; }
 
 
 namespace {
