@@ -280,12 +280,20 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
 
 
 KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm_groups_kernel<{lp}>",
-                "PreparedStaged": "spmm_staged_kernel", "PreparedFusedSeg": "gcn_fused_seg_kernel<{lp}, false",
-                "PreparedSeg": "spmm_seg_kernel<{lp}, false", "PreparedSegFinish": "spmm_seg_kernel<{lp}, false"}
+                "PreparedStaged": "spmm_staged_kernel", "PreparedFusedSeg": "gcn_fused_seg_kernel<{lp}, {proj}",
+                "PreparedSeg": "spmm_seg_kernel<{lp}, {proj}", "PreparedSegFinish": "spmm_seg_kernel<{lp}, {proj}"}
 
 
-def _kernel_label(launch, lp):
-    pat = KERNEL_NAMES.get(type(launch).__name__, "?").format(lp=lp)
+def _kernel_pat(launch, d):
+    """The kernel-name prefix of a launch at layer width d (the reassociated seg forms — d_in 64
+    → d_out 32 — are their <16, true> instances)."""
+    proj = getattr(launch, "d_in", None) is not None and launch.d_in != launch.d_out
+    lp = 16 if proj else 1 << max(0, (max(1, d // 4) - 1).bit_length())
+    return KERNEL_NAMES.get(type(launch).__name__, "?").format(lp=lp, proj="true" if proj else "false")
+
+
+def _kernel_label(launch, d):
+    pat = _kernel_pat(launch, d)
     return pat if pat.endswith(">") or pat == "spmm_staged_kernel" else pat + ", …>"
 
 
@@ -302,8 +310,7 @@ def pmc_traffic(config, launch, d, layer=1):
         return None, None, None
     src = str(files[-1].relative_to(ROOT))
     rec = json.load(open(files[-1])).get(config, {})
-    lp = 1 << max(0, (max(1, d // 4) - 1).bit_length())
-    pat = KERNEL_NAMES.get(type(launch).__name__, "?").format(lp=lp)
+    pat = _kernel_pat(launch, d)
     hit = [v for k, v in rec.items() if k.replace("void ", "").startswith(pat)]
     if not hit:
         return None, src, None
@@ -406,21 +413,23 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
         el_max, tot_edges = float(tm[0]), float(t[1])
     value = tot_edges * steps / el_max
 
-    # the roofline covers the dominant kernel: the longest layer-1 SpMM launch (config S: the
-    # one fused launch; config P: the staged drug x drug SpMM), its algorithmic bytes over its
-    # own duration; the whole layer-1 SpMM (launches as the forward runs them — concurrent
-    # streams at P) is reported beside it
+    # the roofline covers the dominant kernel: the longest SpMM launch of either layer (config
+    # S: layer 2's fused, reassociated launch; config P: layer 1's staged drug x drug SpMM), its
+    # algorithmic bytes over its own duration; each whole layer's SpMM (launches as the forward
+    # runs them) is reported beside it
     l1, l2 = plan.spmm_launches
-    per = [(time_kernel(lambda l=l: l(), kernel_reps, stream), i) for i, l in enumerate(l1)]
-    k_ms, di = max(per)
-    dom = l1[di]
-    k_bytes = plan.launch_bytes(dom, 1)
+    per = [(time_kernel(lambda l=l: l(), kernel_reps, stream), 1, i) for i, l in enumerate(l1)]
+    per += [(time_kernel(lambda l=l: l(), kernel_reps, stream), 2, i) for i, l in enumerate(l2)]
+    k_ms, dom_layer, di = max(per)
+    dom = (l1 if dom_layer == 1 else l2)[di]
+    dom_d = H1 if dom_layer == 1 else H2
+    k_bytes = plan.launch_bytes(dom, dom_layer)
     achieved = k_bytes / (k_ms * 1e-3) / 1e9
     l1_ms = time_kernel(plan._layer1.run_spmm, kernel_reps, stream)
     l1_bytes = plan.layer_bytes(1)
     k2_ms = time_kernel(plan._layer2.run_spmm, kernel_reps, stream)
-    traffic, traffic_src, traffic_ms = pmc_traffic(config if world == 1 else None, dom, H1)
-    lp = 1 << max(0, (max(1, H1 // 4) - 1).bit_length())
+    l2_bytes = plan.layer_bytes(2)
+    traffic, traffic_src, traffic_ms = pmc_traffic(config if world == 1 else None, dom, dom_d, dom_layer)
     rec = {
         "value": value,
         "unit": "edges/s",
@@ -435,12 +444,20 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "traffic_profiled_kernel_ms": traffic_ms,
-                     "kernel": _kernel_label(dom, lp) + " (layer 1)",
-                     "kernel_ms": k_ms, "algorithmic_bytes": k_bytes},
+                     "kernel": _kernel_label(dom, dom_d) + f" (layer {dom_layer})",
+                     "kernel_ms": k_ms, "algorithmic_bytes": k_bytes,
+                     "launches_us": {f"layer{ly} {_kernel_label((l1 if ly == 1 else l2)[i], H1 if ly == 1 else H2)}":
+                                     ms * 1e3 for ms, ly, i in per}},
         "spmm_layer1": {"launches": [type(x).__name__ for x in l1], "ms": l1_ms,
                         "algorithmic_bytes": l1_bytes, "GB_s": l1_bytes / (l1_ms * 1e-3) / 1e9,
                         "frac": l1_bytes / (l1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "edges_per_s": dg.total_nnz / (l1_ms * 1e-3)},
+        # layer 2's compulsory bytes: the CSR once, H1_j (reassociated / staged forms) or P_k
+        # once, W2 once where the launch reads it, the output once (ForwardPlan.layer_bytes)
+        "spmm_layer2": {"launches": [type(x).__name__ for x in l2], "ms": k2_ms,
+                        "algorithmic_bytes": l2_bytes, "GB_s": l2_bytes / (k2_ms * 1e-3) / 1e9,
+                        "frac": l2_bytes / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "edges_per_s": dg.total_nnz / (k2_ms * 1e-3)},
         "spmm_layer2_ms": k2_ms,
     }
     if sharded:
