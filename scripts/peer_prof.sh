@@ -7,7 +7,7 @@ ex=${2:-peer}
 out=gpurun_out/$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_$ex -o run -- python3 bench.py --config S \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_$ex -o run -- python3 bench.py --config S \
     --simulate-world 8 --simulate-rank 0 --exchange $ex --steps 100 --warmup 10 > $out/prof_$ex.json 2> $out/prof_$ex.err \
     || { tail -5 $out/prof_$ex.err; exit 1; }
 f=$(find $out/prof_$ex -name "*kernel_stats.csv" | head -1)
