@@ -44,6 +44,9 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 #ifndef DG_DEC_CS16_PIN
 #define DG_DEC_CS16_PIN 1
 #endif
+#ifndef DG_DEC_CS16_TL
+#define DG_DEC_CS16_TL 0       // epilogue: D_k folded into T once for both rows (A/B)
+#endif
 
 struct Bf16DecArgs {
     const uint16_t* row_table;
@@ -557,10 +560,19 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
 #pragma unroll
                     for (int r2 = 0; r2 < 2; ++r2) {  // elements 4h + 2r2, 4h + 2r2 + 1: word 2h + r2
                         const float l0 = bf_lo(lw[2 * h + r2]), l1 = bf_hi(lw[2 * h + r2]);
+#if DG_DEC_CS16_TL
+                        // (D_k∘T)[i] once for both rows: 2 products instead of 4
+                        const float t0 = acc[b][h][2 * r2] * l0, t1 = acc[b][h][2 * r2 + 1] * l1;
+                        pp[b] = fmaf(t0, bf_lo(pw[2 * h + r2]), pp[b]);
+                        pp[b] = fmaf(t1, bf_hi(pw[2 * h + r2]), pp[b]);
+                        pn[b] = fmaf(t0, bf_lo(nw[2 * h + r2]), pn[b]);
+                        pn[b] = fmaf(t1, bf_hi(nw[2 * h + r2]), pn[b]);
+#else
                         pp[b] = fmaf(acc[b][h][2 * r2], bf_lo(pw[2 * h + r2]) * l0, pp[b]);
                         pp[b] = fmaf(acc[b][h][2 * r2 + 1], bf_hi(pw[2 * h + r2]) * l1, pp[b]);
                         pn[b] = fmaf(acc[b][h][2 * r2], bf_lo(nw[2 * h + r2]) * l0, pn[b]);
                         pn[b] = fmaf(acc[b][h][2 * r2 + 1], bf_hi(nw[2 * h + r2]) * l1, pn[b]);
+#endif
                     }
                 }
                 // Each half's sums pass through an opaque copy, so the compiler cannot pair

@@ -89,6 +89,11 @@ STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
 # and relations, Σ_k (Â_k·H1_j)·W2_k in dg_spmm_seg_f32, instead of every rank projecting all of
 # H1_j·W2_k (config P's PPI: 19,085 rows x 2 relations, 9.4 µs on every rank at N = 8)
 REASSOC_ROWS = os.environ.get("DG_REASSOC_ROWS", "1") != "0"
+# sharded forward plans: layer 1 of the row-split, non-windowed, non-staged groups in
+# dg_spmm_seg_f32 (one wave per (row, relation), its segment's pairs in one load) instead of
+# dg_spmm_groups_f32 (one wave per two (chunk, row) items): a rank's short row block (config P
+# at N = 8: 2,386 protein rows, the PPI's two relations in one chunk) keeps more waves in flight
+SEG_ROWS_L1 = os.environ.get("DG_SEG_ROWS_L1", "0") != "0"
 # row-split layers in seg mode (config S at N >= 3): DG_SEG_FINISH=1 runs dg_spmm_seg_finish_f32 —
 # the seg launch also finishes each row (its last arriving workgroup), no epilogue launch.  Off
 # by default: measured slower (loopback N = 8 rank share over RCCL 29.1 µs against 25.4 for the
@@ -497,6 +502,11 @@ class ForwardPlan:
                           if REASSOC_ROWS and shard is not None and not keep_sums and self.drop_state is None
                           and h1 == 64 and h2 == 32 and dgraph.groups[et].n_rels and not dgraph.groups[et].staged
                           and (dgraph.groups[et].seg is not None or dgraph.groups[et].seg2 is not None)}
+        self.seg_l1 = {et for et in self.edge_types
+                       if SEG_ROWS_L1 and shard is not None and not self.seg_mode and not keep_sums
+                       and self.drop_state is None and h1 in (32, 64) and et[0] in self.row_block
+                       and dgraph.groups[et].n_rels and not dgraph.groups[et].staged
+                       and dgraph.groups[et].seg is not None}
         self.proj: Dict[EdgeType, torch.Tensor] = {}
         for et in self.edge_types:
             grp = dgraph.groups[et]
@@ -709,7 +719,9 @@ class ForwardPlan:
                 off += sz
         partials, specs, staged, reduces, segs = {}, [], [], [], []
         seg_by_et = {}
-        reassoc = set(seg_w or {}) if not self.seg_mode else set()  # layer 2 reassociated outside seg mode
+        # outside seg mode: layer 2 reassociated (seg_w) and, in layer 1, the row-split groups of
+        # SEG_ROWS_L1 — both in dg_spmm_seg_f32
+        reassoc = (set(seg_w or {}) | (self.seg_l1 if relu else set())) if not self.seg_mode else set()
         for et in rest:
             grp = g.groups[et]
             n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
