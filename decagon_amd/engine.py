@@ -92,7 +92,10 @@ REASSOC_ROWS = os.environ.get("DG_REASSOC_ROWS", "1") != "0"
 # sharded forward plans: layer 1 of the row-split, non-windowed, non-staged groups in
 # dg_spmm_seg_f32 (one wave per (row, relation), its segment's pairs in one load) instead of
 # dg_spmm_groups_f32 (one wave per two (chunk, row) items): a rank's short row block (config P
-# at N = 8: 2,386 protein rows, the PPI's two relations in one chunk) keeps more waves in flight
+# at N = 8: 2,386 protein rows, the PPI's two relations in one chunk) keeps more waves in flight.
+# Off: at P's N = 8 share it took 3-5 us off seven ranks (107.1-108.0 -> 102.7-104.1 us) but
+# added 1.7 us to the slowest (rank 4, 110.6 -> 112.3: a wave per (row, relation) walks a hub
+# row's long segment alone), so the max over ranks got worse
 SEG_ROWS_L1 = os.environ.get("DG_SEG_ROWS_L1", "0") != "0"
 # row-split layers in seg mode (config S at N >= 3): DG_SEG_FINISH=1 runs dg_spmm_seg_finish_f32 —
 # the seg launch also finishes each row (its last arriving workgroup), no epilogue launch.  Off
