@@ -40,12 +40,10 @@ __global__ __launch_bounds__(256) void decoder_score_kernel(const DecArgs a) {
     const bool valid = p < a.n_pairs;
     float part[16];
     score_tile(a.t, valid ? a.row_idx[p] : 0, valid ? a.col_idx[p] : 0, valid, part);
-    if (i == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int pp = p0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (pp < a.n_pairs) a.out[pp] = part[r];
-        }
+    if ((i & 1) == 0) {  // lane 2r holds score r of its half
+        const int r = i >> 1;
+        const int pp = p0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (pp < a.n_pairs) a.out[pp] = part[0];
     }
 }
 
@@ -128,14 +126,12 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
     } else {
         score_tile(a.t, ridx, cidx, valid, part);
     }
-    if (i == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float v = (b0 + q < a.n) ? part[r] : 0.f;
-            sc[side][q] = v;
-            if (b0 + q < a.n) (side == 0 ? a.pos : a.neg)[b0 + q] = v;
-        }
+    if ((i & 1) == 0) {  // lane 2r holds score r of its half
+        const int r = i >> 1;
+        const int q = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = (b0 + q < a.n) ? part[0] : 0.f;
+        sc[side][q] = v;
+        if (b0 + q < a.n) (side == 0 ? a.pos : a.neg)[b0 + q] = v;
     }
     __syncthreads();
     if (threadIdx.x < 64) {

@@ -45,7 +45,7 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 #define DG_DEC_CS16_PIN 1
 #endif
 #ifndef DG_DEC_CS16_TL
-#define DG_DEC_CS16_TL 0       // epilogue: D_k folded into T once for both rows (A/B)
+#define DG_DEC_CS16_TL 1       // epilogue: D_k folded into T once for both rows (0: per row; 205.8-206.1 -> 203.5-204.2 us)
 #endif
 
 struct Bf16DecArgs {
@@ -81,6 +81,31 @@ constexpr int threads_for() { return D == 256 ? 768 : 1024; }
 
 // HAS_L: per-relation diagonals present (DEDICOM) — a template flag, so no load sits behind a
 // branch (a runtime `if (L)` split every load into its own basic block, each waited on alone)
+// R (D x D bf16, row-major) into LDS, row i's 16-byte slot q at rs[i*SL + (q ^ (i % SL))]: every
+// load of the thread's share issued before its first LDS store (a load-store-per-iteration loop
+// waits one L2 round trip per slot: 11 in a row at D = 256 and 768 threads, before any work).
+template <int D, int THREADS>
+__device__ __forceinline__ void stage_r(uint4* rs, const uint16_t* R) {
+    constexpr int SL = D / 8, N = D * SL, PER = (N + THREADS - 1) / THREADS, B = 4;
+#pragma unroll
+    for (int k0 = 0; k0 < PER; k0 += B) {  // B slots in flight per thread
+        uint4 t[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const int e = (int)threadIdx.x + (k0 + k) * THREADS;
+            t[k] = (k0 + k < PER && e < N) ? *reinterpret_cast<const uint4*>(R + (int64_t)e * 8) : uint4{};
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const int e = (int)threadIdx.x + (k0 + k) * THREADS;
+            if (k0 + k < PER && e < N) {
+                const int i = e / SL, q = e - i * SL;  // row e / SL, slot e % SL
+                rs[i * SL + (q ^ (i % SL))] = t[k];
+            }
+        }
+    }
+}
+
 template <int D, bool HAS_L>
 __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf16DecArgs a) {
     constexpr int kThreads = threads_for<D>();
@@ -217,10 +242,7 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
     constexpr int SL = D / 8;
     extern __shared__ uint4 rs[];  // R: row i, slot q (n = 8q .. 8q+7) at rs[i*SL + (q ^ (i % SL))]
     const int tid = threadIdx.x;
-    for (int e = tid; e < D * SL; e += THREADS) {
-        const int i = e / SL, q = e - i * SL;
-        rs[i * SL + (q ^ (i % SL))] = *reinterpret_cast<const uint4*>(a.R + (int64_t)i * D + 8 * q);
-    }
+    stage_r<D, THREADS>(rs, a.R);
     __syncthreads();
 
     const int lane = tid & 63;
@@ -396,10 +418,7 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
     constexpr int WAVES = THREADS / 64;
     extern __shared__ uint4 rs[];             // R: row i, slot q at rs[i*SL + (q ^ (i % SL))]; then D_k rows
     const int tid = threadIdx.x;
-    for (int e = tid; e < D * SL; e += THREADS) {
-        const int i = e / SL, q = e - i * SL;
-        rs[i * SL + (q ^ (i % SL))] = *reinterpret_cast<const uint4*>(a.R + (int64_t)i * D + 8 * q);
-    }
+    stage_r<D, THREADS>(rs, a.R);
     __syncthreads();
     const int lane = tid & 63;
     const int wave = tid >> 6;

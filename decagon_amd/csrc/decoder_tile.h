@@ -77,7 +77,9 @@ __device__ __forceinline__ float4 ld_emb4(const float* p) {
 // past the end.  T = (U∘l)·G runs on v_mfma_f32_32x32x2_f32 in k-blocks of 32 whose A/B
 // fragments are loaded up front (one memory round trip per block, not per k-step); then
 // score[p] = Σ_j T[p][j]·l[j]·V[p][j] is folded over the 32 lanes of each half-wave.
-// Returns the score of pair (r&3)+8(r>>2)+4h in part[r] of lane 0 / 32.  kSc1: every load of
+// Returns the score of pair (r&3)+8(r>>2)+4h, r = (lane & 31) >> 1, in part[0] of lanes 2r and
+// 2r+1 of each half (a reduce-scatter over the half's 32 lanes: 16 shuffles instead of a
+// butterfly per score's 80).  kSc1: every load of
 // row_table / col_table is an sc1 load (the tables were written in this launch).  kD: the width
 // when known at compile time (only that path is compiled: fewer registers), else 0.
 template <bool kSc1 = false, int kD = 0>
@@ -174,11 +176,20 @@ __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, 
 #pragma unroll
         for (int r = 0; r < 16; ++r) part[r] = fmaf(acc[r] * lj, v[r], part[r]);
     }
+    // reduce-scatter over the half's 32 lanes: at each step a lane keeps the half of its
+    // remaining scores that its lane bit selects and adds its partner's copy of them
+    const int b4 = (i >> 4) & 1, b3 = (i >> 3) & 1, b2 = (i >> 2) & 1, b1 = (i >> 1) & 1;
+    float v8[8], v4[4], v2[2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int j = 0; j < 8; ++j)
+        v8[j] = (b4 ? part[8 + j] : part[j]) + __shfl_xor(b4 ? part[j] : part[8 + j], 16);
 #pragma unroll
-        for (int m = 1; m < 32; m <<= 1) part[r] += __shfl_xor(part[r], m);
-    }
+    for (int j = 0; j < 4; ++j) v4[j] = (b3 ? v8[4 + j] : v8[j]) + __shfl_xor(b3 ? v8[j] : v8[4 + j], 8);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) v2[j] = (b2 ? v4[2 + j] : v4[j]) + __shfl_xor(b2 ? v4[j] : v4[2 + j], 4);
+    float v1 = (b1 ? v2[1] : v2[0]) + __shfl_xor(b1 ? v2[0] : v2[1], 2);
+    v1 += __shfl_xor(v1, 1);
+    part[0] = v1;  // score r = 8·b4 + 4·b3 + 2·b2 + b1 = (lane & 31) >> 1
 }
 
 }  // namespace dg
