@@ -245,6 +245,10 @@ def time_kernel(fn, reps, stream):
     return best
 
 
+WARM_REPLAYS = int(os.environ.get("DG_WARM_REPLAYS", "1"))  # untimed replays after capture
+LAST_TIMING = {}  # timed_steps: the last timed region's device-side span (HIP events), untimed rerun
+
+
 def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
     """W eager warm-up steps, then `steps` steps as steps/G replays of one hipGraph of G
     steps (one untimed replay first: graph upload), bracketed by barrier + synchronize."""
@@ -261,7 +265,8 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
             with torch.cuda.graph(cg, stream=stream, capture_error_mode="thread_local"):
                 for _ in range(G):
                     step()
-            cg.replay()
+            for _ in range(WARM_REPLAYS):
+                cg.replay()
             run = cg.replay
         else:
             G = 1
@@ -276,7 +281,22 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
         torch.cuda.synchronize()
         if barrier:
             barrier()
-        return time.perf_counter() - t0
+        el = time.perf_counter() - t0
+        # (untimed) the same replays once more between HIP events on the stream: the device's
+        # own span, against which the wall-clock figure above shows the host's launch and
+        # completion-wait cost of the timed region
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        h0 = time.perf_counter()
+        for _ in range(steps // G):
+            run()
+        h1 = time.perf_counter()
+        e1.record(stream)
+        e1.synchronize()
+        LAST_TIMING.clear()
+        LAST_TIMING.update({"device_ms_per_step": e0.elapsed_time(e1) / steps,
+                            "host_enqueue_ms": (h1 - h0) * 1e3, "wall_ms_per_step": el * 1e3 / steps})
+        return el
 
 
 KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm_groups_kernel<{lp}>",
@@ -403,6 +423,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
         else:
             el = timed_steps(step, steps, warmup, 1, stream, False, barrier)
 
+    split = dict(LAST_TIMING)
     local_edges = 2 * dg.total_nnz
     el_max, tot_edges = el, local_edges
     if sharded:
@@ -437,6 +458,7 @@ def forward_bench(args, config, rank, world, sharded, device, dist, steps, warmu
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": el_max * 1e3 / steps,
+        "timing_split": split,
         "scaling": scaling,
         "config": {"workload": workload, "nnz_per_layer_total": int(tot_edges // 2),
                    "parallelism": (plan.parallelism(args.backend) if sharded else "1 GPU"),
@@ -640,6 +662,7 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": el * 1e3 / steps,
+        "timing_split": dict(LAST_TIMING),
         "scaling": "strong",
         "dtype": "bf16 (fp32 accumulation)",
         "data": "synthetic: per-slot relations (Zipf sizes, SURVEY §8d), positives = slot edges, negatives "
