@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 33
+ABI_VERSION = 34
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -235,11 +235,13 @@ SIGNATURES = {
     "dg_staged_block": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p]),
     "dg_decoder_score_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                         c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
-    "dg_slot_score_hinge_bf16": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32,
+    "dg_slot_score_hinge_bf16": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
+                                           c_void_p, c_int32,
                                            c_int64, c_int32, c_int32, c_int32, c_uint64, c_void_p, c_void_p,
                                            c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "dg_decoder_score_bf16_paired": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
-                                        c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "dg_decoder_score_bf16_paired": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_void_p,
+                                               c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
+                                               c_void_p]),
     "dg_decoder_hinge_f32": (
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,

@@ -88,20 +88,12 @@ struct HingeArgs {
     float margin;
 };
 
-#ifndef DG_DEC_SPLIT32
-#define DG_DEC_SPLIT32 0  // d = 32: decoder_hinge32_kernel (the tile's k split over two waves).  Off:
-#endif                    // config S step 18.08-18.15 us without, 18.23-18.28 with (A/B, 200 steps)
-#ifndef DG_DEC_ABL
-#define DG_DEC_ABL 0  // timing ablations only (wrong results): 1 no ticket, 2 no draw, 4 no scores, 8 empty
-#endif
-
 template <bool PACKED>
 __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
     __shared__ float sc[2][32];
     __shared__ float red[128];
     __shared__ int last;
     __shared__ unsigned long long total;
-    if (DG_DEC_ABL & 8) return;
     const int lane = threadIdx.x & 63;
     const int side = threadIdx.x >> 6;  // 0: positives, 1: negatives
     const int i = lane & 31;
@@ -116,19 +108,12 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
             ridx = a.rows[b];
         else if (a.neg_given)
             ridx = a.neg_given[b];
-        else if (DG_DEC_ABL & 2)
-            ridx = cidx;
         else
             ridx = unigram_draw(a.alias, a.range, a.seed, a.offset + (uint64_t)b);
         if (side == 1 && a.neg_rows_out && h == 0) a.neg_rows_out[b] = ridx;
     }
     float part[16];
-    if (DG_DEC_ABL & 4) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) part[r] = (float)(ridx + r);
-    } else {
-        score_tile(a.t, ridx, cidx, valid, part);
-    }
+    score_tile(a.t, ridx, cidx, valid, part);
     if ((i & 1) == 0) {  // lane 2r holds score r of its half
         const int r = i >> 1;
         const int q = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -142,10 +127,7 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
         if (lane < 32 && b0 + lane < a.n) term = fmaxf(sc[1][lane] - (sc[0][lane] - a.margin), 0.f);
 #pragma unroll
         for (int m = 32; m > 0; m >>= 1) term += __shfl_xor(term, m);
-        if (lane == 0 && (DG_DEC_ABL & 1)) {
-            a.partial[blockIdx.x] = term;
-            last = 0;
-        } else if (lane == 0 && PACKED) {
+        if (lane == 0 && PACKED) {
             unsigned long long add = 1ull << 56;
             if (term < 256.0f) {  // (false for NaN and inf too)
                 add += static_cast<unsigned long long>(static_cast<double>(term) * 4294967296.0 + 0.5);  // nearest
@@ -202,159 +184,6 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
         a.loss[0] = red[0];
         atomicExch(a.ticket, 0u);
     }
-}
-
-// The fused decoder step at d = 32 (config S's decoders) on FOUR waves per 32 pairs: wave w is
-// side w & 1 (positives / negatives) and k half kh = w >> 1.  The d = 32 tile is 16 dependent
-// v_mfma_f32_32x32x2_f32 (64 cycles each on its SIMD: ≈ 0.4 µs on the step's critical path);
-// split by k over two waves on two SIMDs it is 8 each, the kh = 1 wave's accumulator added to
-// the kh = 0 wave's through LDS.  Each lane also loads the 16 column indices its V rows need
-// straight from `cols` (in parallel with its own index loads) instead of taking them from the
-// pairs' lanes by shuffles.  Scores: Σ_{s<8} then Σ_{s≥8} in fp32, added; the rest as
-// decoder_hinge_kernel<true> (PACKED hand-off: at most 255 workgroups).
-template <bool HL>  // HL: the decoder has a diagonal l (else G alone); row tables allow 16-B loads
-__global__ __launch_bounds__(256) void decoder_hinge32_kernel(const HingeArgs a) {
-    __shared__ float sc[2][32];
-    __shared__ float accx[2][16][64];  // the kh = 1 waves' partial accumulators
-    __shared__ int last;
-    __shared__ unsigned long long total;
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    const int side = w & 1;  // 0: positives, 1: negatives
-    const int kh = w >> 1;   // k half: s in [8 kh, 8 kh + 8), k = 16 h + s
-    const int i = lane & 31;
-    const int h = lane >> 5;
-    const int b0 = blockIdx.x * 32;
-    const int b = b0 + i;
-    const bool valid = b < a.n;
-    const DecTab& t = a.t;
-    // the V rows' column indices first (independent of everything else), then the pair's row
-    int c[16];
-    if (kh == 0) {  // (wave-uniform) the epilogue's V elements: pair (r&3) + 8(r>>2) + 4h, column i
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int bb = b0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            c[r] = a.cols[bb < a.n ? bb : a.n - 1];
-        }
-    }
-    // the pair's row: side-uniform branches, loads at a clamped (valid) index
-    const int bc = valid ? b : a.n - 1;
-    int ridx;
-    if (side == 0)
-        ridx = a.rows[bc];
-    else if (a.neg_given)
-        ridx = a.neg_given[bc];
-    else
-        ridx = unigram_draw(a.alias, a.range, a.seed, a.offset + (uint64_t)bc);
-    ridx = valid ? ridx : 0;
-    if (valid && side == 1 && a.neg_rows_out && h == 0 && kh == 0) a.neg_rows_out[b] = ridx;
-    const int k0 = 16 * h + 8 * kh;
-    // every load is unconditional (an invalid pair reads row 0 / the batch's last column index,
-    // selected away after: a conditional load compiles to a branch with its own wait), and the
-    // loads are issued in dependence order — G, U and l, then the V rows — before any
-    // arithmetic waits on them
-    float av[8], bv[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) bv[s] = t.G[(k0 + s) * 32 + i];
-    const float* u = t.row_table + (int64_t)ridx * t.ld_row + k0;
-    float4 u4[2], l4[2];
-#pragma unroll
-    for (int s4 = 0; s4 < 2; ++s4) u4[s4] = *reinterpret_cast<const float4*>(u + 4 * s4);
-    if constexpr (HL) {
-#pragma unroll
-        for (int s4 = 0; s4 < 2; ++s4) l4[s4] = *reinterpret_cast<const float4*>(t.l + k0 + 4 * s4);
-    }
-    float v[16], lj = 1.f;
-    if (kh == 0) {
-        if constexpr (HL) lj = t.l[i];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int bb = b0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            v[r] = t.col_table[(int64_t)(bb < a.n ? c[r] : 0) * t.ld_col + i];
-        }
-    }
-#pragma unroll
-    for (int s4 = 0; s4 < 2; ++s4) {
-        av[4 * s4] = u4[s4].x;
-        av[4 * s4 + 1] = u4[s4].y;
-        av[4 * s4 + 2] = u4[s4].z;
-        av[4 * s4 + 3] = u4[s4].w;
-        if constexpr (HL) {
-            av[4 * s4] *= l4[s4].x;
-            av[4 * s4 + 1] *= l4[s4].y;
-            av[4 * s4 + 2] *= l4[s4].z;
-            av[4 * s4 + 3] *= l4[s4].w;
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) av[s] = valid ? av[s] : 0.f;
-    f32x16 acc = {};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
-    if (kh == 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) accx[side][r][lane] = acc[r];
-    }
-    __syncthreads();
-    if (kh == 0) {
-        float part[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) part[r] = fmaf((acc[r] + accx[side][r][lane]) * lj, v[r], 0.f);
-        // reduce-scatter over the half's 32 lanes (score_tile's): lanes 2r, 2r+1 hold score r
-        const int b4 = (i >> 4) & 1, b3 = (i >> 3) & 1, b2 = (i >> 2) & 1, b1 = (i >> 1) & 1;
-        float v8[8], v4[4], v2[2];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            v8[j] = (b4 ? part[8 + j] : part[j]) + __shfl_xor(b4 ? part[j] : part[8 + j], 16);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = (b3 ? v8[4 + j] : v8[j]) + __shfl_xor(b3 ? v8[j] : v8[4 + j], 8);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) v2[j] = (b2 ? v4[2 + j] : v4[j]) + __shfl_xor(b2 ? v4[j] : v4[2 + j], 4);
-        float v1 = (b1 ? v2[1] : v2[0]) + __shfl_xor(b1 ? v2[0] : v2[1], 2);
-        v1 += __shfl_xor(v1, 1);
-        if ((i & 1) == 0) {
-            const int r = i >> 1;
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float val = (b0 + q < a.n) ? v1 : 0.f;
-            sc[side][q] = val;
-            if (b0 + q < a.n) (side == 0 ? a.pos : a.neg)[b0 + q] = val;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {  // relu(neg − (pos − margin)) over the block, optimizer.py:116-120
-        float term = 0.f;
-        if (lane < 32 && b0 + lane < a.n) term = fmaxf(sc[1][lane] - (sc[0][lane] - a.margin), 0.f);
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) term += __shfl_xor(term, m);
-        if (lane == 0) {  // the PACKED hand-off of decoder_hinge_kernel<true>
-            unsigned long long add = 1ull << 56;
-            if (term < 256.0f) {  // (false for NaN and inf too)
-                add += static_cast<unsigned long long>(static_cast<double>(term) * 4294967296.0 + 0.5);  // nearest
-            } else {
-                __hip_atomic_store(a.partial + blockIdx.x, term, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                add += 1ull << 48;
-            }
-            const unsigned long long old =
-                __hip_atomic_fetch_add(a.word, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = (old >> 56) == gridDim.x - 1 ? 1 : 0;
-            total = old + add;
-        }
-    }
-    __syncthreads();
-    if (!last || threadIdx.x != 0) return;
-    double sum = static_cast<double>(total & ((1ull << 48) - 1)) * (1.0 / 4294967296.0);
-    if ((total >> 48) & 0xFF) {  // partials outside the fixed-point range, in block order
-        for (int k = 0; k < (int)gridDim.x; ++k) {
-            const float pv = __hip_atomic_load(a.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (pv != 0.f) {
-                sum += static_cast<double>(pv);
-                __hip_atomic_store(a.partial + k, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-    a.loss[0] = static_cast<float>(sum);
-    __hip_atomic_store(a.word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Fixed-order block reduction (deterministic): thread t sums t, t+256, ... then a tree.
@@ -516,12 +345,6 @@ extern "C" int dg_unigram_sample_slots(const uint32_t* alias_table, int32_t rang
     return dg::launch_status();
 }
 
-// DG_DEC_TICKET=1: the ticket hand-off at any size (A/B and tests of both forms)
-static bool getenv_ticket() {
-    static const bool t = [] { const char* e = getenv("DG_DEC_TICKET"); return e && e[0] == '1'; }();
-    return t;
-}
-
 extern "C" int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, const float* col_table,
                                     int64_t ld_col, const int32_t* rows, const int32_t* cols,
                                     const int32_t* neg_rows, const uint32_t* alias_table,
@@ -555,14 +378,8 @@ extern "C" int dg_decoder_hinge_f32(const float* row_table, int64_t ld_row, cons
     a.range = range;
     a.n = n;
     a.margin = margin;
-    if (DG_DEC_SPLIT32 && d == 32 && a.t.vec4 && blocks <= 255 && !DG_DEC_ABL && !getenv_ticket()) {
-        if (l)
-            hipLaunchKernelGGL(decoder_hinge32_kernel<true>, dim3(blocks), dim3(256), 0,
-                               reinterpret_cast<hipStream_t>(stream), a);
-        else
-            hipLaunchKernelGGL(decoder_hinge32_kernel<false>, dim3(blocks), dim3(256), 0,
-                               reinterpret_cast<hipStream_t>(stream), a);
-    } else if (blocks <= 255 && !(DG_DEC_ABL & 1) && !getenv_ticket())
+    // ≤ 255 workgroups: one returning 64-bit atomic per block (PACKED); more: the sc1 ticket
+    if (blocks <= 255)
         hipLaunchKernelGGL(decoder_hinge_kernel<true>, dim3(blocks), dim3(128), 0,
                            reinterpret_cast<hipStream_t>(stream), a);
     else

@@ -32,21 +32,8 @@ typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-#ifndef DG_DEC_CS_THREADS
-#define DG_DEC_CS_THREADS 768  // column-shared paired kernel: threads per workgroup (one per CU)
-#endif
-#ifndef DG_DEC_CS16
-#define DG_DEC_CS16 1          // config 5's fused step on the 16x16x32 form (0: the 32x32x16 one)
-#endif
-#ifndef DG_DEC_CS16_THREADS
-#define DG_DEC_CS16_THREADS 768
-#endif
-#ifndef DG_DEC_CS16_PIN
-#define DG_DEC_CS16_PIN 1
-#endif
-#ifndef DG_DEC_CS16_TL
-#define DG_DEC_CS16_TL 1       // epilogue: D_k folded into T once for both rows (0: per row; 205.8-206.1 -> 203.5-204.2 us)
-#endif
+constexpr int kCsThreads = 768;    // column-shared paired kernel: threads per workgroup (one per CU)
+constexpr int kCs16Threads = 768;  // config 5's 16x16x32 kernel (704: 208.6 vs 205.6 us)
 
 struct Bf16DecArgs {
     const uint16_t* row_table;
@@ -557,9 +544,7 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
                     acc[1][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa), bq[1][s],
                                                                         acc[1][h], 0, 0, 0);
                     wa = xa;
-#if DG_DEC_CS16_PIN
                     __builtin_amdgcn_sched_barrier(0);  // one A fragment ahead, no deeper
-#endif
                 }
                 // (keeps the second tile's A reads from being hoisted above the first tile's
                 // MFMAs: 64 more live VGPRs, spilled at 3 waves per SIMD)
@@ -579,19 +564,12 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
 #pragma unroll
                     for (int r2 = 0; r2 < 2; ++r2) {  // elements 4h + 2r2, 4h + 2r2 + 1: word 2h + r2
                         const float l0 = bf_lo(lw[2 * h + r2]), l1 = bf_hi(lw[2 * h + r2]);
-#if DG_DEC_CS16_TL
                         // (D_k∘T)[i] once for both rows: 2 products instead of 4
                         const float t0 = acc[b][h][2 * r2] * l0, t1 = acc[b][h][2 * r2 + 1] * l1;
                         pp[b] = fmaf(t0, bf_lo(pw[2 * h + r2]), pp[b]);
                         pp[b] = fmaf(t1, bf_hi(pw[2 * h + r2]), pp[b]);
                         pn[b] = fmaf(t0, bf_lo(nw[2 * h + r2]), pn[b]);
                         pn[b] = fmaf(t1, bf_hi(nw[2 * h + r2]), pn[b]);
-#else
-                        pp[b] = fmaf(acc[b][h][2 * r2], bf_lo(pw[2 * h + r2]) * l0, pp[b]);
-                        pp[b] = fmaf(acc[b][h][2 * r2 + 1], bf_hi(pw[2 * h + r2]) * l1, pp[b]);
-                        pn[b] = fmaf(acc[b][h][2 * r2], bf_lo(nw[2 * h + r2]) * l0, pn[b]);
-                        pn[b] = fmaf(acc[b][h][2 * r2 + 1], bf_hi(nw[2 * h + r2]) * l1, pn[b]);
-#endif
                     }
                 }
                 // Each half's sums pass through an opaque copy, so the compiler cannot pair
@@ -683,11 +661,16 @@ extern "C" int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, 
     return dg::launch_status();
 }
 
-extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
-                                            int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
+// The 16x16x32 kernel's row loads are buffer loads with 32-bit byte offsets.
+static bool fits_32bit_offsets(int64_t n_rows, int64_t ld) { return n_rows * ld * 2 < 0x7fffffffLL; }
+
+extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, int64_t n_row_table,
+                                            const uint16_t* col_table, int64_t ld_col, int64_t n_col_table,
+                                            const int32_t* row_idx, const int32_t* col_idx,
                                             const int32_t* rel_idx, int32_t n_half, const uint16_t* G,
                                             const uint16_t* l_table, int32_t d, float* out, void* stream) {
     if (n_half < 0 || !row_table || !col_table || !row_idx || !col_idx || !G || !out) return DG_EINVAL;
+    if (n_row_table < 1 || n_col_table < 1) return DG_EINVAL;
     if (d != 64 && d != 128 && d != 256) return DG_EINVAL;
     if (ld_row < d || ld_col < d || (ld_row & 7) || (ld_col & 7)) return DG_EALIGN;
     if (!dg::aligned16(row_table) || !dg::aligned16(col_table) || (l_table && !dg::aligned16(l_table)))
@@ -698,10 +681,10 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
     const int lds = d * d * 2;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (!dg::aligned16(G)) return DG_EALIGN;  // R rows are staged into LDS in 16-byte pieces
-    if (DG_DEC_CS16 && d == 256) {
+    if (d == 256 && fits_32bit_offsets(n_row_table, ld_row) && fits_32bit_offsets(n_col_table, ld_col)) {
         // the 16x16x32 form (decoder_bf16_cs16_kernel, FUSED = false): bit-identical scores to
         // dg_slot_score_hinge_bf16's; 32-bit byte offsets into the tables are required
-        constexpr int kT16 = DG_DEC_CS16_THREADS;
+        constexpr int kT16 = kCs16Threads;
         const int lds16 = d * d * 2 + (kT16 / 64) * d * 2;
         int blocks16 = (n_tiles + kT16 / 64 - 1) / (kT16 / 64);
         if (blocks16 > 256) blocks16 = 256;
@@ -710,7 +693,7 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
         hipLaunchKernelGGL((decoder_bf16_cs16_kernel<kT16, false>), dim3(blocks16), dim3(kT16), lds16, st, a);
         return dg::launch_status();
     }
-    constexpr int kThreads = DG_DEC_CS_THREADS;
+    constexpr int kThreads = kCsThreads;
     static std::atomic<uint64_t> configured_l{0}, configured_nl{0};
     dg::lds_optin(reinterpret_cast<const void*>(&decoder_bf16_colshared_kernel<256, true, kThreads, false>),
                   160 * 1024, configured_l);
@@ -733,14 +716,16 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
     return dg::launch_status();
 }
 
-extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
-                                        int64_t ld_col, const int32_t* pos_rows, const int32_t* pos_cols,
+extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_row, int64_t n_row_table,
+                                        const uint16_t* col_table, int64_t ld_col, int64_t n_col_table,
+                                        const int32_t* pos_rows, const int32_t* pos_cols,
                                         const uint32_t* alias_table, int32_t range, int64_t alias_stride,
                                         int32_t slot0, int32_t n_slots, int32_t batch, uint64_t seed,
                                         const uint16_t* G, const uint16_t* l_table, int32_t d, float margin,
                                         float* out, int32_t* neg_rows, float* loss, void* workspace,
                                         void* stream) {
     if (n_slots < 0 || batch < 1 || slot0 < 0 || range < 1 || alias_stride < 0) return DG_EINVAL;
+    if (n_row_table < range || n_col_table < 1) return DG_EINVAL;
     if (!row_table || !col_table || !pos_rows || !pos_cols || !alias_table || !G || !l_table || !out ||
         !neg_rows || !loss || !workspace)
         return DG_EINVAL;
@@ -765,15 +750,14 @@ extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_ro
     a.slot0 = slot0;
     a.batch = batch;
     a.margin = margin;
-    constexpr int kThreads = DG_DEC_CS_THREADS;
+    constexpr int kThreads = kCsThreads;
     const int n_tiles = (nh + 31) / 32;
     int blocks = (n_tiles + kThreads / 64 - 1) / (kThreads / 64);
     if (blocks > DG_HINGE_WS_BLOCKS) blocks = DG_HINGE_WS_BLOCKS;  // persistent; the workspace's partials
     // the 16x16x32 form: every 32-pair tile inside one slot (one D_k), tables within 32-bit
     // byte offsets (its row loads are buffer loads)
-    if (DG_DEC_CS16 && batch % 32 == 0 && (int64_t)range * ld_row * 2 < 0x7fffffffLL &&
-        (int64_t)range * ld_col * 2 < 0x7fffffffLL) {
-        constexpr int kT16 = DG_DEC_CS16_THREADS;
+    if (batch % 32 == 0 && fits_32bit_offsets(n_row_table, ld_row) && fits_32bit_offsets(n_col_table, ld_col)) {
+        constexpr int kT16 = kCs16Threads;
         const int lds16 = d * d * 2 + (kT16 / 64) * d * 2;  // R + a D_k row per wave
         int blocks16 = (n_tiles + kT16 / 64 - 1) / (kT16 / 64);
         if (blocks16 > DG_HINGE_WS_BLOCKS) blocks16 = DG_HINGE_WS_BLOCKS;

@@ -627,7 +627,7 @@ extern "C" int dg_gemm_f32(const dg_gemm_desc* descs, int32_t n_desc, void* stre
                (g.c_bs & 3) == 0 && dg::aligned16(g.c) && g.b_sn == 1 && (g.b_sk & 3) == 0 && (g.b_bs & 3) == 0 &&
                dg::aligned16(g.b);
     }
-    static const int proj_blocks = [] { const char* e = getenv("DG_PROJ_BLOCKS"); return e ? atoi(e) : 512; }();
+    constexpr int proj_blocks = 512;  // grid target (sweep 256-4,096 at config P: 512 fastest)
     if (proj) {
         // waves per block: the m tiles split evenly over ceil(tiles/8) blocks (>= 4 waves)
         int tiles_m_max = 0;

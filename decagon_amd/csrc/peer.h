@@ -16,8 +16,9 @@
 //            (hipDeviceMallocUncached), so polls never hit a stale cache line;
 //   wait     the same wave polls this rank's own block, words [slot][0..world) (lane s: source
 //            s), relaxed at system scope with s_sleep, until every peer's epoch arrived — BOUNDED: after
-//            timeout ticks of s_memrealtime (100 MHz) it sets the error word and gives up, and
-//            a set error word skips every later wait (fail fast, the host raises);
+//            timeout ticks of s_memrealtime (100 MHz) it sets the error word and gives up; a
+//            set error word poisons the exchange: later launches raise no flag and wait for
+//            none (fail fast), so the peers' waits time out as well and every host raises;
 //   consume  the kernels that read the gathered rows start after this kernel ends: the
 //            dispatch's acquire makes the bytes the peers wrote into this GPU's memory visible
 //            as it does for any earlier kernel's stores.
@@ -128,6 +129,10 @@ __device__ __forceinline__ void peer_arrive(const PeerK& P) {
     }
     epoch = __shfl(epoch, 0);
     failed = __shfl(failed, 0);
+    // A set error word poisons the exchange: this rank raises no flag and waits for none, so
+    // every peer's next wait times out too and every rank's host raises at its next check
+    // (PeerExchange.check, Session.run) instead of computing on rows that never arrived.
+    if (failed) return;
     // lane p < world: rank p's flag block (a select chain over the kernel arguments: no scratch)
     uint32_t* fp = nullptr;
 #pragma unroll
@@ -136,7 +141,7 @@ __device__ __forceinline__ void peer_arrive(const PeerK& P) {
     if (lane < P.world)
         __hip_atomic_store(fp + P.slot * DG_PEER_MAX + (P.loopback ? lane : P.rank), epoch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-    if (!failed) peer_poll(P, epoch, lane);  // (a set error word: fail fast)
+    peer_poll(P, epoch, lane);
     if (lane == 0) __hip_atomic_store(ep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

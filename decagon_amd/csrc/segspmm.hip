@@ -28,39 +28,19 @@
 #include "common.h"
 #include "peer.h"
 
-// gathers in flight per lane (U: plain sums, UP: the reassociated form, whose W slice holds
-// 32 VGPRs), per kernel — measured at config S (rows 4-81 nonzeros per relation), the
-// occupancy they leave matters more than the round trips they save:
+// gathers in flight per lane (U: plain sums, UP: the reassociated form), per kernel —
+// measured at config S (rows 4-81 nonzeros per relation), the occupancy they leave matters
+// more than the round trips they save:
 //   spmm_seg (N = 8 rank share, ≈ 650 workgroups): U 8 / UP 4 → 27.1 µs a step (U 4 / UP 2 27.3,
-//   UP 8 28.4, U 16 32.7);  fused seg (N = 1, 900 workgroups): U 4 / UP 2 → 20.4 µs (8 / 4 21.4)
-#ifndef DG_SEG_U
-#define DG_SEG_U 8
-#endif
-#ifndef DG_SEG_UP
-#define DG_SEG_UP 4
-#endif
-#ifndef DG_FSEG_U
-#define DG_FSEG_U 4
-#endif
-#ifndef DG_FSEG_UP
-#define DG_FSEG_UP 2
-#endif
-#ifndef DG_FSEG_UP_WL
-#define DG_FSEG_UP_WL 4  // the reassociated fused form with W in LDS (no 32-VGPR W slice per wave)
-#endif
-#ifndef DG_FSEG_WL
-#define DG_FSEG_WL 2     // the fused layer 2's W slabs: 0 in registers through the gathers (round 3),
-#endif                   // 1 staged in LDS per workgroup, 2 read after the gathers (config S layer 2
-                         // 7.35 / 9.45 / 6.87 us, step 19.66 / 21.88 / 19.36 us at 200 steps)
-#ifndef DG_SEG_UP_WL
-#define DG_SEG_UP_WL 4   // the reassociated seg form with the W slice read after the gathers
-#endif
-#ifndef DG_SEG_WL
-#define DG_SEG_WL 2      // spmm_seg_kernel's W slice: 0 in registers through the gathers, 2 read after
-#endif                   // them (config S's N = 8 rank share 31.0 -> 30.6 us, loopback exchange)
-#ifndef DG_SEG_MIN_NW
-#define DG_SEG_MIN_NW 1  // waves per workgroup, at least (else: the launch's largest chunk)
-#endif
+//   UP 8 28.4, U 16 32.7);  fused seg (N = 1, 900 workgroups): U 4 → 20.4 µs (8: 21.4)
+constexpr int kSegU = 8;     // spmm_seg, plain sums
+constexpr int kSegUP = 4;    // spmm_seg, reassociated (W slice read after the gathers)
+constexpr int kFsegU = 4;    // fused seg, plain sums
+constexpr int kFsegUP = 4;   // fused seg, reassociated (W slabs read after the gathers: layer 2 at
+                             // config S 6.87 us, against 7.35 with the slice held in 32 VGPRs through
+                             // the gathers and 9.45 staged in LDS per workgroup; step 19.36 / 19.66 /
+                             // 21.88 us at 200 steps)
+constexpr int kSegMinNW = 1; // waves per workgroup, at least (else: the launch's largest chunk)
 
 namespace {
 
@@ -261,76 +241,32 @@ __device__ __forceinline__ float4 seg_gather_shfl(const int32_t* __restrict__ vc
     return acc;
 }
 
-// One wave's share: relation t (local relation k) of chunk c in row r — its segment's sum
-// y = Σ val·X[vcol] and, with PROJ, z = y·W[slab(k)] (ybuf: the wave's 16-float4 LDS slot).
-// Returns the wave's row in the output layout (lanes < DOUT4 hold float4 lane of it).
-template <int LP, bool PROJ, int U, int UP>
-__device__ __forceinline__ float4 seg_wave(const SegGroupK& g, int c, int r, int t, int k, float4* ybuf) {
-    const int lane = threadIdx.x & 63;
+// One wave's share: relation t of chunk c in row r — its segment's sum y = Σ val·X[vcol]
+// (lanes hold float4 lane % LP of the row).
+template <int LP, int U>
+__device__ __forceinline__ float4 seg_wave(const SegGroupK& g, int c, int r, int t) {
     const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
     const int beg = g.seg[si];
     const int end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
-    if constexpr (PROJ) {
-        const int s = g.slab ? g.slab[k] : k;
-        // this lane's W_s slice: rows 8(l>>3) .. +8, columns 4(l&7) .. +4
-        const float* W = g.w + (int64_t)s * (64 * 32) + (lane >> 3) * (8 * 32) + (lane & 7) * 4;
-        float4 wv[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wv[i] = *reinterpret_cast<const float4*>(W + i * 32);
-        // H is shared by the relations: vcol = s·n_cols + col addresses row col
-        const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;
-        const float4 y = seg_gather_shfl<16, UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
-        if (lane < 16) ybuf[lane] = y;
-        __builtin_amdgcn_wave_barrier();
-        const int ms = lane >> 3;
-        const float4 ya = ybuf[2 * ms];
-        const float4 yb = ybuf[2 * ms + 1];
-        float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        dg::fma4(z, ya.x, wv[0]);
-        dg::fma4(z, ya.y, wv[1]);
-        dg::fma4(z, ya.z, wv[2]);
-        dg::fma4(z, ya.w, wv[3]);
-        dg::fma4(z, yb.x, wv[4]);
-        dg::fma4(z, yb.y, wv[5]);
-        dg::fma4(z, yb.z, wv[6]);
-        dg::fma4(z, yb.w, wv[7]);
-        dg::add4(z, dg::shfl_xor4(z, 8));
-        dg::add4(z, dg::shfl_xor4(z, 16));
-        dg::add4(z, dg::shfl_xor4(z, 32));
-        return z;
-    } else {
-        return seg_gather<LP, U>(g.vcol, g.val, g.x, g.x_ld, beg, end);
-    }
+    return seg_gather<LP, U>(g.vcol, g.val, g.x, g.x_ld, beg, end);
 }
 
-// The reassociated wave with its W_k slab in LDS (wl: 64 x 32 floats as 512 float4, row-major,
-// staged once per workgroup for every row slot that uses relation k) instead of 32 VGPRs of
-// W slice per wave held across the gathers: the registers go to gathers in flight (UP).
-// beg / end: the segment, loaded by the caller before the staging barrier.
-// wl == nullptr: the slab is read from global memory after the gathers (one more L2 round trip
-// at the end instead of 32 VGPRs held through them).
-// WL 0: the W slice loaded from global memory before the gathers (held through them), as
-// seg_wave; WL 1: from the workgroup's LDS copy after them; WL 2: from global after them.
-template <int UP, int WL>
-__device__ __forceinline__ float4 seg_wave_wl(const SegGroupK& g, int k, int beg, int end, float4* ybuf,
-                                              const float4* wl) {
+// The reassociated wave (layer 2, d_in 64 -> d_out 32): y = Â_k[r]·H, then z = y·W_k with
+// this lane's W_k slice (rows 8(l>>3) .. +8, output float4 l & 7) read from global memory after
+// the gathers — one more L2 round trip at the end instead of 32 VGPRs held through them, which
+// buys gathers in flight (config S layer 2: 6.87 us, against 7.35 with the slice held and 9.45
+// with the workgroup's slabs staged in LDS).  beg / end: the segment.
+template <int UP>
+__device__ __forceinline__ float4 seg_wave_proj(const SegGroupK& g, int k, int beg, int end, float4* ybuf) {
     const int lane = threadIdx.x & 63;
     const int s = g.slab ? g.slab[k] : k;
     const int ms = lane >> 3;
-    // rows 8·ms .. +8 of the slab, output float4 lane & 7
-    const float4* w = (WL == 1 ? wl : reinterpret_cast<const float4*>(g.w + (int64_t)s * (64 * 32))) + (8 * ms) * 8 +
-                      (lane & 7);
+    const float4* w = reinterpret_cast<const float4*>(g.w + (int64_t)s * (64 * 32)) + (8 * ms) * 8 + (lane & 7);
     float4 wv[8];
-    if constexpr (WL == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wv[i] = w[8 * i];
-    }
     const float* xb = g.x - (int64_t)s * g.n_cols * g.x_ld;  // vcol = s·n_cols + col addresses row col
     const float4 y = seg_gather_shfl<16, UP>(g.vcol, g.val, xb, g.x_ld, beg, end);
-    if constexpr (WL != 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) wv[i] = w[8 * i];
-    }
+    for (int i = 0; i < 8; ++i) wv[i] = w[8 * i];
     if (lane < 16) ybuf[lane] = y;
     __builtin_amdgcn_wave_barrier();
     const float4 ya = ybuf[2 * ms];
@@ -411,13 +347,12 @@ __device__ __forceinline__ void seg_finish_row(const SegArgs& a, const FinTarget
 // PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.  a.nw waves per
 // workgroup (the launch's largest chunk, so a chunk-6 group wastes no wave slot; rows per
 // workgroup nw / chunk), at most NW.
-// WL (PROJ only): seg_wave_wl's W-slice modes (0: seg_wave's, in registers through the gathers).
 // FIN (dg_spmm_seg_finish_f32): the partials are stored write-through and drained, each row of
 // the workgroup counts one arrival, and the workgroup that brings a row's count to the target's
 // expect finishes that row (seg_finish_row) and resets its counter — the seg + epilogue pair in
 // one launch.  PEER (with FIN): the finished rows of pushing targets also go to every peer and
 // the launch ends with the exchange.
-template <int LP, bool PROJ, int NW, int WL = 0, bool FIN = false, bool PEER = false>
+template <int LP, bool PROJ, int NW, bool FIN = false, bool PEER = false>
 __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     static_assert(FIN || !PEER, "the peer form finishes its rows");
     constexpr int DOUT4 = PROJ ? 8 : LP;  // float4s of an output row
@@ -425,11 +360,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     __shared__ float4 zbuf[NW][DOUT4];
     __shared__ int fin[NW];
     const int lane = threadIdx.x & 63;
-#ifdef DG_SEG_VECTOR_BOUNDS
-    const int wave = threadIdx.x >> 6;
-#else
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (segment bounds: scalar loads)
-#endif
     int gi = 0;
 #pragma unroll 1
     while (gi + 1 < a.n_groups && (int)blockIdx.x >= a.g[gi + 1].block_begin) ++gi;
@@ -449,7 +380,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     const bool row_ok = wg_live && slot < g.rpb && r < g.n_rows;
     const int k = c * g.chunk + t;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (PROJ && WL != 0) {
+    if constexpr (PROJ) {
         const bool live = row_ok && k < g.n_rels;
         int beg = 0, end = 0;
         if (live) {
@@ -457,9 +388,9 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
             beg = g.seg[si];
             end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
         }
-        if (live) res = seg_wave_wl<DG_SEG_UP_WL, 2>(g, k, beg, end, ybuf[wave], nullptr);
+        if (live) res = seg_wave_proj<kSegUP>(g, k, beg, end, ybuf[wave]);
     } else if (row_ok && k < g.n_rels) {
-        res = seg_wave<LP, PROJ, DG_SEG_U, DG_SEG_UP>(g, c, r, t, k, ybuf[wave]);  // wave-uniform
+        res = seg_wave<LP, kSegU>(g, c, r, t);  // wave-uniform
     }
     if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
     __syncthreads();
@@ -523,23 +454,14 @@ struct FsArgs {
     dg::PeerK P;  // PEER: every finished row also goes to every peer's copy (peer.h)
 };
 
-#ifdef DG_FS_RPB1
-constexpr int kFsMaxRpb = 1;  // A/B: one row per workgroup
-#else
-constexpr int kFsMaxRpb = 4;
-#endif
+constexpr int kFsMaxRpb = 4;  // rows per workgroup, at most (1: no change at config S)
 
-// WL (PROJ only): the layer-2 W slab of each wave's relation not held in registers through the
-// gathers.  WL 1: every relation's slab staged in (dynamic) LDS once per workgroup by row slot
-// 0's waves — the segment bounds are loaded first, so the staging barrier costs no extra round
-// trip; WL 2: each wave reads its slab from global memory after its gathers.
-template <int LP, bool PROJ, int NW, bool PEER, int WL = 0>
+template <int LP, bool PROJ, int NW, bool PEER>
 __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
     __shared__ float4 nbuf[kFsMaxRpb][DG_MAX_GROUPS][DOUT4];
-    extern __shared__ __attribute__((aligned(16))) float4 wdyn[];  // WL 1: [waves][512]
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int ti = 0;
@@ -557,38 +479,24 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 #pragma unroll 1
     while (gl < T.g_count && wi >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (PROJ && WL != 0) {
+    if constexpr (PROJ) {
         const bool live = slot < T.rpb && r < T.n_rows && gl < T.g_count;
         const int gi = T.g_begin + (gl < T.g_count ? gl : 0);
         const int k = wi - base;
         int beg = 0, end = 0;
-        if (live) {  // the segment bounds, issued before the staging loads
+        if (live) {
             const SegGroupK& g = a.g[gi];
             const int c = k / g.chunk, t = k - c * g.chunk;
             const int64_t si = ((int64_t)c * g.n_rows + r) * g.chunk + t;
             beg = g.seg[si];
             end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
         }
-        if constexpr (WL == 1) {
-            if (slot == 0 && wi < T.waves) {  // row slot 0's waves stage their relations' W slabs
-                const SegGroupK& g = a.g[gi];
-                const int sl = g.slab ? g.slab[k] : k;
-                const float4* W = reinterpret_cast<const float4*>(g.w + (int64_t)sl * (64 * 32));
-                float4 tmp[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) tmp[i] = W[lane + 64 * i];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) wdyn[wi * 512 + lane + 64 * i] = tmp[i];
-            }
-            __syncthreads();
-        }
-        if (live)
-            res = seg_wave_wl<DG_FSEG_UP_WL, WL>(a.g[gi], k, beg, end, ybuf[wave], WL == 1 ? wdyn + wi * 512 : nullptr);
+        if (live) res = seg_wave_proj<kFsegUP>(a.g[gi], k, beg, end, ybuf[wave]);
     } else if (slot < T.rpb && r < T.n_rows && gl < T.g_count) {
         const SegGroupK& g = a.g[T.g_begin + gl];
         const int k = wi - base;
         const int c = k / g.chunk;
-        res = seg_wave<LP, PROJ, DG_FSEG_U, DG_FSEG_UP>(g, c, r, k - c * g.chunk, k, ybuf[wave]);
+        res = seg_wave<LP, kFsegU>(g, c, r, k - c * g.chunk);
     }
     if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
@@ -672,24 +580,18 @@ int seg_shape(int32_t d_in, int32_t d_out, bool& proj) {
 namespace {
 // The launch dispatch of both kernels: runtime switches onto the instantiated template forms.
 template <int NW, bool FIN = false, bool PEER = false>
-void launch_seg(bool proj, int d_in, int wl, dim3 grid, dim3 block, hipStream_t st, const SegArgs& a) {
-    if (proj && wl != 0)
-        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW, 2, FIN, PEER>), grid, block, 0, st, a);
-    else if (proj)
-        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW, 0, FIN, PEER>), grid, block, 0, st, a);
+void launch_seg(bool proj, int d_in, dim3 grid, dim3 block, hipStream_t st, const SegArgs& a) {
+    if (proj)
+        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW, FIN, PEER>), grid, block, 0, st, a);
     else if (d_in == 64)
-        hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW, 0, FIN, PEER>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW, FIN, PEER>), grid, block, 0, st, a);
     else
-        hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW, 0, FIN, PEER>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW, FIN, PEER>), grid, block, 0, st, a);
 }
 
 template <int NW, bool PEER>
-void launch_fs(bool proj, int d_in, int wl, size_t lds, dim3 grid, dim3 block, hipStream_t st, const FsArgs& a) {
-    if (proj && wl == 1)
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER, 1>), grid, block, lds, st, a);
-    else if (proj && wl == 2)
-        hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER, 2>), grid, block, 0, st, a);
-    else if (proj)
+void launch_fs(bool proj, int d_in, dim3 grid, dim3 block, hipStream_t st, const FsArgs& a) {
+    if (proj)
         hipLaunchKernelGGL((gcn_fused_seg_kernel<16, true, NW, PEER>), grid, block, 0, st, a);
     else if (d_in == 64)
         hipLaunchKernelGGL((gcn_fused_seg_kernel<16, false, NW, PEER>), grid, block, 0, st, a);
@@ -750,7 +652,7 @@ int seg_launch(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32
     }
     int64_t blocks = 0;
     int ng = 0;
-    int nw = DG_SEG_MIN_NW;
+    int nw = kSegMinNW;
     for (int i = 0; i < n_groups; ++i)
         if (groups[i].chunk > nw && groups[i].n_rows > 0 && groups[i].n_rels > 0) nw = groups[i].chunk;
     if (nw > 16) return DG_EINVAL;
@@ -795,25 +697,26 @@ int seg_launch(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32
         args.g[0] = SegGroupK{};
         args.g[0].chunk = 1;
         args.g[0].rpb = 1;
+        args.g[0].row_blocks = 1;  // (no items: every workgroup is dead; no division by zero)
         args.g[0].n_blocks = 8;
     }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);  // (launch bounds: 8 or 16 waves)
     if (!fin) {
         if (nw <= 8)
-            launch_seg<8>(proj, d_in, DG_SEG_WL, grid, block, st, args);
+            launch_seg<8>(proj, d_in, grid, block, st, args);
         else
-            launch_seg<16>(proj, d_in, DG_SEG_WL, grid, block, st, args);
+            launch_seg<16>(proj, d_in, grid, block, st, args);
     } else if (!xchg) {
         if (nw <= 8)
-            launch_seg<8, true, false>(proj, d_in, DG_SEG_WL, grid, block, st, args);
+            launch_seg<8, true, false>(proj, d_in, grid, block, st, args);
         else
-            launch_seg<16, true, false>(proj, d_in, DG_SEG_WL, grid, block, st, args);
+            launch_seg<16, true, false>(proj, d_in, grid, block, st, args);
     } else {
         if (nw <= 8)
-            launch_seg<8, true, true>(proj, d_in, DG_SEG_WL, grid, block, st, args);
+            launch_seg<8, true, true>(proj, d_in, grid, block, st, args);
         else
-            launch_seg<16, true, true>(proj, d_in, DG_SEG_WL, grid, block, st, args);
+            launch_seg<16, true, true>(proj, d_in, grid, block, st, args);
     }
     return dg::launch_status();
 }
@@ -875,19 +778,15 @@ int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fuse
     if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);
-    // WL 1: LDS for the widest target's slabs (8 KB a relation), at most 64 KB (8 relations a row;
-    // wider rows — config S's N = 2 form — read the slabs after the gathers instead, WL 2)
-    const int wl = !proj ? 0 : (DG_FSEG_WL == 1 && nw > 8 ? 2 : DG_FSEG_WL);
-    const size_t wl_lds = wl == 1 ? (size_t)nw * 512 * 16 : 0;
     if (xchg) {
         if (nw <= 8)
-            launch_fs<8, true>(proj, d_in, wl, wl_lds, grid, block, st, a);
+            launch_fs<8, true>(proj, d_in, grid, block, st, a);
         else
-            launch_fs<16, true>(proj, d_in, wl, wl_lds, grid, block, st, a);
+            launch_fs<16, true>(proj, d_in, grid, block, st, a);
     } else if (nw <= 8) {
-        launch_fs<8, false>(proj, d_in, wl, wl_lds, grid, block, st, a);
+        launch_fs<8, false>(proj, d_in, grid, block, st, a);
     } else {
-        launch_fs<16, false>(proj, d_in, wl, wl_lds, grid, block, st, a);
+        launch_fs<16, false>(proj, d_in, grid, block, st, a);
     }
     return dg::launch_status();
 }

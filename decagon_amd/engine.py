@@ -906,6 +906,8 @@ class ForwardPlan:
         self._layer2.run()
 
     def run(self) -> None:
+        if self.peer is not None:
+            self.peer.ensure_ok()  # a timed-out exchange found by an earlier check poisons the plan
         self.run_layer1()
         self.run_layer2()
 

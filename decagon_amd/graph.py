@@ -246,6 +246,12 @@ class Session:
 
         out = ev(fetches)
         torch.cuda.current_stream().synchronize()
+        # a sharded plan's peer exchange: a timed-out wait raises here, at this run's
+        # synchronisation, not silently in a later step (PeerExchange.check)
+        for v in list(ctx.cache.values()):
+            peer = getattr(v, "peer", None)
+            if peer is not None:
+                peer.check()
 
         def conv(v):
             if isinstance(v, dict):

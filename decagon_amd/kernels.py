@@ -908,11 +908,17 @@ def decoder_score_bf16(row_table: torch.Tensor, col_table: torch.Tensor, rows: t
         raise ValueError("tables must have d contiguous columns")
     if out is None:
         out = torch.empty(n, device=rows.device, dtype=torch.float32)
-    name = "dg_decoder_score_bf16_paired" if paired else "dg_decoder_score_bf16"
+    if paired:
+        name = "dg_decoder_score_bf16_paired"
+        tabs = (row_table.data_ptr(), row_table.stride(0), row_table.shape[0], col_table.data_ptr(),
+                col_table.stride(0), col_table.shape[0])
+    else:
+        name = "dg_decoder_score_bf16"
+        tabs = (row_table.data_ptr(), row_table.stride(0), col_table.data_ptr(), col_table.stride(0))
     check(getattr(_lib.load(), name)(
-        row_table.data_ptr(), row_table.stride(0), col_table.data_ptr(), col_table.stride(0), rows.data_ptr(),
-        cols.data_ptr(), rel.data_ptr() if rel is not None else None, n // 2 if paired else n, G.data_ptr(),
-        l_table.data_ptr() if l_table is not None else None, d, out.data_ptr(), _stream_ptr(stream)), name)
+        *tabs, rows.data_ptr(), cols.data_ptr(), rel.data_ptr() if rel is not None else None,
+        n // 2 if paired else n, G.data_ptr(), l_table.data_ptr() if l_table is not None else None, d,
+        out.data_ptr(), _stream_ptr(stream)), name)
     return out
 
 
@@ -1032,7 +1038,8 @@ def slot_score_hinge_bf16(E_row: torch.Tensor, E_col: torch.Tensor, pos_rows: to
     if workspace.numel() * workspace.element_size() < _lib.DG_HINGE_WS_BYTES or not workspace.is_cuda:
         raise ValueError("hinge workspace too small")
     check(_lib.load().dg_slot_score_hinge_bf16(
-        E_row.data_ptr(), E_row.stride(0), E_col.data_ptr(), E_col.stride(0), pos_rows.data_ptr(), pos_cols.data_ptr(),
+        E_row.data_ptr(), E_row.stride(0), E_row.shape[0], E_col.data_ptr(), E_col.stride(0), E_col.shape[0],
+        pos_rows.data_ptr(), pos_cols.data_ptr(),
         table.data_ptr(), rng, stride, slot0, n_slots, batch, seed & (2**64 - 1), G.data_ptr(), D.data_ptr(), d,
         float(margin), out.data_ptr(), neg_rows.data_ptr(), loss.data_ptr(), workspace.data_ptr(),
         _stream_ptr(stream)), "dg_slot_score_hinge_bf16")

@@ -119,6 +119,7 @@ class PeerExchange:
         if any(d % 16 for d in self.delta):
             raise RuntimeError("peer exchange: a peer region is not 16-byte aligned")
         self._descs = {}
+        self.failed = 0  # the error word last read by check() (nonzero: the exchange is poisoned)
 
     # ---- IPC ----
     def _handle(self, ptr: int) -> Tuple[bytes, int]:
@@ -183,10 +184,21 @@ class PeerExchange:
         return int(self.state[_lib.DG_PEER_ERROR_WORD].item())
 
     def check(self) -> None:
+        """Raise if any wait so far timed out (synchronises the device).  A timed-out wait
+        poisons the exchange on the device (csrc/peer.h: this rank then raises no flag and
+        waits for none, so every peer's next wait times out too); here it poisons the host
+        side: every later ensure_ok() — ForwardPlan.run's entry — raises as well."""
         e = self.error()
         if e:
+            self.failed = e
+        self.ensure_ok()
+
+    def ensure_ok(self) -> None:
+        """Raise if an earlier check() found a timed-out wait (no device access)."""
+        e = self.failed
+        if e:
             raise RuntimeError(f"peer exchange timed out: slot {(e >> 8) & 0xff}, waiting for rank {e & 0xff} "
-                               f"(error word {e:#x})")
+                               f"(error word {e:#x}); the exchange is poisoned, rebuild the plan")
 
     def close(self) -> None:
         """Unmap the peers' regions and free the flag block (after the last exchange)."""

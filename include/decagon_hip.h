@@ -521,9 +521,12 @@ int dg_decoder_score_bf16(const uint16_t* row_table, int64_t ld_row, const uint1
  * accumulation), then out[p] = sum_i u_p[i] l_k[i] T[i] and out[p + n_half] = sum_i u_n[i] l_k[i] T[i]
  * in fp32 — half the MFMA work of scoring the two pairs apart.  The bf16 operand rounding sits
  * on l_k∘v instead of u∘l_k, so the scores agree with dg_decoder_score_bf16 to bf16 operand
- * rounding.  G must be 16-byte aligned. */
-int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
-                                 int64_t ld_col, const int32_t* row_idx, const int32_t* col_idx,
+ * rounding.  G must be 16-byte aligned.  n_row_table / n_col_table: the tables' row counts
+ * (every index must be below them); tables whose byte offsets exceed 31 bits take the 64-bit
+ * addressed kernel (ABI 34). */
+int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, int64_t n_row_table,
+                                 const uint16_t* col_table, int64_t ld_col, int64_t n_col_table,
+                                 const int32_t* row_idx, const int32_t* col_idx,
                                  const int32_t* rel_idx, int32_t n_half, const uint16_t* G,
                                  const uint16_t* l_table, int32_t d, float* out, void* stream);
 
@@ -541,9 +544,11 @@ int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t ld_row, cons
  * workspace: DG_HINGE_WS_BYTES bytes, 16-byte aligned, first word zero before the first call
  * (left zero).  d == 256; G, tables and l_table 16-byte aligned.  Replaces optimizer.py:38-47
  * (fixed_unigram_candidate_sampler over the relation's degrees), :51-57 / :63-85 (batch_predict,
- * G = R, L = D_k: model.py:130-134) and :116-120 (_hinge_loss). */
-int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_row, const uint16_t* col_table,
-                             int64_t ld_col, const int32_t* pos_rows, const int32_t* pos_cols,
+ * G = R, L = D_k: model.py:130-134) and :116-120 (_hinge_loss).  n_row_table / n_col_table:
+ * the tables' row counts (range <= n_row_table), as for dg_decoder_score_bf16_paired. */
+int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_row, int64_t n_row_table,
+                             const uint16_t* col_table, int64_t ld_col, int64_t n_col_table,
+                             const int32_t* pos_rows, const int32_t* pos_cols,
                              const uint32_t* alias_table, int32_t range, int64_t alias_stride,
                              int32_t slot0, int32_t n_slots, int32_t batch, uint64_t seed,
                              const uint16_t* G, const uint16_t* l_table, int32_t d, float margin,

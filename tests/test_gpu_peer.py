@@ -17,7 +17,9 @@ the stores reach the peer's memory without crossing xGMI.  Checked:
   * the same for the scaled-down config P (proteins row-split; the drug sums still all-reduced);
   * the one-process loopback rehearsal (bench.py --simulate-world --exchange peer) equals the
     unsharded forward's rank block;
-  * a wait that cannot complete times out, sets the error word and later waits fail fast.
+  * a wait that cannot complete times out, sets the error word and later waits fail fast;
+    the exchange is then poisoned (no flag raised, no epoch advanced) and the host raises at
+    every later check and ForwardPlan.run.
 """
 import numpy as np
 import pytest
@@ -298,8 +300,47 @@ def test_peer_wait_times_out_and_fails_fast():
     err = ex.error()
     assert err == 0x10000 | (3 << 8) | 1, hex(err)
     assert 0.15 <= t1 - t0 <= 5.0, t1 - t0
+    assert int(ex.state[2 * 3 + 1]) == 1  # slot 3's epoch: one exchange (timed out) so far
     fn()
     torch.cuda.synchronize()
     assert time.perf_counter() - t1 < 0.15  # fails fast once the error word is set
     assert int(ex.state[_lib.DG_PEER_ERROR_WORD]) == err
+    assert int(ex.state[2 * 3 + 1]) == 1  # poisoned: no flag raised, no epoch advanced
+    with pytest.raises(RuntimeError, match="timed out"):
+        ex.check()
+    with pytest.raises(RuntimeError, match="poisoned"):
+        ex.ensure_ok()
     ex.close()
+
+
+def test_peer_timeout_poisons_the_plan():
+    """A sharded forward whose peer never arrives: the step's bounded wait times out, the
+    host's check at its synchronisation point raises, and every later run raises before it
+    launches anything (a failed wait must not fall through to later exchanges)."""
+    _need_gpu()
+    from decagon_amd.peer import PeerConfig
+    from decagon_amd.sharding import RelationShard, _no_op, _no_op_reduce
+
+    world, rank = 4, 1
+    g = _graph("S", world)
+    sh = RelationShard.weak_sets(g.edge_types, g.n_nodes, rank, world, _no_op_reduce, _no_op)
+    sh.peer = PeerConfig(mode="fused", loopback=True, timeout_s=0.2)
+    from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
+
+    dev = torch.device("cuda", 0)
+    w1, w2 = _weights(g)
+    dg = DeviceGraph(g.edge_types, sh.local_csr(g.csr()), dev, sh.local, row_block=sh.row_block,
+                     chunk=sh.chunks, segments=sh.seg_rows)
+    plan = ForwardPlan(dg, {0: None, 1: None},
+                       LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w1.items()}),
+                       LayerWeights({et: torch.from_numpy(w).to(dev) for et, w in w2.items()}), 64, 32, shard=sh)
+    plan.run()
+    plan.peer.check()  # loopback: every flag raised by this rank itself — completes
+    for d in plan.peer._descs.values():
+        d.loopback = 0  # now only this rank's own word is raised: the other ranks never arrive
+    plan.run()
+    with pytest.raises(RuntimeError, match="timed out"):
+        plan.peer.check()
+    with pytest.raises(RuntimeError, match="poisoned"):
+        plan.run()
+    plan.peer.close()
