@@ -117,7 +117,7 @@ class DgSegFinish(ctypes.Structure):
 
 
 class DgEpiGroup(ctypes.Structure):
-    _fields_ = [("partial", c_void_p), ("sum_out", c_void_p), ("n_chunks", c_int32), ("reserved", c_int32)]
+    _fields_ = [("partial", c_void_p), ("sum_out", c_void_p), ("n_chunks", c_int32), ("group_flags", c_int32)]
 
 
 class DgEpiTarget(ctypes.Structure):

@@ -31,6 +31,10 @@
 
 #include "common.h"
 
+#ifndef DG_PEER_FENCES
+#define DG_PEER_FENCES 1
+#endif
+
 namespace dg {
 
 struct PeerK {
@@ -93,7 +97,15 @@ __device__ __forceinline__ void peer_poll(const PeerK& P, uint32_t epoch, int la
     for (;;) {
         const uint32_t v = mine ? __hip_atomic_load(own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : epoch;
         const uint64_t who = __ballot((int32_t)(v - epoch) < 0);
-        if (!who) return;
+        if (!who) {
+            // system-scope acquire after the flags matched (buffer_inv sc0 sc1): this wave's
+            // later loads see what the peers released before raising them; the launches that
+            // read the gathered rows start after this one ends, behind their own acquire
+#if DG_PEER_FENCES
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
+            return;
+        }
         if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)P.timeout) {
             if (lane == 0)
                 __hip_atomic_store(P.state + 2 * DG_PEER_SLOTS,
@@ -133,6 +145,16 @@ __device__ __forceinline__ void peer_arrive(const PeerK& P) {
     // every peer's next wait times out too and every rank's host raises at its next check
     // (PeerExchange.check, Session.run) instead of computing on rows that never arrived.
     if (failed) return;
+    // System-scope release before the flags (AMDGPU memory model, gfx942/gfx950: a release at
+    // system scope is buffer_wbl2 sc0 sc1 + s_waitcnt vmcnt(0)): every byte this agent wrote
+    // before — the other workgroups' payload stores, each drained before its arrival add — is
+    // visible to the other agents before any flag store is.  The asm wait keeps the write-back
+    // ahead of the flag store even where the compiler drops the fence's own wait
+    // (MI355X_MICROARCH.md, "Compiler hazard").
+#if DG_PEER_FENCES
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     // lane p < world: rank p's flag block (a select chain over the kernel arguments: no scratch)
     uint32_t* fp = nullptr;
 #pragma unroll

@@ -316,8 +316,12 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, const int b) {
     if (live && gl < t.g_count) {
         const SpmmGroupK& g = a.g[t.g_begin + gl];
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!g.rowptr) {  // DG_GROUP_DENSE_ROWS: the sum is x[r] (the group's first wave loads it)
-            if (part == 0 && q * 4 < d) s = *reinterpret_cast<const float4*>(g.x + (int64_t)r * g.x_ld + q * 4);
+        if (!g.rowptr) {  // DG_GROUP_DENSE_ROWS: the sum is x[r], or Σ of its n_chunks slots in slot order
+            if (part == 0 && q * 4 < d) {
+                const float* xr = g.x + (int64_t)r * g.x_ld + q * 4;
+#pragma unroll 1
+                for (int c = 0; c < g.n_chunks; ++c) dg::add4(s, *reinterpret_cast<const float4*>(xr + c * g.chunk_x));
+            }
         } else {
             s = range_sum<LP>(g, g.x, g.rowptr[r], g.rowptr[r + 1], d, part, W);
         }
@@ -403,7 +407,7 @@ struct EpiGroupK {
     const float* partial;
     float* sum;  // the group's pre-normalisation sum, or nullptr
     int32_t n_chunks;
-    int32_t pad;
+    int32_t push;  // PEER launches: the sum also goes to every peer's copy (the peer all-reduce's slot)
 };
 
 struct EpiTargetK {
@@ -466,7 +470,11 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK&
         }
 #pragma unroll
         for (int m = LP; m < dg::kWave; m <<= 1) dg::add4(s, dg::shfl_xor4(s, m));
-        if (a.g[gi].sum && qok && cg == 0) *reinterpret_cast<float4*>(a.g[gi].sum + off) = s;
+        if (a.g[gi].sum && qok && cg == 0) {
+            *reinterpret_cast<float4*>(a.g[gi].sum + off) = s;
+            if constexpr (PEER)
+                if (a.g[gi].push) dg::peer_store4(a.P, a.g[gi].sum, (uint32_t)(plane * 4), (uint32_t)(off * 4), s);
+        }
         if (a.flags & DG_EPI_L2NORM) {
             // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); all-zero rows stay zero.
             float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
@@ -660,7 +668,8 @@ int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k, bo
     if (s.n_rows < 0 || s.n_chunks < 1 || s.x_rows < 0) return DG_EINVAL;
     if (s.flags & ~(DG_GROUP_SHARED_PATTERN | DG_GROUP_DROPOUT | DG_GROUP_DENSE_ROWS)) return DG_EINVAL;
     if (s.flags & DG_GROUP_DENSE_ROWS) {  // row r of the sum is x[r]: no adjacency
-        if (!allow_dense || s.flags != DG_GROUP_DENSE_ROWS || s.n_chunks != 1 || s.x_rows < s.n_rows || !s.x)
+        if (!allow_dense || s.flags != DG_GROUP_DENSE_ROWS || s.n_chunks < 1 || s.n_chunks > DG_PEER_MAX ||
+            s.x_rows < s.n_rows || !s.x)
             return DG_EINVAL;
         if (!dg::aligned16(s.x) || (s.x_ld & 3)) return DG_EALIGN;
         if (s.x_ld < d || (int64_t)s.x_rows * s.x_ld > 0x7fffffffLL) return DG_EINVAL;
@@ -668,7 +677,8 @@ int convert_group(const dg_rel_group& s, int d, bool need_out, SpmmGroupK& k, bo
         k.x = s.x;
         k.x_ld = static_cast<int32_t>(s.x_ld);
         k.n_rows = s.n_rows;
-        k.n_chunks = 1;
+        k.n_chunks = s.n_chunks;                  // slots, summed in slot order
+        k.chunk_x = (int64_t)s.x_rows * s.x_ld;  // slot c at x + c·x_rows·x_ld
         k.drop_keep = 1.f;
         return DG_OK;  // k.rowptr == nullptr marks the dense form in the kernel
     }
@@ -758,7 +768,8 @@ int prep_fused(const dg_rel_group* groups, int32_t n_groups, const dg_fused_targ
     a.n_projs = n_projs;
     a.wpg = waves_per_group;
     for (int i = 0; i < n_groups; ++i) {
-        if (groups[i].n_chunks != 1) return DG_EINVAL;  // fused mode: the whole group is one chunk
+        // fused mode: the whole group is one chunk (dense rows: n_chunks slots)
+        if (groups[i].n_chunks != 1 && !(groups[i].flags & DG_GROUP_DENSE_ROWS)) return DG_EINVAL;
         const int rc = convert_group(groups[i], d, false, a.g[i], false, true);
         if (rc != DG_OK) return rc;
     }
@@ -867,6 +878,9 @@ int epilogue_launch(const dg_epi_target* targets, int32_t n_targets, int32_t d, 
             a.g[ng].partial = T.groups[i].partial;
             a.g[ng].sum = T.groups[i].sum_out;
             a.g[ng].n_chunks = T.groups[i].n_chunks;
+            if (T.groups[i].group_flags & ~DG_EPI_PUSH) return DG_EINVAL;
+            if ((T.groups[i].group_flags & DG_EPI_PUSH) && !T.groups[i].sum_out) return DG_EINVAL;
+            a.g[ng].push = (xchg && (T.groups[i].group_flags & DG_EPI_PUSH)) ? 1 : 0;
             ++ng;
         }
         blocks += dg::ceil_div(T.n_rows, 4);  // one wave per row

@@ -457,6 +457,15 @@ class ForwardPlan:
         self.xregion: Optional[torch.Tensor] = None
         self.peer = None
         split_nodes = [i for i in self.targets if i in self.row_block]
+        # the peer all-reduce (config P's drug rows, peer mode "fused"): the relation-sharded
+        # groups' pre-normalisation sums of layer L live in `world` slots of the region, slot r
+        # written by rank r's epilogue launch into every rank's copy; the finishing launch adds
+        # the slots in rank order (dense-rows groups with n_chunks = world) — no RCCL all-reduce
+        pc = getattr(shard, "peer", None)
+        self.peer_reduce = (pc is not None and pc.mode == "fused" and self.flat_mode and not keep_sums
+                            and self.drop_state is None and bool(split_nodes) and not self.seg_mode
+                            and not self._fused_targets())
+        self._red_slots: Dict[Tuple[int, EdgeType], torch.Tensor] = {}  # (layer, et) -> [world, n_i, d] view
         if split_nodes:
             layout, off = {}, 0
             for layer, d in ((1, h1), (2, h2)):
@@ -464,10 +473,25 @@ class ForwardPlan:
                     nb = self.world * self.row_block[i][2] * d
                     layout[i, layer] = (off, nb, d)
                     off += -(-nb // 64) * 64  # 256-byte aligned
-            self.xregion = torch.empty(max(off, 64), **f32)
+            red_layout = {}
+            if self.peer_reduce:
+                for layer, d in ((1, h1), (2, h2)):
+                    red = [et for et in self.edge_types if et[0] not in self.row_block]
+                    per = sum(n[et[0]] * d for et in red)  # one slot: every group's rows, in order
+                    per = -(-per // 64) * 64
+                    o2 = 0
+                    for et in red:
+                        red_layout[layer, et] = (off, o2, per, n[et[0]], d)
+                        o2 += n[et[0]] * d
+                    off += self.world * per
+            # zeros: a slot no rank ever pushes (a group without relations on that rank) reads as
+            # zeros forever
+            self.xregion = torch.zeros(max(off, 64), **f32)
             for (i, layer), (o, nb, d) in layout.items():
                 self._pad[i, layer] = self.xregion[o:o + nb].view(-1, d)
-            pc = getattr(shard, "peer", None)
+            for key, (base, o2, per, rows, d) in red_layout.items():
+                self._red_slots[key] = torch.as_strided(self.xregion, (self.world, rows, d), (per, d, 1),
+                                                        base + o2)
             if pc is not None:
                 from .peer import PeerExchange
 
@@ -707,7 +731,14 @@ class ForwardPlan:
         split_t = [i for i in self.targets if i in self.row_block and i not in fused_t]
         red = [et for et in rest if et[0] not in self.row_block]
         flat, views, send, sviews = None, {}, None, {}
-        if self.flat_mode and red:
+        layer_no = 1 if relu else 2
+        # the peer all-reduce: each relation-sharded group's sum goes to this rank's slot (and
+        # every peer's copy of it) from the epilogue launch; no flat buffer, no RCCL all-reduce
+        peer_red = self.peer_reduce and bool(red) and bool(split_t)
+        if peer_red:
+            for et in red:
+                sviews[et] = self._red_slots[layer_no, et][self.shard.rank]
+        elif self.flat_mode and red:
             # flat (the reduced sums, read by the finishing launch and the backward) and, when
             # sharded, send (this rank's partial sums, written by its SpMM / reduces): the
             # all-reduce runs out of place, so the regions of groups without local relations
@@ -814,14 +845,27 @@ class ForwardPlan:
             # the relation-sharded node types' chunk reduces ride in the same launch: a target
             # whose groups write their pre-normalisation sums into the send buffer (its
             # finished rows go to a scratch buffer, unread) — one launch per layer instead of two
-            red_t = [i for i in self.targets if i not in self.row_block
-                     and any(et in views and g.groups[et].n_rels and partials[et][1] > 1 for et in self.targets[i])]
+            if peer_red:
+                # every relation-sharded group with local relations: its sum into this rank's
+                # slot, pushed to every peer (the rest of the slot stays zero)
+                red_t = [i for i in self.targets if i not in self.row_block
+                         and any(g.groups[et].n_rels for et in self.targets[i])]
+            else:
+                red_t = [i for i in self.targets if i not in self.row_block
+                         and any(et in views and g.groups[et].n_rels and partials[et][1] > 1
+                                 for et in self.targets[i])]
             n_groups = sum(len(self.targets[i]) for i in split_t + red_t)
-            if reduces and len(split_t) + len(red_t) <= 8 and n_groups <= DG_MAX_GROUPS:
+            fits = len(split_t) + len(red_t) <= 8 and n_groups <= DG_MAX_GROUPS
+            if peer_red and not fits:
+                raise ValueError("peer all-reduce: the layer's targets do not fit one epilogue launch")
+            if (reduces or peer_red) and fits:
                 for i in red_t:
                     grp_parts = []
                     for et in self.targets[i]:
                         part, nc = partials[et][:2]
+                        if peer_red:
+                            grp_parts.append((part, nc, sviews[et] if g.groups[et].n_rels else None, True))
+                            continue
                         reduced = et in views and g.groups[et].n_rels and nc > 1
                         grp_parts.append((part, nc, sviews[et] if reduced else None))
                     blocks.append((grp_parts, torch.empty((n[i], d), **f32), n[i]))
@@ -829,7 +873,24 @@ class ForwardPlan:
             local_epis.append(kernels.PreparedEpilogueMulti(
                 blocks, d, flags, peer=epi_peer, push=[t < n_push for t in range(len(blocks))]))
         launches += reduces
-        if flat is not None:
+        if peer_red:
+            # the relation-sharded rows finished from the world slots, added in rank order by
+            # the dense-rows groups of ONE fused launch (l2norm, Σ_j, relu, layer-1 projections)
+            tl = [i for i in self.targets if i not in self.row_block]
+            pspecs = []
+            for tgt_node, pj in projs:
+                pj.target = tl.index(tgt_node)
+                pspecs.append(pj)
+
+            def slots_spec(i, et):
+                sl = self._red_slots[layer_no, et]
+                per = sl.stride(0)
+                x = torch.as_strided(self.xregion, ((self.world - 1) * per + n[i] * d,), (1,), sl.storage_offset())
+                return kernels.RelGroupSpec(None, None, None, x, None, n[i], self.world, d, per // d, dense=True)
+
+            epis.append(kernels.PreparedFused(
+                [(outs[i], n[i], [slots_spec(i, et) for et in self.targets[i]], relu) for i in tl], d, pspecs, 1))
+        elif flat is not None:
             # sharded: the all-reduced group sums S_ij are finished by ONE fused launch whose
             # groups are the dense rows S_ij[r] themselves (DG_GROUP_DENSE_ROWS), so the l2norm,
             # Σ_j, relu and (layer 1) the layer-2 projections of every node type run in one

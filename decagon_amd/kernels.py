@@ -63,17 +63,19 @@ class RelGroupSpec:
                                   # nonzero p by mask element c·nnz + (drop_index[p] or p)
     drop_index: Optional[torch.Tensor] = None
     dense: bool = False           # DG_GROUP_DENSE_ROWS (dg_gcn_fused_f32 only): row r of the sum
-                                  # is x[r]; rowptr / vcol / val unused (may be None)
+                                  # is x[r] — or, with n_chunks = S slots, Σ_c x[c·x_rows·x_ld + r]
+                                  # in slot order; rowptr / vcol / val unused (may be None)
 
     def validate(self, d: int, need_out: bool = True) -> None:
         if self.dense:
             _dev(self.x, torch.float32, "x")
-            if self.n_chunks != 1 or self.shared or self.drop is not None:
-                raise ValueError("a dense-rows group is one chunk, no shared pattern, no dropout")
+            if not 1 <= self.n_chunks <= _lib.DG_PEER_MAX or self.shared or self.drop is not None:
+                raise ValueError("a dense-rows group has 1..8 slots, no shared pattern, no dropout")
             if self.x_ld < d or self.x_ld % 4:
                 raise ValueError("x_ld must be >= d and a multiple of 4")
-            if self.x_rows < self.n_rows or (self.n_rows and self.x.numel() < (self.n_rows - 1) * self.x_ld + d):
-                raise ValueError("x smaller than the group's rows")
+            last = (self.n_chunks - 1) * self.x_rows * self.x_ld + (self.n_rows - 1) * self.x_ld + d
+            if self.x_rows < self.n_rows or (self.n_rows and self.x.numel() < last):
+                raise ValueError("x smaller than the group's rows (slots)")
             return
         _dev(self.rowptr, torch.int32, "rowptr")
         _dev(self.vcol, torch.int32, "vcol")
@@ -122,7 +124,7 @@ def _fill_group(g, s: RelGroupSpec) -> None:
     if s.dense:
         g.rowptr = g.vcol = g.val = g.out = None
         g.x = s.x.data_ptr()
-        g.x_ld, g.n_rows, g.n_chunks, g.x_rows = s.x_ld, s.n_rows, 1, s.x_rows
+        g.x_ld, g.n_rows, g.n_chunks, g.x_rows = s.x_ld, s.n_rows, s.n_chunks, s.x_rows
         g.flags = _lib.DG_GROUP_DENSE_ROWS
         g.drop_state = g.drop_index = None
         return
@@ -648,8 +650,9 @@ class PreparedEpilogue:
 
 class PreparedEpilogueMulti:
     """dg_gcn_epilogue_multi_f32: several node types' epilogues in one launch —
-    targets = [(partials [(tensor, n_chunks[, sum_out])], out, n_rows)], one flag set; a
-    group's optional sum_out [n_rows, d] receives its pre-normalisation sum S_ij."""
+    targets = [(partials [(tensor, n_chunks[, sum_out[, push]])], out, n_rows)], one flag set;
+    a group's optional sum_out [n_rows, d] receives its pre-normalisation sum S_ij (with a peer
+    exchange and push: also every peer's copy of it — this rank's slot of the all-reduce)."""
 
     def __init__(self, targets: Sequence[Tuple[Sequence[Tuple[torch.Tensor, int]], torch.Tensor, int]], d: int,
                  flags: int, peer=None, push: Optional[Sequence[bool]] = None):
@@ -681,6 +684,11 @@ class PreparedEpilogueMulti:
                         raise ValueError("sum_out too small for [n_rows, d]")
                     garr[i].sum_out = so[0].data_ptr()
                     self._keep.append(so[0])
+                    if len(so) > 1 and so[1]:
+                        if peer is None:
+                            raise ValueError("a pushed sum needs a peer exchange")
+                        peer[0].offset(so[0])  # raises unless inside the region
+                        garr[i].group_flags = _lib.DG_EPI_PUSH
                 self._keep.append(p)
             self._keep.append(out)
             self._garrs.append(garr)

@@ -96,9 +96,12 @@ typedef struct dg_rel_group {
 #define DG_GROUP_DROPOUT 2
 
 /* dg_gcn_fused_f32 only: the group has no adjacency — row r of its sum IS row r of X
- * (x[r * x_ld ..], n_chunks == 1, x_rows >= n_rows; rowptr / vcol / val unused, may be NULL).
- * The sharded forward finishes its all-reduced pre-normalisation sums S_ij this way
- * (layers.py:92-93 after the cross-rank Σ_k), without an identity CSR's two dependent loads. */
+ * (x[r * x_ld ..], x_rows >= n_rows; rowptr / vcol / val unused, may be NULL), or with
+ * n_chunks = S > 1 (S <= DG_PEER_MAX) the sum of S slots of such rows, slot c at
+ * x + c*x_rows*x_ld, added in slot order (fp32, deterministic).  The sharded forward finishes
+ * its all-reduced pre-normalisation sums S_ij this way (layers.py:92-93 after the cross-rank
+ * Σ_k), without an identity CSR's two dependent loads; with the peer exchange the slots are
+ * the ranks' partial sums, so the all-reduce's addition happens here. */
 #define DG_GROUP_DENSE_ROWS 4
 
 int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups,
@@ -317,7 +320,9 @@ typedef struct dg_epi_group {
     float* sum_out;             /* device, [n_rows][d]: the group's pre-normalisation sum
                                    S_ij (what the backward of l2_normalize needs), or NULL */
     int32_t n_chunks;
-    int32_t reserved;
+    int32_t group_flags;        /* 0, or DG_EPI_PUSH (dg_gcn_epilogue_peer_f32 only): sum_out also
+                                 * stored into every peer's copy — the rank's slot of the peer
+                                 * all-reduce of the sums (ABI 34) */
 } dg_epi_group;
 
 int dg_gcn_epilogue_f32(const dg_epi_group* groups /* HOST array */, int32_t n_groups,

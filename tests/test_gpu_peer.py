@@ -14,7 +14,11 @@ the stores reach the peer's memory without crossing xGMI.  Checked:
     stand-alone launches — equals the float64 oracle (decagon/deep/layers.py:85-118,
     model.py:64-88) within 1e-4 and the RCCL-free gloo form bit for bit, eager and replayed
     from a hipGraph, at 2 / 4 / 8 ranks;
-  * the same for the scaled-down config P (proteins row-split; the drug sums still all-reduced);
+  * the same for the scaled-down config P (proteins row-split) at 2 / 4 / 8 ranks, its drug
+    rows' pre-normalisation sums all-reduced by peer stores too (each rank's sums into its slot of
+    every peer's copy, the finishing launch adding the slots in rank order — bit for bit the
+    reference form whose all-reduce adds the gathered sums in rank order); "kernel" mode keeps
+    the all-reduce on the process group;
   * the one-process loopback rehearsal (bench.py --simulate-world --exchange peer) equals the
     unsharded forward's rank block;
   * a wait that cannot complete times out, sets the error word and later waits fail fast;
@@ -94,6 +98,23 @@ def _weights(g, seed=5):
     return w1, w2
 
 
+def _rank_order_allreduce():
+    """The reference all-reduce of the peer form: every rank's tensor gathered, then added in
+    rank order from zeros in fp32 — the order in which the peer all-reduce's finishing launch
+    adds the slots (dense-rows groups), so the two forms agree bit for bit."""
+    import torch.distributed as dist
+
+    def _ar(t, out=None):
+        parts = [torch.empty_like(t.cpu()) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, t.cpu())
+        acc = torch.zeros_like(parts[0])
+        for q in parts:
+            acc += q
+        (t if out is None else out).copy_(acc.to(t.device))
+
+    return _ar
+
+
 def _shard(kind, g, rank, world, peer):
     from decagon_amd.sharding import RelationShard, torch_allgather, torch_allreduce
 
@@ -101,8 +122,8 @@ def _shard(kind, g, rank, world, peer):
         sh = RelationShard.weak_sets(g.edge_types, g.n_nodes, rank, world, torch_allreduce(), torch_allgather())
     else:
         nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
-        sh = RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
-                                 row_split_min=1000)
+        sh = RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, _rank_order_allreduce(),
+                                 torch_allgather(), row_split_min=1000)
     sh.peer = peer
     return sh
 
@@ -143,6 +164,7 @@ def _forward_rank(rank, world, kind, mode):
     if mode == "fused-finish":
         assert any(isinstance(l, kernels.PreparedSegFinish) for l in plan._layer1.launches)
     info = {"seg": plan.seg_mode, "exchanges": sum(L.has_exchange for L in (plan._layer1, plan._layer2)),
+            "peer_reduce": plan.peer_reduce,
             "fused_kinds": sorted({type(l).__name__ for l in plan._layer1.launches}),
             "gather_all": [L.gather_all is not None for L in (plan._layer1, plan._layer2)]}
     outs = []
@@ -212,7 +234,8 @@ def _oracle(kind, g):
 
 @pytest.mark.parametrize("kind,world,mode", [("S", 2, "fused"), ("S", 4, "fused"), ("S", 8, "fused"),
                                              ("S", 2, "kernel"), ("S", 8, "kernel"), ("P", 2, "fused"),
-                                             ("P", 4, "kernel"), ("S", 4, "fused-finish")])
+                                             ("P", 4, "fused"), ("P", 8, "fused"), ("P", 4, "kernel"),
+                                             ("S", 4, "fused-finish")])
 def test_peer_exchange_forward_matches_oracle(kind, world, mode):
     _need_gpu()
     got = run_ranks(_forward_rank, world, (kind, mode))
@@ -221,8 +244,11 @@ def test_peer_exchange_forward_matches_oracle(kind, world, mode):
     for r in range(world):
         info, outs, base, state = got[r]
         assert state[16] == 0, (r, hex(state[16]))  # the error word
-        if mode.startswith("fused") and kind == "S":
-            assert info["exchanges"] == 0, info     # the finishing launches exchange
+        if mode.startswith("fused"):
+            # the finishing launches exchange (config P: the drug sums by the peer all-reduce
+            # too — no RCCL / gloo collective left in the step)
+            assert info["exchanges"] == 0, info
+            assert info["peer_reduce"] == (kind == "P"), info
         if mode == "kernel":
             assert all(info["gather_all"]), info
         for form in outs:
