@@ -41,6 +41,9 @@ constexpr int kFsegUP = 4;   // fused seg, reassociated (W slabs read after the 
                              // the gathers and 9.45 staged in LDS per workgroup; step 19.36 / 19.66 /
                              // 21.88 us at 200 steps)
 constexpr int kSegMinNW = 1; // waves per workgroup, at least (else: the launch's largest chunk)
+#ifndef DG_FSEG_XCD
+#define DG_FSEG_XCD 0        // A/B build only: XCD-contiguous row blocks in gcn_fused_seg_kernel
+#endif
 
 namespace {
 
@@ -468,7 +471,15 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 #pragma unroll 1
     while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
     const FsTargetK& T = a.t[ti];
+#if DG_FSEG_XCD
+    // A/B: XCD-contiguous row blocks (block lb runs on XCD lb % 8)
+    const int lb = blockIdx.x - T.block_begin;
+    const int nb8 = (T.n_rows + T.rpb - 1) / T.rpb;
+    const int per = (nb8 + 7) >> 3;
+    const int r0 = ((lb & 7) * per + (lb >> 3)) * T.rpb;
+#else
     const int r0 = (blockIdx.x - T.block_begin) * T.rpb;
+#endif
     // wave -> (row slot, group gl, relation k of the group): each slot's groups' relations back
     // to back; k = c·chunk + t (chunk c, relation t: a rank's row block of several relation
     // sets keeps one chunk per set)
@@ -763,7 +774,11 @@ int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fuse
         FsTargetK& k = a.t[t];
         k.rpb = nw / k.waves < kFsMaxRpb ? nw / k.waves : kFsMaxRpb;
         k.block_begin = static_cast<int32_t>(blocks);
+#if DG_FSEG_XCD
+        blocks += 8 * dg::ceil_div(dg::ceil_div(k.n_rows, k.rpb), 8);
+#else
         blocks += dg::ceil_div(k.n_rows, k.rpb);
+#endif
     }
     if (blocks > 0x7fffffff) return DG_EINVAL;
     a.n_targets = n_targets;

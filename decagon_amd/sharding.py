@@ -184,7 +184,10 @@ class RelationShard:
         if form == "seg":
             if any(K % world_size for K in edge_types.values()):
                 raise ValueError("every group must hold world_size relation sets")
-            sh.chunks = {et: K // world_size for et, K in edge_types.items()}
+            # relation sets per chunk (A/B knob DG_S_SETS: 2 halves the chunk partials a row's
+            # finish adds, at twice the waves per workgroup)
+            spc = max(1, int(os.environ.get("DG_S_SETS", "1")))
+            sh.chunks = {et: K // world_size * spc for et, K in edge_types.items()}
             sh.seg_rows = True
         else:
             sh.chunks = dict(edge_types)
