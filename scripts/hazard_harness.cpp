@@ -1,0 +1,161 @@
+// Attribute config 5's intermittent wrong scores to one instruction sequence.
+//
+// Loads several builds of the round-4 fused config-5 kernel (decoder_bf16_cs16_kernel<768, true>)
+// as code objects: the first is the reference (the shipped form, whose per-half sums are kept
+// unpaired), the others the failing build assembled from its own .s — unchanged, or with
+// wait states inserted at ONE candidate site each (scripts/hazard_variants.sh).  Every build
+// runs on the same config-5-shaped inputs (1,928 slots x 512 pairs, d = 256, 30,848 tiles); the
+// outputs are compared bit for bit with the reference's, and each run reports how many 16-pair
+// half tiles differ, for the positive and the negative scores separately.
+//
+// Build: hipcc -O3 --offload-arch=gfx950 -o scripts/hazard_harness scripts/hazard_harness.cpp
+// Run:   scripts/hazard_harness RUNS ref.hsaco variant.hsaco ...   (one JSON line per variant)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+struct Args {  // Bf16DecArgs of the round-4 source
+    const uint16_t* row_table;
+    const uint16_t* col_table;
+    const uint16_t* R;
+    const uint16_t* L;
+    const int32_t* rows;
+    const int32_t* cols;
+    const int32_t* rel;
+    float* out;
+    int64_t ld_row, ld_col;
+    int32_t n_pairs, d;
+    const uint2* alias;
+    int64_t alias_stride;
+    uint64_t seed;
+    int32_t* neg_out;
+    float* loss;
+    float* partial;
+    uint32_t* ticket;
+    int32_t range, slot0, batch;
+    float margin;
+};
+
+#define CK(x)                                                                       \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(2);                                                                \
+        }                                                                           \
+    } while (0)
+
+static uint16_t bf16(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (uint16_t)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: %s RUNS ref.hsaco variant.hsaco ...\n", argv[0]);
+        return 1;
+    }
+    const int runs = atoi(argv[1]);
+    const int D = 256, ND = 645, SLOTS = 1928, B = 512;
+    const int nh = SLOTS * B;
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<float> U(-1.f, 1.f);
+    std::vector<uint16_t> E((size_t)ND * D), R((size_t)D * D), L((size_t)SLOTS * D);
+    for (auto& x : E) x = bf16(U(rng));
+    for (auto& x : R) x = bf16(0.1f * U(rng));
+    for (auto& x : L) x = bf16(U(rng));
+    std::vector<int32_t> rows(nh), cols(nh);
+    for (int i = 0; i < nh; ++i) {
+        rows[i] = (int)(rng() % ND);
+        cols[i] = (int)(rng() % ND);
+    }
+    std::vector<uint2> alias((size_t)SLOTS * ND);
+    for (auto& a : alias) {
+        const float p = 0.5f + 0.5f * U(rng);
+        memcpy(&a.x, &p, 4);
+        a.y = rng() % ND;
+    }
+    auto up = [](const void* h, size_t n) {
+        void* d;
+        CK(hipMalloc(&d, n));
+        CK(hipMemcpy(d, h, n, hipMemcpyHostToDevice));
+        return d;
+    };
+    Args a{};
+    a.row_table = (const uint16_t*)up(E.data(), E.size() * 2);
+    a.col_table = a.row_table;
+    a.R = (const uint16_t*)up(R.data(), R.size() * 2);
+    a.L = (const uint16_t*)up(L.data(), L.size() * 2);
+    a.rows = (const int32_t*)up(rows.data(), nh * 4);
+    a.cols = (const int32_t*)up(cols.data(), nh * 4);
+    a.ld_row = a.ld_col = D;
+    a.n_pairs = nh;
+    a.d = D;
+    a.alias = (const uint2*)up(alias.data(), alias.size() * 8);
+    a.alias_stride = ND;
+    a.seed = 11;
+    a.range = ND;
+    a.slot0 = 0;
+    a.batch = B;
+    a.margin = 0.1f;
+    CK(hipMalloc(&a.neg_out, nh * 4));
+    CK(hipMalloc(&a.loss, 16));
+    void* ws;
+    CK(hipMalloc(&ws, 8192));
+    CK(hipMemset(ws, 0, 8192));
+    a.ticket = (uint32_t*)ws;
+    a.partial = (float*)ws + 4;
+    float* out;
+    CK(hipMalloc(&out, (size_t)2 * nh * 4));
+    a.out = out;
+    const int threads = 768, waves = threads / 64;
+    const int n_tiles = (nh + 31) / 32;
+    int blocks = (n_tiles + waves - 1) / waves;
+    if (blocks > 256) blocks = 256;
+    const unsigned lds = D * D * 2 + waves * D * 2;
+    const char* name = "_ZN12_GLOBAL__N_124decoder_bf16_cs16_kernelILi768ELb1EEEvNS_11Bf16DecArgsE";
+    std::vector<float> ref((size_t)2 * nh), got((size_t)2 * nh);
+    for (int v = 2; v < argc; ++v) {
+        hipModule_t m;
+        hipFunction_t f;
+        CK(hipModuleLoad(&m, argv[v]));
+        CK(hipModuleGetFunction(&f, m, name));
+        size_t sz = sizeof(a);
+        void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+        const int nr = v == 2 ? 1 : runs;
+        long bad_pos = 0, bad_neg = 0, bad_halves = 0, max_halves = 0;
+        for (int r = 0; r < nr; ++r) {
+            CK(hipMemset(out, 0, (size_t)2 * nh * 4));
+            CK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, lds, 0, nullptr, extra));
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(v == 2 ? ref.data() : got.data(), out, (size_t)2 * nh * 4, hipMemcpyDeviceToHost));
+            if (v == 2) break;
+            long halves = 0;
+            for (int h = 0; h < nh / 16; ++h) {
+                bool bp = false, bn = false;
+                for (int i = 16 * h; i < 16 * h + 16; ++i) {
+                    bp |= memcmp(&got[i], &ref[i], 4) != 0;
+                    bn |= memcmp(&got[nh + i], &ref[nh + i], 4) != 0;
+                }
+                bad_pos += bp;
+                bad_neg += bn;
+                halves += bp || bn;
+            }
+            bad_halves += halves;
+            if (halves > max_halves) max_halves = halves;
+        }
+        if (v > 2)
+            printf("{\"build\": \"%s\", \"runs\": %d, \"half_tiles\": %d, \"bad_halves\": %ld, \"max_per_run\": %ld, "
+                   "\"bad_pos_halves\": %ld, \"bad_neg_halves\": %ld}\n",
+                   argv[v], nr, nh / 16, bad_halves, max_halves, bad_pos, bad_neg);
+        fflush(stdout);
+        CK(hipModuleUnload(m));
+    }
+    return 0;
+}

@@ -1,0 +1,130 @@
+"""Build the code objects scripts/hazard_harness compares (DESIGN.md §5, config 5's hazard).
+
+Run on the CPU container (needs git and the ROCm toolchain):  python scripts/hazard_variants.py
+Writes scripts/hazard/*.hsaco (git-ignored; they travel to the GPU box with the tree):
+
+  ref.hsaco          the round-4 source as shipped (commit 3b0d266: per-half sums kept
+                     unpaired by an opaque copy)
+  failing.hsaco      the same source without the opaque copy — the build that returned wrong
+                     half-0 scores on ~2 % of tiles — assembled from its own .s, unchanged
+  <site>.hsaco       that .s with wait states inserted at ONE candidate site (below), nothing
+                     else changed, so a build that stops failing names the sequence
+"""
+from __future__ import annotations
+
+import re
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+OUT = ROOT / "scripts" / "hazard"
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+COMMIT = "3b0d266"
+KERNEL = "_ZN12_GLOBAL__N_124decoder_bf16_cs16_kernelILi768ELb1EEEvNS_11Bf16DecArgsE"
+FENCE = 'asm volatile("" : "+v"(pp[b]), "+v"(pn[b]));'
+
+
+def git_show(path: str) -> str:
+    return subprocess.run(["git", "-C", str(ROOT), "show", f"{COMMIT}:{path}"], check=True, capture_output=True,
+                          text=True).stdout
+
+
+def compile_s(src: str, inc: Path, work: Path, name: str) -> str:
+    (work / f"{name}.hip").write_text(src)
+    s = work / f"{name}.s"
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--offload-device-only",
+                    f"-I{inc}", "-S", str(work / f"{name}.hip"), "-o", str(s)], check=True, capture_output=True)
+    return s.read_text()
+
+
+def assemble(asm: str, work: Path, name: str) -> Path:
+    s = work / f"{name}.s"
+    s.write_text(asm)
+    o = work / f"{name}.o"
+    subprocess.run([str(LLVM / "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
+                    str(s), "-o", str(o)], check=True, capture_output=True)
+    out = OUT / f"{name}.hsaco"
+    subprocess.run([str(LLVM / "ld.lld"), "-shared", str(o), "-o", str(out)], check=True, capture_output=True)
+    return out
+
+
+def kernel_span(lines):
+    a = next(i for i, l in enumerate(lines) if l.startswith(KERNEL + ":"))
+    b = next(i for i in range(a + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    return a, b
+
+
+_VR = re.compile(r"v\[(\d+):(\d+)\]")
+
+
+def edit_pk(lines):
+    """s_nop 1 between a v_mov_b32 that writes one VGPR and the v_pk_fma_f32 right after it
+    reading that VGPR inside a 64-bit source pair (the failing build's four epilogue sites)."""
+    a, b = kernel_span(lines)
+    out, n = list(lines), 0
+    for i in range(b, a, -1):
+        cur, prev = lines[i].strip(), lines[i - 1].strip()
+        m = re.match(r"v_mov_b32_e32 v(\d+),", prev)
+        if not (cur.startswith("v_pk_fma_f32") and m):
+            continue
+        w = int(m.group(1))
+        if any(int(x) <= w <= int(y) for x, y in _VR.findall(cur.split(",", 1)[1])):
+            out.insert(i, "\ts_nop 1")
+            n += 1
+    return out, n
+
+
+def edit_srcc(lines):
+    """s_nop 7 before every ds_read whose destination is the SrcC of an MFMA at most 4
+    instructions earlier (the failing build's one such site, in half 0's chain)."""
+    a, b = kernel_span(lines)
+    out, n = list(lines), 0
+    for i in range(b, a, -1):
+        cur = lines[i].strip()
+        if not cur.startswith("ds_read_b128"):
+            continue
+        dst = _VR.match(cur.split()[1])
+        if not dst:
+            continue
+        for j in range(i - 1, max(a, i - 5), -1):
+            prev = lines[j].strip()
+            if prev.startswith("v_mfma"):
+                regs = _VR.findall(prev)
+                if len(regs) >= 4 and regs[3] == dst.groups():
+                    out.insert(i, "\ts_nop 7")
+                    n += 1
+                break
+    return out, n
+
+
+def main() -> int:
+    OUT.mkdir(parents=True, exist_ok=True)
+    with tempfile.TemporaryDirectory() as td:
+        work = Path(td)
+        inc = work / "inc"
+        inc.mkdir()
+        for f in ("common.h", "decoder_tile.h", "dropout.h", "peer.h"):
+            try:
+                (inc / f).write_text(git_show(f"decagon_amd/csrc/{f}"))
+            except subprocess.CalledProcessError:
+                pass
+        (inc / "decagon_hip.h").write_text(git_show("include/decagon_hip.h"))
+        src = git_show("decagon_amd/csrc/decoder_bf16.hip")
+        assert FENCE in src
+        ref = compile_s(src, inc, work, "ref")
+        assemble(ref, work, "ref")
+        failing = compile_s(src.replace(FENCE, "/* opaque copy removed */"), inc, work, "failing")
+        assemble(failing, work, "failing")
+        lines = failing.splitlines()
+        for name, fn in (("pk_nop", edit_pk), ("srcc_nop", edit_srcc)):
+            edited, n = fn(lines)
+            assemble("\n".join(edited) + "\n", work, name)
+            print(f"{name}: {n} site(s) edited")
+    print("wrote", sorted(p.name for p in OUT.glob("*.hsaco")))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
