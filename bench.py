@@ -301,7 +301,7 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
 
 KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm_groups_kernel<{lp}>",
                 "PreparedStaged": "spmm_staged_kernel", "PreparedFusedSeg": "gcn_fused_seg_kernel<{lp}, {proj}",
-                "PreparedSeg": "spmm_seg_kernel<{lp}, {proj}", "PreparedSegFinish": "spmm_seg_kernel<{lp}, {proj}"}
+                "PreparedSeg": "spmm_seg_kernel<{lp}, {proj}"}
 
 
 def _kernel_pat(launch, d):

@@ -111,11 +111,6 @@ class DgFusedTarget(ctypes.Structure):
                 ("flags", c_int32)]
 
 
-class DgSegFinish(ctypes.Structure):
-    _fields_ = [("out", c_void_p), ("n_rows", c_int32), ("g_begin", c_int32), ("g_count", c_int32),
-                ("target_flags", c_int32)]
-
-
 class DgEpiGroup(ctypes.Structure):
     _fields_ = [("partial", c_void_p), ("sum_out", c_void_p), ("n_chunks", c_int32), ("group_flags", c_int32)]
 
@@ -205,8 +200,6 @@ SIGNATURES = {
                                            c_void_p]),
     "dg_gcn_fused_seg_peer_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32,
                                             c_int32, POINTER(DgPeerXchg), c_void_p]),
-    "dg_spmm_seg_finish_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgSegFinish), c_int32, c_int32,
-                                         c_int32, c_int32, c_void_p, POINTER(DgPeerXchg), c_void_p]),
     "dg_peer_alloc": (c_int32, [c_int64, c_int32, POINTER(c_void_p)]),
     "dg_peer_free": (c_int32, [c_void_p]),
     "dg_ipc_get_handle": (c_int32, [c_void_p, c_void_p, POINTER(c_int64)]),

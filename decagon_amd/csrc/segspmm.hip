@@ -41,9 +41,6 @@ constexpr int kFsegUP = 4;   // fused seg, reassociated (W slabs read after the 
                              // the gathers and 9.45 staged in LDS per workgroup; step 19.36 / 19.66 /
                              // 21.88 us at 200 steps)
 constexpr int kSegMinNW = 1; // waves per workgroup, at least (else: the launch's largest chunk)
-#ifndef DG_FSEG_XCD
-#define DG_FSEG_XCD 0        // A/B build only: XCD-contiguous row blocks in gcn_fused_seg_kernel
-#endif
 
 namespace {
 
@@ -66,32 +63,12 @@ struct SegGroupK {
     int32_t row_blocks;
     int32_t block_begin;
     int32_t n_blocks;
-    int32_t tgt;         // FIN: the target node type whose rows this group's partials finish
-};
-
-// FIN (dg_spmm_seg_finish_f32): a target node type — its finished rows, its groups, and its
-// rows' arrival counters (cnt[cnt_off + r]; expect = Σ n_chunks of its groups: one arrival per
-// (group, chunk) workgroup that covers the row).
-struct FinTargetK {
-    float* out;
-    int32_t n_rows;
-    int32_t g_begin;
-    int32_t g_count;
-    int32_t push;      // PEER: its finished rows also go to every peer's copy
-    int32_t cnt_off;
-    int32_t expect;
 };
 
 struct SegArgs {
     SegGroupK g[DG_MAX_GROUPS];
     int32_t n_groups;
     int32_t nw;  // waves per workgroup
-    // FIN only:
-    FinTargetK t[DG_MAX_GROUPS];
-    int32_t n_targets;
-    int32_t flags;     // DG_EPI_L2NORM | DG_EPI_RELU
-    uint32_t* cnt;     // arrival counters, zero between launches (the finishing wave resets its row's)
-    dg::PeerK P;       // PEER: the exchange the launch ends with (peer.h)
 };
 
 // Broadcast lane m of each 16-lane row to the row (DPP row_newbcast:m — VALU, no LDS).  m
@@ -289,79 +266,17 @@ __device__ __forceinline__ float4 seg_wave_proj(const SegGroupK& g, int k, int b
     return z;
 }
 
-// FIN: finish row r of target T — for each of its groups the chunk partials summed in chunk
-// order (read with sc1 loads: other workgroups, maybe on other XCDs, stored them write-through
-// and drained before their arrival), L2-normalised; the groups summed in order, relu.  The same
-// lanes, loads and sums as epilogue_row (spmm.hip) with LP = 4·DOUT4 floats a row, so the
-// finished rows are bitwise those of the seg + epilogue pair.
-template <int LP, bool PEER>
-__device__ __forceinline__ void seg_finish_row(const SegArgs& a, const FinTargetK& T, int r, int lane) {
-    constexpr int CG = dg::kWave / LP;
-    constexpr int D = 4 * LP;
-    const int cg = lane / LP, q = lane % LP;
-    float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 1
-    for (int gi = T.g_begin; gi < T.g_begin + T.g_count; ++gi) {
-        const SegGroupK& g = a.g[gi];
-        const uint32_t plane = (uint32_t)g.n_rows * (D * 4);  // bytes per chunk partial
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(g.out, 0, 0x7fffffff, 0x00020000);
-        const uint32_t base = ((uint32_t)r * D + 4 * q) * 4;
-        const int nc = g.n_chunks;
-        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        int c = cg;
-#pragma unroll 1
-        for (; c + 3 * CG < nc; c += 4 * CG) {
-            float4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rs, (int)(base + (uint32_t)(c + u * CG) * plane), 0, 16));
-#pragma unroll
-            for (int u = 0; u < 4; ++u) dg::add4(s, v[u]);
-        }
-#pragma unroll 1
-        for (; c < nc; c += CG)
-            dg::add4(s, __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       rs, (int)(base + (uint32_t)c * plane), 0, 16)));
-#pragma unroll
-        for (int m = LP; m < dg::kWave; m <<= 1) dg::add4(s, dg::shfl_xor4(s, m));
-        if (a.flags & DG_EPI_L2NORM) {  // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
-            float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
-#pragma unroll
-            for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
-            const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
-            s.x *= inv;
-            s.y *= inv;
-            s.z *= inv;
-            s.w *= inv;
-        }
-        dg::add4(tot, s);
-    }
-    if (a.flags & DG_EPI_RELU)
-        tot = make_float4(fmaxf(tot.x, 0.f), fmaxf(tot.y, 0.f), fmaxf(tot.z, 0.f), fmaxf(tot.w, 0.f));
-    if (cg == 0) {
-        const int64_t off = (int64_t)r * D + 4 * q;
-        *reinterpret_cast<float4*>(T.out + off) = tot;
-        if constexpr (PEER)
-            if (T.push) dg::peer_store4(a.P, T.out, (uint32_t)T.n_rows * (D * 4), (uint32_t)off * 4, tot);
-    }
-}
-
 // PROJ: d_in = 64 (LP = 16), d_out = 32; otherwise d_out = d_in = 4·LP.  a.nw waves per
 // workgroup (the launch's largest chunk, so a chunk-6 group wastes no wave slot; rows per
-// workgroup nw / chunk), at most NW.
-// FIN (dg_spmm_seg_finish_f32): the partials are stored write-through and drained, each row of
-// the workgroup counts one arrival, and the workgroup that brings a row's count to the target's
-// expect finishes that row (seg_finish_row) and resets its counter — the seg + epilogue pair in
-// one launch.  PEER (with FIN): the finished rows of pushing targets also go to every peer and
-// the launch ends with the exchange.
-template <int LP, bool PROJ, int NW, bool FIN = false, bool PEER = false>
+// workgroup nw / chunk), at most NW.  (A form whose last-arriving workgroup also finished
+// each row — write-through partials, an arrival counter per row, no epilogue launch — measured
+// slower at every N: 29.1 against 25.4 µs a rank share at N = 8, 42.8 against 30.5 with the peer
+// exchange, 25.7 / 33.3 with two relation sets per chunk; removed in round 5)
+template <int LP, bool PROJ, int NW>
 __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
-    static_assert(FIN || !PEER, "the peer form finishes its rows");
     constexpr int DOUT4 = PROJ ? 8 : LP;  // float4s of an output row
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
-    __shared__ int fin[NW];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (segment bounds: scalar loads)
     int gi = 0;
@@ -373,14 +288,13 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     const int per = g.n_blocks >> 3;
     const int item = (lb & 7) * per + (lb >> 3);
     const bool wg_live = item < g.n_chunks * g.row_blocks;
-    if (!PEER && !wg_live) return;  // workgroup-uniform, before any barrier (PEER: every
-                                    // workgroup takes part in the exchange)
+    if (!wg_live) return;  // workgroup-uniform, before any barrier
     const int c = item / g.row_blocks;
     const int r0 = (item - c * g.row_blocks) * g.rpb;
     const int slot = wave / g.chunk;
     const int t = wave - slot * g.chunk;
     const int r = r0 + slot;
-    const bool row_ok = wg_live && slot < g.rpb && r < g.n_rows;
+    const bool row_ok = slot < g.rpb && r < g.n_rows;
     const int k = c * g.chunk + t;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (PROJ) {
@@ -400,35 +314,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_seg_kernel(const SegArgs a) {
     if (row_ok && t == 0 && lane < DOUT4) {
         float4 s = zbuf[wave][lane];
         for (int u = 1; u < g.chunk; ++u) dg::add4(s, zbuf[wave + u][lane]);
-        float* po = g.out + ((int64_t)c * g.n_rows + r) * (4 * DOUT4) + 4 * lane;
-        if constexpr (FIN) {  // write-through (sc1): the finishing workgroup reads it with sc1 loads
-            const auto rs = __builtin_amdgcn_make_buffer_rsrc(po, 0, 16, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dg::u32x4, s), rs, 0, 0, 16);
-        } else {
-            *reinterpret_cast<float4*>(po) = s;
-        }
-    }
-    if constexpr (FIN) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial is out
-        __syncthreads();
-        const FinTargetK& T = a.t[g.tgt];
-        if (wg_live && (int)threadIdx.x < g.rpb) {  // one arrival per row of the workgroup
-            const int rr = r0 + threadIdx.x;
-            int f = 0;
-            if (rr < g.n_rows) {
-                const uint32_t old =
-                    __hip_atomic_fetch_add(a.cnt + T.cnt_off + rr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                f = old + 1u == (uint32_t)T.expect;
-            }
-            fin[threadIdx.x] = f;
-        }
-        __syncthreads();
-        if (wg_live && wave < g.rpb && fin[wave]) {  // wave-uniform: the row's last arrival finishes it
-            const int rr = r0 + wave;
-            seg_finish_row<DOUT4, PEER>(a, T, rr, lane);
-            if (lane == 0) __hip_atomic_store(a.cnt + T.cnt_off + rr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if constexpr (PEER) dg::peer_arrive(a.P);
+        *reinterpret_cast<float4*>(g.out + ((int64_t)c * g.n_rows + r) * (4 * DOUT4) + 4 * lane) = s;
     }
 }
 
@@ -471,15 +357,9 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 #pragma unroll 1
     while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
     const FsTargetK& T = a.t[ti];
-#if DG_FSEG_XCD
-    // A/B: XCD-contiguous row blocks (block lb runs on XCD lb % 8)
-    const int lb = blockIdx.x - T.block_begin;
-    const int nb8 = (T.n_rows + T.rpb - 1) / T.rpb;
-    const int per = (nb8 + 7) >> 3;
-    const int r0 = ((lb & 7) * per + (lb >> 3)) * T.rpb;
-#else
+    // (rows in dispatch order: XCD-contiguous row blocks measured slower at config S, 18.60 vs
+    // 18.16 µs a step — a random graph's rows gather from every XCD's share of the operand)
     const int r0 = (blockIdx.x - T.block_begin) * T.rpb;
-#endif
     // wave -> (row slot, group gl, relation k of the group): each slot's groups' relations back
     // to back; k = c·chunk + t (chunk c, relation t: a rank's row block of several relation
     // sets keeps one chunk per set)
@@ -590,14 +470,14 @@ int seg_shape(int32_t d_in, int32_t d_out, bool& proj) {
 
 namespace {
 // The launch dispatch of both kernels: runtime switches onto the instantiated template forms.
-template <int NW, bool FIN = false, bool PEER = false>
+template <int NW>
 void launch_seg(bool proj, int d_in, dim3 grid, dim3 block, hipStream_t st, const SegArgs& a) {
     if (proj)
-        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW, FIN, PEER>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((spmm_seg_kernel<16, true, NW>), grid, block, 0, st, a);
     else if (d_in == 64)
-        hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW, FIN, PEER>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((spmm_seg_kernel<16, false, NW>), grid, block, 0, st, a);
     else
-        hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW, FIN, PEER>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((spmm_seg_kernel<8, false, NW>), grid, block, 0, st, a);
 }
 
 template <int NW, bool PEER>
@@ -610,57 +490,12 @@ void launch_fs(bool proj, int d_in, dim3 grid, dim3 block, hipStream_t st, const
         hipLaunchKernelGGL((gcn_fused_seg_kernel<8, false, NW, PEER>), grid, block, 0, st, a);
 }
 
-// fin: the finishing form's targets (nullptr: plain partials); every group then belongs to
-// exactly one target, in target order.
-int seg_launch(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out, void* stream,
-               const dg_seg_finish* fin = nullptr, int32_t n_fin = 0, int32_t flags = 0, uint32_t* counters = nullptr,
-               const dg_peer_xchg* xchg = nullptr) {
+int seg_launch(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out, void* stream) {
     if (n_groups < 0 || (n_groups > 0 && groups == nullptr)) return DG_EINVAL;
     if (n_groups > DG_MAX_GROUPS) return DG_ETOOMANY;
     bool proj = false;
     if (seg_shape(d_in, d_out, proj) != DG_OK) return DG_EINVAL;
     SegArgs args{};
-    std::vector<int> tgt_of(n_groups > 0 ? n_groups : 1, -1);
-    if (fin) {
-        if (n_fin < 1 || n_fin > DG_MAX_GROUPS || !counters) return DG_EINVAL;
-        if (flags & ~(DG_EPI_L2NORM | DG_EPI_RELU)) return DG_EINVAL;
-        int next = 0;
-        int64_t cnt_off = 0;
-        for (int t = 0; t < n_fin; ++t) {
-            const dg_seg_finish& F = fin[t];
-            if (F.g_begin != next || F.g_count < 1 || F.g_begin + F.g_count > n_groups || F.n_rows < 0)
-                return DG_EINVAL;  // the targets partition the groups, in order
-            if (F.n_rows > 0 && (!F.out || !dg::aligned16(F.out))) return F.out ? DG_EALIGN : DG_EINVAL;
-            if (F.target_flags & ~DG_EPI_PUSH) return DG_EINVAL;
-            if ((int64_t)F.n_rows * d_out * 4 > 0x7fffffffLL) return DG_EINVAL;  // 32-bit byte offsets
-            FinTargetK& k = args.t[t];
-            k.out = F.out;
-            k.n_rows = F.n_rows;
-            k.g_begin = F.g_begin;
-            k.g_count = F.g_count;
-            k.push = (xchg && (F.target_flags & DG_EPI_PUSH)) ? 1 : 0;
-            k.cnt_off = static_cast<int32_t>(cnt_off);
-            int expect = 0;
-            for (int gi = F.g_begin; gi < F.g_begin + F.g_count; ++gi) {
-                if (groups[gi].n_rows != F.n_rows) return DG_EINVAL;
-                if ((int64_t)groups[gi].n_chunks * groups[gi].n_rows * d_out * 4 > 0x7fffffffLL) return DG_EINVAL;
-                if (groups[gi].n_rels > 0) expect += groups[gi].n_chunks;
-                tgt_of[gi] = t;
-            }
-            k.expect = expect;
-            next = F.g_begin + F.g_count;
-            cnt_off += F.n_rows;
-        }
-        if (next != n_groups) return DG_EINVAL;
-        if (cnt_off > 0x7fffffff) return DG_EINVAL;
-        args.n_targets = n_fin;
-        args.flags = flags;
-        args.cnt = counters;
-        if (xchg) {
-            const int rc = dg::peer_convert(xchg, args.P);
-            if (rc != DG_OK) return rc;
-        }
-    }
     int64_t blocks = 0;
     int ng = 0;
     int nw = kSegMinNW;
@@ -677,7 +512,6 @@ int seg_launch(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32
         SegGroupK& k = args.g[ng++];
         if (!s.out) return DG_EINVAL;
         if (!dg::aligned16(s.out)) return DG_EALIGN;
-        k.tgt = fin ? tgt_of[i] : 0;
         k.rpb = nw / s.chunk;
         k.row_blocks = dg::ceil_div(s.n_rows, k.rpb);
         const int64_t items = (int64_t)s.n_chunks * k.row_blocks;
@@ -687,48 +521,13 @@ int seg_launch(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32
         if (blocks > 0x7fffffff) return DG_EINVAL;
     }
     args.n_groups = ng;
-    if (fin) {  // the targets' group ranges in the compacted array (skipped groups add nothing)
-        for (int t = 0; t < n_fin; ++t) {
-            int b = ng, n = 0;
-            for (int i = 0; i < ng; ++i)
-                if (args.g[i].tgt == t) {
-                    if (b == ng) b = i;
-                    ++n;
-                }
-            args.t[t].g_begin = n ? b : 0;
-            args.t[t].g_count = n;
-        }
-    }
-    if (blocks == 0) {
-        if (!xchg) return DG_OK;
-        // no rows here: one workgroup still takes part in the exchange (its group: a stand-in
-        // with no items, so the workgroup only arrives)
-        blocks = 8;
-        args.n_groups = 1;
-        args.g[0] = SegGroupK{};
-        args.g[0].chunk = 1;
-        args.g[0].rpb = 1;
-        args.g[0].row_blocks = 1;  // (no items: every workgroup is dead; no division by zero)
-        args.g[0].n_blocks = 8;
-    }
+    if (blocks == 0) return DG_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(blocks)), block(64 * nw);  // (launch bounds: 8 or 16 waves)
-    if (!fin) {
-        if (nw <= 8)
-            launch_seg<8>(proj, d_in, grid, block, st, args);
-        else
-            launch_seg<16>(proj, d_in, grid, block, st, args);
-    } else if (!xchg) {
-        if (nw <= 8)
-            launch_seg<8, true, false>(proj, d_in, grid, block, st, args);
-        else
-            launch_seg<16, true, false>(proj, d_in, grid, block, st, args);
-    } else {
-        if (nw <= 8)
-            launch_seg<8, true, true>(proj, d_in, grid, block, st, args);
-        else
-            launch_seg<16, true, true>(proj, d_in, grid, block, st, args);
-    }
+    if (nw <= 8)
+        launch_seg<8>(proj, d_in, grid, block, st, args);
+    else
+        launch_seg<16>(proj, d_in, grid, block, st, args);
     return dg::launch_status();
 }
 
@@ -774,11 +573,7 @@ int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fuse
         FsTargetK& k = a.t[t];
         k.rpb = nw / k.waves < kFsMaxRpb ? nw / k.waves : kFsMaxRpb;
         k.block_begin = static_cast<int32_t>(blocks);
-#if DG_FSEG_XCD
-        blocks += 8 * dg::ceil_div(dg::ceil_div(k.n_rows, k.rpb), 8);
-#else
         blocks += dg::ceil_div(k.n_rows, k.rpb);
-#endif
     }
     if (blocks > 0x7fffffff) return DG_EINVAL;
     a.n_targets = n_targets;
@@ -810,13 +605,6 @@ int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fuse
 extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out,
                                void* stream) {
     return seg_launch(groups, n_groups, d_in, d_out, stream);
-}
-
-extern "C" int dg_spmm_seg_finish_f32(const dg_seg_group* groups, int32_t n_groups, const dg_seg_finish* targets,
-                                      int32_t n_targets, int32_t d_in, int32_t d_out, int32_t flags,
-                                      uint32_t* counters, const dg_peer_xchg* xchg, void* stream) {
-    if (!targets) return DG_EINVAL;
-    return seg_launch(groups, n_groups, d_in, d_out, stream, targets, n_targets, flags, counters, xchg);
 }
 
 extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets,

@@ -97,13 +97,6 @@ REASSOC_ROWS = os.environ.get("DG_REASSOC_ROWS", "1") != "0"
 # added 1.7 us to the slowest (rank 4, 110.6 -> 112.3: a wave per (row, relation) walks a hub
 # row's long segment alone), so the max over ranks got worse
 SEG_ROWS_L1 = os.environ.get("DG_SEG_ROWS_L1", "0") != "0"
-# row-split layers in seg mode (config S at N >= 3): DG_SEG_FINISH=1 runs dg_spmm_seg_finish_f32 —
-# the seg launch also finishes each row (its last arriving workgroup), no epilogue launch.  Off
-# by default: measured slower (loopback N = 8 rank share over RCCL 29.1 µs against 25.4 for the
-# seg + epilogue pair, with the peer exchange 42.8 against 30.5; N = 4: 26.3 against 25.0) —
-# every workgroup's write-through partial, drain and arrival atomic cost more latency than the
-# epilogue launch, and with the exchange ≈ 650 workgroups serialise on its arrival counter
-SEG_FINISH = os.environ.get("DG_SEG_FINISH", "0") != "0"
 
 
 def staged_out_chunk(grp, d: int) -> int:
@@ -752,7 +745,6 @@ class ForwardPlan:
                 sviews[et] = send[off:off + sz]
                 off += sz
         partials, specs, staged, reduces, segs = {}, [], [], [], []
-        seg_by_et = {}
         # outside seg mode: layer 2 reassociated (seg_w) and, in layer 1, the row-split groups of
         # SEG_ROWS_L1 — both in dg_spmm_seg_f32
         reassoc = (set(seg_w or {}) | (self.seg_l1 if relu else set())) if not self.seg_mode else set()
@@ -780,33 +772,8 @@ class ForwardPlan:
                     segs.append(self._seg_spec(et, seg_w[et][0], part, seg_w[et][1]))
                 else:
                     segs.append(self._seg_spec(et, xs[et], part))
-                seg_by_et[et] = segs[-1]
             else:
                 specs.append(self._spec(et, xs[et], part, d))
-        if (SEG_FINISH and self.seg_mode and split_t and flat is None and not self.keep_sums and not staged
-                and not specs and len(segs) <= DG_MAX_GROUPS and all(et[0] in split_t for et in rest)
-                and all(any(g.groups[et].n_rels for et in self.targets[i]) for i in split_t)):
-            # every node type row-split and finished by the seg launch itself
-            # (dg_spmm_seg_finish_f32): no epilogue launch, then the exchange — or, with a peer
-            # exchange, the launch pushes the rows and ends with it
-            fin_peer = self._peer_fused(relu)
-            fin_specs, fin_tgts, fin_ets = [], [], []
-            for i in split_t:
-                a, b, blk = self.row_block[i]
-                pad = self._pad[i, 1 if relu else 2]
-                r0 = self.shard.rank * blk
-                ets = [et for et in self.targets[i] if g.groups[et].n_rels]
-                fin_specs += [seg_by_et[et] for et in ets]
-                fin_ets += ets
-                fin_tgts.append((pad[r0:r0 + (b - a)], b - a, len(ets), fin_peer is not None))
-                if fin_peer is None:
-                    gathers.append((pad, pad[r0:r0 + blk]))
-            counters = torch.zeros(sum(t[1] for t in fin_tgts), dtype=torch.int32, device=g.device)
-            launches.append(kernels.PreparedSegFinish(fin_specs, self.h1 if seg_w else d, d, fin_tgts, flags, counters,
-                                                      peer=fin_peer))
-            self.launch_groups[id(launches[-1])] = fin_ets
-            return _Layer(launches, None, False, self.allreduce, [], [], {}, self.side_stream, None, (), gathers,
-                          self.allgather, self._peer_gather_all(gathers, relu))
         if segs:
             d_in = self.h1 if seg_w else d
             seg_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged
@@ -1006,7 +973,7 @@ class ForwardPlan:
     def spmm_launches(self):
         """(layer-1, layer-2) SpMM launches (fused or partial) — what the roofline times."""
         kinds = (kernels.PreparedSpmm, kernels.PreparedFused, kernels.PreparedStaged, kernels.PreparedSeg,
-                 kernels.PreparedFusedSeg, kernels.PreparedSegFinish)
+                 kernels.PreparedFusedSeg)
         pick = lambda L: [l for l in L.launches if isinstance(l, kinds)]
         return pick(self._layer1), pick(self._layer2)
 

@@ -283,53 +283,6 @@ class PreparedSeg:
         check(self._fn(self._arr, self._n, self.d_in, self.d_out, _stream_ptr(stream)), "dg_spmm_seg_f32")
 
 
-class PreparedSegFinish:
-    """A fixed dg_spmm_seg_finish_f32 launch: the groups' chunk partials (each SegSpec's out)
-    and, in the same launch, each target's finished rows — targets = [(out, n_rows, n_groups,
-    push)], the specs listed target by target; counters: int32 [Σ n_rows] zeros (the launch
-    leaves them zero).  peer = (PeerExchange, slot): pushing targets' rows also go to every peer
-    and the launch ends with the exchange."""
-
-    def __init__(self, specs: Sequence[SegSpec], d_in: int, d_out: int, targets, flags: int,
-                 counters: torch.Tensor, peer=None):
-        self._garr = _seg_array(specs, d_in, d_out, True)
-        tarr = (_lib.DgSegFinish * max(1, len(targets)))()
-        if not 1 <= len(targets) <= _lib.DG_MAX_GROUPS:
-            raise ValueError(f"1..{_lib.DG_MAX_GROUPS} targets per launch")
-        g0 = 0
-        for t, (out, n_rows, n_groups, push) in enumerate(targets):
-            _dev(out, torch.float32, "out")
-            if out.numel() < n_rows * d_out:
-                raise ValueError("finished output too small")
-            for s in specs[g0:g0 + n_groups]:
-                if s.n_rows != n_rows:
-                    raise ValueError("a target's groups must have its rows")
-            tarr[t].out, tarr[t].n_rows, tarr[t].g_begin, tarr[t].g_count = out.data_ptr(), n_rows, g0, n_groups
-            tarr[t].target_flags = _lib.DG_EPI_PUSH if (push and peer is not None) else 0
-            if push and peer is not None:
-                peer[0].offset(out)  # raises unless inside the region
-            g0 += n_groups
-        if g0 != len(specs):
-            raise ValueError("the targets must list every group")
-        _dev(counters, torch.int32, "counters")
-        if counters.numel() < sum(t[1] for t in targets):
-            raise ValueError("counters: one per target row")
-        self.specs = list(specs)
-        self._tarr, self._ng, self._nt, self.d_in, self.d_out, self.flags = tarr, len(specs), len(targets), d_in, \
-            d_out, flags
-        self._keep = (list(specs), [t[0] for t in targets], counters)
-        self._cnt = counters.data_ptr()
-        self._xchg = None
-        if peer is not None:
-            self._xchg = ctypes.byref(peer[0].xchg(peer[1]))
-            self._keep = self._keep + (peer[0],)
-        self._fn = _lib.load().dg_spmm_seg_finish_f32
-
-    def __call__(self, stream=None) -> None:
-        check(self._fn(self._garr, self._ng, self._tarr, self._nt, self.d_in, self.d_out, self.flags, self._cnt,
-                       self._xchg, _stream_ptr(stream)), "dg_spmm_seg_finish_f32")
-
-
 class PreparedFusedSeg:
     """A fixed dg_gcn_fused_seg_f32 launch: targets = [(out tensor, n_rows, [SegSpec], relu)],
     each output row finished by one workgroup, one wave per relation (at most 16 a row; groups

@@ -184,10 +184,9 @@ class RelationShard:
         if form == "seg":
             if any(K % world_size for K in edge_types.values()):
                 raise ValueError("every group must hold world_size relation sets")
-            # relation sets per chunk (A/B knob DG_S_SETS: 2 halves the chunk partials a row's
-            # finish adds, at twice the waves per workgroup)
-            spc = max(1, int(os.environ.get("DG_S_SETS", "1")))
-            sh.chunks = {et: K // world_size * spc for et, K in edge_types.items()}
+            # one relation set per chunk (two sets a chunk — half the partials a row's epilogue
+            # adds, twice the waves a workgroup — measured the same: 24.35 vs 24.38 µs at N = 8)
+            sh.chunks = {et: K // world_size for et, K in edge_types.items()}
             sh.seg_rows = True
         else:
             sh.chunks = dict(edge_types)

@@ -412,34 +412,6 @@ int dg_gcn_fused_seg_peer_f32(const dg_seg_group* groups /* HOST */, int32_t n_g
                               const dg_fused_target* targets /* HOST */, int32_t n_targets, int32_t d_in,
                               int32_t d_out, const dg_peer_xchg* xchg /* HOST */, void* stream);
 
-/* dg_spmm_seg_f32 that also finishes the rows: the seg + epilogue pair of a row-split layer
- * (config S at N >= 4) in ONE launch.  Every group belongs to exactly one target, the targets
- * listing the groups in order (g_begin = the previous target's end); each group's `out` holds
- * its chunk partials as for dg_spmm_seg_f32 (stored write-through).  Per target t and row
- * r < n_rows, once every (group, chunk) workgroup covering the row has stored its partial
- * (arrival counters[off_t + r], off_t = the earlier targets' rows; zero before the first launch,
- * left zero), the last of them writes
- *
- *   out_t[r] = act( sum_g l2norm( sum_c partial_g[c][r] ) )
- *
- * with l2norm / act as dg_gcn_epilogue_multi_f32's flags (DG_EPI_L2NORM, DG_EPI_RELU) — the same
- * sums in the same order, so the rows are bitwise the pair's.  xchg != NULL: the rows of
- * targets with DG_EPI_PUSH (their `out` inside the exchange region) also go to every peer and
- * the launch ends with the exchange (dg_gcn_epilogue_peer_f32's).
- * Replaces layers.py:85-94 / 109-118 and model.py:74-75, 85-88 for a rank's row block. */
-typedef struct dg_seg_finish {
-    float* out;                 /* device [n_rows][d_out]                                   */
-    int32_t n_rows;             /* every group of the target has n_rows rows                */
-    int32_t g_begin;
-    int32_t g_count;
-    int32_t target_flags;       /* 0 or DG_EPI_PUSH                                         */
-} dg_seg_finish;
-
-int dg_spmm_seg_finish_f32(const dg_seg_group* groups /* HOST */, int32_t n_groups,
-                           const dg_seg_finish* targets /* HOST */, int32_t n_targets, int32_t d_in,
-                           int32_t d_out, int32_t flags, uint32_t* counters /* device */,
-                           const dg_peer_xchg* xchg /* HOST, or NULL */, void* stream);
-
 /* --------------------------------------------------------------------------------------
  * Batched strided fp32 GEMM on the f32-input MFMA (v_mfma_f32_32x32x2_f32, exact fp32):
  *

@@ -108,16 +108,11 @@ def test_abi_rejects_bad_arguments_without_a_device():
     e = (_lib.DgEpiGroup * 1)()
     assert lib.dg_gcn_epilogue_f32(e, 1, None, 10, 64, 128, None) == _lib.DG_EINVAL  # bad flags
     assert lib.dg_unigram_sample(None, 0, 5, 0, 0, None, None) == _lib.DG_EINVAL
-    # the finishing seg launch: targets must exist, partition the groups in order, and carry
-    # only the epilogue's flags; counters are required
-    sg = (_lib.DgSegGroup * 1)()
-    fin = (_lib.DgSegFinish * 1)()
-    assert lib.dg_spmm_seg_finish_f32(sg, 1, None, 1, 64, 64, 1, 16, None, None) == _lib.DG_EINVAL
-    fin[0].g_begin, fin[0].g_count, fin[0].n_rows = 0, 2, 10  # two groups, one given
-    assert lib.dg_spmm_seg_finish_f32(sg, 1, fin, 1, 64, 64, 1, 16, None, None) == _lib.DG_EINVAL
-    fin[0].g_count = 1
-    assert lib.dg_spmm_seg_finish_f32(sg, 1, fin, 1, 64, 64, 8, 16, None, None) == _lib.DG_EINVAL  # bad flags
-    assert lib.dg_spmm_seg_finish_f32(sg, 1, fin, 1, 64, 64, 1, None, None, None) == _lib.DG_EINVAL  # no counters
+    # a pushed group sum needs a peer exchange descriptor (dg_gcn_epilogue_peer_f32), and the
+    # bf16 scorers need the tables' row counts (ABI 34)
+    t = (_lib.DgEpiTarget * 1)()
+    assert lib.dg_gcn_epilogue_peer_f32(t, 1, 64, 1, None, None) == _lib.DG_EINVAL
+    assert lib.dg_decoder_score_bf16_paired(*([None, 256, 0, None, 256, 0] + [None] * 3 + [1, None, None, 256, None, None])) == _lib.DG_EINVAL
 
 
 def test_merge_chunks_layout():

@@ -152,17 +152,8 @@ def _forward_rank(rank, world, kind, mode):
 
     from decagon_amd.peer import PeerConfig, dist_gather
 
-    from decagon_amd import engine, kernels
-
     g = _graph(kind, world)
-    saved = engine.SEG_FINISH
-    engine.SEG_FINISH = mode == "fused-finish"  # the seg launches finish their rows and exchange
-    try:
-        plan = _plan(kind, g, rank, world, PeerConfig(mode=mode.split("-")[0], gather=dist_gather()))
-    finally:
-        engine.SEG_FINISH = saved
-    if mode == "fused-finish":
-        assert any(isinstance(l, kernels.PreparedSegFinish) for l in plan._layer1.launches)
+    plan = _plan(kind, g, rank, world, PeerConfig(mode=mode, gather=dist_gather()))
     info = {"seg": plan.seg_mode, "exchanges": sum(L.has_exchange for L in (plan._layer1, plan._layer2)),
             "peer_reduce": plan.peer_reduce,
             "fused_kinds": sorted({type(l).__name__ for l in plan._layer1.launches}),
@@ -234,8 +225,7 @@ def _oracle(kind, g):
 
 @pytest.mark.parametrize("kind,world,mode", [("S", 2, "fused"), ("S", 4, "fused"), ("S", 8, "fused"),
                                              ("S", 2, "kernel"), ("S", 8, "kernel"), ("P", 2, "fused"),
-                                             ("P", 4, "fused"), ("P", 8, "fused"), ("P", 4, "kernel"),
-                                             ("S", 4, "fused-finish")])
+                                             ("P", 4, "fused"), ("P", 8, "fused"), ("P", 4, "kernel")])
 def test_peer_exchange_forward_matches_oracle(kind, world, mode):
     _need_gpu()
     got = run_ranks(_forward_rank, world, (kind, mode))
@@ -244,7 +234,7 @@ def test_peer_exchange_forward_matches_oracle(kind, world, mode):
     for r in range(world):
         info, outs, base, state = got[r]
         assert state[16] == 0, (r, hex(state[16]))  # the error word
-        if mode.startswith("fused"):
+        if mode == "fused":
             # the finishing launches exchange (config P: the drug sums by the peer all-reduce
             # too — no RCCL / gloo collective left in the step)
             assert info["exchanges"] == 0, info
