@@ -7,8 +7,9 @@ Writes scripts/hazard/*.hsaco (git-ignored; they travel to the GPU box with the 
                      unpaired by an opaque copy)
   failing.hsaco      the same source without the opaque copy — the build that returned wrong
                      half-0 scores on ~2 % of tiles — assembled from its own .s, unchanged
-  <site>.hsaco       that .s with wait states inserted at ONE candidate site (below), nothing
-                     else changed, so a build that stops failing names the sequence
+  <site>.hsaco       that .s with ONE candidate site changed (wait states inserted, or one
+                     register renamed), nothing else, so a build that stops failing names the
+                     sequence
 """
 from __future__ import annotations
 
@@ -99,6 +100,39 @@ def edit_srcc(lines):
     return out, n
 
 
+def _find(lines, text, start=0):
+    return next(i for i in range(start, len(lines)) if lines[i].strip() == text)
+
+
+def edit_addr_own(lines):
+    """ep[0]'s load addressed through its own destination register (v114) instead of v66,
+    which the next load (en[0]) overwrites with its returning data."""
+    out = list(lines)
+    i = _find(out, "v_add_u32_e32 v66, s6, v109")
+    j = _find(out, "buffer_load_dwordx4 v[114:117], v66, s[44:47], 0 offen", i)
+    out[i] = "\tv_add_u32_e32 v114, s6, v109"
+    out[j] = "\tbuffer_load_dwordx4 v[114:117], v114, s[44:47], 0 offen"
+    return out, 1
+
+
+def edit_drain_ep0(lines):
+    """s_waitcnt vmcnt(0) right after ep[0]'s load: en[0]'s load issues once ep[0]'s data is in."""
+    out = list(lines)
+    j = _find(out, "buffer_load_dwordx4 v[114:117], v66, s[44:47], 0 offen")
+    out.insert(j + 1, "\ts_waitcnt vmcnt(0)")
+    return out, 1
+
+
+def edit_wait_all(lines):
+    """The q loop's first row-load waits (vmcnt(3), vmcnt(1)) as vmcnt(0)."""
+    out = list(lines)
+    i = _find(out, "v_add_u32_e32 v66, s6, v109")
+    a = _find(out, "s_waitcnt vmcnt(3)", i)
+    b = _find(out, "s_waitcnt vmcnt(1)", a)
+    out[a] = out[b] = "\ts_waitcnt vmcnt(0)"
+    return out, 2
+
+
 def main() -> int:
     OUT.mkdir(parents=True, exist_ok=True)
     with tempfile.TemporaryDirectory() as td:
@@ -118,7 +152,8 @@ def main() -> int:
         failing = compile_s(src.replace(FENCE, "/* opaque copy removed */"), inc, work, "failing")
         assemble(failing, work, "failing")
         lines = failing.splitlines()
-        for name, fn in (("pk_nop", edit_pk), ("srcc_nop", edit_srcc)):
+        for name, fn in (("pk_nop", edit_pk), ("srcc_nop", edit_srcc), ("addr_own", edit_addr_own),
+                         ("drain_ep0", edit_drain_ep0), ("wait_all", edit_wait_all)):
             edited, n = fn(lines)
             assemble("\n".join(edited) + "\n", work, name)
             print(f"{name}: {n} site(s) edited")
