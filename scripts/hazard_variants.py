@@ -133,6 +133,34 @@ def edit_wait_all(lines):
     return out, 2
 
 
+def _q_loop(lines):
+    """(first, last) line of the fused kernel's q loop: from the row loads' address adds to
+    the loop's back-edge branch."""
+    i = _find(lines, "v_add_u32_e32 v66, s6, v109")
+    j = next(k for k in range(i, len(lines)) if lines[k].strip().startswith("s_cbranch_scc0"))
+    return i, j
+
+
+def edit_pk_nop_all(lines):
+    """s_nop 4 before every v_pk_* instruction of the q loop (the whole packed epilogue)."""
+    a, b = _q_loop(lines)
+    out, n = list(lines), 0
+    for i in range(b, a, -1):
+        if lines[i].strip().startswith("v_pk_"):
+            out.insert(i, "\ts_nop 4")
+            n += 1
+    return out, n
+
+
+def edit_bperm_nop(lines):
+    """s_nop 7 before the first cross-lane shuffle of the sums after the q loop."""
+    a, b = _q_loop(lines)
+    out = list(lines)
+    k = next(i for i in range(b, len(lines)) if lines[i].strip().startswith("ds_bpermute_b32"))
+    out.insert(k, "\ts_nop 7")
+    return out, 1
+
+
 def main() -> int:
     OUT.mkdir(parents=True, exist_ok=True)
     with tempfile.TemporaryDirectory() as td:
@@ -153,7 +181,8 @@ def main() -> int:
         assemble(failing, work, "failing")
         lines = failing.splitlines()
         for name, fn in (("pk_nop", edit_pk), ("srcc_nop", edit_srcc), ("addr_own", edit_addr_own),
-                         ("drain_ep0", edit_drain_ep0), ("wait_all", edit_wait_all)):
+                         ("drain_ep0", edit_drain_ep0), ("wait_all", edit_wait_all),
+                         ("pk_nop_all", edit_pk_nop_all), ("bperm_nop", edit_bperm_nop)):
             edited, n = fn(lines)
             assemble("\n".join(edited) + "\n", work, name)
             print(f"{name}: {n} site(s) edited")
