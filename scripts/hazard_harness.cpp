@@ -130,6 +130,7 @@ int main(int argc, char** argv) {
         void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
         const int nr = v == 2 ? 1 : runs;
         long bad_pos = 0, bad_neg = 0, bad_halves = 0, max_halves = 0;
+        std::vector<int> hits(nh / 16, 0);  // per half tile: runs in which it differed
         for (int r = 0; r < nr; ++r) {
             CK(hipMemset(out, 0, (size_t)2 * nh * 4));
             CK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, lds, 0, nullptr, extra));
@@ -146,14 +147,24 @@ int main(int argc, char** argv) {
                 bad_pos += bp;
                 bad_neg += bn;
                 halves += bp || bn;
+                hits[h] += bp || bn;
             }
             bad_halves += halves;
             if (halves > max_halves) max_halves = halves;
         }
+        // how repeatable: half tiles that differed in every run, in some, and the tile / half /
+        // lane-position spread of the failures (a wave's tile slot is tile % 3072, etc.)
+        long always = 0, some = 0, half0 = 0, half1 = 0;
+        for (int h = 0; h < nh / 16; ++h) {
+            always += hits[h] == nr;
+            some += hits[h] > 0;
+            if (hits[h]) (h % 2 ? half1 : half0) += 1;
+        }
         if (v > 2)
             printf("{\"build\": \"%s\", \"runs\": %d, \"half_tiles\": %d, \"bad_halves\": %ld, \"max_per_run\": %ld, "
-                   "\"bad_pos_halves\": %ld, \"bad_neg_halves\": %ld}\n",
-                   argv[v], nr, nh / 16, bad_halves, max_halves, bad_pos, bad_neg);
+                   "\"bad_pos_halves\": %ld, \"bad_neg_halves\": %ld, \"halves_bad_in_every_run\": %ld, "
+                   "\"halves_bad_in_some_run\": %ld, \"first_half\": %ld, \"second_half\": %ld}\n",
+                   argv[v], nr, nh / 16, bad_halves, max_halves, bad_pos, bad_neg, always, some, half0, half1);
         fflush(stdout);
         CK(hipModuleUnload(m));
     }
