@@ -34,12 +34,7 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 
 constexpr int kCsThreads = 768;    // column-shared paired kernel: threads per workgroup (one per CU)
 constexpr int kCs16Threads = 768;
-#ifndef DG_DEC_UAUX
-#define DG_DEC_UAUX 0  // A/B: cache policy of the u-row loads (16: sc1, L1 bypassed; 2: nt)
-#endif
-#ifndef DG_DEC_VAUX
-#define DG_DEC_VAUX 0
-#endif  // config 5's 16x16x32 kernel (704: 208.6 vs 205.6 us)
+  // config 5's 16x16x32 kernel (704: 208.6 vs 205.6 us)
 
 struct Bf16DecArgs {
     const uint16_t* row_table;
@@ -499,7 +494,7 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
             const int vo = 2 * (cur.pc[b] * (int)a.ld_col + 8 * g);
 #pragma unroll
             for (int s = 0; s < 8; ++s)
-                vv[b][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(crs, vo + 64 * s, 0, DG_DEC_VAUX));
+                vv[b][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(crs, vo + 64 * s, 0, 0));
         }
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
@@ -526,8 +521,8 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
             uint4 ep[2], en[2];
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
-                ep[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, up[b] + 64 * q, 0, DG_DEC_UAUX));
-                en[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, un[b] + 64 * q, 0, DG_DEC_UAUX));
+                ep[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, up[b] + 64 * q, 0, 0));
+                en[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, un[b] + 64 * q, 0, 0));
             }
 
             f32x4 acc[2][2] = {};
