@@ -161,6 +161,16 @@ def edit_bperm_nop(lines):
     return out, 1
 
 
+def edit_mfma_drain(lines):
+    """24 wait states after the q loop's last MFMA, before the epilogue touches any register:
+    every MFMA has finished writing its accumulator, even behind other waves' MFMAs."""
+    a, b = _q_loop(lines)
+    last = max(i for i in range(a, b) if lines[i].strip().startswith("v_mfma"))
+    out = list(lines)
+    out[last + 1:last + 1] = ["\ts_nop 7", "\ts_nop 7", "\ts_nop 7"]
+    return out, 1
+
+
 def main() -> int:
     OUT.mkdir(parents=True, exist_ok=True)
     with tempfile.TemporaryDirectory() as td:
@@ -182,7 +192,8 @@ def main() -> int:
         lines = failing.splitlines()
         for name, fn in (("pk_nop", edit_pk), ("srcc_nop", edit_srcc), ("addr_own", edit_addr_own),
                          ("drain_ep0", edit_drain_ep0), ("wait_all", edit_wait_all),
-                         ("pk_nop_all", edit_pk_nop_all), ("bperm_nop", edit_bperm_nop)):
+                         ("pk_nop_all", edit_pk_nop_all), ("bperm_nop", edit_bperm_nop),
+                         ("mfma_drain", edit_mfma_drain)):
             edited, n = fn(lines)
             assemble("\n".join(edited) + "\n", work, name)
             print(f"{name}: {n} site(s) edited")
