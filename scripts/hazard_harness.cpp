@@ -131,6 +131,10 @@ int main(int argc, char** argv) {
         const int nr = v == 2 ? 1 : runs;
         long bad_pos = 0, bad_neg = 0, bad_halves = 0, max_halves = 0;
         std::vector<int> hits(nh / 16, 0);  // per half tile: runs in which it differed
+        long pairs_hist[17] = {0};          // failing half tiles by how many of their 16 pairs differ
+        long iter_hist[16] = {0};           // ... by the wave's tile iteration (tile / (blocks * waves))
+        long wave_hist[12] = {0};           // ... by the wave within its workgroup
+        int shown = 0;
         for (int r = 0; r < nr; ++r) {
             CK(hipMemset(out, 0, (size_t)2 * nh * 4));
             CK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, lds, 0, nullptr, extra));
@@ -148,6 +152,20 @@ int main(int argc, char** argv) {
                 bad_neg += bn;
                 halves += bp || bn;
                 hits[h] += bp || bn;
+                if (bp || bn) {
+                    int np = 0;
+                    for (int i = 16 * h; i < 16 * h + 16; ++i) np += memcmp(&got[i], &ref[i], 4) != 0;
+                    pairs_hist[np]++;
+                    const int tile = h / 2, stride = blocks * waves;
+                    iter_hist[tile / stride < 15 ? tile / stride : 15]++;
+                    wave_hist[(tile % stride) / blocks]++;
+                    if (shown < 3 && v > 2) {
+                        ++shown;
+                        fprintf(stderr, "%s run %d half %d (tile %d, half %d):", argv[v], r, h, h / 2, h % 2);
+                        for (int i = 16 * h; i < 16 * h + 16; ++i) fprintf(stderr, " %.6g/%.6g", got[i], ref[i]);
+                        fprintf(stderr, "\n");
+                    }
+                }
             }
             bad_halves += halves;
             if (halves > max_halves) max_halves = halves;
@@ -160,11 +178,21 @@ int main(int argc, char** argv) {
             some += hits[h] > 0;
             if (hits[h]) (h % 2 ? half1 : half0) += 1;
         }
+        if (v > 2) {
+            printf("{\"build\": \"%s\", \"by_tile_iteration\": [", argv[v]);
+            for (int i = 0; i < 16; ++i) printf("%ld%s", iter_hist[i], i < 15 ? "," : "]");
+            printf(", \"by_wave\": [");
+            for (int i = 0; i < 12; ++i) printf("%ld%s", wave_hist[i], i < 11 ? "," : "]}\n");
+        }
         if (v > 2)
             printf("{\"build\": \"%s\", \"runs\": %d, \"half_tiles\": %d, \"bad_halves\": %ld, \"max_per_run\": %ld, "
                    "\"bad_pos_halves\": %ld, \"bad_neg_halves\": %ld, \"halves_bad_in_every_run\": %ld, "
-                   "\"halves_bad_in_some_run\": %ld, \"first_half\": %ld, \"second_half\": %ld}\n",
-                   argv[v], nr, nh / 16, bad_halves, max_halves, bad_pos, bad_neg, always, some, half0, half1);
+                   "\"halves_bad_in_some_run\": %ld, \"first_half\": %ld, \"second_half\": %ld, "
+                   "\"failing_halves_by_pairs_wrong\": [%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld]}\n",
+                   argv[v], nr, nh / 16, bad_halves, max_halves, bad_pos, bad_neg, always, some, half0, half1,
+                   pairs_hist[0], pairs_hist[1], pairs_hist[2], pairs_hist[3], pairs_hist[4], pairs_hist[5], pairs_hist[6],
+                   pairs_hist[7], pairs_hist[8], pairs_hist[9], pairs_hist[10], pairs_hist[11], pairs_hist[12],
+                   pairs_hist[13], pairs_hist[14], pairs_hist[15], pairs_hist[16]);
         fflush(stdout);
         CK(hipModuleUnload(m));
     }
