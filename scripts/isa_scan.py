@@ -1,13 +1,12 @@
-"""Scan the gfx950 code objects of a built library for a VALU -> packed-f32 read pattern.
+"""Disassemble the gfx950 code objects of a built library (or a code object) into kernels.
 
 Usage: python scripts/isa_scan.py [LIB_OR_CODE_OBJECT ...]   (default: the shipping library)
 
-It extracts every gfx950 code object (llvm-objdump --offloading, into a temp dir), disassembles
-it, and reports, per kernel, every `v_pk_*` instruction that reads as a 64-bit source a VGPR
-pair one half of which was written by one of the N VALU instructions right before it while
-the other half was not (a pair assembled from two writes just before the packed read).
-DESIGN.md §5 ("The packed-f32 forwarding hazard") says why: that is the sequence config 5's
-fused kernel ran when it returned wrong half-0 sums.
+It extracts every gfx950 code object (llvm-objdump --offloading, into a temp dir, never next
+to the library), disassembles it and parses each kernel's instructions (mnemonic, VGPR
+destination, VGPR sources).  tests/test_cpu_isa.py uses it to pin the config-5 kernel's
+validated instruction selection ("The config-5 miscompile"); run as a script it
+prints, per kernel, the MFMA and packed-fp32 instruction counts.
 """
 from __future__ import annotations
 
@@ -19,7 +18,7 @@ import sys
 import tempfile
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import Dict, List, Optional, Tuple
+from typing import List, Optional, Tuple
 
 LLVM = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib" / "llvm" / "bin"
 ROOT = Path(__file__).resolve().parent.parent
@@ -36,15 +35,6 @@ class Insn:
     dst: Optional[Tuple[int, int]]      # (first VGPR, count) written, VALU only
     srcs: List[Tuple[int, int]]         # VGPR operands read
     text: str
-
-
-@dataclass
-class Finding:
-    kernel: str
-    index: int                          # instruction index in the kernel
-    distance: int                       # 1: the writer is the instruction right before
-    writer: str
-    reader: str
 
 
 @dataclass
@@ -93,27 +83,6 @@ def parse(asm: str) -> List[Kernel]:
     return kernels
 
 
-def scan_kernel(k: Kernel, window: int = 1) -> List[Finding]:
-    """v_pk_* reads of a 64-bit VGPR pair one half of which a VALU instruction at most
-    `window` instructions before wrote alone (32-bit destination)."""
-    found = []
-    for i, ins in enumerate(k.insns):
-        if not ins.op.startswith("v_pk_"):
-            continue
-        for base, n in ins.srcs:
-            if n != 2:
-                continue
-            for d in range(1, window + 1):
-                if i - d < 0:
-                    break
-                w = k.insns[i - d]
-                if w.dst is None or w.dst[1] != 1 or w.op.startswith("v_pk_"):
-                    continue
-                if w.dst[0] in (base, base + 1):
-                    found.append(Finding(k.name, i, d, w.text, ins.text))
-    return found
-
-
 def extract_code_objects(lib: Path, workdir: Path) -> List[Path]:
     """gfx950 code objects inside a host library (or the file itself if it is one)."""
     head = lib.read_bytes()[:64]
@@ -132,29 +101,24 @@ def disassemble(co: Path) -> str:
     return r.stdout
 
 
-def scan_library(lib: Path = DEFAULT_LIB, window: int = 1) -> Tuple[Dict[str, int], List[Finding]]:
-    """(v_pk_* count per kernel, findings) over every gfx950 code object of `lib`."""
-    counts: Dict[str, int] = {}
-    findings: List[Finding] = []
+def kernels(lib: Path = DEFAULT_LIB) -> List[Kernel]:
+    """Every kernel of every gfx950 code object of `lib`."""
+    out: List[Kernel] = []
     with tempfile.TemporaryDirectory() as td:
         for co in extract_code_objects(Path(lib), Path(td)):
-            for k in parse(disassemble(co)):
-                counts[k.name] = counts.get(k.name, 0) + sum(1 for x in k.insns if x.op.startswith("v_pk_"))
-                findings += scan_kernel(k, window)
-    return counts, findings
+            out += parse(disassemble(co))
+    return out
 
 
 def main(argv: List[str]) -> int:
-    libs = [Path(a) for a in argv] or [DEFAULT_LIB]
-    bad = 0
-    for lib in libs:
-        counts, findings = scan_library(lib, window=int(os.environ.get("DG_ISA_WINDOW", "1")))
-        print(f"{lib}: {len(counts)} kernels, {sum(counts.values())} v_pk_* instructions, "
-              f"{len(findings)} findings")
-        for f in findings:
-            print(f"  {f.kernel}  [{f.index}] d={f.distance}\n    {f.writer}\n    {f.reader}")
-        bad += len(findings)
-    return 1 if bad else 0
+    for lib in [Path(a) for a in argv] or [DEFAULT_LIB]:
+        ks = kernels(lib)
+        print(f"{lib}: {len(ks)} kernels")
+        for k in ks:
+            n_mfma = sum(x.op.startswith("v_mfma") for x in k.insns)
+            n_pk = sum(x.op.startswith("v_pk_") for x in k.insns)
+            print(f"  {len(k.insns):6d} insns  {n_mfma:4d} mfma  {n_pk:4d} v_pk  {k.name[:100]}")
+    return 0
 
 
 if __name__ == "__main__":
