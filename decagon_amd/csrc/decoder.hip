@@ -238,7 +238,10 @@ __global__ __launch_bounds__(256) void hinge_multi_kernel(const float* pos, cons
     }
 }
 
-__device__ __forceinline__ float softplus_neg_abs(float x) { return log1pf(expf(-fabsf(x))); }
+// log1p in double: the float log1pf's double-float arithmetic is vectorised by the compiler into
+// packed adds whose low result reads src1's high dword, the form this library keeps out of
+// every kernel (tests/test_cpu_isa.py); the double result rounds to within an ulp
+__device__ __forceinline__ float softplus_neg_abs(float x) { return (float)log1p((double)expf(-fabsf(x))); }
 
 __global__ __launch_bounds__(256) void xent_kernel(const float* pos, const float* neg, int n,
                                                    float w, float* loss) {

@@ -574,11 +574,14 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
                     }
                 }
                 // Each half's sums pass through an opaque copy, so the compiler cannot pair
-                // the two halves' chains into v_pk_fma_f32 (as it does in the FUSED form
-                // without this).  With that pairing the MI355X returned a wrong low-half sum
-                // (pos of half 0) for ≈ 2 % of tiles, varying from run to run. Measured: 15-25
-                // of 640 tiles bad per run without the copy, none in 4 runs with it. The
-                // paired form's epilogue is not paired by the compiler (plain v_fmac_f32).
+                // the two halves' chains into packed fp32 ops (as it does in the FUSED form
+                // without this).  The paired form multiplies u_p[i]·D_k[i] of both halves by
+                // `v_pk_mul_f32 D, A, B op_sel:[0,1]` (low result from src1's high dword), and
+                // on the MI355X that instruction intermittently returned 0 for lanes 48-63 in
+                // this kernel: every wrong score (~2 % of half tiles per launch) is the right
+                // one minus exactly one such product of lane group 3 (DESIGN.md §5,
+                // scripts/hazard_match.py).  tests/test_cpu_isa.py keeps the form out of the
+                // library.
                 asm volatile("" : "+v"(pp[b]), "+v"(pn[b]));
             }
         }

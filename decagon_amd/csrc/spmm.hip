@@ -27,9 +27,6 @@
 #include "dropout.h"
 #include "peer.h"
 
-#ifndef DG_FUSED_ABL
-#define DG_FUSED_ABL 0  // timing ablations only (wrong results): 1 no gathers, 8 empty kernels
-#endif
 #ifndef DG_PROJ_UNROLL
 #define DG_PROJ_UNROLL 16  // W loads per batch of the projection chain (measured: 8 → 16 −0.4 µs at S)
 #endif
@@ -142,9 +139,7 @@ __device__ __forceinline__ void gather_step(float4& acc, const float* __restrict
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const bool ok = qact && (s0 + u * G + sub) < n;
-        xv[u] = ok ? ((DG_FUSED_ABL & 1) ? make_float4(1.f, 1.f, 1.f, 1.f)
-                                         : *reinterpret_cast<const float4*>(xq + o[u]))
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
         if (!ok) w[u] = 0.f;
     }
 #pragma unroll
@@ -352,9 +347,6 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, const int b) {
         reinterpret_cast<float4*>(hrow[slot])[lane] = tot;
     }
     if (a.n_projs == 0) return;  // launch-uniform
-#ifdef DG_FUSED_NOPROJ  // timing ablation only (wrong results)
-    return;
-#endif
     __syncthreads();
     // every projection output (entry, relation, column) of this target in one index space, so
     // the block's threads run a single load/fmaf chain each instead of one chain per entry
@@ -399,7 +391,6 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, const int b) {
 
 template <int LP>
 __global__ __launch_bounds__(1024) void gcn_fused_kernel(const FusedArgs a) {
-    if (DG_FUSED_ABL & 8) return;
     fused_body<LP>(a, blockIdx.x);
 }
 

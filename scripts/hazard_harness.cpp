@@ -121,6 +121,26 @@ int main(int argc, char** argv) {
     const unsigned lds = D * D * 2 + waves * D * 2;
     const char* name = "_ZN12_GLOBAL__N_124decoder_bf16_cs16_kernelILi768ELb1EEEvNS_11Bf16DecArgsE";
     std::vector<float> ref((size_t)2 * nh), got((size_t)2 * nh);
+    // HZ_DUMP=DIR: the inputs and, per variant, the reference's and the first failing run's
+    // scores as raw little-endian arrays, so a failure can be matched against candidate causes
+    // on the host (scripts/hazard_match.py)
+    const char* dump = getenv("HZ_DUMP");
+    auto write = [&](const char* name, const void* p, size_t n) {
+        if (!dump) return;
+        char path[512];
+        snprintf(path, sizeof path, "%s/%s", dump, name);
+        FILE* f = fopen(path, "wb");
+        if (!f || fwrite(p, 1, n, f) != n) {
+            fprintf(stderr, "cannot write %s\n", path);
+            exit(2);
+        }
+        fclose(f);
+    };
+    write("E.bin", E.data(), E.size() * 2);
+    write("R.bin", R.data(), R.size() * 2);
+    write("L.bin", L.data(), L.size() * 2);
+    write("rows.bin", rows.data(), nh * 4);
+    write("cols.bin", cols.data(), nh * 4);
     for (int v = 2; v < argc; ++v) {
         hipModule_t m;
         hipFunction_t f;
@@ -135,12 +155,16 @@ int main(int argc, char** argv) {
         long iter_hist[16] = {0};           // ... by the wave's tile iteration (tile / (blocks * waves))
         long wave_hist[12] = {0};           // ... by the wave within its workgroup
         int shown = 0;
+        bool dumped = false;
         for (int r = 0; r < nr; ++r) {
             CK(hipMemset(out, 0, (size_t)2 * nh * 4));
             CK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, lds, 0, nullptr, extra));
             CK(hipDeviceSynchronize());
             CK(hipMemcpy(v == 2 ? ref.data() : got.data(), out, (size_t)2 * nh * 4, hipMemcpyDeviceToHost));
-            if (v == 2) break;
+            if (v == 2) {
+                write("ref.bin", ref.data(), ref.size() * 4);
+                break;
+            }
             long halves = 0;
             for (int h = 0; h < nh / 16; ++h) {
                 bool bp = false, bn = false;
@@ -166,6 +190,13 @@ int main(int argc, char** argv) {
                         fprintf(stderr, "\n");
                     }
                 }
+            }
+            if (halves && !dumped) {
+                dumped = true;
+                char name[300];
+                const char* base = strrchr(argv[v], '/');
+                snprintf(name, sizeof name, "got_%s.bin", base ? base + 1 : argv[v]);
+                write(name, got.data(), got.size() * 4);
             }
             bad_halves += halves;
             if (halves > max_halves) max_halves = halves;

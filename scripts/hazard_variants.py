@@ -171,6 +171,102 @@ def edit_mfma_drain(lines):
     return out, 1
 
 
+def _reorder_loads(lines, order, waits):
+    """The q loop's four row loads (ep[0], en[0], ep[1], en[1]) issued in `order` (ep[0]
+    addressed through its own destination register, as in addr_own, so no load's returning
+    data overwrites another's address), and its first two waits set to `waits`."""
+    out = list(lines)
+    i = _find(out, "v_add_u32_e32 v66, s6, v109")
+    out[i] = "\tv_add_u32_e32 v114, s6, v109"
+    loads = {"ep0": "\tbuffer_load_dwordx4 v[114:117], v114, s[44:47], 0 offen",
+             "en0": "\tbuffer_load_dwordx4 v[66:69], v67, s[44:47], 0 offen",
+             "ep1": "\tbuffer_load_dwordx4 v[82:85], v70, s[44:47], 0 offen",
+             "en1": "\tbuffer_load_dwordx4 v[70:73], v71, s[44:47], 0 offen"}
+    j = _find(out, "buffer_load_dwordx4 v[114:117], v66, s[44:47], 0 offen", i)
+    assert [out[j + 2 * k].strip() for k in range(1, 4)] == [loads[n].strip() for n in ("en0", "ep1", "en1")]
+    for k, n in enumerate(order):
+        out[j + 2 * k] = loads[n]
+    a = _find(out, "s_waitcnt vmcnt(3)", j)
+    b = _find(out, "s_waitcnt vmcnt(1)", a)
+    out[a], out[b] = (f"\ts_waitcnt vmcnt({w})" for w in waits)
+    return out, 1
+
+
+def edit_ep0_last(lines):
+    """ep[0]'s row load issued last of the four instead of first (both waits vmcnt(0))."""
+    return _reorder_loads(lines, ("en0", "ep1", "en1", "ep0"), (0, 0))
+
+
+def edit_en0_first(lines):
+    """en[0]'s row load issued first, ep[0]'s second (first wait vmcnt(2))."""
+    return _reorder_loads(lines, ("en0", "ep0", "ep1", "en1"), (2, 1))
+
+
+_PK = re.compile(r"(v_pk_(?:fma|mul|add)_f32) v\[(\d+):\d+\], (.*?)(?: op_sel:\[([01,]+)\])?(?: op_sel_hi:\[([01,]+)\])?$")
+
+
+def _unpack(line):
+    """One packed fp32 instruction as two scalar VOP3 ones with the same operands and half
+    selects (lo result: op_sel, hi result: op_sel_hi), ordered so neither clobbers a source
+    of the other."""
+    m = _PK.match(line.strip())
+    op, d, rest, sel, selhi = m.groups()
+    srcs = [int(x) for x in re.findall(r"v\[(\d+):\d+\]", rest)]
+    n = len(srcs)
+    sel = [int(x) for x in sel.split(",")] if sel else [0] * n
+    selhi = [int(x) for x in selhi.split(",")] if selhi else [1] * n
+    sop = {"v_pk_fma_f32": "v_fma_f32", "v_pk_mul_f32": "v_mul_f32", "v_pk_add_f32": "v_add_f32"}[op]
+    d = int(d)
+    lo_src = [s + k for s, k in zip(srcs, sel)]
+    hi_src = [s + k for s, k in zip(srcs, selhi)]
+    lo = f"\t{sop} v{d}, " + ", ".join(f"v{r}" for r in lo_src)
+    hi = f"\t{sop} v{d + 1}, " + ", ".join(f"v{r}" for r in hi_src)
+    if d in hi_src:
+        assert d + 1 not in lo_src, line
+        return [hi, lo]
+    return [lo, hi]
+
+
+def _unpack_where(lines, pred):
+    a, b = _q_loop(lines)
+    out, n = list(lines), 0
+    for i in range(b, a, -1):
+        t = lines[i].strip()
+        if t.startswith("v_pk_") and pred(t):
+            out[i:i + 1] = _unpack(t)
+            n += 1
+    return out, n
+
+
+def edit_unpack_all(lines):
+    """Every packed fp32 instruction of the q loop as two scalar ones (same registers)."""
+    return _unpack_where(lines, lambda t: True)
+
+
+def edit_unpack_sel01(lines):
+    """Only the v_pk_mul_f32 with op_sel:[0,1] (the low result reads src1's high dword)."""
+    return _unpack_where(lines, lambda t: t.startswith("v_pk_mul_f32") and "op_sel:[0,1]" in t)
+
+
+def edit_unpack_selhi10(lines):
+    """Only the v_pk_mul_f32 with op_sel_hi:[1,0] (the high result reads src1's low dword)."""
+    return _unpack_where(lines, lambda t: t.startswith("v_pk_mul_f32") and "op_sel_hi:[1,0]" in t)
+
+
+def edit_swap_sel01(lines):
+    """Each v_pk_mul_f32 D, A, B op_sel:[0,1] as v_pk_mul_f32 D, B, A op_sel:[1,0]: the same
+    products (fp32 multiplication commutes exactly), the broadcast half read through src0."""
+    a, b = _q_loop(lines)
+    out, n = list(lines), 0
+    for i in range(a, b):
+        m = re.match(r"v_pk_mul_f32 (v\[\d+:\d+\]), (v\[\d+:\d+\]), (v\[\d+:\d+\]) op_sel:\[0,1\]$",
+                     lines[i].strip())
+        if m:
+            out[i] = f"\tv_pk_mul_f32 {m.group(1)}, {m.group(3)}, {m.group(2)} op_sel:[1,0]"
+            n += 1
+    return out, n
+
+
 def main() -> int:
     OUT.mkdir(parents=True, exist_ok=True)
     with tempfile.TemporaryDirectory() as td:
@@ -193,7 +289,10 @@ def main() -> int:
         for name, fn in (("pk_nop", edit_pk), ("srcc_nop", edit_srcc), ("addr_own", edit_addr_own),
                          ("drain_ep0", edit_drain_ep0), ("wait_all", edit_wait_all),
                          ("pk_nop_all", edit_pk_nop_all), ("bperm_nop", edit_bperm_nop),
-                         ("mfma_drain", edit_mfma_drain)):
+                         ("mfma_drain", edit_mfma_drain), ("ep0_last", edit_ep0_last),
+                         ("en0_first", edit_en0_first), ("unpack_all", edit_unpack_all),
+                         ("unpack_sel01", edit_unpack_sel01), ("unpack_selhi10", edit_unpack_selhi10),
+                         ("swap_sel01", edit_swap_sel01)):
             edited, n = fn(lines)
             assemble("\n".join(edited) + "\n", work, name)
             print(f"{name}: {n} site(s) edited")

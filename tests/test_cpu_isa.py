@@ -1,15 +1,16 @@
-"""CPU: the shipping library's gfx950 code pinned against the config-5 miscompile of round 4.
+"""CPU: the shipping library's gfx950 code pinned against the config-5 wrong scores of round 4.
 
 The fused config-5 kernel (decoder_bf16_cs16_kernel<768, true>, dg_slot_score_hinge_bf16) once
-returned wrong positive scores of a tile's first 16 pairs on ~1 % of half tiles, at random
-("The config-5 miscompile").  The failing build differed from the correct one in
-one thing the source controls: its score epilogue was compiled to packed fp32 instructions
-(v_pk_fma_f32 / v_pk_mul_f32 pairing the two halves' chains); an opaque register copy per half
-(decoder_bf16.hip) makes the compiler keep them as scalar v_fma_f32 / v_fmac_f32, and that form
-has never returned a wrong score (GPU: tests/test_gpu_config5.py, and the attribution harness
-scripts/hazard_harness over 20 full-size runs).  These tests disassemble the shipping library
-and assert the validated form is what ships, so a compiler or source change that brings the
-packed epilogue back fails on the CPU, before any GPU run.
+returned wrong positive scores for a tile's first 16 pairs on ~1 % of half tiles, at random.
+Round 5 traced them to one instruction form ("The config-5 miscompile"):
+`v_pk_mul_f32 vD, vA, vB op_sel:[0,1]`, a packed multiply whose LOW result reads src1's HIGH
+dword, intermittently returned 0 for lanes 48-63 of the wave in that kernel.  Every failing
+score equals the reference minus exactly one such product of lane group 3; unpacking those
+four instructions, or swapping their operands so the high dword is read through src0, removed
+every failure (scripts/hazard_variants.py + scripts/hazard_harness).  These tests disassemble the
+shipping library and assert that no kernel contains that form, and that config 5's epilogue is
+the validated scalar form, so a compiler or source change that brings it back fails on the CPU,
+before any GPU run.
 """
 import re
 import shutil
@@ -64,6 +65,36 @@ def test_config5_score_epilogue_is_not_packed(kernels):
     assert not packed, f"packed fp32 ops back in the config-5 score epilogue: {packed[:4]}"
     # the validated form: the 32 fmas of the four per-half sums (2 halves x {pos, neg} x 8 terms)
     assert len(scalar) >= 32, [x.text for x in epi][:10]
+
+
+def _src1_high_low_result(k):
+    """Packed fp32 instructions whose low result reads src1's high dword (op_sel bit 1 set)."""
+    out = []
+    for x in k.insns:
+        if not (x.op.startswith("v_pk_") and x.op.endswith("_f32")):
+            continue
+        m = re.search(r"op_sel:\[([01,]+)\]", x.text)
+        if m and m.group(1).split(",")[1] == "1":
+            out.append(x.text)
+    return out
+
+
+def test_no_kernel_has_a_packed_fp32_op_reading_src1_high_for_its_low_result(kernels):
+    bad = {name: _src1_high_low_result(k) for name, k in kernels.items()}
+    bad = {n: v for n, v in bad.items() if v}
+    assert not bad, bad
+
+
+def test_scanner_finds_the_failing_form_in_failing_build():
+    """The failing round-4 build (reassembled from commit 3b0d266's source without the opaque
+    copy) has exactly the four op_sel:[0,1] multiplies per q loop that the GPU attribution named:
+    the scan is not vacuous."""
+    hz = ROOT / "scripts" / "hazard" / "failing.hsaco"
+    if not hz.exists():
+        pytest.skip("scripts/hazard_variants.py not run")
+    ks = {k.name: k for k in isa_scan.parse(isa_scan.disassemble(hz))}
+    found = _src1_high_low_result(ks[FUSED])
+    assert len(found) == 4 and all(t.startswith("v_pk_mul_f32") for t in found), found
 
 
 def test_scanner_finds_packed_epilogue_in_failing_build(tmp_path):
