@@ -32,6 +32,21 @@ typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// LDS-DMA of one dword per lane: lane t's dword at its own global address lands at LDS byte
+// lds + 4 t (wave-uniform base).  Inline asm, so the compiler neither tracks nor drains it: the
+// kernel retires it with its own s_waitcnt vmcnt.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds4(const void* src, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
+}
+
 constexpr int kCsThreads = 768;    // column-shared paired kernel: threads per workgroup (one per CU)
 constexpr int kCs16Threads = 768;
   // config 5's 16x16x32 kernel (704: 208.6 vs 205.6 us)
@@ -399,20 +414,42 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
 // rows, a relation per pair, D_k — or identity — read per lane from global memory); the same
 // arithmetic in the same order, so the fused step and its three-launch decomposition agree bit
 // for bit.
+// FUSED's load path (round 5): the row loads are issued pair-major — lane 4P + c
+// reads 16-B chunk c' of pair P's 64-B run, so each quad of lanes reads one row's contiguous
+// 64 B — and moved to the MFMA layout (lane 16g + p <- the lane holding pair p's chunk g) by 4
+// ds_bpermute per 16 B.  A row load in the MFMA layout, a quad spanning four rows, costs the
+// texture path ≈ 60 cycles an instruction against ≈ 17 for a quad reading one run
+// (scripts/ta_probe.hip): TA busy 96 M → 35 M per launch.  The chunk order is rotated by 2 in
+// pairs 8-15 of a half, so the 32 source lanes of each half-wave's bpermute are distinct mod 32.
+// The next tile's indices (rows, columns, alias entries, the draws' j / u, the D_k row) go to
+// LDS by LDS-DMA instead of 14 VGPRs, which pays for loading both 64-B halves of the u rows'
+// 128-B lines at once (two q per loop iteration).
 template <int THREADS, bool FUSED>
 __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16DecArgs a) {
     constexpr int D = 256;
     constexpr int SL = D / 8;                 // 16-byte slots per R row
     constexpr int WAVES = THREADS / 64;
-    extern __shared__ uint4 rs[];             // R: row i, slot q at rs[i*SL + (q ^ (i % SL))]; then D_k rows
+    // FUSED: per wave two index buffers of kIB bytes — rows[32] cols[32] alias.x[32]
+    // alias.y[32] j[32] u[32] (i32 / f32), then the tile's D_k row (512 B)
+    constexpr int kIB = 1280;
+    extern __shared__ uint4 rs[];  // R: row i, slot q at rs[i*SL + (q ^ (i % SL))]; then the index buffers
     const int tid = threadIdx.x;
-    stage_r<D, THREADS>(rs, a.R);
-    __syncthreads();
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    uint4* dks = rs + D * SL + wave * (D / 8);  // this wave's tile's D_k row (512 B)
+    char* ibase = reinterpret_cast<char*>(rs + D * SL) + wave * 2 * kIB;
     const int pl = lane & 15;                   // the lane's pair in each half
     const int g = lane >> 4;                    // its k / row group
+    const int ml = FUSED ? lane >> 2 : pl;      // the pair this lane's row loads read
+    const int mc = FUSED ? ((lane & 3) + 2 * (lane >> 5)) & 3 : g;  // and their 16-B chunk
+    const int xsrc = 4 * (4 * pl + ((g + 2 * (pl >> 3)) & 3));      // FUSED: bpermute source (bytes)
+                                                                     // of MFMA lane (g, pl)
+    auto xp = [&](const uint4 v) {
+        if constexpr (!FUSED) return v;
+        return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.x),
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.y),
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.z),
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(xsrc, (int)v.w));
+    };
     const int nh = a.n_pairs;
     const int n_tiles = (nh + 31) / 32;
     const int stride = gridDim.x * WAVES;
@@ -425,51 +462,71 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
         int prp[2], pc[2], j[2];  // (non-FUSED: j = the given negative row)
         float u[2];
         uint2 e[2];               // (non-FUSED: e.x = the pair's relation)
-        uint2 dk;                 // FUSED: this lane's 8 bytes of the tile's D_k row
     };
+    // non-FUSED: tile tl's indices into registers, one tile ahead
     auto fetch = [&](int tl, Idx& x) {
         const bool okt = tl < n_tiles;
-        const int pk = okt && FUSED ? a.slot0 + (tl * 32) / a.batch : a.slot0;  // (a tile never straddles slots)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             const int p = tl * 32 + 16 * b + pl;
             const bool ok = okt && p < nh;
             x.prp[b] = ok ? a.rows[p] : 0;
             x.pc[b] = ok ? a.cols[p] : 0;
-            if constexpr (FUSED) {
-                dg::unigram_pick(a.range, a.seed, (uint64_t)a.slot0 * (uint64_t)a.batch + (uint64_t)p, x.j[b],
-                                 x.u[b]);
-                x.e[b] = ok ? a.alias[pk * a.alias_stride + x.j[b]] : make_uint2(0u, 0u);
-            } else {
-                x.j[b] = ok ? a.rows[nh + p] : 0;
-                x.e[b] = make_uint2((ok && a.rel) ? (uint32_t)a.rel[p] : 0u, 0u);
-            }
+            x.j[b] = ok ? a.rows[nh + p] : 0;
+            x.e[b] = make_uint2((ok && a.rel) ? (uint32_t)a.rel[p] : 0u, 0u);
         }
-        if constexpr (FUSED)
-            x.dk = okt ? *reinterpret_cast<const uint2*>(a.L + (int64_t)pk * D + 4 * lane) : make_uint2(0u, 0u);
+    };
+    // FUSED: tile tl's indices into index buffer buf by LDS-DMA (the draws' j, u by ds_write),
+    // one tile ahead; a tile never straddles slots
+    auto prefetch = [&](int tl, int buf) {
+        const int tc = tl < n_tiles ? tl : 0;  // (past the end: tile 0's addresses, never read)
+        const int pk = a.slot0 + (tc * 32) / a.batch;
+        char* B = ibase + buf * kIB;
+        const int i = lane & 31;
+        const int p = tc * 32 + i;
+        glds4((lane < 32 ? a.rows : a.cols) + p, lds_addr(B));
+        int j;
+        float u;
+        dg::unigram_pick(a.range, a.seed, (uint64_t)a.slot0 * (uint64_t)a.batch + (uint64_t)p, j, u);
+        glds4(reinterpret_cast<const uint32_t*>(a.alias + pk * a.alias_stride + j) + (lane >> 5), lds_addr(B + 256));
+        const uint32_t* dsrc = reinterpret_cast<const uint32_t*>(a.L + (int64_t)pk * D) + lane;
+        glds4(dsrc, lds_addr(B + 768));
+        glds4(dsrc + 64, lds_addr(B + 1024));
+        if (lane < 32) {
+            reinterpret_cast<int*>(B + 512)[i] = j;
+            reinterpret_cast<float*>(B + 640)[i] = u;
+        }
     };
     Idx nxt;
     const int first = wave * (int)gridDim.x + (int)blockIdx.x;  // round-major tile order (see above)
-    fetch(first, nxt);
-    // D_k row of a tile, lane l: elements 4l .. 4l+3.  (The 8-byte store and the 16-byte reads
-    // are different types to the compiler — no assumed aliasing — so explicit compiler barriers
-    // keep a tile's reads before the next tile's store and after its own; the LDS executes one
-    // wave's accesses in order.)  The first tile's row is stored here, every later one at the
-    // end of the tile before it, where its load has long completed (the rows' waits in the q
-    // loop) — at the top of the tile the store would wait for the just-issued index loads.
-    auto put_dk = [&](const uint2 dk) {
-        if constexpr (FUSED) {
-            asm volatile("" ::: "memory");
-            reinterpret_cast<uint2*>(dks)[lane] = dk;
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-        }
-    };
-    put_dk(nxt.dk);
+    if constexpr (FUSED) prefetch(first, 0);
+    stage_r<D, THREADS>(rs, a.R);
+    if constexpr (FUSED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA is not tracked)
+    __syncthreads();
+    if constexpr (!FUSED) fetch(first, nxt);
+    int cur_buf = 0;
 #pragma unroll 1
     for (int tile = first; tile < n_tiles; tile += stride) {
-        const Idx cur = nxt;
-        fetch(tile + stride, nxt);
+        Idx cur;
+        const uint4* dkt = nullptr;  // FUSED: this tile's D_k row in LDS
+        if constexpr (FUSED) {
+            const char* B = ibase + cur_buf * kIB;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int i = 16 * b + ml;
+                cur.prp[b] = reinterpret_cast<const int*>(B)[i];
+                cur.pc[b] = reinterpret_cast<const int*>(B + 128)[i];
+                cur.e[b] = make_uint2(reinterpret_cast<const uint32_t*>(B + 256)[i],
+                                      reinterpret_cast<const uint32_t*>(B + 384)[i]);
+                cur.j[b] = reinterpret_cast<const int*>(B + 512)[i];
+                cur.u[b] = reinterpret_cast<const float*>(B + 640)[i];
+            }
+            dkt = reinterpret_cast<const uint4*>(B + 768);
+            prefetch(tile + stride, cur_buf ^ 1);
+        } else {
+            cur = nxt;
+            fetch(tile + stride, nxt);
+        }
         const uint16_t* lk[2];  // non-FUSED: each half's pairs' D_k rows (NULL: identity)
         // rows through buffer loads from the uniform table bases: a 32-bit byte offset per row
         // (1 VGPR) instead of a 64-bit address (2)
@@ -481,17 +538,19 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
         for (int b = 0; b < 2; ++b) {  // every v load first (16 in flight), then the B operand
             const int p = tile * 32 + 16 * b + pl;
             valid[b] = p < nh;
+            const int pm = tile * 32 + 16 * b + ml;  // the pair this lane's loads read
+            const bool vm = pm < nh;
             int prn;
             if constexpr (FUSED) {
-                prn = valid[b] ? dg::unigram_take(cur.j[b], cur.u[b], cur.e[b]) : 0;
-                if (valid[b] && g == 0) a.neg_out[p] = prn;
+                prn = vm ? dg::unigram_take(cur.j[b], cur.u[b], cur.e[b]) : 0;
+                if (vm && mc == 0) a.neg_out[pm] = prn;
             } else {
                 prn = cur.j[b];
                 lk[b] = a.L ? a.L + (int64_t)cur.e[b].x * D + 8 * g : nullptr;
             }
-            up[b] = 2 * (cur.prp[b] * (int)a.ld_row + 8 * g);
-            un[b] = 2 * (prn * (int)a.ld_row + 8 * g);
-            const int vo = 2 * (cur.pc[b] * (int)a.ld_col + 8 * g);
+            up[b] = 2 * (cur.prp[b] * (int)a.ld_row + 8 * mc);
+            un[b] = 2 * (prn * (int)a.ld_row + 8 * mc);
+            const int vo = 2 * (cur.pc[b] * (int)a.ld_col + 8 * mc);
 #pragma unroll
             for (int s = 0; s < 8; ++s)
                 vv[b][s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(crs, vo + 64 * s, 0, 0));
@@ -499,13 +558,14 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             uint4 llf = ones;
-            if constexpr (FUSED) llf = dks[4 * s + g];  // D_k[32s + 8g .. +8], shared by both halves
+            if constexpr (FUSED) llf = dkt[4 * s + g];  // D_k[32s + 8g .. +8], shared by both halves
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
                 uint4 ll = llf;
                 if constexpr (!FUSED) ll = lk[b] ? *reinterpret_cast<const uint4*>(lk[b] + 32 * s) : ones;
                 const uint32_t lw[4] = {ll.x, ll.y, ll.z, ll.w};
-                const uint32_t vw[4] = {vv[b][s].x, vv[b][s].y, vv[b][s].z, vv[b][s].w};
+                const uint4 vt = xp(vv[b][s]);
+                const uint32_t vw[4] = {vt.x, vt.y, vt.z, vt.w};
                 bf16v8 x;  // round-to-nearest-even by the cast (v_cvt_pk_bf16_f32)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -516,15 +576,9 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
             }
         }
         float pp[2] = {0.f, 0.f}, pn[2] = {0.f, 0.f};
-#pragma unroll 1
-        for (int q = 0; q < 8; ++q) {  // M-tiles 2q, 2q+1: rows i = 32q + 8g + [0, 8) of this lane group
-            uint4 ep[2], en[2];
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                ep[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, up[b] + 64 * q, 0, 0));
-                en[b] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, un[b] + 64 * q, 0, 0));
-            }
-
+        // M-tiles 2q, 2q+1: rows i = 32q + 8g + [0, 8) of this lane group; ep / en: the lane's
+        // 16 B of u_p / u_n at those rows
+        auto qbody = [&](const int q, const uint4 (&ep)[2], const uint4 (&en)[2]) {
             f32x4 acc[2][2] = {};
 
             // the row's swizzle key, opaque per iteration: its 16 slot offsets are q-invariant,
@@ -552,14 +606,15 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
                 __builtin_amdgcn_sched_barrier(0);
             }
             uint4 elf = ones;
-            if constexpr (FUSED) elf = dks[4 * q + g];  // D_k[32q + 8g .. +8]
+            if constexpr (FUSED) elf = dkt[4 * q + g];  // D_k[32q + 8g .. +8]
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
                 uint4 el = elf;
                 if constexpr (!FUSED) el = lk[b] ? *reinterpret_cast<const uint4*>(lk[b] + 32 * q) : ones;
                 const uint32_t lw[4] = {el.x, el.y, el.z, el.w};
-                const uint32_t pw[4] = {ep[b].x, ep[b].y, ep[b].z, ep[b].w};
-                const uint32_t nw[4] = {en[b].x, en[b].y, en[b].z, en[b].w};
+                const uint4 ept = xp(ep[b]), ent = xp(en[b]);
+                const uint32_t pw[4] = {ept.x, ept.y, ept.z, ept.w};
+                const uint32_t nw[4] = {ent.x, ent.y, ent.z, ent.w};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {  // accumulator register r of tile 2q + h is row 32q + 8g + 4h + r
 #pragma unroll
@@ -584,8 +639,40 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
                 // library.
                 asm volatile("" : "+v"(pp[b]), "+v"(pn[b]));
             }
+        };
+        auto uload = [&](int off) {
+            return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrs, off, 0, 0));
+        };
+        if constexpr (FUSED) {
+#pragma unroll 1
+            for (int q = 0; q < 8; q += 2) {  // both 64-B halves of the pairs' 128-B lines at once
+                uint4 ep0[2], en0[2], ep1[2], en1[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    ep0[b] = uload(up[b] + 64 * q);
+                    ep1[b] = uload(up[b] + 64 * q + 64);
+                    en0[b] = uload(un[b] + 64 * q);
+                    en1[b] = uload(un[b] + 64 * q + 64);
+                }
+                qbody(q, ep0, en0);
+                qbody(q + 1, ep1, en1);
+            }
+        } else {
+#pragma unroll 1
+            for (int q = 0; q < 8; ++q) {
+                uint4 ep[2], en[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    ep[b] = uload(up[b] + 64 * q);
+                    en[b] = uload(un[b] + 64 * q);
+                }
+                qbody(q, ep, en);
+            }
         }
-        put_dk(nxt.dk);  // (after this tile's last D_k read)
+        if constexpr (FUSED) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's index DMA landed
+            cur_buf ^= 1;
+        }
         float term = 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {  // the pair's 4 lane groups, in a fixed butterfly
@@ -689,7 +776,7 @@ extern "C" int dg_decoder_score_bf16_paired(const uint16_t* row_table, int64_t l
         // the 16x16x32 form (decoder_bf16_cs16_kernel, FUSED = false): bit-identical scores to
         // dg_slot_score_hinge_bf16's; 32-bit byte offsets into the tables are required
         constexpr int kT16 = kCs16Threads;
-        const int lds16 = d * d * 2 + (kT16 / 64) * d * 2;
+        const int lds16 = d * d * 2;  // R
         int blocks16 = (n_tiles + kT16 / 64 - 1) / (kT16 / 64);
         if (blocks16 > 256) blocks16 = 256;
         static std::atomic<uint64_t> configured16p{0};
@@ -762,7 +849,7 @@ extern "C" int dg_slot_score_hinge_bf16(const uint16_t* row_table, int64_t ld_ro
     // byte offsets (its row loads are buffer loads)
     if (batch % 32 == 0 && fits_32bit_offsets(n_row_table, ld_row) && fits_32bit_offsets(n_col_table, ld_col)) {
         constexpr int kT16 = kCs16Threads;
-        const int lds16 = d * d * 2 + (kT16 / 64) * d * 2;  // R + a D_k row per wave
+        const int lds16 = d * d * 2 + (kT16 / 64) * 2 * 1280;  // R + per wave two index buffers
         int blocks16 = (n_tiles + kT16 / 64 - 1) / (kT16 / 64);
         if (blocks16 > DG_HINGE_WS_BLOCKS) blocks16 = DG_HINGE_WS_BLOCKS;
         static std::atomic<uint64_t> configured16{0};
