@@ -61,7 +61,12 @@ STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "256"))  # one rou
 # windows (sparse.merge_windows): each window's gathers stay in its XCDs' L2.  Measured on
 # config P's PPI (scripts/exp_window.py): d=64 63.6 us merged -> 40.0 us with 2 windows
 # (+5.6 us epilogue); 4 windows 40.8, 8 windows 53.7 (the window partials start to cost).
-WINDOW_MIN_ROWS = int(os.environ.get("DG_WINDOW_MIN_ROWS", "4096"))
+# A rank's row block of such a group at N = 8 (2,386 protein rows) is windowed too, in twice
+# as many windows (its launch is short of waves, not of L2): config P's N = 8 rank share
+# (--simulate-world 8, max over ranks) 110.7 us without windows, 106.5 with 2, 106.0 with 4,
+# 109.9 with 8 (round 5).
+WINDOW_MIN_ROWS = int(os.environ.get("DG_WINDOW_MIN_ROWS", "1024"))
+WINDOW_FULL_ROWS = 4096  # below this many rows: 2 x N_WINDOWS windows
 N_WINDOWS = int(os.environ.get("DG_WINDOWS", "2"))
 # node types with at most this many rows finish in the fused row-per-workgroup kernel; larger
 # ones run partial mode + epilogue (one wave per row keeps more gathers in flight)
@@ -280,7 +285,7 @@ class DeviceGraph:
             windows = (not staged and loc and ch >= len(loc) and n_r >= WINDOW_MIN_ROWS
                        and N_WINDOWS > 1 and (chunk is None))
             if windows:
-                m = merge_windows(loc, ids, N_WINDOWS, K)
+                m = merge_windows(loc, ids, N_WINDOWS if n_r >= WINDOW_FULL_ROWS else 2 * N_WINDOWS, K)
             elif loc:
                 m = merge_chunks(loc, ids, ch, K)
             else:
