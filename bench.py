@@ -41,6 +41,8 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+from decagon_amd.tuning import knob, overrides  # noqa: E402
+
 METRIC = "GCN-layer edges/sec + achieved HBM GB/s, 5-relation synthetic, 1/2/4/8 GPU"
 JSON_OUT = sys.stdout
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md §Chip-level parameters)
@@ -245,7 +247,7 @@ def time_kernel(fn, reps, stream):
     return best
 
 
-WARM_REPLAYS = int(os.environ.get("DG_WARM_REPLAYS", "1"))  # untimed replays after capture
+WARM_REPLAYS = knob("DG_WARM_REPLAYS", 1)  # untimed replays after capture
 LAST_TIMING = {}  # timed_steps: the last timed region's device-side span (HIP events), untimed rerun
 
 
@@ -696,6 +698,7 @@ def main_decoder(args):
     torch.cuda.set_device(0)
     rec = decoder_bench(args, torch.device("cuda", 0), args.steps, args.warmup)
     rec.update({"higher_is_better": True, "vs_baseline": None, "cpu_baseline": None})
+    rec["policy_overrides"] = overrides()  # DG_* knobs that differed from the defaults
     print(json.dumps(rec), file=JSON_OUT, flush=True)
 
 
@@ -802,6 +805,7 @@ def main_train(args):
         "cpu_baseline": None,
     }
     if rank == 0:
+        rec["policy_overrides"] = overrides()  # DG_* knobs that differed from the defaults
         print(json.dumps(rec), file=JSON_OUT, flush=True)
     if sharded:
         dist.barrier()
@@ -872,6 +876,7 @@ def main_simulate(args):
     rec = {"metric": f"config {args.config} sharded-step rehearsal on one GPU ({what})", "world": N,
            "steps": args.steps, "warmup": args.warmup, "steps_per_graph": G,
            "max_rank_ms_per_step": max(x["ms_per_step"] for x in ranks), "ranks": ranks}
+    rec["policy_overrides"] = overrides()  # DG_* knobs that differed from the defaults
     print(json.dumps(rec), file=JSON_OUT, flush=True)
 
 
@@ -940,6 +945,7 @@ def main():
                             "random glorot weights",
                     "cpu_baseline": cpu})
         out.update(extra)
+        out["policy_overrides"] = overrides()  # DG_* knobs that differed from the defaults
         print(json.dumps(out), file=JSON_OUT, flush=True)
     if sharded:
         dist.barrier()

@@ -9,6 +9,7 @@ import os
 import shutil
 import subprocess
 from pathlib import Path
+from .tuning import knob
 
 PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
@@ -16,7 +17,7 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 LIBDIR = PKG / "lib"
 LIBNAME = "libdecagon_hip.so"
-ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
+ARCH = knob("DG_OFFLOAD_ARCH", "gfx950")
 
 
 def lib_path() -> Path:

@@ -8,11 +8,11 @@ from __future__ import annotations
 
 import ctypes
 import threading
-import os
 from pathlib import Path
 from ctypes import POINTER, c_float, c_int32, c_int64, c_uint64, c_void_p
 
 from . import _build
+from .tuning import knob
 
 DG_OK = 0
 DG_EINVAL = -1
@@ -297,7 +297,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
 
 
 def _load(build_if_missing: bool) -> ctypes.CDLL:
-    override = os.environ.get("DG_LIB")  # an instrumented build (scripts/staged_prof.py)
+    override = knob("DG_LIB", "")  # an instrumented build (scripts/staged_prof.py)
     path = Path(override) if override else _build.lib_path()
     if not override and (not path.exists() or (build_if_missing and _build.needs_build())):
         if not build_if_missing:

@@ -21,7 +21,6 @@ products X·W1) is indexed by the GLOBAL relation id, so one merged layout serve
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -31,16 +30,17 @@ import torch
 from . import kernels
 from ._lib import DG_EPI_L2NORM, DG_EPI_RELU, DG_MAX_GROUPS
 from .sparse import HostCSR, MergedCSR, chunk_segments, merge_chunks, merge_windows, staged_layout
+from .tuning import knob
 
 EdgeType = Tuple[int, int]
 
 
 # LDS-staged groups (staged.hip): many relations over a column space narrow enough that one
 # relation's 16-float column slice and the output rows' accumulators fit LDS.
-STAGED_MIN_RELS = int(os.environ.get("DG_STAGED_MIN_RELS", "32"))
+STAGED_MIN_RELS = knob("DG_STAGED_MIN_RELS", 32)
 STAGED_MAX_COLS = 1024
 STAGED_MAX_ROWS = 1022
-STAGED_BINS = int(os.environ.get("DG_STAGED_BINS", "128"))
+STAGED_BINS = knob("DG_STAGED_BINS", 128)
 
 
 def drop_tag(layer: int, group: int) -> int:
@@ -50,12 +50,12 @@ def drop_tag(layer: int, group: int) -> int:
 
 
 def stageable(n_rels: int, n_rows: int, n_cols: int) -> bool:
-    return (os.environ.get("DG_STAGED", "1") != "0" and n_rels >= STAGED_MIN_RELS
+    return (knob("DG_STAGED", True) and n_rels >= STAGED_MIN_RELS
             and 0 < n_cols <= STAGED_MAX_COLS and 0 < n_rows <= STAGED_MAX_ROWS
             and kernels.staged_lds_bytes(n_rows, n_cols) <= kernels.STAGED_LDS_BYTES)
 
 
-STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "256"))  # one round: a workgroup per CU
+STAGED_TARGET_BLOCKS = knob("DG_STAGED_BLOCKS", 256)  # one round: a workgroup per CU
 
 # Large groups whose relations fit one chunk (PPI: 2 x 19,085^2) are laid out in column
 # windows (sparse.merge_windows): each window's gathers stay in its XCDs' L2.  Measured on
@@ -65,35 +65,35 @@ STAGED_TARGET_BLOCKS = int(os.environ.get("DG_STAGED_BLOCKS", "256"))  # one rou
 # as many windows (its launch is short of waves, not of L2): config P's N = 8 rank share
 # (--simulate-world 8, max over ranks) 110.7 us without windows, 106.5 with 2, 106.0 with 4,
 # 109.9 with 8 (round 5).
-WINDOW_MIN_ROWS = int(os.environ.get("DG_WINDOW_MIN_ROWS", "1024"))
+WINDOW_MIN_ROWS = knob("DG_WINDOW_MIN_ROWS", 1024)
 WINDOW_FULL_ROWS = 4096  # below this many rows: 2 x N_WINDOWS windows
-N_WINDOWS = int(os.environ.get("DG_WINDOWS", "2"))
+N_WINDOWS = knob("DG_WINDOWS", 2)
 # node types with at most this many rows finish in the fused row-per-workgroup kernel; larger
 # ones run partial mode + epilogue (one wave per row keeps more gathers in flight)
-FUSED_MAX_ROWS = int(os.environ.get("DG_FUSED_MAX_ROWS", "4096"))
+FUSED_MAX_ROWS = knob("DG_FUSED_MAX_ROWS", 4096)
 # a layer's gather-bound launch beside its LDS-bound staged launch on a second stream: no gain
 # measured (config P step 494.8 us concurrent vs 496.5 sequential; the staged kernel slows by
 # what the other saves) and the fork / join cost ~10 us of idle GPU each at small per-rank
 # shares (8-GPU rehearsal), so one stream by default
-CONCURRENT_LAUNCHES = os.environ.get("DG_CONCURRENT", "0") != "0"
+CONCURRENT_LAUNCHES = knob("DG_CONCURRENT", False)
 # layer 2 of staged groups makes its slabs H1_j·W2_k on the MFMA inside the SpMM kernel
-STAGED_PROJ = os.environ.get("DG_STAGED_PROJ", "1") != "0"
+STAGED_PROJ = knob("DG_STAGED_PROJ", True)
 # one-GPU plans whose node types all fit dg_gcn_fused_seg_f32 (config S) use it, layer 2
 # reassociated; DG_FUSED_SEG=0 keeps dg_gcn_fused_f32 with the projection epilogue + P
-FUSED_SEG = os.environ.get("DG_FUSED_SEG", "1") != "0"
+FUSED_SEG = knob("DG_FUSED_SEG", True)
 # config S's N-GPU rank share (seg mode): each row of the rank's block finished by one
 # dg_gcn_fused_seg_f32 workgroup, one wave per relation of the row's N relation sets
 # (DG_SEG_FUSED=0, or more relations a row: dg_spmm_seg_f32 partials + the epilogue launch)
-SEG_FUSED = os.environ.get("DG_SEG_FUSED", "1") != "0"
+SEG_FUSED = knob("DG_SEG_FUSED", True)
 # ... when a row has at most 16 relations (one wave each: N <= 2 for config S).  A form whose 16
 # waves looped over more relations measured 25.2 µs a rank share at N = 4 (seg + epilogue 25.1)
 # and 35.6 at N = 8 (25.6), so it was not kept
 SEG_FUSED_MAX_ITEMS = 16
-STAGED_FIRST = os.environ.get("DG_STAGED_FIRST", "1") != "0"
+STAGED_FIRST = knob("DG_STAGED_FIRST", True)
 # sharded forward plans: layer 2 of the non-staged groups reassociated over the rank's own rows
 # and relations, Σ_k (Â_k·H1_j)·W2_k in dg_spmm_seg_f32, instead of every rank projecting all of
 # H1_j·W2_k (config P's PPI: 19,085 rows x 2 relations, 9.4 µs on every rank at N = 8)
-REASSOC_ROWS = os.environ.get("DG_REASSOC_ROWS", "1") != "0"
+REASSOC_ROWS = knob("DG_REASSOC_ROWS", True)
 # sharded forward plans: layer 1 of the row-split, non-windowed, non-staged groups in
 # dg_spmm_seg_f32 (one wave per (row, relation), its segment's pairs in one load) instead of
 # dg_spmm_groups_f32 (one wave per two (chunk, row) items): a rank's short row block (config P
@@ -101,7 +101,7 @@ REASSOC_ROWS = os.environ.get("DG_REASSOC_ROWS", "1") != "0"
 # Off: at P's N = 8 share it took 3-5 us off seven ranks (107.1-108.0 -> 102.7-104.1 us) but
 # added 1.7 us to the slowest (rank 4, 110.6 -> 112.3: a wave per (row, relation) walks a hub
 # row's long segment alone), so the max over ranks got worse
-SEG_ROWS_L1 = os.environ.get("DG_SEG_ROWS_L1", "0") != "0"
+SEG_ROWS_L1 = knob("DG_SEG_ROWS_L1", False)
 
 
 def staged_out_chunk(grp, d: int) -> int:
@@ -310,8 +310,8 @@ class DeviceGraph:
                           int(m2.vcol.max()) if m2.nnz else -1)
             if staged:
                 lay = staged_layout(loc, kernels.staged_block,
-                                    lanes=int(os.environ.get("DG_STAGED_LANES", "1024")),
-                                    split=os.environ.get("DG_STAGED_SPLIT", "1") != "0")
+                                    lanes=knob("DG_STAGED_LANES", 1024),
+                                    split=knob("DG_STAGED_SPLIT", True))
                 g.layout = kernels.StagedDevice.upload(lay, device)
             self.groups[et] = g
 
@@ -332,7 +332,7 @@ class ForwardPlan:
 
     # a fused launch projects a row onto at most this many layer-2 relations (VALU epilogue);
     # beyond it the batched MFMA GEMM is used
-    FUSED_PROJ_MAX_RELS = int(os.environ.get("DG_FUSED_PROJ_MAX", "64"))
+    FUSED_PROJ_MAX_RELS = knob("DG_FUSED_PROJ_MAX", 64)
 
     def __init__(self, dgraph: DeviceGraph, features: Dict[int, Optional[HostCSR]],
                  w1: LayerWeights, w2: LayerWeights, h1: int, h2: int,
@@ -700,8 +700,8 @@ class ForwardPlan:
             # 0's layer 1: 27.0 µs at 2 waves per group)
             cap = 16 // max_groups if self.row_block else 2
             wpg = 1 if rows >= 4096 else int(max(1, min(cap, 16 // max_groups, math.ceil(avg / 64.0))))
-            if os.environ.get("DG_WPG"):  # tuning override
-                wpg = max(1, min(int(os.environ["DG_WPG"]), 16 // max_groups))
+            if knob("DG_WPG", 0):  # tuning override
+                wpg = max(1, min(knob("DG_WPG", 0), 16 // max_groups))
             pspecs = []
             for tgt_node, pj in projs:
                 if tgt_node in fused_t:  # (sharded: the finishing launch projects the others)

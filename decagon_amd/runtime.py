@@ -17,7 +17,6 @@ bound.
 from __future__ import annotations
 
 import contextlib
-import os
 from collections import OrderedDict
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -30,6 +29,7 @@ from ._lib import DG_EPI_CHUNK_RELU, DG_EPI_L2NORM
 from .engine import DeviceGraph, DeviceGroup
 from .graph import InvalidArgumentError, Node, RunContext
 from .sparse import HostCSR, SparseTensorValue, as_coo_tuple, coo_to_csr, is_identity
+from .tuning import knob
 
 _scope: List[str] = []
 
@@ -122,8 +122,8 @@ class ByteLRU:
         return list(self._d.keys())
 
 
-HOST_CACHE_BYTES = int(os.environ.get("DG_FEED_CACHE_HOST_MB", "8192")) << 20
-DEVICE_CACHE_BYTES = int(os.environ.get("DG_FEED_CACHE_DEVICE_MB", "65536")) << 20
+HOST_CACHE_BYTES = knob("DG_FEED_CACHE_HOST_MB", 8192) << 20
+DEVICE_CACHE_BYTES = knob("DG_FEED_CACHE_DEVICE_MB", 65536) << 20
 
 
 def _lru(ctx: RunContext, name: str) -> ByteLRU:

@@ -22,12 +22,12 @@ replicated (645 × 256 bf16 = 330 KB; the slots' alias tables 1,928 × 645 × 8 
 """
 from __future__ import annotations
 
-import os
 from typing import Callable, Optional, Tuple
 
 import torch
 
 from . import kernels
+from .tuning import knob
 
 
 class SlotScorer:
@@ -67,7 +67,7 @@ class SlotScorer:
         self.E_row, self.E_col, self.R, self.D, self.alias = E_row, E_col, R, D, alias
         self.allreduce = allreduce
         # (DG_C5_FUSED=0: the three-launch form by default — A/B runs)
-        self.fused = (os.environ.get("DG_C5_FUSED", "1") != "0") if fused is None else fused
+        self.fused = knob("DG_C5_FUSED", True) if fused is None else fused
 
     @property
     def neg_rows(self) -> torch.Tensor:

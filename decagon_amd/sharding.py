@@ -30,12 +30,12 @@ relation map of dg_rel_group / dg_gemm_desc, without copies.
 from __future__ import annotations
 
 import heapq
-import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
+from .tuning import knob
 
 EdgeType = Tuple[int, int]
 
@@ -176,7 +176,7 @@ class RelationShard:
         dg_spmm_seg_f32 (one wave per (row, relation), layer 2 reassociated so no rank projects
         every relation) + the epilogue; "fused": one chunk per group in dg_gcn_fused_f32 (one
         workgroup per row) with the layer-2 projection GEMM over every relation on every rank."""
-        form = form or os.environ.get("DG_S_ROWS_FORM", "seg")
+        form = form or knob("DG_S_ROWS_FORM", "seg")
         if form not in ("seg", "fused"):
             raise ValueError(f"unknown weak-scaling form {form!r}")
         nnz = {et: [1.0] * K for et, K in edge_types.items()}

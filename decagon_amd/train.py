@@ -40,7 +40,6 @@ their dH1 contributions join the existing dH1 all-reduce.
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -50,6 +49,7 @@ from . import kernels
 from ._lib import DG_MAX_GROUPS
 from .engine import ForwardPlan, LayerWeights, drop_tag
 from .sparse import HostCSR, merge_chunks
+from .tuning import knob
 
 EdgeType = Tuple[int, int]
 
@@ -204,7 +204,7 @@ class TrainPlan:
             gemm_w2.append(kernels.PreparedGemmTN(H, dP, self.gW2[et]))
             # dH1_j partials = Σ_k M_k∘(dP_k·W2_kᵀ) over runs of R relations: B(c, m) = W2_k[m][c]
             # (M_k: layer 2's dropout mask of relation k, when dropout is on)
-            R = K if K <= 64 else int(os.environ.get("DG_REDUCE_RUN", "16"))
+            R = K if K <= 64 else knob("DG_REDUCE_RUN", 16)
             n_runs = -(-K // R)
             part = torch.zeros((n_runs, n[j], h1), **f32)
             drop = ((fwd.drop_state, drop_tag(2, fwd.et_index[et]), fwd.keep) if fwd.drop_state is not None

@@ -391,3 +391,43 @@ def test_global_variables_are_scoped_to_their_graph():
     init_a._fn(_Ctx())
     assert all(not np.array_equal(va[k], v.eval()) for k, v in a.layers1[0, 0].vars.items())
     assert all(np.array_equal(vb[k], v.eval()) for k, v in b.layers1[0, 0].vars.items())
+
+
+def test_c_library_reads_no_environment():
+    """SURVEY §8b's ABI is arguments-only: no kernel or entry point of the C library consults the
+    process environment (round-4 review item 7), in source or in the built library's imports."""
+    csrc = Path(__file__).resolve().parent.parent / "decagon_amd" / "csrc"
+    hits = [f"{f.name}:{n}" for f in sorted(csrc.iterdir()) if f.suffix in (".hip", ".h", ".cpp")
+            for n, line in enumerate(f.read_text().splitlines(), 1) if re.search(r"\b(getenv|secure_getenv|environ)\b", line)]
+    assert not hits, hits
+    lib = Path(__file__).resolve().parent.parent / "decagon_amd" / "lib" / "libdecagon_hip.so"
+    if lib.exists():
+        import subprocess
+
+        syms = subprocess.run(["nm", "-D", "--undefined-only", str(lib)], capture_output=True, text=True).stdout
+        assert "getenv" not in syms, [l for l in syms.splitlines() if "getenv" in l]
+
+
+def test_dg_environment_reads_go_through_tuning(monkeypatch):
+    """Every DG_* knob of the package is read by decagon_amd.tuning.knob (so bench.py can list
+    the non-default ones on its JSON line), none by a direct os.environ read; the C library
+    reads none at all (test_c_library_reads_no_environment)."""
+    import re
+
+    from decagon_amd import tuning
+
+    pkg = Path(__file__).resolve().parent.parent / "decagon_amd"
+    direct = []
+    for f in sorted(pkg.glob("*.py")):
+        if f.name == "tuning.py":
+            continue
+        for n, line in enumerate(f.read_text().splitlines(), 1):
+            if re.search(r"os\.environ|os\.getenv", line) and "DG_" in line:
+                direct.append(f"{f.name}:{n}")
+    assert not direct, direct
+    monkeypatch.setenv("DG_WINDOWS", "4")
+    assert tuning.knob("DG_WINDOWS", 2) == 4 and tuning.overrides().get("DG_WINDOWS") == 4
+    monkeypatch.setenv("DG_STAGED", "0")
+    assert tuning.knob("DG_STAGED", True) is False
+    monkeypatch.delenv("DG_WINDOWS")
+    assert tuning.knob("DG_WINDOWS", 2) == 2 and "DG_WINDOWS" not in tuning.overrides()
