@@ -67,7 +67,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: Path = No
         "-Wno-pass-failed",
         f"-I{INCLUDE}",
         f"-I{CSRC}",
-        *[f"-D{d}" for d in defines],
+        *[d if d.startswith("-") else f"-D{d}" for d in defines],  # (variants: raw flags too)
         "-o",
         str(tmp),
         *[str(s) for s in _sources()],

@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 34
+ABI_VERSION = 35
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -95,6 +95,17 @@ class DgSegGroup(ctypes.Structure):
         ("n_rels", c_int32),
         ("x_rows", c_int32),
     ]
+
+
+class DgTabDesc(ctypes.Structure):
+    """dg_tab_desc: one wave's 64-byte descriptor (the wave-table fused launch)."""
+    _fields_ = [("x", c_void_p), ("w", c_void_p), ("orow", c_void_p), ("cnt", c_int32), ("x_ld", c_int32),
+                ("ovf", c_int32), ("role", ctypes.c_uint32), ("wr", ctypes.c_uint32), ("pad", c_int32 * 5)]
+
+
+class DgWaveTable(ctypes.Structure):
+    _fields_ = [("pairs", c_void_p), ("ovf", c_void_p), ("desc", c_void_p), ("n_blocks", c_int32),
+                ("nw", c_int32), ("nw_stride", c_int32), ("pad", c_int32)]
 
 
 class DgStagedProj(ctypes.Structure):
@@ -198,6 +209,7 @@ SIGNATURES = {
     "dg_gcn_epilogue_multi_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, c_void_p]),
     "dg_gcn_epilogue_peer_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, POINTER(DgPeerXchg),
                                            c_void_p]),
+    "dg_gcn_fused_tab_f32": (c_int32, [POINTER(DgWaveTable), c_int32, c_int32, c_void_p]),
     "dg_gcn_fused_seg_peer_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32,
                                             c_int32, POINTER(DgPeerXchg), c_void_p]),
     "dg_peer_alloc": (c_int32, [c_int64, c_int32, POINTER(c_void_p)]),

@@ -345,6 +345,18 @@ struct FsArgs {
 
 constexpr int kFsMaxRpb = 4;  // rows per workgroup, at most (1: no change at config S)
 
+#ifdef DG_FSEG_PROF
+// Profiling build only (scripts/fseg_prof.py): per (launch form, workgroup, wave) the
+// s_memrealtime (100 MHz) stamps of the phases below, and the XCC id.
+constexpr int kFsProfSlots = 8;
+constexpr int kFsProfMaxBlocks = 4096;
+__device__ unsigned long long g_fs_prof[2][kFsProfMaxBlocks][16][kFsProfSlots];
+#define DG_FS_STAMP(i) \
+    do { if (lane == 0 && blockIdx.x < kFsProfMaxBlocks) g_fs_prof[PROJ][blockIdx.x][wave][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define DG_FS_STAMP(i) ((void)0)
+#endif
+
 template <int LP, bool PROJ, int NW, bool PEER>
 __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) {
     constexpr int DOUT4 = PROJ ? 8 : LP;
@@ -353,6 +365,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
     __shared__ float4 nbuf[kFsMaxRpb][DG_MAX_GROUPS][DOUT4];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    DG_FS_STAMP(0);  // (profiling build: wave start)
     int ti = 0;
 #pragma unroll 1
     while (ti + 1 < a.n_targets && (int)blockIdx.x >= a.t[ti + 1].block_begin) ++ti;
@@ -370,6 +383,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 #pragma unroll 1
     while (gl < T.g_count && wi >= base + a.g[T.g_begin + gl].n_rels) base += a.g[T.g_begin + gl++].n_rels;
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
+    DG_FS_STAMP(1);  // target / group found
     if constexpr (PROJ) {
         const bool live = slot < T.rpb && r < T.n_rows && gl < T.g_count;
         const int gi = T.g_begin + (gl < T.g_count ? gl : 0);
@@ -382,6 +396,10 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
             beg = g.seg[si];
             end = t + 1 < g.chunk ? g.seg[si + 1] : g.rowptr[(int64_t)c * g.n_rows + r + 1];
         }
+#ifdef DG_FSEG_PROF
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+        DG_FS_STAMP(2);  // segment bounds loaded
         if (live) res = seg_wave_proj<kFsegUP>(a.g[gi], k, beg, end, ybuf[wave]);
     } else if (slot < T.rpb && r < T.n_rows && gl < T.g_count) {
         const SegGroupK& g = a.g[T.g_begin + gl];
@@ -389,8 +407,13 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
         const int c = k / g.chunk;
         res = seg_wave<LP, kFsegU>(g, c, r, k - c * g.chunk);
     }
+#ifdef DG_FSEG_PROF
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+    DG_FS_STAMP(3);  // the wave's relation sum done
     if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
+    DG_FS_STAMP(4);  // every wave of the workgroup done
     // one wave per (row slot, group): its relations summed in order, L2-normalised
     if (wave < T.rpb * T.g_count) {
         const int s2 = wave / T.g_count, gg = wave - s2 * T.g_count;
@@ -410,6 +433,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
         if (lane < DOUT4) nbuf[s2][gg][lane] = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
     }
     __syncthreads();
+    DG_FS_STAMP(5);  // groups normalised
     if (wave < T.rpb && r0 + wave < T.n_rows && lane < DOUT4) {
         float4 tot = nbuf[wave][0][lane];
         for (int u = 1; u < T.g_count; ++u) dg::add4(tot, nbuf[wave][u][lane]);
@@ -423,7 +447,192 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
         *reinterpret_cast<float4*>(T.out + o) = tot;
         if constexpr (PEER) dg::peer_store4(a.P, T.out, (uint32_t)T.n_rows * (16 * DOUT4), (uint32_t)o * 4, tot);
     }
+#ifdef DG_FSEG_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DG_FS_STAMP(6);  // row stored
+    if (lane == 0 && blockIdx.x < kFsProfMaxBlocks) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_fs_prof[PROJ][blockIdx.x][wave][7] = xcc;
+    }
+#endif
     if constexpr (PEER) dg::peer_arrive(a.P);  // the last workgroup raises the flags and waits
+}
+
+// The wave-table form of the fused launch (dg_gcn_fused_tab_f32, round 5): the same rows, waves
+// and arithmetic as gcn_fused_seg_kernel, but every value a wave needs before its gathers —
+// its relation segment's bounds, gather base, W slab, and its roles in the two finishing
+// phases — is precomputed on the host into a 64-byte descriptor per (workgroup, wave), and the
+// segment's first 64 (vcol, value) pairs are stored at a fixed slot per wave.  So a wave's
+// first memory round trip loads its descriptor (one s_load_dwordx16) and its first pairs (one
+// dwordx2 per lane) together, instead of the target / group search over the launch arguments,
+// the segment bounds and then the pairs — three to five dependent round trips (config S,
+// scripts/fseg_prof.py: search 0.64 µs, bounds 0.60 µs median per wave before this).  Pairs
+// past the first 64 follow in batches of 64 from `ovf`.  Batches of 64 as in the seg form, so
+// the results are bitwise the seg form's.
+static_assert(sizeof(dg_tab_desc) == 64, "dg_tab_desc: one s_load_dwordx16");
+// pairs: [blocks * NW * 64] first batch of each wave (hand-out order); desc: [blocks * NW];
+// ovf: later batches, 64 entries each.  (Separate pointer arguments: loaded together.)
+template <bool PROJ, int NW>
+__global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restrict__ pairs,
+                                                          const dg_tab_desc* __restrict__ desc,
+                                                          const uint2* __restrict__ ovf) {
+    constexpr int LP = 16;
+    constexpr int G = dg::kWave / LP;
+    constexpr int DOUT4 = PROJ ? 8 : LP;
+    __shared__ float4 ybuf[NW][16];
+    __shared__ float4 zbuf[NW][DOUT4];
+    __shared__ float4 nbuf[kFsMaxRpb * DG_MAX_GROUPS][DOUT4];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wi = (int64_t)blockIdx.x * NW + wave;
+    // the first pairs issued before anything waits (inline asm: the compiler would sink a plain
+    // load below the descriptor's branch, behind its round trip); retired by the vmcnt(0) below
+    uint2 first;
+    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64)
+                 : "memory");
+    const dg_tab_desc D = desc[wi];  // (uniform: scalar loads)
+    // every descriptor field and the ovf base in SGPRs here, so no scalar load is sunk below
+    // the branch into a round trip of its own
+    asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(D.wr),
+                 "s"(ovf));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (D.cnt > 0) {  // wave-uniform
+        // batches of 64 pairs: the first from the slot, the rest from ovf, each prefetched
+        // before the batch before it is gathered
+        const float* xq = D.x + (lane % LP) * 4;
+        const int sub = lane / LP;
+        const int perm = 4 * (lane & 15) + (lane >> 4);  // (non-PROJ: the DPP hand-out order)
+        int vc = (int)first.x;
+        int vb = (int)first.y;
+        const uint2* nx = ovf + D.ovf;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+        for (int base = 0; base < D.cnt; base += 64) {
+            const int n = min(64, D.cnt - base);
+            const int eoff = vc * D.x_ld;
+            const int vbits = vb;
+            const float v = __int_as_float(vb);
+            vc = 0;
+            vb = 0;
+            if (base + 64 < D.cnt) {
+                const uint2 q = nx[lane];
+                vc = (int)q.x;
+                vb = (int)q.y;
+                nx += 64;
+            }
+            if constexpr (PROJ) {
+                // ds_bpermute hand-out (the seg form's seg_gather_shfl), pair p in lane p
+                constexpr int U = kFsegUP;
+#pragma unroll 1
+                for (int s0 = 0; s0 < n; s0 += U * G) {
+                    int o[U];
+                    float w[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int src = (s0 + u * G + sub) & 63;
+                        o[u] = __shfl(eoff, src);
+                        w[u] = __shfl(v, src);
+                    }
+                    float4 xv[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const bool ok = s0 + u * G + sub < n;
+                        xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (!ok) w[u] = 0.f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
+                }
+            } else {
+                // DPP row broadcasts (the seg form's seg_gather): pair m·G + sub of the batch sits
+                // in lane 16·sub + m
+                (void)perm;
+                constexpr int S = dg::kWave / G;
+                constexpr int U = kFsegU;
+#pragma unroll
+                for (int it = 0; it < S / U; ++it) {
+                    if (it * U * G >= n) break;  // wave-uniform
+                    int o[U];
+                    float w[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        o[u] = row_bcast_rt(eoff, it * U + u);
+                        w[u] = __int_as_float(row_bcast_rt(vbits, it * U + u));
+                    }
+                    float4 xv[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const bool ok = (it * U + u) * G + sub < n;
+                        xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (!ok) w[u] = 0.f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
+                }
+            }
+        }
+#pragma unroll
+        for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+        if constexpr (PROJ) {
+            // z = y·W_k: this lane's W slice (rows 8(l>>3) .. +8, output float4 l & 7) read
+            // after the gathers, as in seg_wave_proj
+            const int ms = lane >> 3;
+            const float4* w = reinterpret_cast<const float4*>(D.w) + (8 * ms) * 8 + (lane & 7);
+            float4 wv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wv[i] = w[8 * i];
+            if (lane < 16) ybuf[wave][lane] = acc;
+            __builtin_amdgcn_wave_barrier();
+            const float4 ya = ybuf[wave][2 * ms];
+            const float4 yb = ybuf[wave][2 * ms + 1];
+            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            dg::fma4(z, ya.x, wv[0]);
+            dg::fma4(z, ya.y, wv[1]);
+            dg::fma4(z, ya.z, wv[2]);
+            dg::fma4(z, ya.w, wv[3]);
+            dg::fma4(z, yb.x, wv[4]);
+            dg::fma4(z, yb.y, wv[5]);
+            dg::fma4(z, yb.z, wv[6]);
+            dg::fma4(z, yb.w, wv[7]);
+            dg::add4(z, dg::shfl_xor4(z, 8));
+            dg::add4(z, dg::shfl_xor4(z, 16));
+            dg::add4(z, dg::shfl_xor4(z, 32));
+            res = z;
+        } else {
+            res = acc;
+        }
+    }
+    if (lane < DOUT4) zbuf[wave][lane] = res;
+    __syncthreads();
+    // one wave per (row slot, group): its relations summed in order, L2-normalised
+    if (D.role >> 31) {
+        const int gb = D.role & 0xff, K = (D.role >> 8) & 0xff, ns = (D.role >> 16) & 0x7fff;
+        const int q = lane % DOUT4;
+        float4 sum = zbuf[gb][q];
+#pragma unroll 1
+        for (int u = 1; u < K; ++u) dg::add4(sum, zbuf[gb + u][q]);
+        // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
+        float ss = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
+#pragma unroll
+        for (int m = 1; m < DOUT4; m <<= 1) ss += __shfl_xor(ss, m);
+        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+        if (lane < DOUT4) nbuf[ns][lane] = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
+    }
+    __syncthreads();
+    if (D.orow != nullptr && lane < DOUT4) {
+        const int gc = D.wr & 0xff, s2 = D.wr >> 16;
+        float4 tot = nbuf[s2 * DG_MAX_GROUPS][lane];
+        for (int u = 1; u < gc; ++u) dg::add4(tot, nbuf[s2 * DG_MAX_GROUPS + u][lane]);
+        if ((D.wr >> 8) & 1) {
+            tot.x = fmaxf(tot.x, 0.f);
+            tot.y = fmaxf(tot.y, 0.f);
+            tot.z = fmaxf(tot.z, 0.f);
+            tot.w = fmaxf(tot.w, 0.f);
+        }
+        reinterpret_cast<float4*>(D.orow)[lane] = tot;
+    }
 }
 
 }  // namespace
@@ -602,6 +811,22 @@ int fused_seg_launch(const dg_seg_group* groups, int32_t n_groups, const dg_fuse
 }
 }  // namespace
 
+#ifdef DG_FSEG_PROF
+// Profiling build only: copy the last fused-seg launch's stamps of form proj (0 / 1).
+extern "C" int64_t dg_fseg_prof_copy(int proj, unsigned long long* host, int64_t max_blocks) {
+    const int64_t n = max_blocks < kFsProfMaxBlocks ? max_blocks : kFsProfMaxBlocks;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fs_prof), n * 16 * kFsProfSlots * 8, (size_t)(proj ? 1 : 0) *
+                            kFsProfMaxBlocks * 16 * kFsProfSlots * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
+}
+extern "C" int dg_fseg_prof_clear() {
+    static unsigned long long zero[2 * kFsProfMaxBlocks * 16 * kFsProfSlots] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fs_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int32_t d_in, int32_t d_out,
                                void* stream) {
     return seg_launch(groups, n_groups, d_in, d_out, stream);
@@ -610,6 +835,33 @@ extern "C" int dg_spmm_seg_f32(const dg_seg_group* groups, int32_t n_groups, int
 extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups, const dg_fused_target* targets,
                                     int32_t n_targets, int32_t d_in, int32_t d_out, void* stream) {
     return fused_seg_launch(groups, n_groups, targets, n_targets, d_in, d_out, nullptr, stream);
+}
+
+extern "C" int dg_gcn_fused_tab_f32(const dg_wave_table* t, int32_t d_in, int32_t d_out, void* stream) {
+    if (!t) return DG_EINVAL;
+    bool proj = false;
+    if (seg_shape(d_in, d_out, proj) != DG_OK || (!proj && d_in != 64)) return DG_EINVAL;
+    if (t->n_blocks < 0 || t->nw < 1 || t->nw > 16 || t->nw_stride != (t->nw <= 8 ? 8 : 16)) return DG_EINVAL;
+    if (t->n_blocks == 0) return DG_OK;
+    if (!t->pairs || !t->desc || !dg::aligned16(t->pairs) || (reinterpret_cast<uintptr_t>(t->desc) & 63))
+        return DG_EALIGN;
+    if ((int64_t)t->n_blocks * t->nw_stride * 64 > 0x7fffffffLL) return DG_EINVAL;
+    const uint2* pr = reinterpret_cast<const uint2*>(t->pairs);
+    const uint2* ov = reinterpret_cast<const uint2*>(t->ovf);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(t->n_blocks)), block(64 * t->nw);
+    if (t->nw_stride == 8) {
+        if (proj)
+            hipLaunchKernelGGL((gcn_tab_kernel<true, 8>), grid, block, 0, st, pr, t->desc, ov);
+        else
+            hipLaunchKernelGGL((gcn_tab_kernel<false, 8>), grid, block, 0, st, pr, t->desc, ov);
+    } else {
+        if (proj)
+            hipLaunchKernelGGL((gcn_tab_kernel<true, 16>), grid, block, 0, st, pr, t->desc, ov);
+        else
+            hipLaunchKernelGGL((gcn_tab_kernel<false, 16>), grid, block, 0, st, pr, t->desc, ov);
+    }
+    return dg::launch_status();
 }
 
 extern "C" int dg_gcn_fused_seg_peer_f32(const dg_seg_group* groups, int32_t n_groups,

@@ -89,6 +89,9 @@ SEG_FUSED = knob("DG_SEG_FUSED", True)
 # waves looped over more relations measured 25.2 µs a rank share at N = 4 (seg + epilogue 25.1)
 # and 35.6 at N = 8 (25.6), so it was not kept
 SEG_FUSED_MAX_ITEMS = 16
+# one-GPU fused-seg launches through dg_gcn_fused_tab_f32 (host-built wave table: each wave's
+# segment bounds, gather base and finishing roles precomputed, its first pairs at a fixed slot)
+FUSED_TAB = knob("DG_FUSED_TAB", True)
 STAGED_FIRST = knob("DG_STAGED_FIRST", True)
 # sharded forward plans: layer 2 of the non-staged groups reassociated over the rank's own rows
 # and relations, Σ_k (Â_k·H1_j)·W2_k in dg_spmm_seg_f32, instead of every rank projecting all of
@@ -687,7 +690,12 @@ class ForwardPlan:
             tgts = [(outs[i], n[i], [self._seg_spec(et, seg_w[et][0], None, seg_w[et][1]) if et in seg_w
                                      else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu)
                     for i in fused_t]
-            launches.append(kernels.PreparedFusedSeg(tgts, self.h1 if seg_w else d, d))
+            d_in = self.h1 if seg_w else d
+            if FUSED_TAB and d_in == 64 and (d == 64 or seg_w):
+                # the wave-table form: the same rows bitwise, fewer dependent loads a wave
+                launches.append(kernels.PreparedFusedTab(tgts, d_in, d))
+            else:
+                launches.append(kernels.PreparedFusedSeg(tgts, d_in, d))
             self.launch_groups[id(launches[-1])] = [et for i in fused_t for et in self.targets[i]]
         elif fused_t:
             # waves per group: small launches (latency-bound) split the densest row group's

@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (33); bumped whenever a struct layout or a signature changes. */
+/* ABI version (35); bumped whenever a struct layout or a signature changes. */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -220,6 +220,44 @@ int dg_spmm_seg_f32(const dg_seg_group* groups /* HOST array */, int32_t n_group
 int dg_gcn_fused_seg_f32(const dg_seg_group* groups /* HOST */, int32_t n_groups,
                          const dg_fused_target* targets /* HOST */, int32_t n_targets, int32_t d_in,
                          int32_t d_out, void* stream);
+
+/* The wave-table form of dg_gcn_fused_seg_f32 (round 5): the same launch — workgroups, waves,
+ * arithmetic and summation order, so bitwise the same rows — with everything a wave needs
+ * before its gathers precomputed on the host (decagon_amd/sparse.py: wave_table) instead of
+ * found at run time from the group and target arguments.  Wave w of workgroup b (slot
+ * i = b * nw_stride + w) reads desc[i] and the first batch of its relation segment's pairs,
+ * pairs[64 i .. 64 i + 63] (vcol, fp32 value bits: int32 pairs), in one round trip; a segment
+ * longer than 64 continues in ovf[desc[i].ovf ..] in batches of 64.  Within a batch, pair
+ * m of a d_in = 64, d_out = 64 table sits in entry 16 (m & 3) + (m >> 2) (the DPP hand-out
+ * order of the seg form), of a d_in = 64, d_out = 32 table (layer 2 reassociated) in entry m.
+ * A wave with cnt 0 gathers nothing; desc.role (active << 31 | nbuf slot << 16 | K << 8 | first
+ * wave) makes it the wave that sums and L2-normalises one (row slot, group); desc.orow != NULL
+ * makes it the writer of that output row (wr = group count | relu << 8 | row slot << 16).
+ * Shapes: d_in = d_out = 64, or d_in = 64, d_out = 32 with W slabs (desc.w).  Replaces
+ * layers.py:85-94 / 109-118 and model.py:74-75, 85-88 as dg_gcn_fused_seg_f32 does. */
+typedef struct dg_tab_desc {
+    const float* x;       /* device: gather base (vcol * x_ld floats from here)             */
+    const float* w;       /* device: the relation's W slab [64][32] (d_out 32), or NULL      */
+    float* orow;          /* device: the output row this wave writes, or NULL               */
+    int32_t cnt;          /* pairs of the wave's segment (0: none)                          */
+    int32_t x_ld;         /* floats                                                          */
+    int32_t ovf;          /* first entry of the later batches in ovf                         */
+    uint32_t role;
+    uint32_t wr;
+    int32_t pad[5];
+} dg_tab_desc;            /* 64 bytes                                                        */
+
+typedef struct dg_wave_table {
+    const int32_t* pairs; /* device, [n_blocks * nw_stride * 64][2], 16-byte aligned         */
+    const int32_t* ovf;   /* device, [..][2], or NULL                                        */
+    const dg_tab_desc* desc; /* device, [n_blocks * nw_stride], 64-byte aligned             */
+    int32_t n_blocks;
+    int32_t nw;           /* waves per workgroup, 1..16                                      */
+    int32_t nw_stride;    /* 8 if nw <= 8, else 16                                           */
+    int32_t pad;
+} dg_wave_table;
+
+int dg_gcn_fused_tab_f32(const dg_wave_table* table /* HOST */, int32_t d_in, int32_t d_out, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * LDS-staged relation SpMM for groups of many relations over a narrow column space

@@ -4,6 +4,10 @@
 //     16 (l >> 4) + 64 q — consecutive lanes (a quad) read four different rows
 //   B ("pair-major"): lane l reads row r[l >> 2] at byte 16 (l & 3) + 64 q — a quad reads 64
 //     contiguous bytes of one row
+//   C: as B with the quad's four chunks in rotated order (2, 3, 0, 1)
+//   E: as B with a quad's 4 lanes XOR-permuted by the row (chunk (l & 3) ^ (row & 3))
+//   S: the staged kernel's slab copy: 5 lanes per row (chunks 0-3 and a pad lane re-reading
+//     chunk 3), so 3 of every 5 quads straddle two rows
 // Both read 16 rows x 64 B per instruction from a 645-row x 512-B bf16 table (L2-resident),
 // 12 waves per CU on every CU, rows drawn by a hash per (wave, iteration).
 // Build: hipcc -O3 --offload-arch=gfx950 -o scripts/ta_probe scripts/ta_probe.hip
@@ -28,11 +32,12 @@ __global__ __launch_bounds__(768) void probe(const uint16_t* table, int n_rows, 
     const int wave = blockIdx.x * 12 + (threadIdx.x >> 6);
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(table), 0, 0x7fffffff, 0x00020000);
     float acc = 0.f;
-    const int pr = MODE == 0 ? (lane & 15) : (lane >> 2);
-    const int ch = MODE == 0 ? (lane >> 4) : (lane & 3);
+    const int pr = MODE == 0 ? (lane & 15) : MODE == 4 ? lane / 5 : (lane >> 2);
+    int ch = MODE == 0 ? (lane >> 4) : MODE == 2 ? ((lane & 3) + 2) & 3 : MODE == 4 ? min(lane % 5, 3) : (lane & 3);
     for (int it = 0; it < iters; ++it) {
         const int row = (int)(hash32((uint32_t)(wave * 131071 + it * 16 + pr)) % (uint32_t)n_rows);
-        const int base = row * 512 + 16 * ch;
+        const int c2 = MODE == 3 ? ch ^ (row & 3) : ch;
+        const int base = row * 512 + 16 * c2;
         uint4 v[ROWS_IN_FLIGHT];
 #pragma unroll
         for (int q = 0; q < ROWS_IN_FLIGHT; ++q)
@@ -77,6 +82,9 @@ int main() {
     run(probe<1, 2>, "B_pair_major_x2", 2);
     run(probe<0, 8>, "A_pair_minor_x8", 8);
     run(probe<1, 8>, "B_pair_major_x8", 8);
+    run(probe<2, 8>, "C_pair_major_rotated_x8", 8);
+    run(probe<3, 8>, "E_pair_major_xor_by_row_x8", 8);
+    run(probe<4, 8>, "S_slab_copy_5_lanes_per_row_x8", 8);
     hipFree(d);
     hipFree(out);
     return 0;

@@ -58,13 +58,15 @@ def _setup(z, edge_order=None):
     return dg, ph, model, opt, feed
 
 
-@pytest.mark.parametrize("fused_seg", [True, False])
-def test_forward_matches_golden(golden_S, monkeypatch, fused_seg):
-    """Config S's golden forward through the Session, in dg_gcn_fused_seg_f32 (layer 2
-    reassociated; the default) and in dg_gcn_fused_f32 with the projection epilogue."""
+@pytest.mark.parametrize("fused_seg,tab", [(True, True), (True, False), (False, False)])
+def test_forward_matches_golden(golden_S, monkeypatch, fused_seg, tab):
+    """Config S's golden forward through the Session, in dg_gcn_fused_tab_f32 (the default: the
+    fused-seg layer from a host-built wave table), dg_gcn_fused_seg_f32 (layer 2 reassociated)
+    and dg_gcn_fused_f32 with the projection epilogue."""
     from decagon_amd import engine
 
     monkeypatch.setattr(engine, "FUSED_SEG", fused_seg)
+    monkeypatch.setattr(engine, "FUSED_TAB", tab)
     z = golden_S
     dg, ph, model, opt, feed = _setup(z)
     sess = dg.Session()

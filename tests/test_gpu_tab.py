@@ -1,0 +1,82 @@
+"""GPU: the wave-table fused launch (dg_gcn_fused_tab_f32) against the fused-seg launch it
+replaces (dg_gcn_fused_seg_f32) — the same workgroups, waves, batches of 64 and summation order,
+so the rows must agree bit for bit — on config S's two layers (the benched form: layer 1 and
+the reassociated layer 2) and on a graph of config S's shape whose rows carry relation segments
+of 0 to 300 pairs, so the first-batch slot, one and several overflow batches and empty waves
+all occur.  Parity with the oracle goes through test_gpu_model.py's golden forward, which runs
+this form by default.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _plan(graph):
+    import bench
+
+    args = bench.parse(["--config", "S"])
+    args.chunk = dict(graph.edge_types)  # one chunk per group (the fused form's layout)
+    plan, _ = bench.make_plan(args, graph, None, torch.device("cuda", 0))
+    return plan
+
+
+def _check(plan):
+    from decagon_amd import kernels
+
+    plan.run()
+    torch.cuda.synchronize()
+    n = 0
+    for layer in plan.spmm_launches:
+        for launch in layer:
+            if not isinstance(launch, kernels.PreparedFusedTab):
+                continue
+            outs = launch._keep[1]
+            launch()
+            torch.cuda.synchronize()
+            tab = [o.clone() for o in outs]
+            for o in outs:
+                o.fill_(float("nan"))
+            launch.seg_form()
+            torch.cuda.synchronize()
+            for a, b in zip(tab, outs):
+                assert torch.isfinite(a).all()
+                assert torch.equal(a, b)
+            n += 1
+    assert n == 2, "both layers run the wave-table form"
+
+
+def test_config_S_wave_table_equals_seg_form_bitwise():
+    from decagon_amd import synthetic
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    _check(_plan(synthetic.load_S()))
+
+
+def test_long_segments_wave_table_equals_seg_form_bitwise():
+    """Rows whose per-relation segments run to 300 pairs (first batch + up to 4 overflow
+    batches), rows with none, on config S's edge types and node counts."""
+    from decagon_amd import synthetic
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    base = synthetic.load_S()
+    rng = np.random.default_rng(3)
+    adj = {}
+    for (i, j), K in base.edge_types.items():
+        n_r, n_c = base.n_nodes[i], base.n_nodes[j]
+        rels = []
+        for k in range(K):
+            lens = rng.choice([0, 3, 17, 63, 64, 65, 129, 300], size=n_r, p=[.1, .2, .2, .1, .1, .1, .1, .1])
+            lens = np.minimum(lens, n_c)
+            rows = np.repeat(np.arange(n_r), lens)
+            cols = np.concatenate([rng.choice(n_c, size=m, replace=False) for m in lens]) if lens.sum() else \
+                np.zeros(0, np.int64)
+            vals = rng.standard_normal(rows.size).astype(np.float32) * 0.1
+            rels.append((np.stack([rows, cols], 1).astype(np.int64), vals, (n_r, n_c)))
+        adj[i, j] = rels
+    g = synthetic.SyntheticGraph("S-long", dict(base.n_nodes), dict(base.edge_types), dict(base.decoders), adj,
+                                 base.degrees)
+    _check(_plan(g))
