@@ -303,7 +303,8 @@ def timed_steps(step, steps, warmup, G, stream, use_graph=True, barrier=None):
 
 KERNEL_NAMES = {"PreparedFused": "gcn_fused_kernel<{lp}>", "PreparedSpmm": "spmm_groups_kernel<{lp}>",
                 "PreparedStaged": "spmm_staged_kernel", "PreparedFusedSeg": "gcn_fused_seg_kernel<{lp}, {proj}",
-                "PreparedSeg": "spmm_seg_kernel<{lp}, {proj}"}
+                "PreparedSeg": "spmm_seg_kernel<{lp}, {proj}", "PreparedFusedTab": "gcn_tab_kernel<{proj}",
+                "PreparedSegTab": "seg_tab_kernel<{proj}"}
 
 
 def _kernel_pat(launch, d):

@@ -473,37 +473,23 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
 static_assert(sizeof(dg_tab_desc) == 64, "dg_tab_desc: one s_load_dwordx16");
 // pairs: [blocks * NW * 64] first batch of each wave (hand-out order); desc: [blocks * NW];
 // ovf: later batches, 64 entries each.  (Separate pointer arguments: loaded together.)
-template <bool PROJ, int NW>
-__global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restrict__ pairs,
-                                                          const dg_tab_desc* __restrict__ desc,
-                                                          const uint2* __restrict__ ovf) {
+// A wave's relation sum from its wave-table slot (the first pairs already in `first`): batches
+// of 64 pairs, the first from the slot, the rest from ovf, each prefetched before the batch
+// before it is gathered; U gathers in flight per lane.  PROJ: ds_bpermute hand-out (pair p in
+// lane p) and the 64-wide aggregate times the relation's W slab (seg_wave_proj's arithmetic);
+// else DPP row broadcasts (seg_gather's: pair m·G + sub of a batch in lane 16·sub + m).
+template <bool PROJ, int U>
+__device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 first, const uint2* __restrict__ ovf,
+                                           float4* ybuf) {
     constexpr int LP = 16;
     constexpr int G = dg::kWave / LP;
-    constexpr int DOUT4 = PROJ ? 8 : LP;
-    __shared__ float4 ybuf[NW][16];
-    __shared__ float4 zbuf[NW][DOUT4];
-    __shared__ float4 nbuf[kFsMaxRpb * DG_MAX_GROUPS][DOUT4];
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t wi = (int64_t)blockIdx.x * NW + wave;
-    // the first pairs issued before anything waits (inline asm: the compiler would sink a plain
-    // load below the descriptor's branch, behind its round trip); retired by the vmcnt(0) below
-    uint2 first;
-    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64)
-                 : "memory");
-    const dg_tab_desc D = desc[wi];  // (uniform: scalar loads)
-    // every descriptor field and the ovf base in SGPRs here, so no scalar load is sunk below
-    // the branch into a round trip of its own
-    asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(D.wr),
-                 "s"(ovf));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
     if (D.cnt > 0) {  // wave-uniform
         // batches of 64 pairs: the first from the slot, the rest from ovf, each prefetched
         // before the batch before it is gathered
         const float* xq = D.x + (lane % LP) * 4;
         const int sub = lane / LP;
-        const int perm = 4 * (lane & 15) + (lane >> 4);  // (non-PROJ: the DPP hand-out order)
         int vc = (int)first.x;
         int vb = (int)first.y;
         const uint2* nx = ovf + D.ovf;
@@ -524,7 +510,6 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
             }
             if constexpr (PROJ) {
                 // ds_bpermute hand-out (the seg form's seg_gather_shfl), pair p in lane p
-                constexpr int U = kFsegUP;
 #pragma unroll 1
                 for (int s0 = 0; s0 < n; s0 += U * G) {
                     int o[U];
@@ -548,9 +533,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
             } else {
                 // DPP row broadcasts (the seg form's seg_gather): pair m·G + sub of the batch sits
                 // in lane 16·sub + m
-                (void)perm;
-                constexpr int S = dg::kWave / G;
-                constexpr int U = kFsegU;
+                                constexpr int S = dg::kWave / G;
 #pragma unroll
                 for (int it = 0; it < S / U; ++it) {
                     if (it * U * G >= n) break;  // wave-uniform
@@ -583,10 +566,10 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
             float4 wv[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) wv[i] = w[8 * i];
-            if (lane < 16) ybuf[wave][lane] = acc;
+            if (lane < 16) ybuf[lane] = acc;
             __builtin_amdgcn_wave_barrier();
-            const float4 ya = ybuf[wave][2 * ms];
-            const float4 yb = ybuf[wave][2 * ms + 1];
+            const float4 ya = ybuf[2 * ms];
+            const float4 yb = ybuf[2 * ms + 1];
             float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
             dg::fma4(z, ya.x, wv[0]);
             dg::fma4(z, ya.y, wv[1]);
@@ -604,6 +587,32 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
             res = acc;
         }
     }
+    return res;
+}
+
+template <bool PROJ, int NW>
+__global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restrict__ pairs,
+                                                          const dg_tab_desc* __restrict__ desc,
+                                                          const uint2* __restrict__ ovf) {
+    constexpr int DOUT4 = PROJ ? 8 : 16;
+    __shared__ float4 ybuf[NW][16];
+    __shared__ float4 zbuf[NW][DOUT4];
+    __shared__ float4 nbuf[kFsMaxRpb * DG_MAX_GROUPS][DOUT4];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wi = (int64_t)blockIdx.x * NW + wave;
+    // the first pairs issued before anything waits (inline asm: the compiler would sink a plain
+    // load below the descriptor's branch, behind its round trip); retired by the vmcnt(0) below
+    uint2 first;
+    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64)
+                 : "memory");
+    const dg_tab_desc D = desc[wi];  // (uniform: scalar loads)
+    // every descriptor field and the ovf base in SGPRs here, so no scalar load is sunk below
+    // the branch into a round trip of its own
+    asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(D.wr),
+                 "s"(ovf));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const float4 res = tab_wave<PROJ, PROJ ? kFsegUP : kFsegU>(D, first, ovf, ybuf[wave]);
     if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
     // one wave per (row slot, group): its relations summed in order, L2-normalised
@@ -632,6 +641,38 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
             tot.w = fmaxf(tot.w, 0.f);
         }
         reinterpret_cast<float4*>(D.orow)[lane] = tot;
+    }
+}
+
+// The wave-table form of spmm_seg_kernel (dg_spmm_seg_tab_f32, round 5): the same workgroups
+// (XCD-contiguous item map included), waves, batches and sums — bitwise its chunk partials —
+// with each wave's segment, gather base, W slab and (for the first wave of a row's chunk) the
+// partial row it writes and the waves it sums precomputed on the host: desc.orow != NULL marks
+// that wave, desc.role bits 8-15 the chunk's waves.
+template <bool PROJ, int NW>
+__global__ __launch_bounds__(64 * NW) void seg_tab_kernel(const uint2* __restrict__ pairs,
+                                                          const dg_tab_desc* __restrict__ desc,
+                                                          const uint2* __restrict__ ovf) {
+    constexpr int DOUT4 = PROJ ? 8 : 16;
+    __shared__ float4 ybuf[NW][16];
+    __shared__ float4 zbuf[NW][DOUT4];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wi = (int64_t)blockIdx.x * NW + wave;
+    uint2 first;
+    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64)
+                 : "memory");
+    const dg_tab_desc D = desc[wi];
+    asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(ovf));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const float4 res = tab_wave<PROJ, PROJ ? kSegUP : kSegU>(D, first, ovf, ybuf[wave]);
+    if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
+    __syncthreads();
+    if (D.orow != nullptr && lane < DOUT4) {
+        const int K = (D.role >> 8) & 0xff;
+        float4 sm = zbuf[wave][lane];
+        for (int u = 1; u < K; ++u) dg::add4(sm, zbuf[wave + u][lane]);
+        reinterpret_cast<float4*>(D.orow)[lane] = sm;
     }
 }
 
@@ -860,6 +901,33 @@ extern "C" int dg_gcn_fused_tab_f32(const dg_wave_table* t, int32_t d_in, int32_
             hipLaunchKernelGGL((gcn_tab_kernel<true, 16>), grid, block, 0, st, pr, t->desc, ov);
         else
             hipLaunchKernelGGL((gcn_tab_kernel<false, 16>), grid, block, 0, st, pr, t->desc, ov);
+    }
+    return dg::launch_status();
+}
+
+extern "C" int dg_spmm_seg_tab_f32(const dg_wave_table* t, int32_t d_in, int32_t d_out, void* stream) {
+    if (!t) return DG_EINVAL;
+    bool proj = false;
+    if (seg_shape(d_in, d_out, proj) != DG_OK || (!proj && d_in != 64)) return DG_EINVAL;
+    if (t->n_blocks < 0 || t->nw < 1 || t->nw > 16 || t->nw_stride != (t->nw <= 8 ? 8 : 16)) return DG_EINVAL;
+    if (t->n_blocks == 0) return DG_OK;
+    if (!t->pairs || !t->desc || !dg::aligned16(t->pairs) || (reinterpret_cast<uintptr_t>(t->desc) & 63))
+        return DG_EALIGN;
+    if ((int64_t)t->n_blocks * t->nw_stride * 64 > 0x7fffffffLL) return DG_EINVAL;
+    const uint2* pr = reinterpret_cast<const uint2*>(t->pairs);
+    const uint2* ov = reinterpret_cast<const uint2*>(t->ovf);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(t->n_blocks)), block(64 * t->nw);
+    if (t->nw_stride == 8) {
+        if (proj)
+            hipLaunchKernelGGL((seg_tab_kernel<true, 8>), grid, block, 0, st, pr, t->desc, ov);
+        else
+            hipLaunchKernelGGL((seg_tab_kernel<false, 8>), grid, block, 0, st, pr, t->desc, ov);
+    } else {
+        if (proj)
+            hipLaunchKernelGGL((seg_tab_kernel<true, 16>), grid, block, 0, st, pr, t->desc, ov);
+        else
+            hipLaunchKernelGGL((seg_tab_kernel<false, 16>), grid, block, 0, st, pr, t->desc, ov);
     }
     return dg::launch_status();
 }

@@ -89,9 +89,11 @@ SEG_FUSED = knob("DG_SEG_FUSED", True)
 # waves looped over more relations measured 25.2 µs a rank share at N = 4 (seg + epilogue 25.1)
 # and 35.6 at N = 8 (25.6), so it was not kept
 SEG_FUSED_MAX_ITEMS = 16
-# one-GPU fused-seg launches through dg_gcn_fused_tab_f32 (host-built wave table: each wave's
-# segment bounds, gather base and finishing roles precomputed, its first pairs at a fixed slot)
-FUSED_TAB = knob("DG_FUSED_TAB", True)
+# fused-seg and seg launches (config S on one GPU and its N-GPU row blocks) through their
+# wave-table forms, dg_gcn_fused_tab_f32 / dg_spmm_seg_tab_f32 (host-built: each wave's segment
+# bounds, gather base and finishing roles precomputed, its first pairs at a fixed slot; bitwise
+# the same rows): config S's step 18.14 -> 15.56 us at 200 steps (round 5)
+WAVE_TABLE = knob("DG_WAVE_TABLE", True)
 STAGED_FIRST = knob("DG_STAGED_FIRST", True)
 # sharded forward plans: layer 2 of the non-staged groups reassociated over the rank's own rows
 # and relations, Σ_k (Â_k·H1_j)·W2_k in dg_spmm_seg_f32, instead of every rank projecting all of
@@ -679,7 +681,11 @@ class ForwardPlan:
                              [self._seg_spec(et, seg_w[et][0], None, seg_w[et][1]) if et in seg_w
                               else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu))
             fused_peer = self._peer_fused(relu)
-            launches.append(kernels.PreparedFusedSeg(tgts, self.h1 if seg_w else d, d, peer=fused_peer))
+            d_in = self.h1 if seg_w else d
+            if fused_peer is None and WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
+                launches.append(kernels.PreparedFusedTab(tgts, d_in, d))  # (the wave-table form)
+            else:
+                launches.append(kernels.PreparedFusedSeg(tgts, d_in, d, peer=fused_peer))
             self.launch_groups[id(launches[-1])] = [et for i in self.targets for et in self.targets[i]]
             if fused_peer is not None:
                 gathers = []  # the launch itself ends with the exchange
@@ -691,7 +697,7 @@ class ForwardPlan:
                                      else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu)
                     for i in fused_t]
             d_in = self.h1 if seg_w else d
-            if FUSED_TAB and d_in == 64 and (d == 64 or seg_w):
+            if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
                 # the wave-table form: the same rows bitwise, fewer dependent loads a wave
                 launches.append(kernels.PreparedFusedTab(tgts, d_in, d))
             else:
@@ -792,7 +798,11 @@ class ForwardPlan:
             seg_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged
                        and (self.seg_mode or et in reassoc)]
             for s in range(0, len(segs), DG_MAX_GROUPS):
-                launches.append(kernels.PreparedSeg(segs[s:s + DG_MAX_GROUPS], d_in, d))
+                part = segs[s:s + DG_MAX_GROUPS]
+                if WAVE_TABLE and kernels._tab_shape(d_in, d, part):
+                    launches.append(kernels.PreparedSegTab(part, d_in, d))  # (the wave-table form)
+                else:
+                    launches.append(kernels.PreparedSeg(part, d_in, d))
                 self.launch_groups[id(launches[-1])] = seg_ets[s:s + DG_MAX_GROUPS]
         staged_ets = [et for et in rest if g.groups[et].n_rels and g.groups[et].staged]
         spmm_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged]

@@ -331,6 +331,73 @@ class PreparedFusedSeg:
               "dg_gcn_fused_seg_f32")
 
 
+class _WaveTable:
+    """Host builder of a dg_wave_table (decagon_hip.h): per wave slot a 64-byte descriptor and
+    the first 64 pairs of its relation segment (in the hand-out order of its gather form), the
+    rest in batches of 64 in an overflow array."""
+
+    DESC = np.dtype([("x", "<u8"), ("w", "<u8"), ("orow", "<u8"), ("cnt", "<i4"), ("x_ld", "<i4"), ("ovf", "<i4"),
+                     ("role", "<u4"), ("wr", "<u4"), ("pad", "<i4", 5)])
+
+    def __init__(self, specs: Sequence[SegSpec], n_slots: int, proj: bool):
+        assert self.DESC.itemsize == 64
+        self.specs, self.proj = list(specs), proj
+        self.host = [(s.rowptr.cpu().numpy(), s.seg.cpu().numpy(), s.vcol.cpu().numpy(), s.val.cpu().numpy(),
+                      None if s.slab is None else s.slab.cpu().numpy()) for s in specs]
+        self.pairs = np.zeros((n_slots * 64, 2), np.int32)
+        self.desc = np.zeros(n_slots, self.DESC)
+        self.ovf: List[np.ndarray] = []
+        self.n_ovf = 0
+        # entry of pair m within a batch: its lane in the DPP hand-out (d_out 64) or m (layer 2)
+        m = np.arange(64)
+        self.lane_of = m if proj else 16 * (m & 3) + (m >> 2)
+
+    def relation(self, i: int, g: int, k: int, r: int) -> None:
+        """Wave slot i gathers relation k (of spec g) of row r."""
+        s = self.specs[g]
+        rowptr, seg, vcol, val, slab = self.host[g]
+        c, t = divmod(k, s.chunk)
+        si = (c * s.n_rows + r) * s.chunk + t
+        beg = int(seg[si])
+        end = int(seg[si + 1]) if t + 1 < s.chunk else int(rowptr[c * s.n_rows + r + 1])
+        vc = vcol[beg:end].astype(np.int64)
+        d = self.desc
+        if self.proj:
+            sl = int(slab[k]) if slab is not None else k
+            vc = vc - sl * s.n_cols  # plain rows of H
+            d["w"][i] = s.w.data_ptr() + sl * 64 * 32 * 4
+        cnt = end - beg
+        d["x"][i], d["x_ld"][i], d["cnt"][i] = s.x.data_ptr(), s.x_ld, cnt
+        pv = np.stack([vc.astype(np.int32), val[beg:end].view(np.int32)], 1)
+        m0 = min(cnt, 64)
+        self.pairs[i * 64 + self.lane_of[:m0]] = pv[:m0]
+        if cnt > 64:
+            d["ovf"][i] = self.n_ovf
+            for q0 in range(64, cnt, 64):
+                blk = np.zeros((64, 2), np.int32)
+                n = min(64, cnt - q0)
+                blk[self.lane_of[:n]] = pv[q0:q0 + n]
+                self.ovf.append(blk)
+                self.n_ovf += 64
+
+    def upload(self, owner, n_blocks: int, nw: int, stride: int, dev) -> "_lib.DgWaveTable":
+        owner._pairs = torch.from_numpy(self.pairs).to(dev)
+        owner._ovf = torch.from_numpy(np.concatenate(self.ovf) if self.ovf else np.zeros((64, 2), np.int32)).to(dev)
+        raw = torch.from_numpy(self.desc.view(np.uint8).copy())
+        owner._desc = torch.empty(raw.numel() + 64, dtype=torch.uint8, device=dev)
+        off = (-owner._desc.data_ptr()) % 64  # 64-byte aligned descriptors
+        owner._desc_v = owner._desc[off:off + raw.numel()]
+        owner._desc_v.copy_(raw.to(dev))
+        tab = _lib.DgWaveTable()
+        tab.pairs, tab.ovf, tab.desc = owner._pairs.data_ptr(), owner._ovf.data_ptr(), owner._desc_v.data_ptr()
+        tab.n_blocks, tab.nw, tab.nw_stride = n_blocks, nw, stride
+        return tab
+
+
+def _tab_shape(d_in: int, d_out: int, specs) -> bool:
+    return d_in == 64 and (d_out == 64 or (d_out == 32 and all(s.w is not None for s in specs)))
+
+
 class PreparedFusedTab(PreparedFusedSeg):
     """The same launch as PreparedFusedSeg (same targets, rows, waves and arithmetic: bitwise the
     same rows) through dg_gcn_fused_tab_f32: the wave table — each wave's 64-byte descriptor and
@@ -340,38 +407,24 @@ class PreparedFusedTab(PreparedFusedSeg):
 
     def __init__(self, targets, d_in: int, d_out: int):
         super().__init__(targets, d_in, d_out)
-        proj = d_out != d_in
-        if not (d_in == 64 and (d_out == 64 or (d_out == 32 and all(s.w is not None for s in self._keep[0])))):
-            raise ValueError("dg_gcn_fused_tab_f32: d_in = d_out = 64, or 64 -> 32 with weight stacks")
         specs = self._keep[0]
-        host = [(s.rowptr.cpu().numpy(), s.seg.cpu().numpy(), s.vcol.cpu().numpy(), s.val.cpu().numpy(),
-                 None if s.slab is None else s.slab.cpu().numpy()) for s in specs]
+        if not _tab_shape(d_in, d_out, specs):
+            raise ValueError("dg_gcn_fused_tab_f32: d_in = d_out = 64, or 64 -> 32 with weight stacks")
         waves_t = [sum(s.n_rels for s in gs) for _, _, gs, _ in targets]
         nw = max([1] + waves_t)
         stride = 8 if nw <= 8 else 16
-        plan = []  # (target index, first row) per workgroup, in launch order
+        plan = []  # (target, first row, rows per workgroup) per workgroup, in launch order
         for t, (_, n_rows, _, _) in enumerate(targets):
             rpb = min(nw // waves_t[t], 4)
             plan += [(t, r0, rpb) for r0 in range(0, n_rows, rpb)]
-        n_blocks = len(plan)
-        pairs = np.zeros((n_blocks * stride * 64, 2), np.int32)
-        desc = np.zeros(n_blocks * stride, dtype=[("x", "<u8"), ("w", "<u8"), ("orow", "<u8"), ("cnt", "<i4"),
-                                                   ("x_ld", "<i4"), ("ovf", "<i4"), ("role", "<u4"), ("wr", "<u4"),
-                                                   ("pad", "<i4", 5)])
-        assert desc.dtype.itemsize == 64
-        ovf = []
-        n_ovf = 0
-        # entry of pair m within a batch: the DPP hand-out order (d_out 64) or m (layer 2)
-        lane_of = np.arange(64) if proj else 16 * (np.arange(64) & 3) + (np.arange(64) >> 2)
+        tb = _WaveTable(specs, len(plan) * stride, d_out != d_in)
         g_first = np.cumsum([0] + [len(gs) for _, _, gs, _ in targets])
         for b, (t, r0, rpb) in enumerate(plan):
             out, n_rows, gspecs, relu = targets[t]
             gc = len(gspecs)
             nr = [s.n_rels for s in gspecs]
-            for w in range(stride):
+            for w in range(nw):
                 i = b * stride + w
-                if w >= nw:
-                    continue
                 slot, wi = divmod(w, waves_t[t])
                 r = r0 + slot
                 if slot < rpb and r < n_rows:
@@ -379,51 +432,16 @@ class PreparedFusedTab(PreparedFusedSeg):
                     while wi >= nr[gl]:
                         wi -= nr[gl]
                         gl += 1
-                    s = gspecs[gl]
-                    rowptr, seg, vcol, val, slab = host[g_first[t] + gl]
-                    k = wi
-                    c, tt = divmod(k, s.chunk)
-                    si = (c * s.n_rows + r) * s.chunk + tt
-                    beg = int(seg[si])
-                    end = int(seg[si + 1]) if tt + 1 < s.chunk else int(rowptr[c * s.n_rows + r + 1])
-                    vc = vcol[beg:end].astype(np.int64)
-                    if proj:
-                        sl = int(slab[k]) if slab is not None else k
-                        vc = vc - sl * s.n_cols  # plain H1 rows
-                        desc["w"][i] = s.w.data_ptr() + sl * 64 * 32 * 4
-                    cnt = end - beg
-                    desc["x"][i], desc["x_ld"][i], desc["cnt"][i] = s.x.data_ptr(), s.x_ld, cnt
-                    pv = np.stack([vc.astype(np.int32), val[beg:end].view(np.int32)], 1)
-                    m0 = min(cnt, 64)
-                    pairs[i * 64 + lane_of[:m0]] = pv[:m0]
-                    if cnt > 64:
-                        desc["ovf"][i] = n_ovf
-                        for q0 in range(64, cnt, 64):
-                            blk = np.zeros((64, 2), np.int32)
-                            m = min(64, cnt - q0)
-                            blk[lane_of[:m]] = pv[q0:q0 + m]
-                            ovf.append(blk)
-                            n_ovf += 64
+                    tb.relation(i, g_first[t] + gl, wi, r)
                 if w < rpb * gc:
                     s2, gg = divmod(w, gc)
                     gb = s2 * waves_t[t] + sum(nr[:gg])
-                    desc["role"][i] = (1 << 31) | ((s2 * DG_MAX_GROUPS_TAB + gg) << 16) | (nr[gg] << 8) | gb
+                    tb.desc["role"][i] = (1 << 31) | ((s2 * DG_MAX_GROUPS_TAB + gg) << 16) | (nr[gg] << 8) | gb
                 if w < rpb and r0 + w < n_rows:
-                    desc["orow"][i] = out.data_ptr() + (r0 + w) * d_out * 4
-                    desc["wr"][i] = gc | ((1 if relu else 0) << 8) | (w << 16)
-        dev = specs[0].x.device
-        self._pairs = torch.from_numpy(pairs).to(dev)
-        self._ovf = torch.from_numpy(np.concatenate(ovf) if ovf else np.zeros((64, 2), np.int32)).to(dev)
-        raw = torch.from_numpy(desc.view(np.uint8).copy())
-        self._desc = torch.empty(raw.numel() + 64, dtype=torch.uint8, device=dev)  # 64-byte aligned view
-        off = (-self._desc.data_ptr()) % 64
-        self._desc_v = self._desc[off:off + raw.numel()]
-        self._desc_v.copy_(raw.to(dev))
-        tab = _lib.DgWaveTable()
-        tab.pairs, tab.ovf, tab.desc = self._pairs.data_ptr(), self._ovf.data_ptr(), self._desc_v.data_ptr()
-        tab.n_blocks, tab.nw, tab.nw_stride = n_blocks, nw, stride
-        self._tab = tab
-        self.n_blocks, self.nw = n_blocks, nw
+                    tb.desc["orow"][i] = out.data_ptr() + (r0 + w) * d_out * 4
+                    tb.desc["wr"][i] = gc | ((1 if relu else 0) << 8) | (w << 16)
+        self._tab = tb.upload(self, len(plan), nw, stride, specs[0].x.device)
+        self.n_blocks, self.nw = len(plan), nw
         self._tfn = _lib.load().dg_gcn_fused_tab_f32
 
     def __call__(self, stream=None) -> None:
@@ -433,6 +451,59 @@ class PreparedFusedTab(PreparedFusedSeg):
     def seg_form(self, stream=None) -> None:
         """The same rows through dg_gcn_fused_seg_f32 (tests: bitwise equal)."""
         PreparedFusedSeg.__call__(self, stream)
+
+
+class PreparedSegTab(PreparedSeg):
+    """The same launch as PreparedSeg (dg_spmm_seg_f32's workgroups in its XCD-contiguous item
+    order, waves and chunk partials — bit for bit) through dg_spmm_seg_tab_f32, from a wave
+    table built here once.  Shapes as PreparedFusedTab."""
+
+    def __init__(self, specs: Sequence[SegSpec], d_in: int, d_out: int):
+        super().__init__(specs, d_in, d_out)
+        if not _tab_shape(d_in, d_out, specs):
+            raise ValueError("dg_spmm_seg_tab_f32: d_in = d_out = 64, or 64 -> 32 with weight stacks")
+        live = [g for g, s in enumerate(specs) if s.n_rows > 0 and s.n_rels > 0]
+        nw = max([1] + [specs[g].chunk for g in live])
+        stride = 8 if nw <= 8 else 16
+        blocks = []  # (spec, chunk c, first row, rows per workgroup) or None (a dead workgroup)
+        for g in live:
+            s = specs[g]
+            rpb = nw // s.chunk
+            row_blocks = -(-s.n_rows // rpb)
+            items = s.n_chunks * row_blocks
+            n_blocks = 8 * (-(-items // 8))
+            per = n_blocks >> 3
+            for lb in range(n_blocks):
+                item = (lb & 7) * per + (lb >> 3)
+                blocks.append(None if item >= items else (g, item // row_blocks, (item % row_blocks) * rpb, rpb))
+        tb = _WaveTable(specs, len(blocks) * stride, d_out != d_in)
+        for b, blk in enumerate(blocks):
+            if blk is None:
+                continue
+            g, c, r0, rpb = blk
+            s = specs[g]
+            for w in range(nw):
+                i = b * stride + w
+                slot, t = divmod(w, s.chunk)
+                r = r0 + slot
+                if not (slot < rpb and r < s.n_rows):
+                    continue
+                k = c * s.chunk + t
+                if k < s.n_rels:
+                    tb.relation(i, g, k, r)
+                if t == 0:
+                    tb.desc["orow"][i] = s.out.data_ptr() + (c * s.n_rows + r) * d_out * 4
+                    tb.desc["role"][i] = s.chunk << 8
+        self._tab = tb.upload(self, len(blocks), nw, stride, specs[0].x.device)
+        self.n_blocks, self.nw = len(blocks), nw
+        self._tfn = _lib.load().dg_spmm_seg_tab_f32
+
+    def __call__(self, stream=None) -> None:
+        check(self._tfn(ctypes.byref(self._tab), self.d_in, self.d_out, _stream_ptr(stream)), "dg_spmm_seg_tab_f32")
+
+    def seg_form(self, stream=None) -> None:
+        """The same partials through dg_spmm_seg_f32 (tests: bitwise equal)."""
+        PreparedSeg.__call__(self, stream)
 
 
 DG_MAX_GROUPS_TAB = 8  # nbuf groups per row slot in gcn_tab_kernel (DG_MAX_GROUPS)

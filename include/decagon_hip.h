@@ -259,6 +259,13 @@ typedef struct dg_wave_table {
 
 int dg_gcn_fused_tab_f32(const dg_wave_table* table /* HOST */, int32_t d_in, int32_t d_out, void* stream);
 
+/* The wave-table form of dg_spmm_seg_f32 (partial mode; config S's N-GPU layers): the same
+ * workgroups (in that entry point's XCD-contiguous item order), waves and chunk partials, bit
+ * for bit, from a host-built table with the layout above.  A wave whose desc.orow != NULL is
+ * the first wave of its (chunk, row): after the barrier it adds the (desc.role >> 8) & 0xff
+ * waves from itself on, in order, and stores the partial row there.  Shapes as above. */
+int dg_spmm_seg_tab_f32(const dg_wave_table* table /* HOST */, int32_t d_in, int32_t d_out, void* stream);
+
 /* --------------------------------------------------------------------------------------
  * LDS-staged relation SpMM for groups of many relations over a narrow column space
  * (polypharmacy drug x drug: 1,928 relations of 645 x 645).  For output chunk c (out_chunk

@@ -66,7 +66,7 @@ def test_forward_matches_golden(golden_S, monkeypatch, fused_seg, tab):
     from decagon_amd import engine
 
     monkeypatch.setattr(engine, "FUSED_SEG", fused_seg)
-    monkeypatch.setattr(engine, "FUSED_TAB", tab)
+    monkeypatch.setattr(engine, "WAVE_TABLE", tab)
     z = golden_S
     dg, ph, model, opt, feed = _setup(z)
     sess = dg.Session()

@@ -80,3 +80,42 @@ def test_long_segments_wave_table_equals_seg_form_bitwise():
     g = synthetic.SyntheticGraph("S-long", dict(base.n_nodes), dict(base.edge_types), dict(base.decoders), adj,
                                  base.degrees)
     _check(_plan(g))
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_row_split_seg_wave_table_equals_seg_form_bitwise(world):
+    """Config S's N-GPU row blocks (weak scaling: N relation sets, every node type row-split,
+    dg_spmm_seg_f32 partials + the epilogue): every rank's seg launches of both layers in the
+    wave-table form equal dg_spmm_seg_f32's chunk partials bit for bit (collectives as no-ops:
+    the inputs need not be exchanged for the comparison)."""
+    import bench
+    from decagon_amd import kernels, synthetic
+    from decagon_amd.sharding import RelationShard
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    graph = synthetic.replicate_sets(synthetic.load_S(), world)
+    noop = lambda *a, **k: None  # noqa: E731
+    for rank in (0, world - 1):
+        shard = RelationShard.weak_sets(graph.edge_types, graph.n_nodes, rank, world, noop, noop)
+        args = bench.parse(["--config", "S"])
+        plan, _ = bench.make_plan(args, graph, shard, torch.device("cuda", 0))
+        plan.run()
+        torch.cuda.synchronize()
+        n = 0
+        for layer in plan.spmm_launches:
+            for launch in layer:
+                if not isinstance(launch, kernels.PreparedSegTab):
+                    continue
+                outs = [s.out for s in launch.specs]
+                launch()
+                torch.cuda.synchronize()
+                tab = [o.clone() for o in outs]
+                for o in outs:
+                    o.fill_(float("nan"))
+                launch.seg_form()
+                torch.cuda.synchronize()
+                for a, b in zip(tab, outs):
+                    assert torch.equal(a, b)
+                n += 1
+        assert n >= 2, "both layers run the wave-table seg form"
