@@ -211,6 +211,7 @@ SIGNATURES = {
                                            c_void_p]),
     "dg_gcn_fused_tab_f32": (c_int32, [POINTER(DgWaveTable), c_int32, c_int32, c_void_p]),
     "dg_spmm_seg_tab_f32": (c_int32, [POINTER(DgWaveTable), c_int32, c_int32, c_void_p]),
+    "dg_gcn_epilogue_tab_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, POINTER(DgPeerXchg), c_void_p]),
     "dg_gcn_fused_seg_peer_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32,
                                             c_int32, POINTER(DgPeerXchg), c_void_p]),
     "dg_peer_alloc": (c_int32, [c_int64, c_int32, POINTER(c_void_p)]),

@@ -490,6 +490,77 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK&
 // PEER: the rows are also stored into every peer's copy of the row-split output and the launch
 // ends with the peer-store exchange (peer.h: the last workgroup raises the flags and waits), so
 // every wave reaches the closing barrier.
+// The row-table form of the epilogue (dg_gcn_epilogue_tab_f32, round 5): one wave per row as
+// above, the same sums in the same order (bitwise its rows), but each row's target, partial
+// bases and chunk counts come from a host-built 64-byte descriptor, and every group's partial
+// loads (up to two a lane a group: n_chunks <= 2·CG) are issued together — one round trip
+// instead of the target search, then a kernel-argument and a partial round trip per group.
+static_assert(sizeof(dg_epi_row_desc) == 64, "dg_epi_row_desc: one s_load_dwordx16");
+template <int LP, bool PEER>
+__global__ __launch_bounds__(256) void epilogue_tab_kernel(const dg_epi_row_desc* __restrict__ rows, int n_rows,
+                                                           int flags, const dg::PeerK P) {
+    constexpr int CG = dg::kWave / LP;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int cg = lane / LP;
+    const int q = lane % LP;
+    const int r = (int)blockIdx.x * 4 + wave;
+    if (r < n_rows) {  // wave-uniform
+        const dg_epi_row_desc D = rows[r];
+        const int ng = D.info & 7;
+        const bool crelu = flags & DG_EPI_CHUNK_RELU;
+        auto relu4 = [](float4 v) {
+            return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+        };
+        float4 v[4][2];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int nc = (D.n_chunks >> (8 * g)) & 0xff;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = cg + j * CG;
+                v[g][j] = (g < ng && c < nc) ? *reinterpret_cast<const float4*>(D.part[g] + (int64_t)c * D.plane + q * 4)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            if (g >= ng) break;  // wave-uniform
+            const int nc = (D.n_chunks >> (8 * g)) & 0xff;
+            float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (cg + j * CG < nc) dg::add4(sm, crelu ? relu4(v[g][j]) : v[g][j]);
+#pragma unroll 1
+            for (int c = cg + 2 * CG; c < nc; c += CG) {  // (more chunks than two a lane group)
+                const float4 w = *reinterpret_cast<const float4*>(D.part[g] + (int64_t)c * D.plane + q * 4);
+                dg::add4(sm, crelu ? relu4(w) : w);
+            }
+#pragma unroll
+            for (int m = LP; m < dg::kWave; m <<= 1) dg::add4(sm, dg::shfl_xor4(sm, m));
+            if (flags & DG_EPI_L2NORM) {
+                float ss = sm.x * sm.x + sm.y * sm.y + sm.z * sm.z + sm.w * sm.w;
+#pragma unroll
+                for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
+                const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+                sm.x *= inv;
+                sm.y *= inv;
+                sm.z *= inv;
+                sm.w *= inv;
+            }
+            dg::add4(tot, sm);
+        }
+        if (flags & DG_EPI_RELU) tot = relu4(tot);
+        if (cg == 0) {
+            *reinterpret_cast<float4*>(D.out + D.off + q * 4) = tot;
+            if constexpr (PEER)
+                if ((D.info >> 8) & 1) dg::peer_store4(P, D.out, (uint32_t)D.bytes, (uint32_t)((D.off + q * 4) * 4), tot);
+        }
+    }
+    if constexpr (PEER) dg::peer_arrive(P);
+}
+
 template <int LP, bool PEER>
 __global__ __launch_bounds__(256) void epilogue_kernel(const EpiArgs a) {
     const int lane = threadIdx.x & 63;
@@ -902,6 +973,37 @@ int epilogue_launch(const dg_epi_target* targets, int32_t n_targets, int32_t d, 
     return dg::launch_status();
 }
 }  // namespace
+
+extern "C" int dg_gcn_epilogue_tab_f32(const dg_epi_row_desc* rows, int32_t n_rows, int32_t d, int32_t flags,
+                                       const dg_peer_xchg* xchg, void* stream) {
+    if (n_rows < 0 || (d != 32 && d != 64)) return DG_EINVAL;
+    if (flags & ~(DG_EPI_L2NORM | DG_EPI_RELU | DG_EPI_CHUNK_RELU)) return DG_EINVAL;
+    if (n_rows > 0 && (!rows || (reinterpret_cast<uintptr_t>(rows) & 63))) return rows ? DG_EALIGN : DG_EINVAL;
+    int64_t blocks = dg::ceil_div(n_rows, 4);
+    if (blocks == 0) {
+        if (!xchg) return DG_OK;
+        blocks = 1;  // no rows here: one workgroup still takes part in the exchange
+    }
+    dg::PeerK P{};
+    if (xchg) {
+        const int rc = dg::peer_convert(xchg, P);
+        if (rc != DG_OK) return rc;
+    }
+    dim3 grid(static_cast<unsigned>(blocks)), block(256);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (d == 64) {
+        if (xchg)
+            hipLaunchKernelGGL((epilogue_tab_kernel<16, true>), grid, block, 0, st, rows, n_rows, flags, P);
+        else
+            hipLaunchKernelGGL((epilogue_tab_kernel<16, false>), grid, block, 0, st, rows, n_rows, flags, P);
+    } else {
+        if (xchg)
+            hipLaunchKernelGGL((epilogue_tab_kernel<8, true>), grid, block, 0, st, rows, n_rows, flags, P);
+        else
+            hipLaunchKernelGGL((epilogue_tab_kernel<8, false>), grid, block, 0, st, rows, n_rows, flags, P);
+    }
+    return dg::launch_status();
+}
 
 extern "C" int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets, int32_t n_targets, int32_t d,
                                          int32_t flags, void* stream) {

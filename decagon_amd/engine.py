@@ -109,6 +109,17 @@ REASSOC_ROWS = knob("DG_REASSOC_ROWS", True)
 SEG_ROWS_L1 = knob("DG_SEG_ROWS_L1", False)
 
 
+def _epilogue(targets, d: int, flags: int, peer=None, push=None):
+    """An epilogue launch in its row-table form when the targets allow it (WAVE_TABLE), else
+    dg_gcn_epilogue_multi_f32 / _peer_f32 — bitwise the same rows either way."""
+    if WAVE_TABLE:
+        try:
+            return kernels.PreparedEpilogueTab(targets, d, flags, peer=peer, push=push)
+        except ValueError:
+            pass
+    return kernels.PreparedEpilogueMulti(targets, d, flags, peer=peer, push=push)
+
+
 def staged_out_chunk(grp, d: int) -> int:
     """Relations per output chunk of a staged group for a layer of width d: a multiple of the
     group's snake-bin size (so chunks stay balanced) giving about STAGED_TARGET_BLOCKS
@@ -860,8 +871,7 @@ class ForwardPlan:
                         grp_parts.append((part, nc, sviews[et] if reduced else None))
                     blocks.append((grp_parts, torch.empty((n[i], d), **f32), n[i]))
                 reduces = []
-            local_epis.append(kernels.PreparedEpilogueMulti(
-                blocks, d, flags, peer=epi_peer, push=[t < n_push for t in range(len(blocks))]))
+            local_epis.append(_epilogue(blocks, d, flags, peer=epi_peer, push=[t < n_push for t in range(len(blocks))]))
         launches += reduces
         if peer_red:
             # the relation-sharded rows finished from the world slots, added in rank order by
@@ -903,8 +913,7 @@ class ForwardPlan:
             # node types with the most chunk partials per row first: their long rows start early
             tl.sort(key=lambda i: -sum(partials[et][1] for et in self.targets[i]))
             if tl:
-                epis.append(kernels.PreparedEpilogueMulti(
-                    [([partials[et] for et in self.targets[i]], outs[i], n[i]) for i in tl], d, flags))
+                epis.append(_epilogue([([partials[et] for et in self.targets[i]], outs[i], n[i]) for i in tl], d, flags))
         return _Layer(launches, flat, need_zero, self.allreduce, epis, fused_t, views, self.side_stream, send,
                       local_epis, gathers, self.allgather, self._peer_gather_all(gathers, relu))
 

@@ -848,6 +848,66 @@ class PreparedEpilogueMulti:
         check(self._fn(self._tarr, n, d, f, _stream_ptr(stream)), "dg_gcn_epilogue_multi_f32")
 
 
+class PreparedEpilogueTab(PreparedEpilogueMulti):
+    """The same launch as PreparedEpilogueMulti (bitwise its rows) through
+    dg_gcn_epilogue_tab_f32: one 64-byte descriptor per output row built here once (its
+    target's output, each group's chunk-0 partial row and chunk count), so a wave issues all its
+    partial loads at once.  Targets whose groups carry sum outputs, or more than four groups,
+    are not supported (ValueError: use PreparedEpilogueMulti)."""
+
+    DESC = np.dtype([("out", "<u8"), ("part", "<u8", 4), ("off", "<i4"), ("plane", "<i4"), ("n_chunks", "<u4"),
+                     ("info", "<u4"), ("bytes", "<i4"), ("pad", "<i4")])
+
+    def __init__(self, targets, d: int, flags: int, peer=None, push: Optional[Sequence[bool]] = None):
+        if d not in (32, 64):
+            raise ValueError("dg_gcn_epilogue_tab_f32: d = 32 or 64")
+        for partials, _, _ in targets:
+            # (all of a row's partial loads in flight at once: at most two a lane a group)
+            if len(partials) > 4 or any(len(p) > 2 and p[2] is not None for p in partials) \
+                    or any(p[1] > 2 * (64 // (d // 4)) for p in partials):
+                raise ValueError("dg_gcn_epilogue_tab_f32: at most 4 groups a row of at most 2·64/(d/4) "
+                                 "chunks, no group sums")
+        super().__init__(targets, d, flags, peer, push)
+        assert self.DESC.itemsize == 64
+        n = sum(nr for _, _, nr in targets)
+        desc = np.zeros(n, self.DESC)
+        i = 0
+        for t, (partials, out, nr) in enumerate(targets):
+            if nr == 0:
+                continue
+            rows = np.arange(nr, dtype=np.int64)
+            sl = slice(i, i + nr)
+            desc["out"][sl] = out.data_ptr()
+            desc["off"][sl] = rows * d
+            desc["plane"][sl] = nr * d
+            desc["bytes"][sl] = nr * d * 4
+            ncs = 0
+            for g, (p, nc, *_) in enumerate(partials):
+                desc["part"][sl, g] = p.data_ptr() + rows * d * 4
+                ncs |= nc << (8 * g)
+            desc["n_chunks"][sl] = ncs
+            pushed = peer is not None and (push is None or push[t])
+            desc["info"][sl] = len(partials) | ((1 if pushed else 0) << 8)
+            i += nr
+        dev = targets[0][1].device
+        raw = torch.from_numpy(desc.view(np.uint8).copy())
+        self._rows = torch.empty(raw.numel() + 64, dtype=torch.uint8, device=dev)
+        off = (-self._rows.data_ptr()) % 64
+        self._rows_v = self._rows[off:off + raw.numel()]
+        self._rows_v.copy_(raw.to(dev))
+        self._n_rows = n
+        self._tfn = _lib.load().dg_gcn_epilogue_tab_f32
+
+    def __call__(self, stream=None) -> None:
+        _, d, f = self._args
+        check(self._tfn(self._rows_v.data_ptr() if self._n_rows else None, self._n_rows, d, f, self._xchg,
+                        _stream_ptr(stream)), "dg_gcn_epilogue_tab_f32")
+
+    def multi_form(self, stream=None) -> None:
+        """The same rows through dg_gcn_epilogue_multi_f32 / _peer_f32 (tests: bitwise equal)."""
+        PreparedEpilogueMulti.__call__(self, stream)
+
+
 def gcn_epilogue(partials, out, n_rows, d, flags, stream=None) -> None:
     PreparedEpilogue(partials, out, n_rows, d, flags)(stream)
 

@@ -389,6 +389,29 @@ typedef struct dg_epi_target {
 int dg_gcn_epilogue_multi_f32(const dg_epi_target* targets /* HOST array */, int32_t n_targets,
                               int32_t d, int32_t flags, void* stream);
 
+/* The row-table form (round 5): the same rows, sums and order — bitwise the multi form's rows —
+ * from a host-built descriptor per output row (decagon_amd/kernels.py: PreparedEpilogueTab), so
+ * a wave issues every group's partial loads at once.  Row i of the table: rows[i].out + off is
+ * the output row (its target's output base in .out); group g < (info & 7) <= 4 has
+ * (n_chunks >> 8g) & 0xff chunk partials at part[g] + c * plane; info bit 8: with xchg, the row
+ * also goes to every peer's copy of .out (bytes = the target's output size).  No group sums
+ * (dg_epi_group.sum_out).  d = 32 or 64; rows 64-byte aligned; xchg as dg_gcn_epilogue_peer_f32
+ * (the launch then ends with the exchange), or NULL. */
+typedef struct dg_epi_row_desc {
+    float* out;
+    const float* part[4];
+    int32_t off;
+    int32_t plane;
+    uint32_t n_chunks;
+    uint32_t info;
+    int32_t bytes;
+    int32_t pad;
+} dg_epi_row_desc;        /* 64 bytes */
+
+struct dg_peer_xchg;
+int dg_gcn_epilogue_tab_f32(const dg_epi_row_desc* rows, int32_t n_rows, int32_t d, int32_t flags,
+                            const struct dg_peer_xchg* xchg /* HOST, or NULL */, void* stream);
+
 /* --------------------------------------------------------------------------------------
  * Peer-store exchange over xGMI: the all-gather of the row-split blocks of the sharded
  * forward (decagon_amd/sharding.py; one per layer, made necessary by the normalisation of

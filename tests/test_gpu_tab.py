@@ -119,3 +119,39 @@ def test_row_split_seg_wave_table_equals_seg_form_bitwise(world):
                     assert torch.equal(a, b)
                 n += 1
         assert n >= 2, "both layers run the wave-table seg form"
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_row_split_epilogue_table_equals_multi_form_bitwise(world):
+    """The finishing launch of config S's N-GPU row blocks (Σ over the N set partials, L2 norm,
+    Σ over edge types, relu) in its row-table form equals dg_gcn_epilogue_multi_f32's rows bit
+    for bit, both layers, first and last rank."""
+    import bench
+    from decagon_amd import kernels, synthetic
+    from decagon_amd.sharding import RelationShard
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    graph = synthetic.replicate_sets(synthetic.load_S(), world)
+    noop = lambda *a, **k: None  # noqa: E731
+    for rank in (0, world - 1):
+        shard = RelationShard.weak_sets(graph.edge_types, graph.n_nodes, rank, world, noop, noop)
+        args = bench.parse(["--config", "S"])
+        plan, _ = bench.make_plan(args, graph, shard, torch.device("cuda", 0))
+        plan.run()
+        torch.cuda.synchronize()
+        n = 0
+        for layer in (plan._layer1, plan._layer2):
+            for e in layer.local_epilogues:
+                if not isinstance(e, kernels.PreparedEpilogueTab):
+                    continue
+                outs = [t for t in e._keep if t.dtype == torch.float32]
+                e()
+                torch.cuda.synchronize()
+                tab = [o.clone() for o in outs]
+                e.multi_form()
+                torch.cuda.synchronize()
+                for a, b in zip(tab, outs):
+                    assert torch.equal(a, b)
+                n += 1
+        assert n == 2, "both layers' finishing launches run the row-table form"
