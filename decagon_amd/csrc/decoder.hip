@@ -68,6 +68,16 @@ __global__ __launch_bounds__(256) void decoder_score_kernel(const DecArgs a) {
 //    takes a ticket; the last one reads every partial with sc1 loads (cdna_hip_programming.md
 //    Guideline 16; no L2 write-back or invalidate) and adds them in block order.
 // The last workgroup resets what it used for the next launch.
+#ifdef DG_DEC_PROF
+extern "C" int64_t dg_dec_prof_copy(unsigned long long* host) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(dg::g_dec_prof), sizeof(dg::g_dec_prof), 0, hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return -1;
+    return 256;
+}
+#endif
+
 struct HingeArgs {
     DecTab t;
     const int32_t* rows;
@@ -101,6 +111,7 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
     const int b0 = blockIdx.x * 32;
     const int b = b0 + i;
     const bool valid = b < a.n;
+    DG_DEC_STAMP(0);  // (profiling build: wave start)
     int ridx = 0, cidx = 0;
     if (valid) {
         cidx = a.cols[b];
@@ -112,6 +123,7 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
             ridx = unigram_draw(a.alias, a.range, a.seed, a.offset + (uint64_t)b);
         if (side == 1 && a.neg_rows_out && h == 0) a.neg_rows_out[b] = ridx;
     }
+    DG_DEC_STAMP(1);  // indices (and the negatives' draws) landed
     float part[16];
     score_tile(a.t, ridx, cidx, valid, part);
     if ((i & 1) == 0) {  // lane 2r holds score r of its half
@@ -151,6 +163,7 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
         }
     }
     __syncthreads();
+    DG_DEC_STAMP(5);  // the block's ticket returned
     if (!last) return;  // block-uniform
     if constexpr (PACKED) {
         if (threadIdx.x == 0) {
@@ -167,6 +180,7 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
             a.loss[0] = static_cast<float>(s);
             __hip_atomic_store(a.word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        DG_DEC_STAMP(6);  // loss stored (last block)
         return;
     }
     float s = 0.f;

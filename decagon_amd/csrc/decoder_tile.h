@@ -82,6 +82,21 @@ __device__ __forceinline__ float4 ld_emb4(const float* p) {
 // butterfly per score's 80).  kSc1: every load of
 // row_table / col_table is an sc1 load (the tables were written in this launch).  kD: the width
 // when known at compile time (only that path is compiled: fewer registers), else 0.
+#ifdef DG_DEC_PROF
+// Profiling build only (scripts/dec_prof.py): s_memrealtime stamps of the hinge decoder's
+// phases per (block, wave).
+constexpr int kDecProfSlots = 8;
+__device__ unsigned long long g_dec_prof[256][2][kDecProfSlots];
+#define DG_DEC_STAMP(i)                                                                                       \
+    do {                                                                                                      \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                           \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)                                                      \
+            dg::g_dec_prof[blockIdx.x][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memrealtime();                 \
+    } while (0)
+#else
+#define DG_DEC_STAMP(i) ((void)0)
+#endif
+
 template <bool kSc1 = false, int kD = 0>
 __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, bool valid,
                                            float (&part)[16]) {
@@ -140,11 +155,13 @@ __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, 
                 for (int s = 0; s < 16; ++s) av[s] *= t.l[16 * h + s];
             }
         }
+        DG_DEC_STAMP(2);  // (profiling build: the tile's loads landed)
         f32x16 acc = {};
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 16; ++r) part[r] = fmaf(acc[r] * lj, v[r], 0.f);
+        DG_DEC_STAMP(3);  // MFMA chain + epilogue products
     }
 #pragma unroll 1
     for (int n0 = 0; d != 32 && n0 < d; n0 += 32) {
@@ -190,6 +207,7 @@ __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, 
     float v1 = (b1 ? v2[1] : v2[0]) + __shfl_xor(b1 ? v2[0] : v2[1], 2);
     v1 += __shfl_xor(v1, 1);
     part[0] = v1;  // score r = 8·b4 + 4·b3 + 2·b2 + b1 = (lane & 31) >> 1
+    DG_DEC_STAMP(4);  // reduce-scatter
 }
 
 }  // namespace dg
