@@ -532,8 +532,19 @@ __global__ __launch_bounds__(256) void epilogue_tab_kernel(const dg_epi_row_desc
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 if (cg + j * CG < nc) dg::add4(sm, crelu ? relu4(v[g][j]) : v[g][j]);
+            // more chunks than two a lane group: four loads in flight, in order
+            int c = cg + 2 * CG;
 #pragma unroll 1
-            for (int c = cg + 2 * CG; c < nc; c += CG) {  // (more chunks than two a lane group)
+            for (; c + 3 * CG < nc; c += 4 * CG) {
+                float4 w[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    w[u] = *reinterpret_cast<const float4*>(D.part[g] + (int64_t)(c + u * CG) * D.plane + q * 4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) dg::add4(sm, crelu ? relu4(w[u]) : w[u]);
+            }
+#pragma unroll 1
+            for (; c < nc; c += CG) {
                 const float4 w = *reinterpret_cast<const float4*>(D.part[g] + (int64_t)c * D.plane + q * 4);
                 dg::add4(sm, crelu ? relu4(w) : w);
             }

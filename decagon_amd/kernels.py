@@ -862,11 +862,9 @@ class PreparedEpilogueTab(PreparedEpilogueMulti):
         if d not in (32, 64):
             raise ValueError("dg_gcn_epilogue_tab_f32: d = 32 or 64")
         for partials, _, _ in targets:
-            # (all of a row's partial loads in flight at once: at most two a lane a group)
             if len(partials) > 4 or any(len(p) > 2 and p[2] is not None for p in partials) \
-                    or any(p[1] > 2 * (64 // (d // 4)) for p in partials):
-                raise ValueError("dg_gcn_epilogue_tab_f32: at most 4 groups a row of at most 2·64/(d/4) "
-                                 "chunks, no group sums")
+                    or any(p[1] > 255 for p in partials):
+                raise ValueError("dg_gcn_epilogue_tab_f32: at most 4 groups a row, 255 chunks, no group sums")
         super().__init__(targets, d, flags, peer, push)
         assert self.DESC.itemsize == 64
         n = sum(nr for _, _, nr in targets)
