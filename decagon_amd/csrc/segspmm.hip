@@ -41,6 +41,11 @@ constexpr int kFsegUP = 4;   // fused seg, reassociated (W slabs read after the 
                              // the gathers and 9.45 staged in LDS per workgroup; step 19.36 / 19.66 /
                              // 21.88 us at 200 steps)
 constexpr int kSegMinNW = 1; // waves per workgroup, at least (else: the launch's largest chunk)
+// the wave-table forms' gathers in flight per lane (config S step at 200 steps, round 5: 4 / 4
+// 15.56-15.63 us; 8 / 8 15.88-15.93; 16 / 16 18.30-18.32; the W slice issued before the gathers
+// instead of after them 15.92-15.97, with 8 / 8 16.75-16.81)
+constexpr int kTabU = 4;
+constexpr int kTabUP = 4;
 
 namespace {
 
@@ -612,7 +617,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
     asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(D.wr),
                  "s"(ovf));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const float4 res = tab_wave<PROJ, PROJ ? kFsegUP : kFsegU>(D, first, ovf, ybuf[wave]);
+    const float4 res = tab_wave<PROJ, PROJ ? kTabUP : kTabU>(D, first, ovf, ybuf[wave]);
     if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
     // one wave per (row slot, group): its relations summed in order, L2-normalised
