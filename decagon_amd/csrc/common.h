@@ -70,4 +70,89 @@ __device__ __forceinline__ float4 shfl_xor4(const float4& v, int m) {
                        __shfl_xor(v.w, m));
 }
 
+// An opaque copy of each component: the compiler cannot pair operations on them into packed
+// fp32 instructions (tests/test_cpu_isa.py bans the op_sel:[0,1] form).
+__device__ __forceinline__ void opaque4(float4& v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
+// Butterfly steps without an LDS round trip (ds_bpermute) where gfx950 allows: the value of
+// lane ^ m from v_permlane32_swap / v_permlane16_swap (m = 32 / 16: lane halves / 16-lane rows
+// exchanged between two copies of x) or DPP (m = 8: row_ror:8 within a row; m = 2 / 1:
+// quad_perm [2,3,0,1] / [1,0,3,2]); m = 4 stays a ds_bpermute.  Exact partner values, and IEEE
+// addition is commutative, so every step is bit for bit x + __shfl_xor(x, m).
+template <int CTRL>
+__device__ __forceinline__ float dpp_get(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int M>
+__device__ __forceinline__ float xor_get(float x) {  // x of lane ^ M
+    static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "xor_get: lane ^ 2^k");
+    const int lane = threadIdx.x & 63;
+    if constexpr (M == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        return __uint_as_float(lane < 32 ? r[1] : r[0]);
+    } else if constexpr (M == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        return __uint_as_float((lane >> 4) & 1 ? r[0] : r[1]);
+    } else if constexpr (M == 8) {
+        return dpp_get<0x128>(x);  // row_ror:8
+    } else if constexpr (M == 4) {
+        return __shfl_xor(x, 4);
+    } else if constexpr (M == 2) {
+        return dpp_get<0x4E>(x);  // quad_perm [2,3,0,1]
+    } else {
+        return dpp_get<0xB1>(x);  // quad_perm [1,0,3,2]
+    }
+}
+template <int M>
+__device__ __forceinline__ float xor_add(float x) {  // x + x of lane ^ M
+    // (own + partner in either order; the opaque copy keeps the compiler from pairing two such
+    // adds into v_pk_add_f32 with op_sel:[0,1] — the form tests/test_cpu_isa.py bans)
+    if constexpr (M == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        float a = __uint_as_float(r[0]);
+        asm volatile("" : "+v"(a));
+        return a + __uint_as_float(r[1]);
+    } else if constexpr (M == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        float a = __uint_as_float(r[0]);
+        asm volatile("" : "+v"(a));
+        return a + __uint_as_float(r[1]);
+    } else {
+        return x + xor_get<M>(x);
+    }
+}
+template <int M>
+__device__ __forceinline__ float4 xor_add4(float4 v) {
+    return make_float4(xor_add<M>(v.x), xor_add<M>(v.y), xor_add<M>(v.z), xor_add<M>(v.w));
+}
+// v summed over the butterfly m = M0, 2·M0, ..., 32 (the loop `for (m = M0; m < 64; m <<= 1)
+// v += shfl_xor(v, m)`)
+template <int M0>
+__device__ __forceinline__ float4 xor_sum4_from(float4 v) {
+    if constexpr (M0 >= 64) {
+        return v;
+    } else {
+        return xor_sum4_from<M0 * 2>(xor_add4<M0>(v));
+    }
+}
+template <int M0>
+__device__ __forceinline__ float xor_sum_from(float v) {
+    if constexpr (M0 >= 64) {
+        return v;
+    } else {
+        return xor_sum_from<M0 * 2>(xor_add<M0>(v));
+    }
+}
+// x summed over m = 1, 2, ..., P/2 (the loop `for (m = 1; m < P; m <<= 1) x += shfl_xor(x, m)`)
+template <int P, int M = 1>
+__device__ __forceinline__ float xor_sum_below(float x) {
+    if constexpr (M >= P) {
+        return x;
+    } else {
+        return xor_sum_below<P, M * 2>(xor_add<M>(x));
+    }
+}
+
 }  // namespace dg

@@ -137,8 +137,7 @@ __global__ __launch_bounds__(128) void decoder_hinge_kernel(const HingeArgs a) {
     if (threadIdx.x < 64) {
         float term = 0.f;
         if (lane < 32 && b0 + lane < a.n) term = fmaxf(sc[1][lane] - (sc[0][lane] - a.margin), 0.f);
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) term += __shfl_xor(term, m);
+        term = dg::xor_add<1>(dg::xor_add<2>(dg::xor_add<4>(dg::xor_add<8>(dg::xor_add<16>(dg::xor_add<32>(term))))));
         if (lane == 0 && PACKED) {
             unsigned long long add = 1ull << 56;
             if (term < 256.0f) {  // (false for NaN and inf too)

@@ -199,13 +199,13 @@ __device__ __forceinline__ void score_tile(const DecTab& t, int ridx, int cidx, 
     float v8[8], v4[4], v2[2];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-        v8[j] = (b4 ? part[8 + j] : part[j]) + __shfl_xor(b4 ? part[j] : part[8 + j], 16);
+        v8[j] = (b4 ? part[8 + j] : part[j]) + xor_get<16>(b4 ? part[j] : part[8 + j]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v4[j] = (b3 ? v8[4 + j] : v8[j]) + __shfl_xor(b3 ? v8[j] : v8[4 + j], 8);
+    for (int j = 0; j < 4; ++j) v4[j] = (b3 ? v8[4 + j] : v8[j]) + xor_get<8>(b3 ? v8[j] : v8[4 + j]);
 #pragma unroll
     for (int j = 0; j < 2; ++j) v2[j] = (b2 ? v4[2 + j] : v4[j]) + __shfl_xor(b2 ? v4[j] : v4[2 + j], 4);
-    float v1 = (b1 ? v2[1] : v2[0]) + __shfl_xor(b1 ? v2[0] : v2[1], 2);
-    v1 += __shfl_xor(v1, 1);
+    float v1 = (b1 ? v2[1] : v2[0]) + xor_get<2>(b1 ? v2[0] : v2[1]);
+    v1 = xor_add<1>(v1);
     part[0] = v1;  // score r = 8·b4 + 4·b3 + 2·b2 + b1 = (lane & 31) >> 1
     DG_DEC_STAMP(4);  // reduce-scatter
 }

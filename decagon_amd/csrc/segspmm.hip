@@ -165,8 +165,7 @@ __device__ __forceinline__ float4 seg_gather(const int32_t* __restrict__ vcol, c
             for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
         }
     }
-#pragma unroll
-    for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+    acc = dg::xor_sum4_from<LP>(acc);
     return acc;
 }
 
@@ -221,8 +220,7 @@ __device__ __forceinline__ float4 seg_gather_shfl(const int32_t* __restrict__ vc
             for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
         }
     }
-#pragma unroll
-    for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+    acc = dg::xor_sum4_from<LP>(acc);
     return acc;
 }
 
@@ -265,9 +263,7 @@ __device__ __forceinline__ float4 seg_wave_proj(const SegGroupK& g, int k, int b
     dg::fma4(z, yb.y, wv[5]);
     dg::fma4(z, yb.z, wv[6]);
     dg::fma4(z, yb.w, wv[7]);
-    dg::add4(z, dg::shfl_xor4(z, 8));
-    dg::add4(z, dg::shfl_xor4(z, 16));
-    dg::add4(z, dg::shfl_xor4(z, 32));
+    z = dg::xor_sum4_from<8>(z);
     return z;
 }
 
@@ -432,8 +428,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_fused_seg_kernel(const FsArgs a) 
         for (int u = 1; u < K; ++u) dg::add4(sum, zbuf[gb + u][q]);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
         float ss = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
-#pragma unroll
-        for (int m = 1; m < DOUT4; m <<= 1) ss += __shfl_xor(ss, m);
+        ss = dg::xor_sum_below<DOUT4>(ss);
         const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
         if (lane < DOUT4) nbuf[s2][gg][lane] = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
     }
@@ -561,8 +556,7 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
                 }
             }
         }
-#pragma unroll
-        for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+        acc = dg::xor_sum4_from<LP>(acc);
         if constexpr (PROJ) {
             // z = y·W_k: this lane's W slice (rows 8(l>>3) .. +8, output float4 l & 7) read
             // after the gathers, as in seg_wave_proj
@@ -584,9 +578,7 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
             dg::fma4(z, yb.y, wv[5]);
             dg::fma4(z, yb.z, wv[6]);
             dg::fma4(z, yb.w, wv[7]);
-            dg::add4(z, dg::shfl_xor4(z, 8));
-            dg::add4(z, dg::shfl_xor4(z, 16));
-            dg::add4(z, dg::shfl_xor4(z, 32));
+            z = dg::xor_sum4_from<8>(z);
             res = z;
         } else {
             res = acc;
@@ -629,8 +621,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
         for (int u = 1; u < K; ++u) dg::add4(sum, zbuf[gb + u][q]);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
         float ss = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
-#pragma unroll
-        for (int m = 1; m < DOUT4; m <<= 1) ss += __shfl_xor(ss, m);
+        ss = dg::xor_sum_below<DOUT4>(ss);
         const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
         if (lane < DOUT4) nbuf[ns][lane] = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
     }

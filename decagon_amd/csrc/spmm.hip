@@ -179,8 +179,7 @@ __device__ __forceinline__ float4 range_body(const SpmmGroupK& g, const float* x
 #pragma unroll 1
         for (int s0 = 0; s0 < n; s0 += U * G) gather_step<LP, U>(acc, xq, qact, eoff, v, s0, n, sub);
     }
-#pragma unroll
-    for (int off = LP; off < dg::kWave; off <<= 1) dg::add4(acc, dg::shfl_xor4(acc, off));
+    acc = dg::xor_sum4_from<LP>(acc);
     return acc;
 }
 
@@ -328,8 +327,7 @@ __device__ __forceinline__ void fused_body(const FusedArgs& a, const int b) {
         for (int w = 1; w < W; ++w) dg::add4(s, pbuf[wave + w][q]);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); columns >= d hold zeros
         float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
-#pragma unroll
-        for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
+        ss = dg::xor_sum_below<LP>(ss);
         const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
         if (lane < LP) ybuf[slot][gl][lane] = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
     }
@@ -459,8 +457,7 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK&
                 dg::add4(s, crelu ? relu4(v) : v);
             }
         }
-#pragma unroll
-        for (int m = LP; m < dg::kWave; m <<= 1) dg::add4(s, dg::shfl_xor4(s, m));
+        s = dg::xor_sum4_from<LP>(s);
         if (a.g[gi].sum && qok && cg == 0) {
             *reinterpret_cast<float4*>(a.g[gi].sum + off) = s;
             if constexpr (PEER)
@@ -469,14 +466,14 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK&
         if (a.flags & DG_EPI_L2NORM) {
             // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12)); all-zero rows stay zero.
             float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
-#pragma unroll
-            for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
+            ss = dg::xor_sum_below<LP>(ss);
             const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
             s.x *= inv;
             s.y *= inv;
             s.z *= inv;
             s.w *= inv;
         }
+        dg::opaque4(s);
         dg::add4(tot, s);
     }
     if (a.flags & DG_EPI_RELU) tot = relu4(tot);
@@ -548,18 +545,17 @@ __global__ __launch_bounds__(256) void epilogue_tab_kernel(const dg_epi_row_desc
                 const float4 w = *reinterpret_cast<const float4*>(D.part[g] + (int64_t)c * D.plane + q * 4);
                 dg::add4(sm, crelu ? relu4(w) : w);
             }
-#pragma unroll
-            for (int m = LP; m < dg::kWave; m <<= 1) dg::add4(sm, dg::shfl_xor4(sm, m));
+            sm = dg::xor_sum4_from<LP>(sm);
             if (flags & DG_EPI_L2NORM) {
                 float ss = sm.x * sm.x + sm.y * sm.y + sm.z * sm.z + sm.w * sm.w;
-#pragma unroll
-                for (int m = 1; m < LP; m <<= 1) ss += __shfl_xor(ss, m);
+                ss = dg::xor_sum_below<LP>(ss);
                 const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
                 sm.x *= inv;
                 sm.y *= inv;
                 sm.z *= inv;
                 sm.w *= inv;
             }
+            dg::opaque4(sm);
             dg::add4(tot, sm);
         }
         if (flags & DG_EPI_RELU) tot = relu4(tot);
