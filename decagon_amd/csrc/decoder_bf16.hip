@@ -219,7 +219,7 @@ __global__ __launch_bounds__(threads_for<D>()) void decoder_bf16_kernel(const Bf
                 }
             }
         }
-        part += __shfl_xor(part, 32);
+        part = dg::xor_add<32>(part);
         if (h == 0 && valid) a.out[p] = part;
     }
 }
@@ -357,16 +357,15 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
                 }
             }
         }
-        partp += __shfl_xor(partp, 32);
-        partn += __shfl_xor(partn, 32);
+        partp = dg::xor_add<32>(partp);
+        partn = dg::xor_add<32>(partn);
         if (h == 0 && valid) {
             a.out[p] = partp;
             a.out[nh + p] = partn;
         }
         if constexpr (FUSED) {  // relu(neg − (pos − margin)), optimizer.py:116-120: a fixed butterfly
             float term = (h == 0 && valid) ? fmaxf(partn - (partp - a.margin), 0.f) : 0.f;
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off);
+            term = dg::xor_add<1>(dg::xor_add<2>(dg::xor_add<4>(dg::xor_add<8>(dg::xor_add<16>(dg::xor_add<32>(term))))));
             wsum += term;
         }
     }
@@ -676,10 +675,8 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
         float term = 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {  // the pair's 4 lane groups, in a fixed butterfly
-            pp[b] += __shfl_xor(pp[b], 16);
-            pp[b] += __shfl_xor(pp[b], 32);
-            pn[b] += __shfl_xor(pn[b], 16);
-            pn[b] += __shfl_xor(pn[b], 32);
+            pp[b] = dg::xor_add<32>(dg::xor_add<16>(pp[b]));
+            pn[b] = dg::xor_add<32>(dg::xor_add<16>(pn[b]));
             const int p = tile * 32 + 16 * b + pl;
             if (g == 0 && valid[b]) {
                 a.out[p] = pp[b];
@@ -688,8 +685,7 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
             if (FUSED && g == 0 && valid[b]) term += fmaxf(pn[b] - (pp[b] - a.margin), 0.f);  // optimizer.py:116-120
         }
         if constexpr (FUSED) {
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off);
+            term = dg::xor_add<1>(dg::xor_add<2>(dg::xor_add<4>(dg::xor_add<8>(dg::xor_add<16>(dg::xor_add<32>(term))))));
             wsum += term;
         }
     }
