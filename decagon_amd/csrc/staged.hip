@@ -168,26 +168,6 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     // 16-byte bank slot of float4 j of column v is (5v + j) mod 16, a bijection of v & 15 for
     // every j.  Wave w copies slots 64(w + 16r) .. +63; the zero column is never written.
     const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xs0));
-#ifdef DG_STAGED_COPYWAVE
-    // copy-wave form (A/B only, scripts/ab_copywave.sh; DESIGN §5: not faster): the last
-    // DG_STAGED_COPYWAVE waves (no pairs: the layout's lanes stop before them, DG_STAGED_LANES)
-    // issue the whole slab copy of every relation after the first, so no gathering wave's
-    // pair loads queue behind the DMA (vmcnt retires in order, per wave)
-    constexpr int kCopyWaves = DG_STAGED_COPYWAVE;
-    auto slab_copy_wave = [&](int i, int cw) {
-        const float* xk = g.x + (int64_t)__builtin_amdgcn_readfirstlane(slb[i]) * n_cols * g.x_ld + col0;
-        const uint32_t dst = lds0 + (i & 1) * a.xs_f4 * 16;
-        const int n5 = n_cols * 5;
-#pragma unroll 4
-        for (int q0 = 64 * cw; q0 < n5; q0 += 64 * kCopyWaves) {
-            const int q = q0 + lane;
-            const int v = (q * 52429) >> 18;  // q / 5 (q < 5120)
-            const int j = min(q - 5 * v, 3);
-            const int off = __umul24(v, g.x_ld) + min(col0 + 4 * j, d - 4) - col0;
-            if (q < n5) glds16(xk, off * 4, dst + q0 * 16);
-        }
-    };
-#endif
     auto slab_copy = [&](int i) {
         const float* xk = g.x + (int64_t)__builtin_amdgcn_readfirstlane(slb[i]) * n_cols * g.x_ld + col0;
         const uint32_t dst = lds0 + (i & 1) * a.xs_f4 * 16;
@@ -320,14 +300,9 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
         } else {
             // un (relation i's first diagonals) must arrive before the slab copy is queued
             // behind it: vmcnt retires in order
-#ifdef DG_STAGED_COPYWAVE
-            const int cw = wave - (kMaxThreads / 64 - kCopyWaves);
-            if (cw >= 0 && i + 1 < nk) slab_copy_wave(i + 1, cw);
-#else
             asm volatile("" :: "v"(un[0].x), "v"(un[0].y), "v"(un[1].x), "v"(un[1].y), "v"(un[2].x),
                          "v"(un[2].y), "v"(un[3].x), "v"(un[3].y));
             if (i + 1 < nk) slab_copy(i + 1);  // the other buffer: last read by relation i-1
-#endif
         }
         DG_TICK(c_put);
         int nwoff, nrlw, nbig, nvi;
@@ -472,7 +447,6 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
     a.acc_f4 = max_rows * 4;
     int64_t lds = 2 * (int64_t)a.xs_f4 * 16 + kMetaInts * 4 + (int64_t)a.acc_f4 * 16;
     if (lds > kLdsBytes) return DG_EINVAL;
-#ifndef DG_STAGED_ACC4  // A/B builds: 64-byte accumulator rows
     // 80-byte accumulator rows when they fit: a wave's row updates (rows of consecutive virtual
     // rows) then spread over the 16 bank slots instead of 4 (64-byte rows: slot (4·row + j) mod 16)
     if (lds + (int64_t)max_rows * 16 <= kLdsBytes) {
@@ -480,7 +454,6 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
         a.acc_f4 = max_rows * 5;
         lds += (int64_t)max_rows * 16;
     }
-#endif
 #ifdef DG_STAGED_PROF
     {
         static unsigned long long* buf = nullptr;
