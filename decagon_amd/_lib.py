@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 35
+ABI_VERSION = 36
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -31,7 +31,8 @@ DG_GROUP_DENSE_ROWS = 4  # dg_gcn_fused_f32 only: row r of the group's sum is x[
 DG_MAX_ADAM_SEGS = 32
 DG_PEER_MAX = 8  # peer exchange (decagon_hip.h)
 DG_PEER_SLOTS = 8
-DG_PEER_STATE_WORDS = 2 * DG_PEER_SLOTS + 1
+DG_PEER_SUB_BASE, DG_PEER_SUB_STRIDE = 64, 16
+DG_PEER_STATE_WORDS = DG_PEER_SUB_BASE + DG_PEER_SLOTS * 8 * DG_PEER_SUB_STRIDE
 DG_PEER_ERROR_WORD = 2 * DG_PEER_SLOTS
 DG_IPC_HANDLE_BYTES = 64
 DG_EPI_PUSH = 1

@@ -9,7 +9,8 @@
 //   payload  every 16-B piece stored WRITE-THROUGH at system scope (buffer_store_dwordx4 ...
 //            sc0 sc1) into the peer's buffer; every storing wave then `s_waitcnt vmcnt(0)`
 //            (the stores are complete at the peer's memory), a workgroup barrier, and ONE lane
-//            adds to this rank's arrival counter (agent scope);
+//            adds to this rank's arrival counter (agent scope) — in launches of >= 128
+//            workgroups through one of 8 sub-counters first, whose last arriver adds to it;
 //   flag     the workgroup whose add returns grid-1 (the last) stores epoch into word
 //            [slot][rank] of every peer's flag block (lane p: peer p) (a system-scope relaxed atomic store:
 //            global_store ... sc0 sc1) — the flag blocks live in uncached device memory
@@ -22,7 +23,8 @@
 //   consume  the kernels that read the gathered rows start after this kernel ends: the
 //            dispatch's acquire makes the bytes the peers wrote into this GPU's memory visible
 //            as it does for any earlier kernel's stores.
-// Epochs: state[2·slot] counts a launch's arrivals (the last arriver resets it), state[2·slot+1]
+// Epochs: state[2·slot] counts a launch's arrivals (the last arriver resets it; sub-counters at
+// state[DG_PEER_SUB_BASE + (8·slot + s)·DG_PEER_SUB_STRIDE], reset by their last arriver), state[2·slot+1]
 // is the slot's epoch (launches completed), so no flag is ever reset and a graph replay needs
 // no memset.  Reuse is safe with ONE buffer per slot: a rank can only overwrite a peer's copy
 // of step t's rows after passing a later wait that needs that peer's next exchange, which the
@@ -48,6 +50,9 @@ struct PeerK {
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// launches of at least this many workgroups count their arrivals in two levels (peer_arrive)
+constexpr uint32_t kPeerSubMin = 128;
 
 // Validate a host descriptor and copy it into the kernel form.
 inline int peer_convert(const dg_peer_xchg* x, PeerK& k) {
@@ -128,9 +133,30 @@ __device__ __forceinline__ void peer_arrive(const PeerK& P) {
     const int lane = threadIdx.x;
     uint32_t* arrivals = P.state + 2 * P.slot;
     uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __shfl(old, 0);
-    if (old + 1u != gridDim.x) return;
+    if (gridDim.x >= kPeerSubMin) {
+        // two-level count: workgroup b arrives on sub-counter b & 7 of the slot (one 64-B line
+        // each, so the ≈ gridDim / 8 returning adds of each proceed beside the others' instead of
+        // queueing on one word); the last of each sub-group arrives on the slot's counter.
+        // Loopback A/B (scripts/sim_ab.sh): config P at N = 8 (≈ 760 workgroups a pushing
+        // epilogue) 122 → 112.7 µs a rank, config S at N = 2 (≈ 450) 26.0 → 24.5; config S at
+        // N = 8 (29) 25.9 → 26.6, hence the threshold
+        const uint32_t sub = blockIdx.x & 7u;
+        const uint32_t n_sub = (gridDim.x - sub + 7u) / 8u;  // workgroups b with b & 7 == sub
+        uint32_t* sc = P.state + DG_PEER_SUB_BASE + (P.slot * 8 + sub) * DG_PEER_SUB_STRIDE;
+        if (lane == 0) old = __hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __shfl(old, 0);
+        if (old + 1u != n_sub) return;
+        if (lane == 0) {
+            __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch counts anew
+            old = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        old = __shfl(old, 0);
+        if (old + 1u != 8u) return;
+    } else {
+        if (lane == 0) old = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __shfl(old, 0);
+        if (old + 1u != gridDim.x) return;
+    }
     uint32_t* ep = P.state + 2 * P.slot + 1;
     const uint32_t* err = P.state + 2 * DG_PEER_SLOTS;
     uint32_t epoch = 0, failed = 0;

@@ -85,7 +85,7 @@ class PeerExchange:
         self.region, self.rank, self.world, self.cfg = region, rank, world, cfg
         self.nbytes = region.numel() * region.element_size()
         dev = region.device
-        self.state = torch.zeros(32, dtype=torch.int32, device=dev)
+        self.state = torch.zeros(_lib.DG_PEER_STATE_WORDS, dtype=torch.int32, device=dev)
         fp = ctypes.c_void_p()
         check(self.lib.dg_peer_alloc(4 * _lib.DG_PEER_SLOTS * _lib.DG_PEER_MAX, 2, ctypes.byref(fp)), "dg_peer_alloc")
         self._flags = fp.value

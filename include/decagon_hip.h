@@ -36,7 +36,7 @@ extern "C" {
 
 #define DG_MAX_GROUPS 8
 
-/* ABI version (35); bumped whenever a struct layout or a signature changes. */
+/* ABI version (36); bumped whenever a struct layout or a signature changes (36: DG_PEER_STATE_WORDS grew). */
 int32_t dg_abi_version(void);
 
 /* --------------------------------------------------------------------------------------
@@ -426,14 +426,18 @@ int dg_gcn_epilogue_tab_f32(const dg_epi_row_desc* rows, int32_t n_rows, int32_t
  * that read the gathered rows start after that launch ends.  A wait that times out sets the
  * error word state[DG_PEER_ERROR_WORD] (0x10000 | slot << 8 | source rank) and returns; once
  * it is set, every later wait returns at once (the host checks the word and raises).
- * state: this rank's device words, zeroed once: per slot {arrivals, epoch}, then the error word.
+ * state: this rank's device words (DG_PEER_STATE_WORDS), zeroed once: per slot {arrivals, epoch},
+ * then the error word; from DG_PEER_SUB_BASE, 8 arrival sub-counters per slot, DG_PEER_SUB_STRIDE
+ * words apart (launches of >= 128 workgroups count their arrivals in two levels).
  * A slot's launches must all use the same grid (the arrival count), and every rank must run
  * the same sequence of exchanges per slot.
  * Replaces: the RCCL/NCCL all-gather of the sharded step (the reference has no parallelism).
  * -------------------------------------------------------------------------------------- */
 #define DG_PEER_MAX 8
 #define DG_PEER_SLOTS 8
-#define DG_PEER_STATE_WORDS (2 * DG_PEER_SLOTS + 1)
+#define DG_PEER_SUB_BASE 64
+#define DG_PEER_SUB_STRIDE 16
+#define DG_PEER_STATE_WORDS (DG_PEER_SUB_BASE + DG_PEER_SLOTS * 8 * DG_PEER_SUB_STRIDE)
 #define DG_PEER_ERROR_WORD (2 * DG_PEER_SLOTS)
 #define DG_IPC_HANDLE_BYTES 64
 #define DG_EPI_PUSH 1           /* dg_epi_target.target_flags: push this target's rows          */
