@@ -211,6 +211,7 @@ SIGNATURES = {
     "dg_gcn_epilogue_peer_f32": (c_int32, [POINTER(DgEpiTarget), c_int32, c_int32, c_int32, POINTER(DgPeerXchg),
                                            c_void_p]),
     "dg_gcn_fused_tab_f32": (c_int32, [POINTER(DgWaveTable), c_int32, c_int32, c_void_p]),
+    "dg_gcn_fused_tab_peer_f32": (c_int32, [POINTER(DgWaveTable), c_int32, c_int32, POINTER(DgPeerXchg), c_void_p]),
     "dg_spmm_seg_tab_f32": (c_int32, [POINTER(DgWaveTable), c_int32, c_int32, c_void_p]),
     "dg_gcn_epilogue_tab_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, POINTER(DgPeerXchg), c_void_p]),
     "dg_gcn_fused_seg_peer_f32": (c_int32, [POINTER(DgSegGroup), c_int32, POINTER(DgFusedTarget), c_int32, c_int32,

@@ -587,10 +587,13 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
     return res;
 }
 
-template <bool PROJ, int NW>
+// PEER (dg_gcn_fused_tab_peer_f32): each finished row also goes to every peer's copy of its
+// target (desc.pad[0] = the row's byte offset in the target, pad[1] = the target's bytes), and
+// the launch ends with the exchange (peer.h).
+template <bool PROJ, int NW, bool PEER>
 __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restrict__ pairs,
                                                           const dg_tab_desc* __restrict__ desc,
-                                                          const uint2* __restrict__ ovf) {
+                                                          const uint2* __restrict__ ovf, const dg::PeerK P) {
     constexpr int DOUT4 = PROJ ? 8 : 16;
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
@@ -637,7 +640,11 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
             tot.w = fmaxf(tot.w, 0.f);
         }
         reinterpret_cast<float4*>(D.orow)[lane] = tot;
+        if constexpr (PEER)
+            dg::peer_store4(P, reinterpret_cast<const float*>(reinterpret_cast<const char*>(D.orow) - D.pad[0]),
+                            (uint32_t)D.pad[1], (uint32_t)D.pad[0] + 16u * lane, tot);
     }
+    if constexpr (PEER) dg::peer_arrive(P);  // the last workgroup raises the flags and waits
 }
 
 // The wave-table form of spmm_seg_kernel (dg_spmm_seg_tab_f32, round 5): the same workgroups
@@ -874,31 +881,53 @@ extern "C" int dg_gcn_fused_seg_f32(const dg_seg_group* groups, int32_t n_groups
     return fused_seg_launch(groups, n_groups, targets, n_targets, d_in, d_out, nullptr, stream);
 }
 
-extern "C" int dg_gcn_fused_tab_f32(const dg_wave_table* t, int32_t d_in, int32_t d_out, void* stream) {
+namespace {
+int fused_tab_launch(const dg_wave_table* t, int32_t d_in, int32_t d_out, const dg_peer_xchg* xchg, void* stream) {
     if (!t) return DG_EINVAL;
     bool proj = false;
     if (seg_shape(d_in, d_out, proj) != DG_OK || (!proj && d_in != 64)) return DG_EINVAL;
     if (t->n_blocks < 0 || t->nw < 1 || t->nw > 16 || t->nw_stride != (t->nw <= 8 ? 8 : 16)) return DG_EINVAL;
-    if (t->n_blocks == 0) return DG_OK;
+    if (t->n_blocks == 0) return xchg ? DG_EINVAL : DG_OK;  // (an exchange needs a workgroup a rank)
     if (!t->pairs || !t->desc || !dg::aligned16(t->pairs) || (reinterpret_cast<uintptr_t>(t->desc) & 63))
         return DG_EALIGN;
     if ((int64_t)t->n_blocks * t->nw_stride * 64 > 0x7fffffffLL) return DG_EINVAL;
+    dg::PeerK P{};
+    if (xchg) {
+        const int rc = dg::peer_convert(xchg, P);
+        if (rc != DG_OK) return rc;
+    }
     const uint2* pr = reinterpret_cast<const uint2*>(t->pairs);
     const uint2* ov = reinterpret_cast<const uint2*>(t->ovf);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(t->n_blocks)), block(64 * t->nw);
-    if (t->nw_stride == 8) {
-        if (proj)
-            hipLaunchKernelGGL((gcn_tab_kernel<true, 8>), grid, block, 0, st, pr, t->desc, ov);
-        else
-            hipLaunchKernelGGL((gcn_tab_kernel<false, 8>), grid, block, 0, st, pr, t->desc, ov);
+#define DG_TAB_LAUNCH(PR, NWV, PE) \
+    hipLaunchKernelGGL((gcn_tab_kernel<PR, NWV, PE>), grid, block, 0, st, pr, t->desc, ov, P)
+    if (xchg) {
+        if (t->nw_stride == 8) {
+            if (proj) DG_TAB_LAUNCH(true, 8, true); else DG_TAB_LAUNCH(false, 8, true);
+        } else {
+            if (proj) DG_TAB_LAUNCH(true, 16, true); else DG_TAB_LAUNCH(false, 16, true);
+        }
     } else {
-        if (proj)
-            hipLaunchKernelGGL((gcn_tab_kernel<true, 16>), grid, block, 0, st, pr, t->desc, ov);
-        else
-            hipLaunchKernelGGL((gcn_tab_kernel<false, 16>), grid, block, 0, st, pr, t->desc, ov);
+        if (t->nw_stride == 8) {
+            if (proj) DG_TAB_LAUNCH(true, 8, false); else DG_TAB_LAUNCH(false, 8, false);
+        } else {
+            if (proj) DG_TAB_LAUNCH(true, 16, false); else DG_TAB_LAUNCH(false, 16, false);
+        }
     }
+#undef DG_TAB_LAUNCH
     return dg::launch_status();
+}
+}  // namespace
+
+extern "C" int dg_gcn_fused_tab_f32(const dg_wave_table* t, int32_t d_in, int32_t d_out, void* stream) {
+    return fused_tab_launch(t, d_in, d_out, nullptr, stream);
+}
+
+extern "C" int dg_gcn_fused_tab_peer_f32(const dg_wave_table* t, int32_t d_in, int32_t d_out,
+                                         const dg_peer_xchg* xchg, void* stream) {
+    if (!xchg) return DG_EINVAL;
+    return fused_tab_launch(t, d_in, d_out, xchg, stream);
 }
 
 extern "C" int dg_spmm_seg_tab_f32(const dg_wave_table* t, int32_t d_in, int32_t d_out, void* stream) {

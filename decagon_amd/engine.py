@@ -693,8 +693,8 @@ class ForwardPlan:
                               else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu))
             fused_peer = self._peer_fused(relu)
             d_in = self.h1 if seg_w else d
-            if fused_peer is None and WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
-                launches.append(kernels.PreparedFusedTab(tgts, d_in, d))  # (the wave-table form)
+            if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
+                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, peer=fused_peer))  # (the wave-table form)
             else:
                 launches.append(kernels.PreparedFusedSeg(tgts, d_in, d, peer=fused_peer))
             self.launch_groups[id(launches[-1])] = [et for i in self.targets for et in self.targets[i]]

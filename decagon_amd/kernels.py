@@ -403,10 +403,12 @@ class PreparedFusedTab(PreparedFusedSeg):
     same rows) through dg_gcn_fused_tab_f32: the wave table — each wave's 64-byte descriptor and
     its segment's first 64 pairs at a fixed slot — is built here once, on the host, from the
     chunk-merged CSR and segment starts of the specs (decagon_hip.h documents the layout).
-    Shapes: d_in = d_out = 64, or 64 -> 32 with weight stacks; no peer exchange."""
+    Shapes: d_in = d_out = 64, or 64 -> 32 with weight stacks.  peer = (PeerExchange, slot):
+    the rows also go to every peer and the launch ends with the exchange
+    (dg_gcn_fused_tab_peer_f32; PreparedFusedSeg's peer form, bitwise the same rows)."""
 
-    def __init__(self, targets, d_in: int, d_out: int):
-        super().__init__(targets, d_in, d_out)
+    def __init__(self, targets, d_in: int, d_out: int, peer=None):
+        super().__init__(targets, d_in, d_out, peer=peer)
         specs = self._keep[0]
         if not _tab_shape(d_in, d_out, specs):
             raise ValueError("dg_gcn_fused_tab_f32: d_in = d_out = 64, or 64 -> 32 with weight stacks")
@@ -440,13 +442,23 @@ class PreparedFusedTab(PreparedFusedSeg):
                 if w < rpb and r0 + w < n_rows:
                     tb.desc["orow"][i] = out.data_ptr() + (r0 + w) * d_out * 4
                     tb.desc["wr"][i] = gc | ((1 if relu else 0) << 8) | (w << 16)
+                    tb.desc["pad"][i, 0] = (r0 + w) * d_out * 4  # (the peer form: row offset,
+                    tb.desc["pad"][i, 1] = n_rows * d_out * 4     # target bytes)
+        if not plan and peer is not None:
+            raise ValueError("dg_gcn_fused_tab_peer_f32: the exchange needs at least one row a rank")
         self._tab = tb.upload(self, len(plan), nw, stride, specs[0].x.device)
         self.n_blocks, self.nw = len(plan), nw
-        self._tfn = _lib.load().dg_gcn_fused_tab_f32
+        if self._xchg is not None:
+            self._tfn, self._tname = _lib.load().dg_gcn_fused_tab_peer_f32, "dg_gcn_fused_tab_peer_f32"
+        else:
+            self._tfn, self._tname = _lib.load().dg_gcn_fused_tab_f32, "dg_gcn_fused_tab_f32"
 
     def __call__(self, stream=None) -> None:
-        check(self._tfn(ctypes.byref(self._tab), self.d_in, self.d_out, _stream_ptr(stream)),
-              "dg_gcn_fused_tab_f32")
+        if self._xchg is not None:
+            check(self._tfn(ctypes.byref(self._tab), self.d_in, self.d_out, self._xchg, _stream_ptr(stream)),
+                  self._tname)
+        else:
+            check(self._tfn(ctypes.byref(self._tab), self.d_in, self.d_out, _stream_ptr(stream)), self._tname)
 
     def seg_form(self, stream=None) -> None:
         """The same rows through dg_gcn_fused_seg_f32 (tests: bitwise equal)."""

@@ -259,6 +259,15 @@ typedef struct dg_wave_table {
 
 int dg_gcn_fused_tab_f32(const dg_wave_table* table /* HOST */, int32_t d_in, int32_t d_out, void* stream);
 
+/* dg_gcn_fused_tab_f32 with the peer-store exchange (config S at N = 2 with --exchange peer):
+ * every finished row also goes to every peer's copy of its target — desc.pad[0] = the row's
+ * byte offset in its target, desc.pad[1] = the target's bytes, the target inside the exchange
+ * region — and the launch ends with the exchange, as dg_gcn_fused_seg_peer_f32.  xchg as
+ * dg_peer_allgather; at least one workgroup. */
+struct dg_peer_xchg;
+int dg_gcn_fused_tab_peer_f32(const dg_wave_table* table /* HOST */, int32_t d_in, int32_t d_out,
+                              const struct dg_peer_xchg* xchg /* HOST */, void* stream);
+
 /* The wave-table form of dg_spmm_seg_f32 (partial mode; config S's N-GPU layers): the same
  * workgroups (in that entry point's XCD-contiguous item order), waves and chunk partials, bit
  * for bit, from a host-built table with the layout above.  A wave whose desc.orow != NULL is

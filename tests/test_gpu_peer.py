@@ -241,6 +241,8 @@ def test_peer_exchange_forward_matches_oracle(kind, world, mode):
             assert info["peer_reduce"] == (kind == "P"), info
         if mode == "kernel":
             assert all(info["gather_all"]), info
+        if kind == "S" and world == 2:  # one launch per layer: the wave-table fused form
+            assert "PreparedFusedTab" in info["fused_kinds"], info
         for form in outs:
             for t in (0, 1):
                 assert rel_err(form[0][t], h1[t]) <= TOL, (r, "hidden1", t)
