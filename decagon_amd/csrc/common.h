@@ -76,6 +76,35 @@ __device__ __forceinline__ void opaque4(float4& v) {
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
 
+// Σ partial[0 .. n) in block order, t = (((0 + p0) + p1) + ...) — the fp32 sum one lane gets
+// reading them one by one — computed by one whole wave: lane l loads blocks l, l + 64, l + 128,
+// l + 192 of each 256 at once (agent-scope loads: the partials were published from other XCDs),
+// then the values are added in order through v_readlane.  One round trip per 256 partials
+// instead of one per partial (a serial loop of sc1 loads waits ≈ 1 µs each).  Wave-uniform n.
+__device__ __forceinline__ float block_order_sum(const float* partial, int n, int lane) {
+    float t = 0.f;
+#pragma unroll 1
+    for (int b0 = 0; b0 < n; b0 += 4 * kWave) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int b = b0 + kWave * j + lane;
+            v[j] = b < n ? __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (b0 + kWave * j >= n) break;  // wave-uniform
+            const int m = n - (b0 + kWave * j) < kWave ? n - (b0 + kWave * j) : kWave;
+#pragma unroll
+            for (int l = 0; l < kWave; ++l) {
+                if (l >= m) break;
+                t += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[j]), l));
+            }
+        }
+    }
+    return t;
+}
+
 // Butterfly steps without an LDS round trip (ds_bpermute) where gfx950 allows: the value of
 // lane ^ m from v_permlane32_swap / v_permlane16_swap (m = 32 / 16: lane halves / 16-lane rows
 // exchanged between two copies of x) or DPP (m = 8: row_ror:8 within a row; m = 2 / 1:

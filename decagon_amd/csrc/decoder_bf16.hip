@@ -385,12 +385,12 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_colshared_kernel(const B
             last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
         }
         __syncthreads();
-        if (last && tid == 0) {
-            float t = 0.f;
-            for (int b = 0; b < (int)gridDim.x; ++b)
-                t += __hip_atomic_load(a.partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            a.loss[0] = t;
-            __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last && tid < 64) {  // wave 0 of the last workgroup
+            const float t = dg::block_order_sum(a.partial, (int)gridDim.x, lane);
+            if (tid == 0) {
+                a.loss[0] = t;
+                __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }
@@ -704,12 +704,12 @@ __global__ __launch_bounds__(THREADS) void decoder_bf16_cs16_kernel(const Bf16De
         last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
     __syncthreads();
-    if (last && tid == 0) {
-        float t = 0.f;
-        for (int b = 0; b < (int)gridDim.x; ++b)
-            t += __hip_atomic_load(a.partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a.loss[0] = t;
-        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last && tid < 64) {  // wave 0 of the last workgroup
+        const float t = dg::block_order_sum(a.partial, (int)gridDim.x, lane);
+        if (tid == 0) {
+            a.loss[0] = t;
+            __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 }  // namespace
