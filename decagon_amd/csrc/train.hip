@@ -108,12 +108,21 @@ __global__ __launch_bounds__(256) void decoder_grad_dm_kernel(const float* xw, c
     const int ta = t / tiles, tb = t - ta * tiles;
     const int p0 = ch * kPairChunk;
     f32x16 acc = {};
-#pragma unroll 4
-    for (int k0 = 0; k0 < kPairChunk; k0 += 2) {
-        const int p = p0 + k0 + h;
-        const float av = p < n ? xw[(int64_t)p * d + ta * 32 + i] : 0.f;
-        const float bv = p < n ? vw[(int64_t)p * d + tb * 32 + i] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    // every row load of the chunk issued before the MFMA chain: unconditional loads (a pair past
+    // n reads pair n - 1, then contributes zeros) — conditional ones were each waited for in turn
+    constexpr int kSteps = kPairChunk / 2;
+    float av[kSteps], bv[kSteps];
+#pragma unroll
+    for (int s2 = 0; s2 < kSteps; ++s2) {
+        const int p = p0 + 2 * s2 + h;
+        const int pc = p < n ? p : n - 1;
+        av[s2] = xw[(int64_t)pc * d + ta * 32 + i];
+        bv[s2] = vw[(int64_t)pc * d + tb * 32 + i];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < kSteps; ++s2) {
+        const bool ok = p0 + 2 * s2 + h < n;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ok ? av[s2] : 0.f, ok ? bv[s2] : 0.f, acc, 0, 0, 0);
     }
     float* out = part + (int64_t)ch * d * d;
 #pragma unroll
@@ -129,7 +138,8 @@ __global__ __launch_bounds__(256) void decoder_grad_reduce_kernel(const float* p
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= d * d) return;
     float s = 0.f;
-    for (int c = 0; c < nch; ++c) s += part[(int64_t)c * d * d + e];
+#pragma unroll 16
+    for (int c = 0; c < nch; ++c) s += part[(int64_t)c * d * d + e];  // (loads ahead of the adds)
     dM[e] = s;
     if (dG) {
         const int ra = e / d, cb = e - ra * d;
@@ -144,8 +154,10 @@ __global__ __launch_bounds__(256) void decoder_grad_vec_kernel(const float* dM, 
     const int a = blockIdx.x * 256 + threadIdx.x;
     if (a >= d) return;
     if (dl) {
-        float s = 0.f;
+        float s = 0.f;  // (unrolled: the loads run ahead of the dependent fma chain)
+#pragma unroll 16
         for (int b = 0; b < d; ++b) s = fmaf(dM[(int64_t)a * d + b] * G[(int64_t)a * d + b], l[b], s);
+#pragma unroll 16
         for (int c = 0; c < d; ++c) s = fmaf(dM[(int64_t)c * d + a] * G[(int64_t)c * d + a], l[c], s);
         dl[a] = s;
     }
