@@ -178,21 +178,35 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const int32_t* idx, i
     if (q >= n) return;
     const int r = idx[q];
     if (r < 0 || r >= n_out) return;  // outside the table: no row to update (wave-uniform)
-    for (int q0 = 0; q0 < q; q0 += 64) {
-        const int j = q0 + lane;
-        if (__any(j < q && idx[j] == r)) return;  // an earlier occurrence owns the row
-    }
+    // idx scanned 16 chunks of 64 at a time, their loads all in flight (one chunk per round
+    // trip before: n / 64 dependent round trips for every wave); chunks in order, so a wave
+    // returns on an earlier occurrence before it adds anything, and adds its occurrences in
+    // index order as before
+    constexpr int kScanU = 16;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};  // columns lane + 64t, d <= 256
-    for (int q0 = q; q0 < n; q0 += 64) {
-        const int j = q0 + lane;
-        uint64_t m = __ballot(j < n && idx[j] == r);
-        while (m) {
-            const int b = __builtin_ctzll(m);
-            m &= m - 1;
-            const float* s = src + (int64_t)(q0 + b) * d;
+    for (int q0 = 0; q0 < n; q0 += 64 * kScanU) {
+        int v[kScanU];
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (lane + 64 * t < d) acc[t] += s[lane + 64 * t];
+        for (int u = 0; u < kScanU; ++u) {
+            const int j = q0 + 64 * u + lane;
+            v[u] = idx[j < n ? j : n - 1];  // unconditional (clamped) loads
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const int c0 = q0 + 64 * u;
+            if (c0 >= n) break;  // wave-uniform
+            const int j = c0 + lane;
+            const bool hit = j < n && v[u] == r;
+            if (__any(hit && j < q)) return;  // an earlier occurrence owns the row
+            uint64_t m = __ballot(hit && j >= q);
+            while (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                const float* s = src + (int64_t)(c0 + b) * d;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (lane + 64 * t < d) acc[t] += s[lane + 64 * t];
+            }
         }
     }
     float* o = out + (int64_t)r * ld_out;
@@ -232,9 +246,15 @@ __global__ __launch_bounds__(256) void l2norm_grad_kernel(const L2gArgs a) {
         dy.z = m.z > 0.f ? dy.z : 0.f;
         dy.w = m.w > 0.f ? dy.w : 0.f;
     }
-#pragma unroll 1
-    for (int g = 0; g < a.n_groups; ++g) {
-        const float4 s = ok ? *reinterpret_cast<const float4*>(a.s[g] + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // every group's S row loaded before the first group's sums (one round trip, not one a group)
+    float4 sv[DG_MAX_GROUPS];
+#pragma unroll
+    for (int g = 0; g < DG_MAX_GROUPS; ++g)
+        sv[g] = ok && g < a.n_groups ? *reinterpret_cast<const float4*>(a.s[g] + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int g = 0; g < DG_MAX_GROUPS; ++g) {
+        if (g >= a.n_groups) break;  // wave-uniform
+        const float4 s = sv[g];
         float ss = s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w;
         float dot = s.x * dy.x + s.y * dy.y + s.z * dy.z + s.w * dy.w;
 #pragma unroll
