@@ -48,7 +48,7 @@ def _allgather_rank(rank, world, rounds):
     dev = torch.device("cuda", 0)
     blk = 3000  # floats per rank's block (12 KB: the push kernel's partial workgroup path)
     region = torch.full((world * blk + 64,), float("nan"), dtype=torch.float32, device=dev)
-    ex = PeerExchange(region, rank, world, PeerConfig(mode="kernel", gather=dist_gather()))
+    ex = PeerExchange(region, rank, world, PeerConfig(mode="kernel", gather=dist_gather(), timeout_s=20.0))
     fn = ex.allgather_fn([region[rank * blk:(rank + 1) * blk]], 2)
     seen = []
     for it in range(rounds):
@@ -153,7 +153,10 @@ def _forward_rank(rank, world, kind, mode):
     from decagon_amd.peer import PeerConfig, dist_gather
 
     g = _graph(kind, world)
-    plan = _plan(kind, g, rank, world, PeerConfig(mode=mode, gather=dist_gather()))
+    # (the ranks time-slice the test box's one GPU: a rank's graph replay can start seconds after
+    # another's — one run of the S-8 case timed out at the 2-s production bound — so the waits
+    # here are bounded at 20 s; the timeout tests below keep short bounds)
+    plan = _plan(kind, g, rank, world, PeerConfig(mode=mode, gather=dist_gather(), timeout_s=20.0))
     info = {"seg": plan.seg_mode, "exchanges": sum(L.has_exchange for L in (plan._layer1, plan._layer2)),
             "peer_reduce": plan.peer_reduce,
             "fused_kinds": sorted({type(l).__name__ for l in plan._layer1.launches}),
