@@ -643,14 +643,15 @@ def decoder_bench(args, device, steps, warmup, rank=0, world=1, dist=None):
     E, R, Dk = up(c5.E, bf), up(c5.R, bf), up(c5.D, bf)
     slots, B, d = Dk.shape[0], c5.batch, E.shape[1]
     s0, s1 = slot_range(slots, rank, world)
+    # (dist None at world > 1: a --simulate-world rank share, the loss all-reduce a no-op)
     sc = SlotScorer(E, E, R, Dk, up(c5.pos_rows), up(c5.pos_cols), kernels.upload_alias(c5.degrees, device), B,
                     MARGIN, seed=11, slots=(s0, s1),
-                    allreduce=collectives(args.backend)[0] if world > 1 else None)
+                    allreduce=collectives(args.backend)[0] if world > 1 and dist is not None else None)
     stream = torch.cuda.Stream(device)
     G = steps_per_graph(steps, args.graph_steps)
     el = timed_steps(sc, steps, warmup, G, stream, not args.no_graph,
                      dist.barrier if dist is not None and world > 1 else None)
-    if world > 1:
+    if world > 1 and dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
@@ -697,6 +698,22 @@ def main_decoder(args):
     import torch
 
     torch.cuda.set_device(0)
+    if args.simulate_world:
+        # config 5 at N GPUs, each rank's share timed on this one GPU (its contiguous block of
+        # slots; the scalar loss all-reduce — the only collective — a no-op)
+        N = args.simulate_world
+        ranks = []
+        for r in (range(N) if args.simulate_rank < 0 else [args.simulate_rank]):
+            x = decoder_bench(args, torch.device("cuda", 0), args.steps, args.warmup, r, N, None)
+            ranks.append({"rank": r, "ms_per_step": x["ms_per_step"], "kernel_ms": x["roofline"]["kernel_ms"],
+                          "slots": x["config"]["slots_this_rank"]})
+            print(f"rank {r}/{N}: {ranks[-1]['ms_per_step'] * 1e3:.1f} us/step", file=sys.stderr, flush=True)
+        rec = {"metric": "config D sharded-step rehearsal on one GPU (the loss all-reduce not run)", "world": N,
+               "steps": args.steps, "warmup": args.warmup,
+               "max_rank_ms_per_step": max(x["ms_per_step"] for x in ranks), "ranks": ranks,
+               "policy_overrides": overrides()}
+        print(json.dumps(rec), file=JSON_OUT, flush=True)
+        return
     rec = decoder_bench(args, torch.device("cuda", 0), args.steps, args.warmup)
     rec.update({"higher_is_better": True, "vs_baseline": None, "cpu_baseline": None})
     rec["policy_overrides"] = overrides()  # DG_* knobs that differed from the defaults

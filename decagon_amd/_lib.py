@@ -22,7 +22,7 @@ DG_MAX_GROUPS = 8
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 36
+ABI_VERSION = 37
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -34,6 +34,7 @@ DG_PEER_SLOTS = 8
 DG_PEER_SUB_BASE, DG_PEER_SUB_STRIDE = 64, 16
 DG_PEER_STATE_WORDS = DG_PEER_SUB_BASE + DG_PEER_SLOTS * 8 * DG_PEER_SUB_STRIDE
 DG_PEER_ERROR_WORD = 2 * DG_PEER_SLOTS
+DG_PEER_DIAG_BASE, DG_PEER_DIAG_WORDS, DG_PEER_SLOW_TICKS = 24, 18, 10000  # wait records (round 6)
 DG_IPC_HANDLE_BYTES = 64
 DG_EPI_PUSH = 1
 
@@ -200,8 +201,9 @@ SIGNATURES = {
     "dg_spmm_csr_f32": (
         c_int32,
         [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32,
-         c_void_p],
+         c_float, c_void_p],
     ),
+    "dg_rownorm_l2_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p]),
     "dg_gcn_fused_f32": (
         c_int32,
         [POINTER(DgRelGroup), c_int32, POINTER(DgFusedTarget), c_int32, POINTER(DgProj), c_int32, c_int32,
@@ -221,6 +223,7 @@ SIGNATURES = {
     "dg_ipc_get_handle": (c_int32, [c_void_p, c_void_p, POINTER(c_int64)]),
     "dg_ipc_open": (c_int32, [c_void_p, POINTER(c_void_p)]),
     "dg_ipc_close": (c_int32, [c_void_p]),
+    "dg_peer_read": (c_int32, [c_void_p, c_void_p, c_int64]),
     "dg_peer_allgather": (c_int32, [POINTER(DgPeerXchg), c_void_p, POINTER(c_int64), POINTER(c_int64), c_int32,
                                     c_void_p]),
     "dg_gcn_epilogue_f32": (

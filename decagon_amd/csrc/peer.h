@@ -91,10 +91,16 @@ __device__ __forceinline__ void peer_store4(const PeerK& P, const float* base, u
     }
 }
 
+__device__ __forceinline__ void diag_store(const PeerK& P, int word, uint32_t v) {
+    __hip_atomic_store(P.state + DG_PEER_DIAG_BASE + word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Wave-level bounded wait: lane s polls word [slot][s] of this rank's block (one round trip per
-// poll for every source) until all of [0, world) reached epoch; on timeout lane 0 sets the
-// error word (0x10000 | slot << 8 | the first late source).
-__device__ __forceinline__ void peer_poll(const PeerK& P, uint32_t epoch, int lane) {
+// poll for every source) until all of [0, world) reached epoch; on timeout the wait record
+// (decagon_hip.h, DG_PEER_DIAG_BASE: slot, expected epoch, each source's last flag word, the
+// start / give-up / flag-raise ticks) is written, then lane 0 sets the error word
+// (0x10000 | slot << 8 | the first late source).  t_raise: when this rank raised its flags.
+__device__ __forceinline__ void peer_poll(const PeerK& P, uint32_t epoch, int lane, uint64_t t_raise) {
     const bool mine = lane < P.world;
     const uint32_t* own = P.flags[P.rank] + P.slot * DG_PEER_MAX + lane;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -102,6 +108,7 @@ __device__ __forceinline__ void peer_poll(const PeerK& P, uint32_t epoch, int la
     for (;;) {
         const uint32_t v = mine ? __hip_atomic_load(own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : epoch;
         const uint64_t who = __ballot((int32_t)(v - epoch) < 0);
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (!who) {
             // system-scope acquire after the flags matched (buffer_inv sc0 sc1): this wave's
             // later loads see what the peers released before raising them; the launches that
@@ -109,13 +116,29 @@ __device__ __forceinline__ void peer_poll(const PeerK& P, uint32_t epoch, int la
 #if DG_PEER_FENCES
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #endif
+            if (now - t0 > (uint64_t)DG_PEER_SLOW_TICKS && lane == 0) {  // a slow wait: count it, keep its max
+                __hip_atomic_fetch_add(P.state + DG_PEER_DIAG_BASE + 16, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_max(P.state + DG_PEER_DIAG_BASE + 17, (uint32_t)min(now - t0, (uint64_t)0xffffffffu),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             return;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)P.timeout) {
-            if (lane == 0)
+        if (now - t0 > (uint64_t)P.timeout) {
+            if (mine) diag_store(P, 2 + lane, v);  // each source's flag word as last read
+            if (lane == 0) {
+                diag_store(P, 0, (uint32_t)P.slot);
+                diag_store(P, 1, epoch);
+                diag_store(P, 10, (uint32_t)t0);
+                diag_store(P, 11, (uint32_t)(t0 >> 32));
+                diag_store(P, 12, (uint32_t)now);
+                diag_store(P, 13, (uint32_t)(now >> 32));
+                diag_store(P, 14, (uint32_t)t_raise);
+                diag_store(P, 15, (uint32_t)(t_raise >> 32));
                 __hip_atomic_store(P.state + 2 * DG_PEER_SLOTS,
                                    0x10000u | ((uint32_t)P.slot << 8) | ((uint32_t)__ffsll((long long)who) - 1u),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             return;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -186,10 +209,11 @@ __device__ __forceinline__ void peer_arrive(const PeerK& P) {
 #pragma unroll
     for (int p = 0; p < DG_PEER_MAX; ++p)
         if (lane == p) fp = P.flags[p];
+    const uint64_t t_raise = __builtin_amdgcn_s_memrealtime();
     if (lane < P.world)
         __hip_atomic_store(fp + P.slot * DG_PEER_MAX + (P.loopback ? lane : P.rank), epoch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-    peer_poll(P, epoch, lane);
+    peer_poll(P, epoch, lane, t_raise);
     if (lane == 0) __hip_atomic_store(ep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

@@ -77,6 +77,12 @@ extern "C" int dg_peer_alloc(int64_t bytes, int32_t kind, void** ptr) {
     return DG_OK;
 }
 
+extern "C" int dg_peer_read(const void* device, void* host, int64_t bytes) {
+    if (!device || !host || bytes <= 0) return DG_EINVAL;
+    const hipError_t e = hipMemcpy(host, device, (size_t)bytes, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? DG_OK : static_cast<int>(e);
+}
+
 extern "C" int dg_peer_free(void* ptr) {
     if (!ptr) return DG_OK;
     const hipError_t e = hipFree(ptr);

@@ -587,6 +587,26 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
     return res;
 }
 
+// rows[0][q] + rows[1][q] + ... + rows[K-1][q], added in that order (((r0 + r1) + r2) + ...) —
+// bitwise the serial loop `s = rows[0][q]; for (u = 1; u < K; ++u) s += rows[u][q]` — with the
+// LDS reads of each run of 8 rows issued before the first add of the run, instead of one LDS
+// round trip per row (the one-wave relation sum was 0.44 µs median of config S's layer-1 and
+// layer-2 tab launches, profiles/r06_S_tab_phase_profile.json).  Rows past K are not read.
+template <int W>
+__device__ __forceinline__ float4 lds_ordered_sum(const float4 (*rows)[W], int K, int q) {
+    float4 s = rows[0][q];
+#pragma unroll 1
+    for (int u0 = 1; u0 < K; u0 += 8) {
+        float4 z[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[j] = rows[u0 + j < K ? u0 + j : 0][q];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (u0 + j < K) dg::add4(s, z[j]);
+    }
+    return s;
+}
+
 // PEER (dg_gcn_fused_tab_peer_f32): each finished row also goes to every peer's copy of its
 // target (desc.pad[0] = the row's byte offset in the target, pad[1] = the target's bytes), and
 // the launch ends with the exchange (peer.h).
@@ -601,27 +621,38 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wi = (int64_t)blockIdx.x * NW + wave;
-    // the first pairs issued before anything waits (inline asm: the compiler would sink a plain
-    // load below the descriptor's branch, behind its round trip); retired by the vmcnt(0) below
-    uint2 first;
-    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64)
-                 : "memory");
+    DG_FS_STAMP(0);  // (profiling build: wave start)
+    // The descriptor's scalar loads are issued first (the asm below clobbers memory, so they
+    // cannot sink past it), then the first pairs, and one asm block both issues the pairs load
+    // and waits for it: `first` exists for the compiler only once it has landed, so no copy or
+    // use of it can be scheduled between issue and wait.  Both loads are in flight
+    // together: the wave's first round trip fetches both.
     const dg_tab_desc D = desc[wi];  // (uniform: scalar loads)
+    uint2 first;
+    asm volatile("global_load_dwordx2 %0, %1, %2\n\ts_waitcnt vmcnt(0)"
+                 : "=&v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64) : "memory");
     // every descriptor field and the ovf base in SGPRs here, so no scalar load is sunk below
     // the branch into a round trip of its own
     asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(D.wr),
                  "s"(ovf));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef DG_FSEG_PROF
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+    DG_FS_STAMP(1);  // descriptor and first pairs in registers
+    DG_FS_STAMP(2);  // (no segment-bounds phase in the table form)
     const float4 res = tab_wave<PROJ, PROJ ? kTabUP : kTabU>(D, first, ovf, ybuf[wave]);
+#ifdef DG_FSEG_PROF
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+    DG_FS_STAMP(3);  // the wave's relation sum done
     if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
+    DG_FS_STAMP(4);  // every wave of the workgroup done
     // one wave per (row slot, group): its relations summed in order, L2-normalised
     if (D.role >> 31) {
         const int gb = D.role & 0xff, K = (D.role >> 8) & 0xff, ns = (D.role >> 16) & 0x7fff;
         const int q = lane % DOUT4;
-        float4 sum = zbuf[gb][q];
-#pragma unroll 1
-        for (int u = 1; u < K; ++u) dg::add4(sum, zbuf[gb + u][q]);
+        const float4 sum = lds_ordered_sum<DOUT4>(&zbuf[gb], K, q);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
         float ss = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
         ss = dg::xor_sum_below<DOUT4>(ss);
@@ -629,10 +660,10 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
         if (lane < DOUT4) nbuf[ns][lane] = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
     }
     __syncthreads();
+    DG_FS_STAMP(5);  // groups normalised
     if (D.orow != nullptr && lane < DOUT4) {
         const int gc = D.wr & 0xff, s2 = D.wr >> 16;
-        float4 tot = nbuf[s2 * DG_MAX_GROUPS][lane];
-        for (int u = 1; u < gc; ++u) dg::add4(tot, nbuf[s2 * DG_MAX_GROUPS + u][lane]);
+        float4 tot = lds_ordered_sum<DOUT4>(&nbuf[s2 * DG_MAX_GROUPS], gc, lane);
         if ((D.wr >> 8) & 1) {
             tot.x = fmaxf(tot.x, 0.f);
             tot.y = fmaxf(tot.y, 0.f);
@@ -644,6 +675,15 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
             dg::peer_store4(P, reinterpret_cast<const float*>(reinterpret_cast<const char*>(D.orow) - D.pad[0]),
                             (uint32_t)D.pad[1], (uint32_t)D.pad[0] + 16u * lane, tot);
     }
+#ifdef DG_FSEG_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DG_FS_STAMP(6);  // row stored
+    if (lane == 0 && blockIdx.x < kFsProfMaxBlocks) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_fs_prof[PROJ][blockIdx.x][wave][7] = xcc;
+    }
+#endif
     if constexpr (PEER) dg::peer_arrive(P);  // the last workgroup raises the flags and waits
 }
 
@@ -662,20 +702,17 @@ __global__ __launch_bounds__(64 * NW) void seg_tab_kernel(const uint2* __restric
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wi = (int64_t)blockIdx.x * NW + wave;
+    const dg_tab_desc D = desc[wi];  // (as gcn_tab_kernel: descriptor first, pairs load + wait in one asm)
     uint2 first;
-    asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64)
-                 : "memory");
-    const dg_tab_desc D = desc[wi];
+    asm volatile("global_load_dwordx2 %0, %1, %2\n\ts_waitcnt vmcnt(0)"
+                 : "=&v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64) : "memory");
     asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(ovf));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const float4 res = tab_wave<PROJ, PROJ ? kSegUP : kSegU>(D, first, ovf, ybuf[wave]);
     if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
     __syncthreads();
     if (D.orow != nullptr && lane < DOUT4) {
         const int K = (D.role >> 8) & 0xff;
-        float4 sm = zbuf[wave][lane];
-        for (int u = 1; u < K; ++u) dg::add4(sm, zbuf[wave + u][lane]);
-        reinterpret_cast<float4*>(D.orow)[lane] = sm;
+        reinterpret_cast<float4*>(D.orow)[lane] = lds_ordered_sum<DOUT4>(&zbuf[wave], K, lane);
     }
 }
 

@@ -64,7 +64,7 @@ struct SpmmGroupK {
     uint32_t drop_tag;
     float drop_keep;
     int32_t drop_stride;
-    int32_t pad;
+    float beta;  // dg_spmm_csr_f32: out = acc + beta·out (0: out is written without being read)
 };
 
 // The dropout scale of nonzero p in chunk c (DG_GROUP_DROPOUT, dropout.h's stream).
@@ -231,7 +231,16 @@ __global__ __launch_bounds__(256) void spmm_groups_kernel(const SpmmArgs args) {
         if (j >= nr) break;
         const float4 acc = range_body<LP, U>(g, g.x + c * g.chunk_x, rp[j], rp[j + 1], d, 0, 1, dkey, dbase, vc[j],
                                           vv[j]);
-        if (lane < LP && lane * 4 < d) *reinterpret_cast<float4*>(g.out + (slot0 + j) * d + lane * 4) = acc;
+        if (lane < LP && lane * 4 < d) {
+            float4* o = reinterpret_cast<float4*>(g.out + (slot0 + j) * d + lane * 4);
+            float4 y = acc;
+            if (g.beta != 0.f) {  // kernel-argument uniform: tf.sparse_tensor_dense_matmul + beta·Y
+                const float4 old = *o;
+                y = make_float4(fmaf(g.beta, old.x, acc.x), fmaf(g.beta, old.y, acc.y), fmaf(g.beta, old.z, acc.z),
+                                fmaf(g.beta, old.w, acc.w));
+            }
+            *o = y;
+        }
     }
 }
 
@@ -726,7 +735,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 36; }
+extern "C" int32_t dg_abi_version(void) { return 37; }
 
 
 namespace {
@@ -902,19 +911,45 @@ extern "C" int dg_gcn_fused_f32(const dg_rel_group* groups, int32_t n_groups,
 
 extern "C" int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                                int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx,
-                               float* y, int64_t ldy, int32_t d, void* stream) {
-    if (ldy != d) return DG_EINVAL;
-    dg_rel_group g{};
-    g.rowptr = rowptr;
-    g.vcol = col;
-    g.val = val;
-    g.x = x;
-    g.out = y;
-    g.x_ld = ldx;
-    g.n_rows = n_rows;
-    g.n_chunks = 1;
-    g.x_rows = n_cols;
-    return dg_spmm_groups_f32(&g, 1, d, stream);
+                               float* y, int64_t ldy, int32_t d, float beta, void* stream) {
+    if (ldy != d || !(beta == beta) || beta == INFINITY || beta == -INFINITY) return DG_EINVAL;
+    if (n_rows < 0 || n_cols < 0 || d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
+    if (n_rows == 0) return DG_OK;
+    dg_rel_group s{};
+    s.rowptr = rowptr;
+    s.vcol = col;
+    s.val = val;
+    s.x = x;
+    s.out = y;
+    s.x_ld = ldx;
+    s.n_rows = n_rows;
+    s.n_chunks = 1;
+    s.x_rows = n_cols;
+    SpmmArgs args{};
+    args.d = d;
+    SpmmGroupK& k = args.g[0];
+    const int rc = convert_group(s, d, true, k);
+    if (rc != DG_OK) return rc;
+    k.beta = beta;
+    k.n_blocks = static_cast<int32_t>(8 * ((k.row_blocks + 7) / 8));
+    k.block_begin = 0;
+    args.n_groups = 1;
+    const int lp = dg::lanes_per_row(d);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(k.n_blocks)), block(256);
+#define DG_LAUNCH_CSR(L) hipLaunchKernelGGL((spmm_groups_kernel<L, kUnroll>), grid, block, 0, st, args)
+    DG_LP_SWITCH(lp, DG_LAUNCH_CSR)
+#undef DG_LAUNCH_CSR
+    return dg::launch_status();
+}
+
+extern "C" int dg_rownorm_l2_f32(const float* x, float* y, int32_t n_rows, int32_t d, int32_t flags, void* stream) {
+    if (flags & ~DG_EPI_RELU) return DG_EINVAL;
+    if (n_rows < 0 || d < 4 || d > 256 || (d & 3)) return DG_EINVAL;
+    if (n_rows == 0) return DG_OK;
+    if (!x || !y) return DG_EINVAL;
+    const dg_epi_group g{x, nullptr, 1, 0};
+    return dg_gcn_epilogue_f32(&g, 1, y, n_rows, d, DG_EPI_L2NORM | flags, stream);
 }
 
 namespace {

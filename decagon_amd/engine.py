@@ -94,6 +94,9 @@ SEG_FUSED_MAX_ITEMS = 16
 # bounds, gather base and finishing roles precomputed, its first pairs at a fixed slot; bitwise
 # the same rows): config S's step 18.14 -> 15.56 us at 200 steps (round 5)
 WAVE_TABLE = knob("DG_WAVE_TABLE", True)
+# the one-GPU wave-table launches deal each row's pairs over every wave slot of its workgroup
+# (PreparedFusedTab balance, round 6) instead of one wave per relation
+TAB_BALANCE = knob("DG_TAB_BALANCE", True)
 STAGED_FIRST = knob("DG_STAGED_FIRST", True)
 # sharded forward plans: layer 2 of the non-staged groups reassociated over the rank's own rows
 # and relations, Σ_k (Â_k·H1_j)·W2_k in dg_spmm_seg_f32, instead of every rank projecting all of
@@ -478,7 +481,7 @@ class ForwardPlan:
         pc = getattr(shard, "peer", None)
         self.peer_reduce = (pc is not None and pc.mode == "fused" and self.flat_mode and not keep_sums
                             and self.drop_state is None and bool(split_nodes) and not self.seg_mode
-                            and not self._fused_targets())
+                            and not self._fused_targets() and self._peer_reduce_fits(dgraph, split_nodes))
         self._red_slots: Dict[Tuple[int, EdgeType], torch.Tensor] = {}  # (layer, et) -> [world, n_i, d] view
         if split_nodes:
             layout, off = {}, 0
@@ -694,7 +697,7 @@ class ForwardPlan:
             fused_peer = self._peer_fused(relu)
             d_in = self.h1 if seg_w else d
             if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
-                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, peer=fused_peer))  # (the wave-table form)
+                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, peer=fused_peer, balance=TAB_BALANCE))  # (the wave-table form)
             else:
                 launches.append(kernels.PreparedFusedSeg(tgts, d_in, d, peer=fused_peer))
             self.launch_groups[id(launches[-1])] = [et for i in self.targets for et in self.targets[i]]
@@ -710,7 +713,7 @@ class ForwardPlan:
             d_in = self.h1 if seg_w else d
             if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
                 # the wave-table form: the same rows bitwise, fewer dependent loads a wave
-                launches.append(kernels.PreparedFusedTab(tgts, d_in, d))
+                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, balance=TAB_BALANCE))
             else:
                 launches.append(kernels.PreparedFusedSeg(tgts, d_in, d))
             self.launch_groups[id(launches[-1])] = [et for i in fused_t for et in self.targets[i]]
@@ -857,8 +860,8 @@ class ForwardPlan:
                                  for et in self.targets[i])]
             n_groups = sum(len(self.targets[i]) for i in split_t + red_t)
             fits = len(split_t) + len(red_t) <= 8 and n_groups <= DG_MAX_GROUPS
-            if peer_red and not fits:
-                raise ValueError("peer all-reduce: the layer's targets do not fit one epilogue launch")
+            # (__init__ enabled peer_red only where _peer_reduce_fits said these targets fit)
+            assert fits or not peer_red
             if (reduces or peer_red) and fits:
                 for i in red_t:
                     grp_parts = []
@@ -918,6 +921,16 @@ class ForwardPlan:
                       local_epis, gathers, self.allgather, self._peer_gather_all(gathers, relu))
 
     # ---- peer exchange (peer.py) ----
+    def _peer_reduce_fits(self, dgraph, split_nodes) -> bool:
+        """Whether the pushing epilogue launch can carry the peer all-reduce: the row-split node
+        types plus every relation-sharded node type with local relations as targets of ONE
+        dg_gcn_epilogue_peer_f32 launch (<= 8 targets, <= DG_MAX_GROUPS groups).  A larger graph
+        keeps the flat buffer and the RCCL all-reduce instead (it used to raise)."""
+        red_t = [i for i in self.targets if i not in self.row_block
+                 and any(dgraph.groups[et].n_rels for et in self.targets[i])]
+        t = list(split_nodes) + red_t
+        return len(t) <= 8 and sum(len(self.targets[i]) for i in t) <= DG_MAX_GROUPS
+
     def _peer_fused(self, layer1: bool):
         """(PeerExchange, slot) for a finishing launch that pushes its rows and exchanges, or None."""
         if self.peer is None or self.peer.cfg.mode != "fused":

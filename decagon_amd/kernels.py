@@ -352,23 +352,49 @@ class _WaveTable:
         m = np.arange(64)
         self.lane_of = m if proj else 16 * (m & 3) + (m >> 2)
 
-    def relation(self, i: int, g: int, k: int, r: int) -> None:
-        """Wave slot i gathers relation k (of spec g) of row r."""
+    def bounds(self, g: int, k: int, r: int) -> Tuple[int, int]:
+        """[beg, end) of relation k's segment (of spec g) in row r."""
         s = self.specs[g]
-        rowptr, seg, vcol, val, slab = self.host[g]
+        rowptr, seg = self.host[g][:2]
         c, t = divmod(k, s.chunk)
         si = (c * s.n_rows + r) * s.chunk + t
         beg = int(seg[si])
         end = int(seg[si + 1]) if t + 1 < s.chunk else int(rowptr[c * s.n_rows + r + 1])
-        vc = vcol[beg:end].astype(np.int64)
+        return beg, end
+
+    def seg_len(self, g: int, k: int, r: int) -> int:
+        beg, end = self.bounds(g, k, r)
+        return end - beg
+
+    def relation(self, i: int, g: int, k: int, r: int) -> None:
+        """Wave slot i gathers relation k (of spec g) of row r."""
+        beg, end = self.bounds(g, k, r)
+        self.wave(i, g, r, [(k, 0, end - beg)])
+
+    def wave(self, i: int, g: int, r: int, pieces) -> None:
+        """Wave slot i gathers the pieces [(k, a, b)] of row r, in order: pairs a..b of relation
+        k's segment (of spec g) — with a weight stack (layer 2 reassociated) one relation's only,
+        since the wave multiplies its aggregate by that relation's W slab."""
+        s = self.specs[g]
+        vcol, val, slab = self.host[g][2:]
         d = self.desc
-        if self.proj:
-            sl = int(slab[k]) if slab is not None else k
-            vc = vc - sl * s.n_cols  # plain rows of H
-            d["w"][i] = s.w.data_ptr() + sl * 64 * 32 * 4
-        cnt = end - beg
+        vcs, vvs = [], []
+        for k, a, b in pieces:
+            beg, _ = self.bounds(g, k, r)
+            vc = vcol[beg + a:beg + b].astype(np.int64)
+            if self.proj:
+                sl = int(slab[k]) if slab is not None else k
+                vc = vc - sl * s.n_cols  # plain rows of H
+                d["w"][i] = s.w.data_ptr() + sl * 64 * 32 * 4
+            vcs.append(vc)
+            vvs.append(val[beg + a:beg + b])
+        if self.proj and len({k for k, _, _ in pieces}) > 1:
+            raise ValueError("a reassociated wave gathers one relation")
+        vc = np.concatenate(vcs) if vcs else np.zeros(0, np.int64)
+        vv = np.concatenate(vvs) if vvs else np.zeros(0, np.float32)
+        cnt = len(vc)
         d["x"][i], d["x_ld"][i], d["cnt"][i] = s.x.data_ptr(), s.x_ld, cnt
-        pv = np.stack([vc.astype(np.int32), val[beg:end].view(np.int32)], 1)
+        pv = np.stack([vc.astype(np.int32), vv.astype(np.float32).view(np.int32)], 1)
         m0 = min(cnt, 64)
         self.pairs[i * 64 + self.lane_of[:m0]] = pv[:m0]
         if cnt > 64:
@@ -405,40 +431,64 @@ class PreparedFusedTab(PreparedFusedSeg):
     chunk-merged CSR and segment starts of the specs (decagon_hip.h documents the layout).
     Shapes: d_in = d_out = 64, or 64 -> 32 with weight stacks.  peer = (PeerExchange, slot):
     the rows also go to every peer and the launch ends with the exchange
-    (dg_gcn_fused_tab_peer_f32; PreparedFusedSeg's peer form, bitwise the same rows)."""
+    (dg_gcn_fused_tab_peer_f32; PreparedFusedSeg's peer form, bitwise the same rows).
 
-    def __init__(self, targets, d_in: int, d_out: int, peer=None):
+    balance (round 6): spread each row's pairs over every wave slot its workgroup gives the row
+    instead of one wave per relation.  A relation segment of config S runs 7 to 81 pairs, and a
+    workgroup waits for its slowest wave.  Layer 1 deals each group's pairs (its relations back
+    to back: every pair gathers one row of the stacked operand) in contiguous slices over the
+    group's waves, waves given to groups by their pairs; the reassociated layer 2 keeps one
+    relation per wave (its W slab) and gives the spare slots to the longest segments.  The kernel
+    and its finishing roles are unchanged — a group's normalising wave sums its waves' rows in
+    order — so only the fp32 summation order within a group differs from the per-relation form."""
+
+    def __init__(self, targets, d_in: int, d_out: int, peer=None, balance: bool = False):
         super().__init__(targets, d_in, d_out, peer=peer)
         specs = self._keep[0]
         if not _tab_shape(d_in, d_out, specs):
             raise ValueError("dg_gcn_fused_tab_f32: d_in = d_out = 64, or 64 -> 32 with weight stacks")
+        proj = d_out != d_in
         waves_t = [sum(s.n_rels for s in gs) for _, _, gs, _ in targets]
         nw = max([1] + waves_t)
         stride = 8 if nw <= 8 else 16
+        if balance:
+            nw = stride  # every wave slot of a workgroup takes a share of its rows' pairs
+        self.balance = balance
         plan = []  # (target, first row, rows per workgroup) per workgroup, in launch order
         for t, (_, n_rows, _, _) in enumerate(targets):
             rpb = min(nw // waves_t[t], 4)
             plan += [(t, r0, rpb) for r0 in range(0, n_rows, rpb)]
-        tb = _WaveTable(specs, len(plan) * stride, d_out != d_in)
+        tb = _WaveTable(specs, len(plan) * stride, proj)
         g_first = np.cumsum([0] + [len(gs) for _, _, gs, _ in targets])
         for b, (t, r0, rpb) in enumerate(plan):
             out, n_rows, gspecs, relu = targets[t]
             gc = len(gspecs)
             nr = [s.n_rels for s in gspecs]
+            per_row = nw // rpb if balance else waves_t[t]  # wave slots of one row
+            counts = [[1] * gc for _ in range(rpb)]  # waves per group, per row slot
+            for slot in range(rpb):
+                r = r0 + slot
+                if r >= n_rows:
+                    continue
+                gs = [int(g_first[t]) + gl for gl in range(gc)]
+                if balance:
+                    waves = _balanced_waves(tb, gs, nr, r, per_row, proj)
+                else:  # one wave per relation, groups in order
+                    waves = [[[(k, 0, None)] for k in range(nr[gl])] for gl in range(gc)]
+                counts[slot] = [len(wg) for wg in waves]
+                w = slot * per_row
+                for gl, wg in enumerate(waves):
+                    for pieces in wg:
+                        tb.wave(b * stride + w, gs[gl], r,
+                                [(k, a, e if e is not None else tb.seg_len(gs[gl], k, r)) for k, a, e in pieces])
+                        w += 1
             for w in range(nw):
                 i = b * stride + w
-                slot, wi = divmod(w, waves_t[t])
-                r = r0 + slot
-                if slot < rpb and r < n_rows:
-                    gl = 0
-                    while wi >= nr[gl]:
-                        wi -= nr[gl]
-                        gl += 1
-                    tb.relation(i, g_first[t] + gl, wi, r)
                 if w < rpb * gc:
                     s2, gg = divmod(w, gc)
-                    gb = s2 * waves_t[t] + sum(nr[:gg])
-                    tb.desc["role"][i] = (1 << 31) | ((s2 * DG_MAX_GROUPS_TAB + gg) << 16) | (nr[gg] << 8) | gb
+                    gb = s2 * per_row + sum(counts[s2][:gg])
+                    tb.desc["role"][i] = ((1 << 31) | ((s2 * DG_MAX_GROUPS_TAB + gg) << 16) | (counts[s2][gg] << 8)
+                                          | gb)
                 if w < rpb and r0 + w < n_rows:
                     tb.desc["orow"][i] = out.data_ptr() + (r0 + w) * d_out * 4
                     tb.desc["wr"][i] = gc | ((1 if relu else 0) << 8) | (w << 16)
@@ -461,8 +511,56 @@ class PreparedFusedTab(PreparedFusedSeg):
             check(self._tfn(ctypes.byref(self._tab), self.d_in, self.d_out, _stream_ptr(stream)), self._tname)
 
     def seg_form(self, stream=None) -> None:
-        """The same rows through dg_gcn_fused_seg_f32 (tests: bitwise equal)."""
+        """The same rows through dg_gcn_fused_seg_f32 (tests: bitwise equal unless balanced)."""
         PreparedFusedSeg.__call__(self, stream)
+
+
+def _split_even(n: int, parts: int) -> List[Tuple[int, int]]:
+    """[a, b) slices of n items over `parts` waves, the first n % parts one longer."""
+    q, rem = divmod(n, parts)
+    out, a = [], 0
+    for p in range(parts):
+        e = a + q + (1 if p < rem else 0)
+        out.append((a, e))
+        a = e
+    return out
+
+
+def _balanced_waves(tb: "_WaveTable", gs, nr, r: int, slots: int, proj: bool):
+    """Row r's waves for PreparedFusedTab(balance=True): per group, a list of waves, each a list
+    of pieces (relation k, first pair, end pair) of the relation's segment.  `slots` wave slots
+    in all, at least one per group (per relation with weight stacks); the spare slots go, one at
+    a time, to the job whose share per wave is the largest (ties: the first)."""
+    if proj:  # jobs are relations: a reassociated wave multiplies by one relation's W slab
+        jobs = [(gl, k) for gl in range(len(gs)) for k in range(nr[gl])]
+        sizes = [tb.seg_len(gs[gl], k, r) for gl, k in jobs]
+    else:  # jobs are groups: every pair of a group gathers one row of the stacked operand
+        jobs = [(gl, None) for gl in range(len(gs))]
+        sizes = [sum(tb.seg_len(gs[gl], k, r) for k in range(nr[gl])) for gl in range(len(gs))]
+    if len(jobs) > slots:
+        raise ValueError(f"{len(jobs)} jobs for {slots} wave slots")
+    parts = [1] * len(jobs)
+    for _ in range(slots - len(jobs)):
+        j = max(range(len(jobs)), key=lambda x: (-(-sizes[x] // parts[x]), -x))
+        if sizes[j] <= parts[j]:
+            break  # no job left with more than one pair per wave
+        parts[j] += 1
+    waves = [[] for _ in gs]
+    for (gl, k), n, p in zip(jobs, sizes, parts):
+        if k is not None:
+            waves[gl] += [[(k, a, e)] for a, e in _split_even(n, p)]
+            continue
+        # a group: its relations' segments back to back, cut into p contiguous slices
+        lens = [tb.seg_len(gs[gl], kk, r) for kk in range(nr[gl])]
+        starts = np.cumsum([0] + lens)
+        for a, e in _split_even(n, p):
+            pieces = []
+            for kk in range(nr[gl]):
+                lo, hi = max(a, starts[kk]), min(e, starts[kk + 1])
+                if lo < hi:
+                    pieces.append((kk, int(lo - starts[kk]), int(hi - starts[kk])))
+            waves[gl].append(pieces)
+    return waves
 
 
 class PreparedSegTab(PreparedSeg):
@@ -746,18 +844,47 @@ def spmm_groups(specs: Sequence[RelGroupSpec], d: int, stream=None) -> None:
 
 
 def spmm_csr(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x: torch.Tensor,
-             n_rows: int, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-    """Y = A·X for one CSR relation (tf.sparse_tensor_dense_matmul, layers.py:90): a plain
-    CSR is the merged layout with one chunk and vcol = col."""
+             n_rows: int, out: Optional[torch.Tensor] = None, stream=None, beta: float = 0.0) -> torch.Tensor:
+    """Y = A·X + beta·Y for one CSR relation (tf.sparse_tensor_dense_matmul, layers.py:90, :114),
+    through dg_spmm_csr_f32.  beta = 1 adds the relation's product into a running sum (tf.add_n
+    of layers.py:92 one relation at a time); beta = 0 overwrites out without reading it."""
     if x.dim() != 2:
         raise ValueError("x must be 2-D")
+    if not np.isfinite(beta):
+        raise ValueError("beta must be finite")
     x = x.contiguous()
     n_cols, d = x.shape
     if out is None:
+        if beta != 0.0:
+            raise ValueError("beta != 0 needs out (the running sum)")
         out = torch.empty((n_rows, d), device=x.device, dtype=torch.float32)
     vmax = int(col.max()) if col.numel() else -1
     spec = RelGroupSpec(rowptr, col, val, x, out, n_rows, 1, d, n_cols, vcol_max=vmax)
-    PreparedSpmm([spec], d)(stream)
+    spec.validate(d)
+    if out.dim() != 2 or out.shape[0] < n_rows or out.shape[1] != d:
+        raise ValueError("out must be [n_rows, d]")
+    check(_lib.load().dg_spmm_csr_f32(rowptr.data_ptr(), col.data_ptr(), val.data_ptr(), n_rows, n_cols,
+                                      x.data_ptr(), d, out.data_ptr(), d, d, ctypes.c_float(beta),
+                                      _stream_ptr(stream)), "dg_spmm_csr_f32")
+    return out
+
+
+def rownorm_l2(x: torch.Tensor, out: Optional[torch.Tensor] = None, relu: bool = False,
+               stream=None) -> torch.Tensor:
+    """tf.nn.l2_normalize(x, dim=1) (layers.py:93, :117), then relu if asked (model.py:75), through
+    dg_rownorm_l2_f32.  out may be x (in place)."""
+    _dev(x, torch.float32, "x")
+    if x.dim() != 2:
+        raise ValueError("x must be 2-D")
+    n_rows, d = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    _dev(out, torch.float32, "out")
+    if out.shape != x.shape:
+        raise ValueError("out must have x's shape")
+    flags = _lib.DG_EPI_RELU if relu else 0
+    check(_lib.load().dg_rownorm_l2_f32(x.data_ptr(), out.data_ptr(), n_rows, d, flags, _stream_ptr(stream)),
+          "dg_rownorm_l2_f32")
     return out
 
 

@@ -183,14 +183,54 @@ class PeerExchange:
         torch.cuda.synchronize(self.region.device)
         return int(self.state[_lib.DG_PEER_ERROR_WORD].item())
 
+    def flags_now(self) -> List[int]:
+        """This rank's flag block as it stands now ([DG_PEER_SLOTS][DG_PEER_MAX] words; device
+        synchronised first)."""
+        torch.cuda.synchronize(self.region.device)
+        n = _lib.DG_PEER_SLOTS * _lib.DG_PEER_MAX
+        buf = (ctypes.c_uint32 * n)()
+        check(self.lib.dg_peer_read(self._flags, buf, 4 * n), "dg_peer_read")
+        return list(buf)
+
+    def diagnostics(self) -> dict:
+        """The device's wait records (decagon_hip.h, DG_PEER_DIAG_BASE): the slow completed
+        waits (count, longest in µs) and, after a timeout, the timed-out wait — its slot, the
+        epoch it expected, each source's flag word when it gave up and NOW, and the verdict per
+        late source: "late" (its flag reached the expected epoch after the bound: a host or
+        scheduling skew longer than the bound) or "never raised" (still short of it)."""
+        st = [int(x) & 0xffffffff for x in self.state.cpu().tolist()]
+        b = _lib.DG_PEER_DIAG_BASE
+        out = {"slow_waits": st[b + 16], "slowest_wait_us": st[b + 17] / _TICKS_PER_S * 1e6,
+               "error_word": st[_lib.DG_PEER_ERROR_WORD]}
+        if not out["error_word"]:
+            return out
+        slot, want = st[b], st[b + 1]
+        seen = st[b + 2:b + 2 + self.world]
+        tick = lambda lo: (st[b + lo] | (st[b + lo + 1] << 32))  # noqa: E731
+        now = self.flags_now()[slot * _lib.DG_PEER_MAX:slot * _lib.DG_PEER_MAX + self.world]
+        late = {}
+        for s_, (v, w) in enumerate(zip(seen, now)):
+            if ((v - want) & 0xffffffff) >= 0x80000000:  # short of the expected epoch at the bound
+                late[s_] = "late" if ((w - want) & 0xffffffff) < 0x80000000 else "never raised"
+        out.update({"slot": slot, "expected_epoch": want, "flags_at_bound": seen, "flags_now": now,
+                    "waited_us": (tick(12) - tick(10)) / _TICKS_PER_S * 1e6,
+                    "raised_to_wait_us": (tick(10) - tick(14)) / _TICKS_PER_S * 1e6,
+                    "wait_start_tick": tick(10), "late_sources": late})
+        return out
+
     def check(self) -> None:
         """Raise if any wait so far timed out (synchronises the device).  A timed-out wait
         poisons the exchange on the device (csrc/peer.h: this rank then raises no flag and
         waits for none, so every peer's next wait times out too); here it poisons the host
-        side: every later ensure_ok() — ForwardPlan.run's entry — raises as well."""
+        side: every later ensure_ok() — ForwardPlan.run's entry — raises as well.  The message
+        carries the wait record (diagnostics()): which sources were late or never arrived."""
         e = self.error()
         if e:
             self.failed = e
+            try:
+                self.failed_diag = self.diagnostics()
+            except Exception as exc:  # the record is an aid; the error stands without it
+                self.failed_diag = {"unreadable": repr(exc)}
         self.ensure_ok()
 
     def ensure_ok(self) -> None:
@@ -198,7 +238,8 @@ class PeerExchange:
         e = self.failed
         if e:
             raise RuntimeError(f"peer exchange timed out: slot {(e >> 8) & 0xff}, waiting for rank {e & 0xff} "
-                               f"(error word {e:#x}); the exchange is poisoned, rebuild the plan")
+                               f"(error word {e:#x}); the exchange is poisoned, rebuild the plan; "
+                               f"wait record: {getattr(self, 'failed_diag', None)}")
 
     def close(self) -> None:
         """Unmap the peers' regions and free the flag block (after the last exchange)."""

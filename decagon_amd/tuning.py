@@ -19,11 +19,14 @@ T = TypeVar("T", bool, int, float, str)
 
 # name -> (default, last value read)
 _READ: Dict[str, Tuple[Union[bool, int, float, str], Union[bool, int, float, str]]] = {}
+_FALSE = frozenset({"0", "false", "no", "off"})
+_TRUE = frozenset({"1", "true", "yes", "on"})
 
 
 def knob(name: str, default: T) -> T:
-    """The value of DG_* variable `name` (its type is `default`'s; a bool knob is false for
-    "0" and true otherwise), or `default` when unset.  Read at the call, so a knob consulted
+    """The value of DG_* variable `name` (its type is `default`'s; a bool knob takes
+    0/false/no/off or 1/true/yes/on, case-insensitive, and raises ValueError on anything else),
+    or `default` when unset.  Read at the call, so a knob consulted
     per plan follows the environment of that moment (tests set them with monkeypatch)."""
     if not name.startswith("DG_"):
         raise ValueError(f"tuning knobs are DG_* variables, got {name!r}")
@@ -31,7 +34,13 @@ def knob(name: str, default: T) -> T:
     if raw is None:
         val = default
     elif isinstance(default, bool):
-        val = raw != "0"
+        low = raw.strip().lower()
+        if low in _FALSE:
+            val = False
+        elif low in _TRUE:
+            val = True
+        else:
+            raise ValueError(f"{name}={raw!r}: a switch takes one of {sorted(_FALSE | _TRUE)}")
     else:
         val = type(default)(raw)
     _READ[name] = (default, val)

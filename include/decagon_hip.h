@@ -116,11 +116,24 @@ int dg_spmm_groups_f32(const dg_rel_group* groups /* HOST array */, int32_t n_gr
 int dg_spmm_groups_lds_f32(const dg_rel_group* groups /* HOST array */, int32_t n_groups, int32_t d,
                            void* stream);
 
-/* Single relation, plain CSR: Y[r][:] = sum_p val[p] * X[col[p]][:] (Y dense, ld = ldy).
- * Replaces one tf.sparse_tensor_dense_matmul (layers.py:90).  ldy must equal d. */
+/* Single relation, plain CSR: Y[r][:] = sum_p val[p] * X[col[p]][:] + beta * Y[r][:]
+ * (Y dense, ld = ldy; fmaf(beta, Y, sum) per element).  beta == 0 writes Y without reading it
+ * (no NaN carried over from uninitialised memory); beta == 1 accumulates one relation's product
+ * into a running sum — tf.add_n over the per-relation products (layers.py:92, :116) done one
+ * relation at a time.  Replaces one tf.sparse_tensor_dense_matmul (layers.py:90, :114).  ldy
+ * must equal d; beta must be finite (ABI 37: beta added). */
 int dg_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                     int32_t n_rows, int32_t n_cols, const float* x, int64_t ldx, float* y,
-                    int64_t ldy, int32_t d, void* stream);
+                    int64_t ldy, int32_t d, float beta, void* stream);
+
+/* Row-wise L2 normalisation, stand-alone (ABI 37):
+ *     y[r] = x[r] * rsqrt(max(sum_c x[r][c]^2, 1e-12))          (tf.nn.l2_normalize(x, dim=1))
+ * then relu if flags == DG_EPI_RELU (model.py:75).  x, y: [n_rows][d], contiguous, 16-byte
+ * aligned; y == x is allowed (each row is read whole before it is written).  Replaces
+ * layers.py:93 / :117 when the sum was formed elsewhere (dg_spmm_csr_f32 with beta = 1); the
+ * layer kernels fuse the same arithmetic into their epilogues (dg_gcn_epilogue_f32 with one
+ * group of one chunk runs it: bitwise the same rows). */
+int dg_rownorm_l2_f32(const float* x, float* y, int32_t n_rows, int32_t d, int32_t flags, void* stream);
 
 /* --------------------------------------------------------------------------------------
  * Fused GCN layer (T3 + T4 + T5 + T6, optionally T7 of the next layer, in one launch) for
@@ -448,6 +461,18 @@ int dg_gcn_epilogue_tab_f32(const dg_epi_row_desc* rows, int32_t n_rows, int32_t
 #define DG_PEER_SUB_STRIDE 16
 #define DG_PEER_STATE_WORDS (DG_PEER_SUB_BASE + DG_PEER_SLOTS * 8 * DG_PEER_SUB_STRIDE)
 #define DG_PEER_ERROR_WORD (2 * DG_PEER_SLOTS)
+/* Wait records (round 6), in the state words between the error word and the sub-counters.
+ * The wait that times out writes, before the error word: DIAG+0 its slot, +1 the epoch it
+ * expected, +2..+9 the flag word it last read from each source, +10/+11 the s_memrealtime tick
+ * its wait started (low / high word), +12/+13 the tick it gave up, +14/+15 the tick this rank
+ * raised its own flags.  Every wait that completes after more than DG_PEER_SLOW_TICKS adds 1 to
+ * +16 and max-updates +17 with its ticks (a completed wait costs one compare otherwise).  A
+ * host that finds the error word reads these and, with dg_peer_read, the flag words as they
+ * stand now: a late source's flag that has since reached the expected epoch was late (a host or
+ * scheduling skew longer than the bound); one still short of it was never raised. */
+#define DG_PEER_DIAG_BASE 24
+#define DG_PEER_DIAG_WORDS 18
+#define DG_PEER_SLOW_TICKS 10000 /* 100 µs */
 #define DG_IPC_HANDLE_BYTES 64
 #define DG_EPI_PUSH 1           /* dg_epi_target.target_flags: push this target's rows          */
 
@@ -474,6 +499,9 @@ int dg_peer_free(void* ptr);
 int dg_ipc_get_handle(void* ptr, void* handle /* HOST out */, int64_t* offset /* HOST out */);
 int dg_ipc_open(const void* handle /* HOST */, void** ptr /* HOST out */);
 int dg_ipc_close(void* ptr);
+/* Synchronous copy of `bytes` of device memory (a flag block) to the host: the timeout record's
+ * "flag words now" read (decagon_amd/peer.py PeerExchange.diagnostics). */
+int dg_peer_read(const void* device, void* host /* HOST out */, int64_t bytes);
 
 /* Stand-alone exchange: push bytes [offsets[s], offsets[s] + sizes[s]) of this rank's region
  * (its blocks) into every peer's region at the same offsets, then raise / wait as above. */

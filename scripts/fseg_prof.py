@@ -58,7 +58,12 @@ def main():
         for _ in range(3):
             g.replay()
         stream.synchronize()
-    out = {"steps_per_graph": steps, "launches": {}}
+    from decagon_amd import kernels
+    forms = sorted({type(l).__name__ for L in plan.spmm_launches for l in L})
+    out = {"steps_per_graph": steps, "launch_forms": forms,
+           "note": "the table form (PreparedFusedTab = gcn_tab_kernel) has no search or bounds phase: "
+                   "'search' is its first round trip (descriptor + first 64 pairs), 'bounds' is 0",
+           "launches": {}}
     bufs = {}
     for proj in (0, 1):
         buf = np.zeros((4096, 16, 8), np.uint64)

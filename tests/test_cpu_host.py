@@ -78,7 +78,8 @@ def test_integration_doc_matches_abi():
     stated = {int(x) for x in re.findall(r"`dg_abi_version\(\)` returns (\d+)", doc)}
     asserted = {int(x) for x in re.findall(r"dg_abi_version\(\) == (\d+)", doc)}
     assert stated == {_lib.ABI_VERSION} and asserted == {_lib.ABI_VERSION}, (stated, asserted)
-    names = {"c_void_p": ctypes.c_void_p, "c_int32": ctypes.c_int32, "c_int64": ctypes.c_int64}
+    names = {"c_void_p": ctypes.c_void_p, "c_int32": ctypes.c_int32, "c_int64": ctypes.c_int64,
+             "c_float": ctypes.c_float}
     stubs = re.findall(r"_lib\.(dg_\w+)\.argtypes = \[([^\]]*)\]", doc, re.S)
     assert len(stubs) >= 2
     for fn, body in stubs:
@@ -113,6 +114,15 @@ def test_abi_rejects_bad_arguments_without_a_device():
     t = (_lib.DgEpiTarget * 1)()
     assert lib.dg_gcn_epilogue_peer_f32(t, 1, 64, 1, None, None) == _lib.DG_EINVAL
     assert lib.dg_decoder_score_bf16_paired(*([None, 256, 0, None, 256, 0] + [None] * 3 + [1, None, None, 256, None, None])) == _lib.DG_EINVAL
+    # ABI 37: dg_spmm_csr_f32's beta must be finite; dg_rownorm_l2_f32 takes relu only, d % 4 == 0
+    f = ctypes.c_float
+    assert lib.dg_spmm_csr_f32(16, 16, 16, 10, 10, 16, 64, 16, 64, 64, f(float("nan")), None) == _lib.DG_EINVAL
+    assert lib.dg_spmm_csr_f32(16, 16, 16, 10, 10, 16, 64, 16, 64, 64, f(float("inf")), None) == _lib.DG_EINVAL
+    assert lib.dg_spmm_csr_f32(16, 16, 16, 10, 10, 16, 64, 16, 32, 64, f(0.0), None) == _lib.DG_EINVAL  # ldy != d
+    assert lib.dg_spmm_csr_f32(16, 16, 16, 0, 10, 16, 64, 16, 64, 64, f(1.0), None) == _lib.DG_OK  # no rows
+    assert lib.dg_rownorm_l2_f32(16, 16, 10, 64, _lib.DG_EPI_L2NORM, None) == _lib.DG_EINVAL
+    assert lib.dg_rownorm_l2_f32(16, 16, 10, 62, 0, None) == _lib.DG_EINVAL
+    assert lib.dg_rownorm_l2_f32(None, None, 0, 64, 0, None) == _lib.DG_OK
 
 
 def test_merge_chunks_layout():
@@ -431,3 +441,63 @@ def test_dg_environment_reads_go_through_tuning(monkeypatch):
     assert tuning.knob("DG_STAGED", True) is False
     monkeypatch.delenv("DG_WINDOWS")
     assert tuning.knob("DG_WINDOWS", 2) == 2 and "DG_WINDOWS" not in tuning.overrides()
+
+
+@pytest.mark.parametrize("raw,want", [("0", False), ("false", False), ("No", False), ("OFF", False),
+                                      ("1", True), ("true", True), ("YES", True), ("on", True)])
+def test_bool_knobs_parse_strictly(monkeypatch, raw, want):
+    """A switch takes 0/false/no/off or 1/true/yes/on (DG_WAVE_TABLE=false used to
+    leave the feature on and go unreported); the parsed value is what overrides() reports."""
+    from decagon_amd import tuning
+
+    monkeypatch.setenv("DG_WAVE_TABLE", raw)
+    assert tuning.knob("DG_WAVE_TABLE", not want) is want
+    assert tuning.overrides().get("DG_WAVE_TABLE") is want
+
+
+def test_bool_knob_rejects_other_values(monkeypatch):
+    from decagon_amd import tuning
+
+    for raw in ("2", "enable", ""):
+        monkeypatch.setenv("DG_STAGED", raw)
+        with pytest.raises(ValueError):
+            tuning.knob("DG_STAGED", True)
+
+
+@pytest.mark.parametrize("proj", [False, True])
+def test_balanced_wave_dealing_covers_every_pair_once(proj):
+    """PreparedFusedTab(balance=True)'s host dealing (kernels._balanced_waves): every pair of every
+    relation lands in exactly one wave, in relation order within a group; a reassociated wave
+    (proj) holds one relation only; the waves fit the row's slots and the longest share shrinks."""
+    from decagon_amd.kernels import _balanced_waves
+
+    rng = np.random.default_rng(5)
+    for trial in range(50):
+        n_groups = int(rng.integers(1, 4))
+        nr = [int(rng.integers(1, 4)) for _ in range(n_groups)]
+        lens = {(g, k): int(rng.choice([0, 3, 7, 40, 81, 130])) for g in range(n_groups) for k in range(nr[g])}
+
+        class TB:
+            def seg_len(self, g, k, r):
+                return lens[g, k]
+
+        slots = sum(nr) + int(rng.integers(0, 6))
+        waves = _balanced_waves(TB(), list(range(n_groups)), nr, 0, slots, proj)
+        assert len(waves) == n_groups and sum(len(w) for w in waves) <= slots
+        for g in range(n_groups):
+            assert waves[g], "at least one wave a group"
+            got = [(k, a, e) for w in waves[g] for (k, a, e) in w]
+            if proj:
+                assert all(len({k for k, _, _ in w}) <= 1 for w in waves[g])
+            # the pieces, in wave order, tile each relation's segment from 0 to its end
+            for k in range(nr[g]):
+                pk = [(a, e) for kk, a, e in got if kk == k]
+                pos = 0
+                for a, e in pk:
+                    assert a == pos and (e > a or lens[g, k] == 0)
+                    pos = e
+                assert pos == lens[g, k]
+            assert [k for k, _, _ in got] == sorted(k for k, _, _ in got)
+        longest = max(sum(e - a for _, a, e in w) for wg in waves for w in wg)
+        assert longest <= max(lens.values()) if proj else longest <= max(
+            sum(lens[g, k] for k in range(nr[g])) for g in range(n_groups))

@@ -10,7 +10,7 @@ The negatives are read back from the device: each slot's are exactly the restate
 of THAT slot's degree^0.75 table (fixed_unigram_candidate_sampler over degrees[i][k],
 optimizer.py:38-47), their pooled counts match the slots' distributions, and they do not
 depend on how the slots are sharded: the 2-rank slot-sharded run (gloo on the one GPU, loss
-all-reduced) reproduces the one-rank draws and scores bit for bit.
+all-reduced) at 2 and 8 ranks reproduces the one-rank draws and scores bit for bit.
 """
 import numpy as np
 import pytest
@@ -103,7 +103,11 @@ def _rank(rank, world):
     return s0, s1, sc.neg_rows.cpu().numpy(), sc.out.cpu().numpy(), float(sc.loss[0])
 
 
-def test_config5_slot_sharded_two_ranks_equal_one_rank():
+@pytest.mark.parametrize("world", [2, 8])
+def test_config5_slot_sharded_ranks_equal_one_rank(world):
+    """north_star configs[4] at 8 GPUs: the 1,928 slots dealt in contiguous blocks over `world`
+    gloo ranks (sharing the one GPU), each rank's draws and scores bit for bit the one-rank
+    run's, the blocks covering every slot once, the loss all-reduced to the one-rank sum."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     c5, sc = _scorer(torch.device("cuda"))
@@ -112,7 +116,10 @@ def test_config5_slot_sharded_two_ranks_equal_one_rank():
     B = c5.batch
     full_neg, full_pos, full_negs = sc.neg_rows.cpu().numpy(), sc.pos.cpu().numpy(), sc.neg.cpu().numpy()
     full_loss = float(sc.loss[0])
-    got = run_ranks(_rank, 2).values()
+    got = list(run_ranks(_rank, world).values())
+    assert sorted((s0, s1) for s0, s1, *_ in got) == [(a, b) for a, b in zip(
+        sorted(x[0] for x in got), sorted(x[0] for x in got)[1:] + [1928])]  # contiguous, no gap
+    assert min(x[0] for x in got) == 0 and max(x[1] for x in got) == 1928
     for s0, s1, negr, out, loss in got:
         m = (s1 - s0) * B
         assert np.array_equal(negr, full_neg[s0 * B:s1 * B])

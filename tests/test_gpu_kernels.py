@@ -80,6 +80,60 @@ def test_spmm_empty_matrix(K):
     assert torch.count_nonzero(y) == 0
 
 
+@pytest.mark.parametrize("d", [32, 64])
+def test_spmm_csr_beta_accumulates_add_n(K, d):
+    """dg_spmm_csr_f32's beta: beta = 1 adds each relation's Â_k·X_k into a running
+    sum — tf.add_n of layers.py:92 one relation at a time — bit for bit fmaf(1, Y, Â_k·X_k);
+    beta = 0 overwrites a NaN-filled out without reading it; beta = 0.5 scales the old sum."""
+    rng = np.random.default_rng(40 + d)
+    mats = [_rand_csr(rng, 203, 150, 0.06, empty_rows=0.1) for _ in range(3)]
+    xs = [rng.standard_normal((150, d)).astype(np.float32) for _ in mats]
+    out = torch.full((203, d), float("nan"), device="cuda")
+    parts = []
+    for k, (m, x) in enumerate(zip(mats, xs)):
+        rp, cl, vl, _ = _dev_csr(m)
+        xd = torch.from_numpy(x).cuda()
+        parts.append(K.spmm_csr(rp, cl, vl, xd, 203))
+        K.spmm_csr(rp, cl, vl, xd, 203, out=out, beta=0.0 if k == 0 else 1.0)
+    # add_n order: ((P0 + P1) + P2), each add one fp32 rounding — what fmaf(1, y, p) gives
+    assert torch.equal(out, (parts[0] + parts[1]) + parts[2])
+    want = sum(orc.sparse_dense_matmul((np.stack(m.nonzero(), 1), m.data, m.shape), x.astype(np.float64))
+               for m, x in zip(mats, xs))
+    assert rel_err(out.cpu().numpy(), want) <= 1e-5
+    rp, cl, vl, _ = _dev_csr(mats[0])
+    old = out.clone()
+    K.spmm_csr(rp, cl, vl, torch.from_numpy(xs[0]).cuda(), 203, out=out, beta=0.5)
+    want_half = torch.addcmul(parts[0], old, torch.full_like(old, 0.5))  # fmaf(0.5, old, p): exact scale
+    assert torch.allclose(out, want_half, rtol=1e-6, atol=1e-6)
+    with pytest.raises(ValueError):
+        K.spmm_csr(rp, cl, vl, torch.from_numpy(xs[0]).cuda(), 203, beta=1.0)  # no running sum given
+
+
+@pytest.mark.parametrize("d", [8, 32, 64, 256])
+@pytest.mark.parametrize("relu", [False, True])
+def test_rownorm_l2_matches_oracle(K, d, relu):
+    """dg_rownorm_l2_f32 against oracle.l2_normalize_rows (TF 1.8: x·rsqrt(max(Σx², 1e-12)),
+    layers.py:93, :117), including all-zero rows (which stay 0), in place and out of place, and
+    bit for bit the fused epilogue's normalisation of the same rows."""
+    rng = np.random.default_rng(7 * d + relu)
+    x = rng.standard_normal((517, d)).astype(np.float32)
+    x[rng.random(517) < 0.1] = 0.0
+    x[3] *= 1e-7  # tiny but nonzero: Σx² below the 1e-12 floor
+    xd = torch.from_numpy(x).cuda()
+    y = K.rownorm_l2(xd, relu=relu)
+    want = orc.l2_normalize_rows(x.astype(np.float64))
+    if relu:
+        want = np.maximum(want, 0.0)
+    assert rel_err(y.cpu().numpy(), want) <= 1e-5
+    assert np.all(y.cpu().numpy()[~x.any(axis=1)] == 0)
+    ref = torch.empty_like(xd)
+    K.PreparedEpilogue([(xd, 1)], ref, 517, d, 1 | (2 if relu else 0))()
+    assert torch.equal(y, ref)
+    z = xd.clone()
+    K.rownorm_l2(z, out=z, relu=relu)
+    assert torch.equal(z, y)
+
+
 @pytest.mark.parametrize("chunk", [1, 2, 3, 7])
 @pytest.mark.parametrize("d", [32, 64])
 def test_spmm_groups_chunks_and_slabs(K, chunk, d):

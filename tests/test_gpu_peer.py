@@ -208,6 +208,7 @@ def _forward_rank(rank, world, kind, mode):
     ref.run()
     torch.cuda.synchronize()
     base = _grab(ref)
+    info["waits"] = plan.peer.diagnostics()  # slow waits (> 100 µs): count and the longest
     state = plan.peer.state.cpu().numpy().tolist()
     dist.barrier()
     plan.peer.close()
@@ -232,6 +233,15 @@ def _oracle(kind, g):
 def test_peer_exchange_forward_matches_oracle(kind, world, mode):
     _need_gpu()
     got = run_ranks(_forward_rank, world, (kind, mode))
+    # the waits' evidence for the bounds: slow waits (> 100 µs) and the longest, per
+    # rank, appended to $PEER_WAIT_LOG when set (scripts: the GPU call's record)
+    import json
+    import os
+
+    if os.environ.get("PEER_WAIT_LOG"):
+        with open(os.environ["PEER_WAIT_LOG"], "a") as f:
+            f.write(json.dumps({"case": f"{kind}-{world}-{mode}",
+                                "waits": [got[r][0]["waits"] for r in range(world)]}) + "\n")
     g = _graph(kind, world)
     h1, emb = _oracle(kind, g)
     for r in range(world):
@@ -246,6 +256,7 @@ def test_peer_exchange_forward_matches_oracle(kind, world, mode):
             assert all(info["gather_all"]), info
         if kind == "S" and world == 2:  # one launch per layer: the wave-table fused form
             assert "PreparedFusedTab" in info["fused_kinds"], info
+        assert info["waits"]["error_word"] == 0, info["waits"]
         for form in outs:
             for t in (0, 1):
                 assert rel_err(form[0][t], h1[t]) <= TOL, (r, "hidden1", t)
@@ -322,12 +333,25 @@ def test_peer_wait_times_out_and_fails_fast():
     assert err == 0x10000 | (3 << 8) | 1, hex(err)
     assert 0.15 <= t1 - t0 <= 5.0, t1 - t0
     assert int(ex.state[2 * 3 + 1]) == 1  # slot 3's epoch: one exchange (timed out) so far
+    # the wait record: slot 3, epoch 1 expected, this rank's own flag raised, rank 1's never
+    diag = ex.diagnostics()
+    assert diag["slot"] == 3 and diag["expected_epoch"] == 1, diag
+    assert diag["flags_at_bound"][0] == 1 and diag["flags_at_bound"][1] == 0, diag
+    assert diag["late_sources"] == {1: "never raised"}, diag
+    assert 150e3 <= diag["waited_us"] <= 5e6 and 0 <= diag["raised_to_wait_us"] < 1e5, diag
+    # rank 1's flag lands after the bound (written here from the host): the record now reads "late"
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    one = ctypes.c_uint32(1)
+    dst = ctypes.c_void_p(ex._flags + 4 * (3 * _lib.DG_PEER_MAX + 1))
+    assert hip.hipMemcpy(dst, ctypes.byref(one), ctypes.c_size_t(4), ctypes.c_int(1)) == 0  # host -> device
+    assert ex.diagnostics()["late_sources"] == {1: "late"}
     fn()
     torch.cuda.synchronize()
     assert time.perf_counter() - t1 < 0.15  # fails fast once the error word is set
     assert int(ex.state[_lib.DG_PEER_ERROR_WORD]) == err
     assert int(ex.state[2 * 3 + 1]) == 1  # poisoned: no flag raised, no epoch advanced
-    with pytest.raises(RuntimeError, match="timed out"):
+    with pytest.raises(RuntimeError, match="timed out.*late_sources"):
         ex.check()
     with pytest.raises(RuntimeError, match="poisoned"):
         ex.ensure_ok()
