@@ -132,7 +132,10 @@ def peer_config(exchange, loopback=False):
     from decagon_amd.peer import PeerConfig, dist_gather
 
     mode = "fused" if exchange == "peer" else "kernel"
-    return PeerConfig(mode=mode, loopback=True) if loopback else PeerConfig(mode=mode, gather=dist_gather())
+    kind = knob("DG_PEER_REGION_KIND", 2)  # the exchange region's memory kind (2: uncached)
+    if loopback:
+        return PeerConfig(mode=mode, loopback=True, region_kind=kind)
+    return PeerConfig(mode=mode, gather=dist_gather(), region_kind=kind)
 
 
 def build_workload(config, rank, world, sharded, backend="nccl", exchange="rccl"):

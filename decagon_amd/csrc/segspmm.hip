@@ -475,9 +475,9 @@ static_assert(sizeof(dg_tab_desc) == 64, "dg_tab_desc: one s_load_dwordx16");
 // ovf: later batches, 64 entries each.  (Separate pointer arguments: loaded together.)
 // A wave's relation sum from its wave-table slot (the first pairs already in `first`): batches
 // of 64 pairs, the first from the slot, the rest from ovf, each prefetched before the batch
-// before it is gathered; U gathers in flight per lane.  PROJ: ds_bpermute hand-out (pair p in
-// lane p) and the 64-wide aggregate times the relation's W slab (seg_wave_proj's arithmetic);
-// else DPP row broadcasts (seg_gather's: pair m·G + sub of a batch in lane 16·sub + m).
+// before it is gathered; U gathers in flight per lane, the pairs handed out by DPP row
+// broadcasts (seg_gather's: pair m·G + sub of a batch in lane 16·sub + m).  PROJ: then the
+// 64-wide aggregate times the relation's W slab (seg_wave_proj's arithmetic).
 template <bool PROJ, int U>
 __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 first, const uint2* __restrict__ ovf,
                                            float4* ybuf) {
@@ -499,7 +499,6 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
             const int n = min(64, D.cnt - base);
             const int eoff = vc * D.x_ld;
             const int vbits = vb;
-            const float v = __int_as_float(vb);
             vc = 0;
             vb = 0;
             if (base + 64 < D.cnt) {
@@ -508,52 +507,31 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
                 vb = (int)q.y;
                 nx += 64;
             }
-            if constexpr (PROJ) {
-                // ds_bpermute hand-out (the seg form's seg_gather_shfl), pair p in lane p
-#pragma unroll 1
-                for (int s0 = 0; s0 < n; s0 += U * G) {
-                    int o[U];
-                    float w[U];
+            // DPP row broadcasts (the seg form's seg_gather): pair m·G + sub of the batch sits in
+            // lane 16·sub + m.  Round 6: layer 2 (PROJ) too — since its W slice is read after the
+            // gathers the unrolled broadcasts' registers fit (46 → 46 VGPRs), and its launch
+            // measured 5.64–5.72 → 5.33–5.48 µs against the ds_bpermute hand-out (same pair order
+            // per lane group: the same bits).
+            constexpr int S = dg::kWave / G;
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int src = (s0 + u * G + sub) & 63;
-                        o[u] = __shfl(eoff, src);
-                        w[u] = __shfl(v, src);
-                    }
-                    float4 xv[U];
+            for (int it = 0; it < S / U; ++it) {
+                if (it * U * G >= n) break;  // wave-uniform
+                int o[U];
+                float w[U];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const bool ok = s0 + u * G + sub < n;
-                        xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-                        if (!ok) w[u] = 0.f;
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
+                for (int u = 0; u < U; ++u) {
+                    o[u] = row_bcast_rt(eoff, it * U + u);
+                    w[u] = __int_as_float(row_bcast_rt(vbits, it * U + u));
                 }
-            } else {
-                // DPP row broadcasts (the seg form's seg_gather): pair m·G + sub of the batch sits
-                // in lane 16·sub + m
-                                constexpr int S = dg::kWave / G;
+                float4 xv[U];
 #pragma unroll
-                for (int it = 0; it < S / U; ++it) {
-                    if (it * U * G >= n) break;  // wave-uniform
-                    int o[U];
-                    float w[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        o[u] = row_bcast_rt(eoff, it * U + u);
-                        w[u] = __int_as_float(row_bcast_rt(vbits, it * U + u));
-                    }
-                    float4 xv[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const bool ok = (it * U + u) * G + sub < n;
-                        xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-                        if (!ok) w[u] = 0.f;
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
+                for (int u = 0; u < U; ++u) {
+                    const bool ok = (it * U + u) * G + sub < n;
+                    xv[u] = ok ? *reinterpret_cast<const float4*>(xq + o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (!ok) w[u] = 0.f;
                 }
+#pragma unroll
+                for (int u = 0; u < U; ++u) dg::fma4(acc, w[u], xv[u]);
             }
         }
         acc = dg::xor_sum4_from<LP>(acc);
@@ -587,23 +565,40 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
     return res;
 }
 
-// rows[0][q] + rows[1][q] + ... + rows[K-1][q], added in that order (((r0 + r1) + r2) + ...) —
-// bitwise the serial loop `s = rows[0][q]; for (u = 1; u < K; ++u) s += rows[u][q]` — with the
-// LDS reads of each run of 8 rows issued before the first add of the run, instead of one LDS
-// round trip per row (the one-wave relation sum was 0.44 µs median of config S's layer-1 and
-// layer-2 tab launches, profiles/r06_S_tab_phase_profile.json).  Rows past K are not read.
+// v of lane ^ M for any M < 64: the power-of-two partners of M's bits composed (lane ^ a ^ b
+// = lane ^ (a | b) for disjoint bits), each an exact value move (common.h's xor_get)
+template <int M>
+__device__ __forceinline__ float xor_get_any(float x) {
+    if constexpr (M == 0) {
+        return x;
+    } else {
+        constexpr int LOW = M & -M;
+        return xor_get_any<M - LOW>(dg::xor_get<LOW>(x));
+    }
+}
+template <int M>
+__device__ __forceinline__ float4 xor_get4_any(const float4& v) {
+    return make_float4(xor_get_any<M>(v.x), xor_get_any<M>(v.y), xor_get_any<M>(v.z), xor_get_any<M>(v.w));
+}
+// tot += the value of lane set V, V + 1, ... (< n, wave-uniform), in that order; lane set v is
+// lanes [W·v, W·(v+1)), read from lane ^ W·v
+template <int W, int V, int SETS>
+__device__ __forceinline__ void add_lane_sets(float4& tot, const float4& v, int n) {
+    if constexpr (V < SETS) {
+        if (V < n) dg::add4(tot, xor_get4_any<W * V>(v));
+        add_lane_sets<W, V + 1, SETS>(tot, v, n);
+    }
+}
+
+// rows[0][q] + rows[1][q] + ... + rows[K-1][q], added in that order (((r0 + r1) + r2) + ...).
+// (Measured, round 6: the LDS reads of each run of 8 rows issued before the first add — predicated
+// reads and selects — made config S's layer 1 0.2 µs slower than this loop: 4.47-4.56 against
+// 4.29-4.34 µs; scripts/variants/serial_lds_sum.py kept the A/B.)
 template <int W>
 __device__ __forceinline__ float4 lds_ordered_sum(const float4 (*rows)[W], int K, int q) {
     float4 s = rows[0][q];
 #pragma unroll 1
-    for (int u0 = 1; u0 < K; u0 += 8) {
-        float4 z[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) z[j] = rows[u0 + j < K ? u0 + j : 0][q];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (u0 + j < K) dg::add4(s, z[j]);
-    }
+    for (int u = 1; u < K; ++u) dg::add4(s, rows[u][q]);
     return s;
 }
 
@@ -617,7 +612,6 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
     constexpr int DOUT4 = PROJ ? 8 : 16;
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
-    __shared__ float4 nbuf[kFsMaxRpb * DG_MAX_GROUPS][DOUT4];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t wi = (int64_t)blockIdx.x * NW + wave;
@@ -648,32 +642,44 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
     if (lane < DOUT4) zbuf[wave][lane] = res;
     __syncthreads();
     DG_FS_STAMP(4);  // every wave of the workgroup done
-    // one wave per (row slot, group): its relations summed in order, L2-normalised
-    if (D.role >> 31) {
-        const int gb = D.role & 0xff, K = (D.role >> 8) & 0xff, ns = (D.role >> 16) & 0x7fff;
-        const int q = lane % DOUT4;
-        const float4 sum = lds_ordered_sum<DOUT4>(&zbuf[gb], K, q);
+    // Round 6: the row's finishing wave (D.orow) does the rest alone, without a second barrier:
+    // lane set u (lanes [DOUT4·u, DOUT4·(u+1))) sums group u's waves in order and L2-normalises
+    // the sum, then the groups are added in order across the lane sets (lane set 0 reads set v
+    // from lane ^ DOUT4·v), relu'd and stored.  The same adds, butterflies and order as the
+    // per-group normalising waves of round 5 plus the nbuf hand-off: the same bits.
+    // desc.pad[2]: K − 1 of group u in bits 4u .. 4u+3; desc.pad[3]: the row slot's first wave.
+    if (D.orow != nullptr) {
+        constexpr int SETS = 64 / DOUT4;
+        const int gc = D.wr & 0xff;
+        const uint32_t kc = (uint32_t)D.pad[2];
+        const int u = lane / DOUT4, q = lane % DOUT4;
+        int gb = D.pad[3];
+#pragma unroll
+        for (int v = 0; v + 1 < SETS; ++v)
+            if (v < u && v < gc) gb += (int)((kc >> (4 * v)) & 15u) + 1;
+        const bool mine = u < gc;
+        const int K = mine ? (int)((kc >> (4 * u)) & 15u) + 1 : 1;
+        const float4 sum = lds_ordered_sum<DOUT4>(&zbuf[mine ? gb : 0], K, q);
         // tf.nn.l2_normalize: x * rsqrt(max(sum(x^2), 1e-12))
         float ss = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
         ss = dg::xor_sum_below<DOUT4>(ss);
         const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
-        if (lane < DOUT4) nbuf[ns][lane] = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
-    }
-    __syncthreads();
-    DG_FS_STAMP(5);  // groups normalised
-    if (D.orow != nullptr && lane < DOUT4) {
-        const int gc = D.wr & 0xff, s2 = D.wr >> 16;
-        float4 tot = lds_ordered_sum<DOUT4>(&nbuf[s2 * DG_MAX_GROUPS], gc, lane);
-        if ((D.wr >> 8) & 1) {
-            tot.x = fmaxf(tot.x, 0.f);
-            tot.y = fmaxf(tot.y, 0.f);
-            tot.z = fmaxf(tot.z, 0.f);
-            tot.w = fmaxf(tot.w, 0.f);
+        const float4 nv = make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
+        float4 tot = nv;
+        add_lane_sets<DOUT4, 1, SETS>(tot, nv, gc);  // ((n0 + n1) + n2) + ...
+        DG_FS_STAMP(5);  // groups normalised and summed
+        if (lane < DOUT4) {
+            if ((D.wr >> 8) & 1) {
+                tot.x = fmaxf(tot.x, 0.f);
+                tot.y = fmaxf(tot.y, 0.f);
+                tot.z = fmaxf(tot.z, 0.f);
+                tot.w = fmaxf(tot.w, 0.f);
+            }
+            reinterpret_cast<float4*>(D.orow)[lane] = tot;
+            if constexpr (PEER)
+                dg::peer_store4(P, reinterpret_cast<const float*>(reinterpret_cast<const char*>(D.orow) - D.pad[0]),
+                                (uint32_t)D.pad[1], (uint32_t)D.pad[0] + 16u * lane, tot);
         }
-        reinterpret_cast<float4*>(D.orow)[lane] = tot;
-        if constexpr (PEER)
-            dg::peer_store4(P, reinterpret_cast<const float*>(reinterpret_cast<const char*>(D.orow) - D.pad[0]),
-                            (uint32_t)D.pad[1], (uint32_t)D.pad[0] + 16u * lane, tot);
     }
 #ifdef DG_FSEG_PROF
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

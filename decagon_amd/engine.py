@@ -94,9 +94,10 @@ SEG_FUSED_MAX_ITEMS = 16
 # bounds, gather base and finishing roles precomputed, its first pairs at a fixed slot; bitwise
 # the same rows): config S's step 18.14 -> 15.56 us at 200 steps (round 5)
 WAVE_TABLE = knob("DG_WAVE_TABLE", True)
-# the one-GPU wave-table launches deal each row's pairs over every wave slot of its workgroup
-# (PreparedFusedTab balance, round 6) instead of one wave per relation
-TAB_BALANCE = knob("DG_TAB_BALANCE", True)
+# the wave-table fused launches deal each row's pairs over every wave slot of its workgroup
+# (PreparedFusedTab balance, round 6) instead of one wave per relation: 0 never, 1 layer 1 only
+# (d_in == d_out), 2 both layers
+TAB_BALANCE = knob("DG_TAB_BALANCE", 1)
 STAGED_FIRST = knob("DG_STAGED_FIRST", True)
 # sharded forward plans: layer 2 of the non-staged groups reassociated over the rank's own rows
 # and relations, Σ_k (Â_k·H1_j)·W2_k in dg_spmm_seg_f32, instead of every rank projecting all of
@@ -194,6 +195,17 @@ def snake_bins(costs: Sequence[float], bin_size: int, max_swaps: int = 4000) -> 
     seq += list(range(full, n_bins))                     # the short bin last
     out = [int(i) for b in seq for i in B[b] if i >= 0]
     return np.asarray(out, np.int64)
+
+
+def _tab_balance(d_in: int, d_out: int) -> bool:
+    """TAB_BALANCE's choice for a wave-table fused launch (layer 1: d_in == d_out)."""
+    return TAB_BALANCE >= 2 or (TAB_BALANCE == 1 and d_in == d_out)
+
+
+def _tab_groups_fit(tgts, d: int) -> bool:
+    """The wave-table fused form finishes a row in one wave, one lane set of d/4 lanes per group
+    (PreparedFusedTab): at most 64 / (d/4) groups a target; otherwise the fused-seg form."""
+    return all(len(gs) <= 64 // (d // 4) for _, _, gs, _ in tgts)
 
 
 def choose_chunk(n_rels: int, n_rows: int, nnz: int, d: int, target_waves: int = 32768) -> int:
@@ -503,7 +515,12 @@ class ForwardPlan:
                     off += self.world * per
             # zeros: a slot no rank ever pushes (a group without relations on that rank) reads as
             # zeros forever
-            self.xregion = torch.zeros(max(off, 64), **f32)
+            if pc is not None and pc.region_kind:  # (uncached by default: peer.PeerConfig)
+                from .peer import device_tensor
+
+                self.xregion = device_tensor(max(off, 64), pc.region_kind, dev)
+            else:
+                self.xregion = torch.zeros(max(off, 64), **f32)
             for (i, layer), (o, nb, d) in layout.items():
                 self._pad[i, layer] = self.xregion[o:o + nb].view(-1, d)
             for key, (base, o2, per, rows, d) in red_layout.items():
@@ -696,8 +713,9 @@ class ForwardPlan:
                               else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu))
             fused_peer = self._peer_fused(relu)
             d_in = self.h1 if seg_w else d
-            if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
-                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, peer=fused_peer, balance=TAB_BALANCE))  # (the wave-table form)
+            if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w) and _tab_groups_fit(tgts, d):
+                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, peer=fused_peer,
+                                                         balance=_tab_balance(d_in, d)))  # (the wave-table form)
             else:
                 launches.append(kernels.PreparedFusedSeg(tgts, d_in, d, peer=fused_peer))
             self.launch_groups[id(launches[-1])] = [et for i in self.targets for et in self.targets[i]]
@@ -711,9 +729,9 @@ class ForwardPlan:
                                      else self._seg_spec(et, xs[et]) for et in self.targets[i]], relu)
                     for i in fused_t]
             d_in = self.h1 if seg_w else d
-            if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w):
+            if WAVE_TABLE and d_in == 64 and (d == 64 or seg_w) and _tab_groups_fit(tgts, d):
                 # the wave-table form: the same rows bitwise, fewer dependent loads a wave
-                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, balance=TAB_BALANCE))
+                launches.append(kernels.PreparedFusedTab(tgts, d_in, d, balance=_tab_balance(d_in, d)))
             else:
                 launches.append(kernels.PreparedFusedSeg(tgts, d_in, d))
             self.launch_groups[id(launches[-1])] = [et for i in fused_t for et in self.targets[i]]

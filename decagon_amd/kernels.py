@@ -348,9 +348,9 @@ class _WaveTable:
         self.desc = np.zeros(n_slots, self.DESC)
         self.ovf: List[np.ndarray] = []
         self.n_ovf = 0
-        # entry of pair m within a batch: its lane in the DPP hand-out (d_out 64) or m (layer 2)
+        # entry of pair m within a batch: its lane in the DPP hand-out (both layers since round 6)
         m = np.arange(64)
-        self.lane_of = m if proj else 16 * (m & 3) + (m >> 2)
+        self.lane_of = 16 * (m & 3) + (m >> 2)
 
     def bounds(self, g: int, k: int, r: int) -> Tuple[int, int]:
         """[beg, end) of relation k's segment (of spec g) in row r."""
@@ -448,6 +448,8 @@ class PreparedFusedTab(PreparedFusedSeg):
         if not _tab_shape(d_in, d_out, specs):
             raise ValueError("dg_gcn_fused_tab_f32: d_in = d_out = 64, or 64 -> 32 with weight stacks")
         proj = d_out != d_in
+        if any(len(gs) > 64 // (d_out // 4) for _, _, gs, _ in targets):
+            raise ValueError("dg_gcn_fused_tab_f32: at most 64 / (d_out / 4) groups a target (one lane set each)")
         waves_t = [sum(s.n_rels for s in gs) for _, _, gs, _ in targets]
         nw = max([1] + waves_t)
         stride = 8 if nw <= 8 else 16
@@ -494,6 +496,11 @@ class PreparedFusedTab(PreparedFusedSeg):
                     tb.desc["wr"][i] = gc | ((1 if relu else 0) << 8) | (w << 16)
                     tb.desc["pad"][i, 0] = (r0 + w) * d_out * 4  # (the peer form: row offset,
                     tb.desc["pad"][i, 1] = n_rows * d_out * 4     # target bytes)
+                    # the row's finishing wave (round 6): each group's wave count − 1 in 4 bits,
+                    # and the row slot's first wave
+                    tb.desc["pad"][i, 2] = np.int32(np.uint32(sum((c - 1) << (4 * u)
+                                                                  for u, c in enumerate(counts[w]))))
+                    tb.desc["pad"][i, 3] = w * per_row
         if not plan and peer is not None:
             raise ValueError("dg_gcn_fused_tab_peer_f32: the exchange needs at least one row a rank")
         self._tab = tb.upload(self, len(plan), nw, stride, specs[0].x.device)

@@ -30,6 +30,7 @@ from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
+import torch.utils.dlpack
 
 from . import _lib
 from ._lib import DgPeerXchg, check
@@ -44,18 +45,86 @@ SLOT_PROBE = 4           # + layer - 1: bench.py's stand-alone exchange timing b
 
 @dataclass
 class PeerConfig:
-    """How a RelationShard's row-split blocks are exchanged when not over RCCL."""
+    """How a RelationShard's row-split blocks are exchanged when not over RCCL.
+
+    region_kind: the memory of the exchange region (dg_peer_alloc kinds): 0 coarse-grained
+    device memory (a torch allocation), 1 fine-grained, 2 uncached (the default since round 6).
+    Uncached, a row a peer stored over xGMI is read from memory by every later kernel of the
+    receiving GPU — no line of it can be stale in an L2 that cached it before the peer rewrote
+    it — and it measured no slower in loopback (config S at N = 8: 25.35 µs a rank against
+    25.91 coarse-grained and 26.00 fine-grained; config P: 114.3 against 114.6 / 116.7;
+    DESIGN §6)."""
 
     mode: str = "fused"                                       # "fused" | "kernel"
     gather: Optional[Callable[[object], List[object]]] = None  # all-gather of picklable objects
     loopback: bool = False
     timeout_s: float = TIMEOUT_S
+    region_kind: int = 2
 
     def __post_init__(self):
         if self.mode not in ("fused", "kernel"):
             raise ValueError(f"unknown peer exchange mode {self.mode!r}")
         if not self.loopback and self.gather is None:
             raise ValueError("a peer exchange across processes needs an object all-gather")
+        if self.region_kind not in (0, 1, 2):
+            raise ValueError("region_kind: 0 (coarse-grained), 1 (fine-grained) or 2 (uncached)")
+
+
+# ---- device memory of a given kind as a torch tensor (DLPack) ----
+class _DLDevice(ctypes.Structure):
+    _fields_ = [("device_type", ctypes.c_int), ("device_id", ctypes.c_int)]
+
+
+class _DLDataType(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_uint8), ("bits", ctypes.c_uint8), ("lanes", ctypes.c_uint16)]
+
+
+class _DLTensor(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("device", _DLDevice), ("ndim", ctypes.c_int), ("dtype", _DLDataType),
+                ("shape", ctypes.POINTER(ctypes.c_int64)), ("strides", ctypes.POINTER(ctypes.c_int64)),
+                ("byte_offset", ctypes.c_uint64)]
+
+
+class _DLManagedTensor(ctypes.Structure):
+    pass
+
+
+_DELETER = ctypes.CFUNCTYPE(None, ctypes.POINTER(_DLManagedTensor))
+_DLManagedTensor._fields_ = [("dl_tensor", _DLTensor), ("manager_ctx", ctypes.c_void_p), ("deleter", _DELETER)]
+_LIVE = {}  # id -> (managed struct, shape, deleter, pointer): alive until torch releases the tensor
+
+
+def device_tensor(numel: int, kind: int, device: torch.device) -> torch.Tensor:
+    """A zeroed float32 device tensor of `numel` elements in dg_peer_alloc memory of `kind`
+    (0 coarse-grained, 1 fine-grained, 2 uncached), owned by torch: the memory is freed with
+    dg_peer_free when the last view of the tensor is released."""
+    lib = _lib.load()
+    ptr = ctypes.c_void_p()
+    check(lib.dg_peer_alloc(4 * max(1, numel), kind, ctypes.byref(ptr)), "dg_peer_alloc")
+    shape = (ctypes.c_int64 * 1)(numel)
+    m = _DLManagedTensor()
+    key = id(m)
+
+    def _free(_):
+        ent = _LIVE.pop(key, None)
+        if ent is not None:
+            lib.dg_peer_free(ent[3])
+
+    deleter = _DELETER(_free)
+    m.dl_tensor.data = ptr.value
+    m.dl_tensor.device = _DLDevice(10, device.index or 0)  # kDLROCM
+    m.dl_tensor.ndim = 1
+    m.dl_tensor.dtype = _DLDataType(2, 32, 1)  # kDLFloat, 32 bits
+    m.dl_tensor.shape = shape
+    m.dl_tensor.strides = None
+    m.dl_tensor.byte_offset = 0
+    m.deleter = deleter
+    _LIVE[key] = (m, shape, deleter, ptr.value)
+    pycapsule_new = ctypes.pythonapi.PyCapsule_New
+    pycapsule_new.restype = ctypes.py_object
+    pycapsule_new.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    cap = pycapsule_new(ctypes.addressof(m), b"dltensor", None)
+    return torch.utils.dlpack.from_dlpack(cap)
 
 
 def dist_gather(group=None) -> Callable[[object], List[object]]:
@@ -97,8 +166,9 @@ class PeerExchange:
             for p in range(world):
                 if p == rank:
                     bases[p] = base
-                else:
-                    self._scratch.append(torch.empty_like(region))
+                else:  # (the peers' regions stand-ins: of the configured memory kind too)
+                    self._scratch.append(torch.empty_like(region) if cfg.region_kind == 0
+                                         else device_tensor(region.numel(), cfg.region_kind, dev))
                     bases[p] = self._scratch[-1].data_ptr()
                 flags[p] = self._flags
         else:

@@ -265,10 +265,34 @@ def test_peer_exchange_forward_matches_oracle(kind, world, mode):
                 assert np.array_equal(form[0][t], base[0][t]) and np.array_equal(form[1][t], base[1][t]), (r, t)
 
 
-def test_peer_loopback_rehearsal_matches_rank_block():
+def test_device_tensor_kinds():
+    """peer.device_tensor: dg_peer_alloc memory of each kind as a torch tensor — zeroed,
+    read and written by kernels, views kept alive by torch, freed with the last view."""
+    _need_gpu()
+    from decagon_amd import peer
+
+    for kind in (0, 1, 2):
+        t = peer.device_tensor(4099, kind, torch.device("cuda", 0))
+        assert t.is_cuda and t.dtype == torch.float32 and t.shape == (4099,)
+        assert int(torch.count_nonzero(t)) == 0
+        v = t[3:1003].view(10, 100)
+        v.copy_(torch.arange(1000, dtype=torch.float32, device="cuda").view(10, 100))
+        torch.cuda.synchronize()
+        assert float(t[3:1003].sum()) == 999 * 1000 / 2
+        n_live = len(peer._LIVE)
+        del t
+        assert len(peer._LIVE) == n_live  # the view still holds the allocation
+        del v
+        torch.cuda.synchronize()
+        assert len(peer._LIVE) == n_live - 1
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_peer_loopback_rehearsal_matches_rank_block(kind):
     """One process standing in for rank r of N (bench.py --simulate-world N --exchange peer):
     the "peers" are local scratch copies and the last workgroup raises every flag itself; the
-    rank's own rows equal the unsharded forward's, the scratch copies hold them too."""
+    rank's own rows equal the unsharded forward's, the scratch copies hold them too — with the
+    exchange region (and the scratch copies) in each dg_peer_alloc memory kind."""
     _need_gpu()
     from decagon_amd.peer import PeerConfig
     from decagon_amd.sharding import _no_op, _no_op_reduce
@@ -280,7 +304,7 @@ def test_peer_loopback_rehearsal_matches_rank_block():
         from decagon_amd.sharding import RelationShard
 
         sh = RelationShard.weak_sets(g.edge_types, g.n_nodes, rank, world, _no_op_reduce, _no_op)
-        sh.peer = PeerConfig(mode="fused", loopback=True)
+        sh.peer = PeerConfig(mode="fused", loopback=True, region_kind=kind)
         from decagon_amd.engine import DeviceGraph, ForwardPlan, LayerWeights
 
         dev = torch.device("cuda", 0)

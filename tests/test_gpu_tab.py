@@ -17,7 +17,7 @@ def _plan(graph, balance=False):
     import bench
     from decagon_amd import engine
 
-    engine.TAB_BALANCE = balance  # (module policy read at plan build; restored by the fixture)
+    engine.TAB_BALANCE = 2 if balance else 0  # (module policy read at plan build; restored by the fixture)
     args = bench.parse(["--config", "S"])
     args.chunk = dict(graph.edge_types)  # one chunk per group (the fused form's layout)
     plan, _ = bench.make_plan(args, graph, None, torch.device("cuda", 0))
