@@ -107,7 +107,7 @@ class DgTabDesc(ctypes.Structure):
 
 class DgWaveTable(ctypes.Structure):
     _fields_ = [("pairs", c_void_p), ("ovf", c_void_p), ("desc", c_void_p), ("n_blocks", c_int32),
-                ("nw", c_int32), ("nw_stride", c_int32), ("pad", c_int32)]
+                ("nw", c_int32), ("nw_stride", c_int32), ("slot_pairs", c_int32)]
 
 
 class DgStagedProj(ctypes.Structure):

@@ -480,7 +480,7 @@ static_assert(sizeof(dg_tab_desc) == 64, "dg_tab_desc: one s_load_dwordx16");
 // 64-wide aggregate times the relation's W slab (seg_wave_proj's arithmetic).
 template <bool PROJ, int U>
 __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 first, const uint2* __restrict__ ovf,
-                                           float4* ybuf) {
+                                           float4* ybuf, const int S) {
     constexpr int LP = 16;
     constexpr int G = dg::kWave / LP;
     const int lane = threadIdx.x & 63;
@@ -494,14 +494,18 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
         int vb = (int)first.y;
         const uint2* nx = ovf + D.ovf;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        // the first batch is the slot's S pairs (round 6: slot_pairs), the rest batches of 64;
+        // a lane group takes pairs sub, sub + 4, ... in order across the batches whatever S (a
+        // multiple of 4), so the sums are bitwise those of 64-pair first batches
+        int bsz = S;
 #pragma unroll 1
-        for (int base = 0; base < D.cnt; base += 64) {
-            const int n = min(64, D.cnt - base);
+        for (int base = 0; base < D.cnt; base += bsz, bsz = 64) {
+            const int n = min(bsz, D.cnt - base);
             const int eoff = vc * D.x_ld;
             const int vbits = vb;
             vc = 0;
             vb = 0;
-            if (base + 64 < D.cnt) {
+            if (base + bsz < D.cnt) {
                 const uint2 q = nx[lane];
                 vc = (int)q.x;
                 vb = (int)q.y;
@@ -535,6 +539,13 @@ __device__ __forceinline__ float4 tab_wave(const dg_tab_desc& D, const uint2 fir
             }
         }
         acc = dg::xor_sum4_from<LP>(acc);
+#ifdef DG_FSEG_PROF
+        if constexpr (PROJ) {  // (profiling build: stamp 2 = the gathers done, before the projection)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            DG_FS_STAMP(2);
+        }
+#endif
         if constexpr (PROJ) {
             // z = y·W_k: this lane's W slice (rows 8(l>>3) .. +8, output float4 l & 7) read
             // after the gathers, as in seg_wave_proj
@@ -602,13 +613,22 @@ __device__ __forceinline__ float4 lds_ordered_sum(const float4 (*rows)[W], int K
     return s;
 }
 
+// Byte offset of this lane's first-batch pair in a slot of S pairs: lane 16·sub + m' holds pair
+// 4m' + sub, stored at slot entry sub·S/4 + m'; lanes with m' >= S/4 (no such pair in the slot)
+// read their row's last entry — the same cache lines, never used.
+__device__ __forceinline__ uint32_t slot_lane_offset(int lane, int S) {
+    const int q = S >> 2, m = lane & 15;
+    return 8u * (uint32_t)((lane >> 4) * q + (m < q ? m : q - 1));
+}
+
 // PEER (dg_gcn_fused_tab_peer_f32): each finished row also goes to every peer's copy of its
 // target (desc.pad[0] = the row's byte offset in the target, pad[1] = the target's bytes), and
 // the launch ends with the exchange (peer.h).
 template <bool PROJ, int NW, bool PEER>
 __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restrict__ pairs,
                                                           const dg_tab_desc* __restrict__ desc,
-                                                          const uint2* __restrict__ ovf, const dg::PeerK P) {
+                                                          const uint2* __restrict__ ovf, const int S,
+                                                          const dg::PeerK P) {
     constexpr int DOUT4 = PROJ ? 8 : 16;
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
@@ -624,7 +644,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
     const dg_tab_desc D = desc[wi];  // (uniform: scalar loads)
     uint2 first;
     asm volatile("global_load_dwordx2 %0, %1, %2\n\ts_waitcnt vmcnt(0)"
-                 : "=&v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64) : "memory");
+                 : "=&v"(first) : "v"(slot_lane_offset(lane, S)), "s"(pairs + wi * S) : "memory");
     // every descriptor field and the ovf base in SGPRs here, so no scalar load is sunk below
     // the branch into a round trip of its own
     asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(D.wr),
@@ -633,8 +653,8 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif
     DG_FS_STAMP(1);  // descriptor and first pairs in registers
-    DG_FS_STAMP(2);  // (no segment-bounds phase in the table form)
-    const float4 res = tab_wave<PROJ, PROJ ? kTabUP : kTabU>(D, first, ovf, ybuf[wave]);
+    if constexpr (!PROJ) DG_FS_STAMP(2);  // (layer 2: stamp 2 marks its gathers done, in tab_wave)
+    const float4 res = tab_wave<PROJ, PROJ ? kTabUP : kTabU>(D, first, ovf, ybuf[wave], S);
 #ifdef DG_FSEG_PROF
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif
@@ -701,7 +721,7 @@ __global__ __launch_bounds__(64 * NW) void gcn_tab_kernel(const uint2* __restric
 template <bool PROJ, int NW>
 __global__ __launch_bounds__(64 * NW) void seg_tab_kernel(const uint2* __restrict__ pairs,
                                                           const dg_tab_desc* __restrict__ desc,
-                                                          const uint2* __restrict__ ovf) {
+                                                          const uint2* __restrict__ ovf, const int S) {
     constexpr int DOUT4 = PROJ ? 8 : 16;
     __shared__ float4 ybuf[NW][16];
     __shared__ float4 zbuf[NW][DOUT4];
@@ -711,9 +731,9 @@ __global__ __launch_bounds__(64 * NW) void seg_tab_kernel(const uint2* __restric
     const dg_tab_desc D = desc[wi];  // (as gcn_tab_kernel: descriptor first, pairs load + wait in one asm)
     uint2 first;
     asm volatile("global_load_dwordx2 %0, %1, %2\n\ts_waitcnt vmcnt(0)"
-                 : "=&v"(first) : "v"((uint32_t)lane * 8u), "s"(pairs + wi * 64) : "memory");
+                 : "=&v"(first) : "v"(slot_lane_offset(lane, S)), "s"(pairs + wi * S) : "memory");
     asm volatile("" ::"s"(D.x), "s"(D.w), "s"(D.orow), "s"(D.cnt), "s"(D.x_ld), "s"(D.ovf), "s"(D.role), "s"(ovf));
-    const float4 res = tab_wave<PROJ, PROJ ? kSegUP : kSegU>(D, first, ovf, ybuf[wave]);
+    const float4 res = tab_wave<PROJ, PROJ ? kSegUP : kSegU>(D, first, ovf, ybuf[wave], S);
     if (lane < DOUT4) zbuf[wave][lane] = res;  // relations past the group's end add zeros
     __syncthreads();
     if (D.orow != nullptr && lane < DOUT4) {
@@ -933,7 +953,9 @@ int fused_tab_launch(const dg_wave_table* t, int32_t d_in, int32_t d_out, const 
     if (t->n_blocks == 0) return xchg ? DG_EINVAL : DG_OK;  // (an exchange needs a workgroup a rank)
     if (!t->pairs || !t->desc || !dg::aligned16(t->pairs) || (reinterpret_cast<uintptr_t>(t->desc) & 63))
         return DG_EALIGN;
-    if ((int64_t)t->n_blocks * t->nw_stride * 64 > 0x7fffffffLL) return DG_EINVAL;
+    const int S = t->slot_pairs ? t->slot_pairs : 64;
+    if (S != 16 && S != 32 && S != 48 && S != 64) return DG_EINVAL;
+    if ((int64_t)t->n_blocks * t->nw_stride * S > 0x7fffffffLL) return DG_EINVAL;
     dg::PeerK P{};
     if (xchg) {
         const int rc = dg::peer_convert(xchg, P);
@@ -944,7 +966,7 @@ int fused_tab_launch(const dg_wave_table* t, int32_t d_in, int32_t d_out, const 
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(t->n_blocks)), block(64 * t->nw);
 #define DG_TAB_LAUNCH(PR, NWV, PE) \
-    hipLaunchKernelGGL((gcn_tab_kernel<PR, NWV, PE>), grid, block, 0, st, pr, t->desc, ov, P)
+    hipLaunchKernelGGL((gcn_tab_kernel<PR, NWV, PE>), grid, block, 0, st, pr, t->desc, ov, S, P)
     if (xchg) {
         if (t->nw_stride == 8) {
             if (proj) DG_TAB_LAUNCH(true, 8, true); else DG_TAB_LAUNCH(false, 8, true);
@@ -981,21 +1003,23 @@ extern "C" int dg_spmm_seg_tab_f32(const dg_wave_table* t, int32_t d_in, int32_t
     if (t->n_blocks == 0) return DG_OK;
     if (!t->pairs || !t->desc || !dg::aligned16(t->pairs) || (reinterpret_cast<uintptr_t>(t->desc) & 63))
         return DG_EALIGN;
-    if ((int64_t)t->n_blocks * t->nw_stride * 64 > 0x7fffffffLL) return DG_EINVAL;
+    const int S = t->slot_pairs ? t->slot_pairs : 64;
+    if (S != 16 && S != 32 && S != 48 && S != 64) return DG_EINVAL;
+    if ((int64_t)t->n_blocks * t->nw_stride * S > 0x7fffffffLL) return DG_EINVAL;
     const uint2* pr = reinterpret_cast<const uint2*>(t->pairs);
     const uint2* ov = reinterpret_cast<const uint2*>(t->ovf);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     dim3 grid(static_cast<unsigned>(t->n_blocks)), block(64 * t->nw);
     if (t->nw_stride == 8) {
         if (proj)
-            hipLaunchKernelGGL((seg_tab_kernel<true, 8>), grid, block, 0, st, pr, t->desc, ov);
+            hipLaunchKernelGGL((seg_tab_kernel<true, 8>), grid, block, 0, st, pr, t->desc, ov, S);
         else
-            hipLaunchKernelGGL((seg_tab_kernel<false, 8>), grid, block, 0, st, pr, t->desc, ov);
+            hipLaunchKernelGGL((seg_tab_kernel<false, 8>), grid, block, 0, st, pr, t->desc, ov, S);
     } else {
         if (proj)
-            hipLaunchKernelGGL((seg_tab_kernel<true, 16>), grid, block, 0, st, pr, t->desc, ov);
+            hipLaunchKernelGGL((seg_tab_kernel<true, 16>), grid, block, 0, st, pr, t->desc, ov, S);
         else
-            hipLaunchKernelGGL((seg_tab_kernel<false, 16>), grid, block, 0, st, pr, t->desc, ov);
+            hipLaunchKernelGGL((seg_tab_kernel<false, 16>), grid, block, 0, st, pr, t->desc, ov, S);
     }
     return dg::launch_status();
 }

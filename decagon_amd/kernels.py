@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .tuning import knob
 from ._lib import (DgAdamSeg, DgEpiGroup, DgFusedTarget, DgGemmDesc, DgL2gGroup, DgProj, DgRelGroup,
                    DgStagedGroup, DgStagedProj, check)
 
@@ -333,8 +334,13 @@ class PreparedFusedSeg:
 
 class _WaveTable:
     """Host builder of a dg_wave_table (decagon_hip.h): per wave slot a 64-byte descriptor and
-    the first 64 pairs of its relation segment (in the hand-out order of its gather form), the
-    rest in batches of 64 in an overflow array."""
+    the first S pairs of its segment (in the hand-out order of its gather form: pair m in lane
+    16·(m & 3) + (m >> 2), stored compactly at (m & 3)·S/4 + (m >> 2)), the rest in batches of
+    64 in an overflow array.  S (slot_pairs, round 6) is the smallest of 16 / 32 / 48 / 64
+    holding the first batch of ≥ SLOT_COVER of the non-empty waves: a wave then fetches S·8 B
+    where round 5 fetched 512 B whatever its length (a config-S wave holds 7–81 pairs)."""
+
+    SLOT_COVER = 0.97
 
     DESC = np.dtype([("x", "<u8"), ("w", "<u8"), ("orow", "<u8"), ("cnt", "<i4"), ("x_ld", "<i4"), ("ovf", "<i4"),
                      ("role", "<u4"), ("wr", "<u4"), ("pad", "<i4", 5)])
@@ -344,10 +350,9 @@ class _WaveTable:
         self.specs, self.proj = list(specs), proj
         self.host = [(s.rowptr.cpu().numpy(), s.seg.cpu().numpy(), s.vcol.cpu().numpy(), s.val.cpu().numpy(),
                       None if s.slab is None else s.slab.cpu().numpy()) for s in specs]
-        self.pairs = np.zeros((n_slots * 64, 2), np.int32)
+        self.n_slots = n_slots
+        self.pv: dict = {}  # wave slot -> its pairs [cnt, 2] (laid out at upload, once S is known)
         self.desc = np.zeros(n_slots, self.DESC)
-        self.ovf: List[np.ndarray] = []
-        self.n_ovf = 0
         # entry of pair m within a batch: its lane in the DPP hand-out (both layers since round 6)
         m = np.arange(64)
         self.lane_of = 16 * (m & 3) + (m >> 2)
@@ -394,21 +399,47 @@ class _WaveTable:
         vv = np.concatenate(vvs) if vvs else np.zeros(0, np.float32)
         cnt = len(vc)
         d["x"][i], d["x_ld"][i], d["cnt"][i] = s.x.data_ptr(), s.x_ld, cnt
-        pv = np.stack([vc.astype(np.int32), vv.astype(np.float32).view(np.int32)], 1)
-        m0 = min(cnt, 64)
-        self.pairs[i * 64 + self.lane_of[:m0]] = pv[:m0]
-        if cnt > 64:
-            d["ovf"][i] = self.n_ovf
-            for q0 in range(64, cnt, 64):
-                blk = np.zeros((64, 2), np.int32)
-                n = min(64, cnt - q0)
-                blk[self.lane_of[:n]] = pv[q0:q0 + n]
-                self.ovf.append(blk)
-                self.n_ovf += 64
+        self.pv[i] = np.stack([vc.astype(np.int32), vv.astype(np.float32).view(np.int32)], 1)
+
+    def slot_pairs(self) -> int:
+        fixed = knob("DG_TAB_SLOT", 0)  # (A/B: a fixed slot size; 0 = by SLOT_COVER)
+        if fixed:
+            if fixed not in (16, 32, 48, 64):
+                raise ValueError("DG_TAB_SLOT: 16, 32, 48 or 64")
+            return fixed
+        cnts = np.array([len(p) for p in self.pv.values() if len(p)], np.int64)
+        if not len(cnts):
+            return 16
+        need = float(np.quantile(cnts, self.SLOT_COVER))
+        return next(S for S in (16, 32, 48, 64) if S >= need or S == 64)
+
+    def layout(self, S: int):
+        """(pairs [n_slots·S, 2], ovf [.., 2]) for first-batch slots of S pairs; sets desc.ovf."""
+        pairs = np.zeros((self.n_slots * S, 2), np.int32)
+        ovf: List[np.ndarray] = []
+        n_ovf = 0
+        m = np.arange(S)
+        compact = (m & 3) * (S // 4) + (m >> 2)  # slot entry of pair m (its lane's row-major rank)
+        for i, pv in self.pv.items():
+            cnt = len(pv)
+            m0 = min(cnt, S)
+            pairs[i * S + compact[:m0]] = pv[:m0]
+            if cnt > S:
+                self.desc["ovf"][i] = n_ovf
+                for q0 in range(S, cnt, 64):
+                    blk = np.zeros((64, 2), np.int32)
+                    n = min(64, cnt - q0)
+                    blk[self.lane_of[:n]] = pv[q0:q0 + n]
+                    ovf.append(blk)
+                    n_ovf += 64
+        return pairs, (np.concatenate(ovf) if ovf else np.zeros((64, 2), np.int32))
 
     def upload(self, owner, n_blocks: int, nw: int, stride: int, dev) -> "_lib.DgWaveTable":
-        owner._pairs = torch.from_numpy(self.pairs).to(dev)
-        owner._ovf = torch.from_numpy(np.concatenate(self.ovf) if self.ovf else np.zeros((64, 2), np.int32)).to(dev)
+        S = self.slot_pairs()
+        pairs, ovf = self.layout(S)
+        owner._pairs = torch.from_numpy(pairs).to(dev)
+        owner._ovf = torch.from_numpy(ovf).to(dev)
+        owner.slot_pairs = S
         raw = torch.from_numpy(self.desc.view(np.uint8).copy())
         owner._desc = torch.empty(raw.numel() + 64, dtype=torch.uint8, device=dev)
         off = (-owner._desc.data_ptr()) % 64  # 64-byte aligned descriptors
@@ -416,7 +447,7 @@ class _WaveTable:
         owner._desc_v.copy_(raw.to(dev))
         tab = _lib.DgWaveTable()
         tab.pairs, tab.ovf, tab.desc = owner._pairs.data_ptr(), owner._ovf.data_ptr(), owner._desc_v.data_ptr()
-        tab.n_blocks, tab.nw, tab.nw_stride = n_blocks, nw, stride
+        tab.n_blocks, tab.nw, tab.nw_stride, tab.slot_pairs = n_blocks, nw, stride, S
         return tab
 
 

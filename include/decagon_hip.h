@@ -261,13 +261,16 @@ typedef struct dg_tab_desc {
 } dg_tab_desc;            /* 64 bytes                                                        */
 
 typedef struct dg_wave_table {
-    const int32_t* pairs; /* device, [n_blocks * nw_stride * 64][2], 16-byte aligned         */
+    const int32_t* pairs; /* device, [n_blocks * nw_stride * slot_pairs][2], 16-byte aligned */
     const int32_t* ovf;   /* device, [..][2], or NULL                                        */
     const dg_tab_desc* desc; /* device, [n_blocks * nw_stride], 64-byte aligned             */
     int32_t n_blocks;
     int32_t nw;           /* waves per workgroup, 1..16                                      */
     int32_t nw_stride;    /* 8 if nw <= 8, else 16                                           */
-    int32_t pad;
+    int32_t slot_pairs;   /* S: pairs of a wave's first batch, 16 / 32 / 48 / 64 (ABI 37;     */
+                          /* 0 means 64): pair m < S of the segment at slot entry             */
+                          /* (m & 3)·S/4 + (m >> 2); pairs S, S+1, ... in batches of 64 from  */
+                          /* ovf + desc.ovf, pair j of a batch at entry 16·(j & 3) + (j >> 2) */
 } dg_wave_table;
 
 int dg_gcn_fused_tab_f32(const dg_wave_table* table /* HOST */, int32_t d_in, int32_t d_out, void* stream);

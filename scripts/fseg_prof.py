@@ -62,7 +62,10 @@ def main():
     forms = sorted({type(l).__name__ for L in plan.spmm_launches for l in L})
     out = {"steps_per_graph": steps, "launch_forms": forms,
            "note": "the table form (PreparedFusedTab = gcn_tab_kernel) has no search or bounds phase: "
-                   "'search' is its first round trip (descriptor + first 64 pairs), 'bounds' is 0",
+                   "'search' is its first round trip (descriptor + first 64 pairs); in layer 2 'bounds' "
+                   "is its gathers (first pairs in registers -> aggregate folded) and 'relation' the "
+                   "projection by W2_k (W slice load, LDS hand-off, FMAs, butterfly); 'normalise' is the "
+                   "finishing wave's group sums, norms and cross-group sum (no second barrier since round 6)",
            "launches": {}}
     bufs = {}
     for proj in (0, 1):
