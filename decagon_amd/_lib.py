@@ -19,10 +19,11 @@ DG_EINVAL = -1
 DG_EALIGN = -2
 DG_ETOOMANY = -3
 DG_MAX_GROUPS = 8
+DG_STAGED_MAX_CHUNKS = 128
 DG_EPI_L2NORM = 1
 DG_EPI_RELU = 2
 DG_EPI_CHUNK_RELU = 4
-ABI_VERSION = 37
+ABI_VERSION = 38
 DG_HINGE_WS_BYTES = 16 + 4 * 256  # decagon_hip.h
 DG_RANK_LOGIT, DG_RANK_SIGMOID64, DG_RANK_SIGMOID32 = 0, 1, 2  # decagon_hip.h
 DG_GROUP_SHARED_PATTERN = 1  # dg_rel_group.flags
@@ -76,6 +77,9 @@ class DgStagedGroup(ctypes.Structure):
         ("out_chunk", c_int32),
         ("x_rows", c_int32),
         ("jm_len", c_int32),
+        ("chunk_start", c_void_p),   # HOST int32 [n_chunks + 1] or NULL (fixed out_chunk)
+        ("n_chunks", c_int32),
+        ("pad", c_int32),
     ]
 
 

@@ -735,7 +735,7 @@ __global__ __launch_bounds__(1024) void spmm_lds_kernel(const LdsArgs a) {
 
 }  // namespace
 
-extern "C" int32_t dg_abi_version(void) { return 37; }
+extern "C" int32_t dg_abi_version(void) { return 38; }
 
 
 namespace {

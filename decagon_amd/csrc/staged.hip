@@ -43,6 +43,7 @@ constexpr int kMaxThreads = 1024;
 constexpr int kLdsBytes = 160 * 1024;
 constexpr int kMetaInts = 256;  // a chunk's tables: jm offsets (nk + 1) and slabs (nk), nk <= 64
 constexpr int kDummyRow = 1023;
+constexpr int kMaxVarChunks = DG_STAGED_MAX_CHUNKS;  // variable output chunks a group (kernarg table)
 #ifdef DG_STAGED_PROF
 constexpr int kProfSlots = 6;  // per wave: barrier, put+prefetch, tables, gather, accumulate, relations
 #endif
@@ -63,13 +64,16 @@ struct StagedGroupK {
     int32_t n_slices;
     int32_t block_begin;
     int32_t n_blocks;
-    int32_t pad;
+    int32_t var;       // 1: chunk c is relations [cstart[c], cstart[c + 1]) (variable sizes)
     // PROJ form: the slab of relation k is H · W[slab(k)] (H [n_cols][64], W [K][64][d]),
     // computed in the workgroup on the fp32 MFMA instead of read from x
     const float* h;
     const float* w;
     int32_t h_ld;
     int32_t pad2;
+    // var form: the output chunks' first relations (kernarg: a block-uniform scalar read, no
+    // dependent global load before the chunk's tables)
+    uint16_t cstart[kMaxVarChunks + 1];
 };
 
 struct StagedArgs {
@@ -144,8 +148,9 @@ __global__ __launch_bounds__(kMaxThreads) void spmm_staged_kernel(const StagedAr
     const int col0 = s * 16;
     const int n_rows = g.n_rows;
     const int n_cols = g.n_cols;
-    const int k0 = c * g.out_chunk;
-    const int nk = min(g.out_chunk, g.n_rels - k0);  // relations of this chunk
+    const int k0 = g.var ? static_cast<int>(g.cstart[c]) : c * g.out_chunk;
+    const int nk = g.var ? static_cast<int>(g.cstart[c + 1]) - k0
+                         : min(g.out_chunk, g.n_rels - k0);  // relations of this chunk
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -428,6 +433,19 @@ int staged_launch(const dg_staged_group* groups, const dg_staged_proj* projs, in
         k.n_rels = s.n_rels;
         k.out_chunk = s.out_chunk < s.n_rels ? s.out_chunk : s.n_rels;
         k.n_out_chunks = dg::ceil_div(s.n_rels, k.out_chunk);
+        if (s.chunk_start) {  // variable chunks: 0 = c_0 < c_1 < ... < c_n = n_rels, each <= 64
+            const int32_t nc = s.n_chunks;
+            if (nc < 1 || nc > kMaxVarChunks || s.n_rels > 65535 || s.chunk_start[0] != 0 || s.chunk_start[nc] != s.n_rels)
+                return DG_EINVAL;
+            for (int32_t c = 0; c < nc; ++c) {
+                const int32_t len = s.chunk_start[c + 1] - s.chunk_start[c];
+                if (len < 1 || len > 64) return DG_EINVAL;
+                k.cstart[c] = static_cast<uint16_t>(s.chunk_start[c]);
+            }
+            k.cstart[nc] = static_cast<uint16_t>(s.n_rels);
+            k.var = 1;
+            k.n_out_chunks = nc;
+        }
         k.n_slices = dg::ceil_div(d, 16);
         // XCD-aligned at chunk granularity: XCD x takes chunks [x·cpx, (x+1)·cpx) with all their
         // slices, so a chunk's pairs are read into one L2 (the kernel's item map is

@@ -20,6 +20,7 @@ products X·W1) is indexed by the GLOBAL relation id, so one merged layout serve
 """
 from __future__ import annotations
 
+import heapq
 import math
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -124,10 +125,90 @@ def _epilogue(targets, d: int, flags: int, peer=None, push=None):
     return kernels.PreparedEpilogueMulti(targets, d, flags, peer=peer, push=push)
 
 
+# staged groups in variable-size output chunks (dg_staged_group.chunk_start): the relations are
+# dealt LPT into about STAGED_TARGET_BLOCKS / 4 chunks (a 64-wide layer's), each split LPT in two
+# for a 32-wide layer — instead of fixed runs of snake-binned relations, which at a rank's share
+# (config P at N = 8: ~241 relations, 4 a chunk) put a 43 k-nonzero relation beside three others
+STAGED_VAR = knob("DG_STAGED_VAR", True)
+
+
+def _lpt_bins(costs: np.ndarray, items: np.ndarray, n_bins: int, cap: int) -> List[List[int]]:
+    """items dealt largest first to the least-loaded bin that has room (< cap items); ties to the
+    lower bin index (deterministic).  Every bin gets an item when len(items) >= n_bins."""
+    order = items[np.argsort(-costs[items], kind="stable")]
+    bins: List[List[int]] = [[] for _ in range(n_bins)]
+    heap = [(0.0, b) for b in range(n_bins)]
+    for it in order:
+        full = []
+        while True:
+            load, b = heapq.heappop(heap)
+            if len(bins[b]) < cap:
+                break
+            full.append((load, b))
+        bins[b].append(int(it))
+        heapq.heappush(heap, (load + float(costs[it]), b))
+        for f in full:
+            heapq.heappush(heap, f)
+    return bins
+
+
+def staged_var_chunks(costs: Sequence[float], n_top: int, split: int = 2, cap: int = 64):
+    """Variable output chunks of a staged group: (device order of the relations, top-level chunk
+    starts, sub-chunk starts).  The relations are dealt LPT into n_top chunks of <= cap, each
+    chunk's relations LPT into <= split sub-chunks; the device order lists the chunks heaviest,
+    lightest, second heaviest, ... (so runs of two merge evenly), sub-chunk by sub-chunk."""
+    c = np.asarray(costs, np.float64)
+    n = len(c)
+    n_top = max(1, min(n_top, n))
+    if n > n_top * cap:
+        raise ValueError("more relations than chunks x cap")
+    top = _lpt_bins(c, np.arange(n), n_top, cap)
+    loads = np.array([c[b].sum() for b in top])
+    by = list(np.argsort(-loads, kind="stable"))
+    seq = []
+    while by:
+        seq.append(by.pop(0))
+        if by:
+            seq.append(by.pop())
+    order, tops, subs = [], [0], [0]
+    for b in seq:
+        items = np.asarray(top[b], np.int64)
+        for sb in _lpt_bins(c, items, min(split, len(items)), cap):
+            order += sb
+            subs.append(len(order))
+        tops.append(len(order))
+    return np.asarray(order, np.int64), np.asarray(tops, np.int32), np.asarray(subs, np.int32)
+
+
+def staged_chunk_starts(grp, d: int) -> Optional[np.ndarray]:
+    """The variable output chunks of a staged group for a layer of width d (None: fixed runs of
+    staged_out_chunk relations): the sub-chunks when the layer wants at least twice the top-level
+    chunks of workgroups' worth (STAGED_TARGET_BLOCKS / slices), the top-level chunks when it
+    wants at least as many, else runs of consecutive top-level chunks (heavy-light pairs)."""
+    if grp.var_chunks is None:
+        return None
+    tops, subs = grp.var_chunks
+    want = max(1, STAGED_TARGET_BLOCKS // -(-d // 16))
+    n_top = len(tops) - 1
+    if want >= 2 * n_top and len(subs) - 1 <= kernels.STAGED_MAX_CHUNKS:
+        return subs
+    if want >= n_top:
+        return tops
+    f = -(-n_top // want)
+    st = tops[::f] if (n_top % f == 0) else np.concatenate([tops[::f], tops[-1:]])
+    if np.diff(st).max() > 64:
+        return None
+    return st.astype(np.int32)
+
+
 def staged_out_chunk(grp, d: int) -> int:
     """Relations per output chunk of a staged group for a layer of width d: a multiple of the
     group's snake-bin size (so chunks stay balanced) giving about STAGED_TARGET_BLOCKS
-    workgroups of (chunk, 16-float slice) — one round on the chip, one LDS-full workgroup per CU."""
+    workgroups of (chunk, 16-float slice) — one round on the chip, one LDS-full workgroup per CU.
+    (With variable chunks, staged_chunk_starts: the largest chunk.)"""
+    st = staged_chunk_starts(grp, d)
+    if st is not None:
+        return int(np.diff(st).max())
     n_slices = -(-d // 16)
     want = max(1, STAGED_TARGET_BLOCKS // n_slices)        # output chunks
     per = max(1, -(-grp.n_rels // want))
@@ -247,6 +328,8 @@ class DeviceGroup:
     rel_map: Optional[torch.Tensor] = None   # device rel_ids, when not 0..K-1
     staged: bool = False           # runs through dg_spmm_staged_f32 (layout: chunk = 1)
     out_chunk: int = 1             # staged: snake-bin size (a layer's output chunk is a multiple)
+    # staged, variable chunks (STAGED_VAR): (top-level chunk starts, sub-chunk starts), device order
+    var_chunks: Optional[Tuple[np.ndarray, np.ndarray]] = None
     layout: Optional["kernels.StagedDevice"] = None  # staged: the diagonal-major layout
     host: Optional[List[HostCSR]] = None  # the local relations (host CSR), device order
     seg: Optional[torch.Tensor] = None    # dg_spmm_seg_f32's segment starts (sparse.chunk_segments)
@@ -307,7 +390,14 @@ class DeviceGraph:
                 # one chunk per relation; output chunks of out_chunk relations with balanced
                 # nonzero counts (relation sizes are Zipf-skewed)
                 out_chunk = max(1, -(-len(loc) // STAGED_BINS))
-                perm = snake_bins([c.nnz + STAGED_REL_OVERHEAD for c in loc], out_chunk)
+                costs = [c.nnz + STAGED_REL_OVERHEAD for c in loc]
+                var = None
+                n_top = max(1, STAGED_TARGET_BLOCKS // -(-d_policy // 16))
+                if STAGED_VAR and len(loc) <= 65535 and len(loc) <= 64 * n_top:
+                    perm, tops, subs = staged_var_chunks(costs, n_top)
+                    var = (tops, subs)
+                else:
+                    perm = snake_bins(costs, out_chunk)
                 ids = ids[perm]
                 loc = [loc[i] for i in perm]
                 ch = 1
@@ -330,6 +420,8 @@ class DeviceGraph:
             if ids.size and not np.array_equal(ids, np.arange(K)):
                 g.rel_map = torch.from_numpy(ids).to(device)
             g.staged, g.out_chunk = staged, out_chunk
+            if staged:
+                g.var_chunks = var
             g.host = loc  # local relations in device order (the backward builds Âᵀ from them)
             if segments and loc and not staged and not windows and m.chunk <= 16:
                 g.seg = torch.from_numpy(chunk_segments(loc, m)).to(device)
@@ -803,7 +895,9 @@ class ForwardPlan:
         reassoc = (set(seg_w or {}) | (self.seg_l1 if relu else set())) if not self.seg_mode else set()
         for et in rest:
             grp = g.groups[et]
-            n_out = -(-grp.n_rels // staged_out_chunk(grp, d)) if grp.staged else grp.n_chunks
+            cst = staged_chunk_starts(grp, d) if grp.staged else None
+            n_out = ((len(cst) - 1 if cst is not None else -(-grp.n_rels // staged_out_chunk(grp, d)))
+                     if grp.staged else grp.n_chunks)
             if et in reassoc:
                 n_out = self._seg_chunks(et)
             if flat is not None and et in views and n_out == 1:
@@ -819,7 +913,7 @@ class ForwardPlan:
                 sp = (staged_proj or {}).get(et)
                 staged.append(kernels.StagedSpec(
                     grp.layout, grp.rel_map, xs.get(et), part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
-                    slab_max=int(grp.rel_ids.max()), proj=sp))
+                    slab_max=int(grp.rel_ids.max()), proj=sp, chunk_start=cst))
             elif self.seg_mode or et in reassoc:
                 if et in (seg_w or {}):  # layer 2 reassociated: H1_j and W2's stack
                     segs.append(self._seg_spec(et, seg_w[et][0], part, seg_w[et][1]))

@@ -774,6 +774,7 @@ class StagedDevice:
 
 
 STAGED_LDS_BYTES = 160 * 1024
+STAGED_MAX_CHUNKS = _lib.DG_STAGED_MAX_CHUNKS
 STAGED_JM_SPARE = 1024
 
 
@@ -799,6 +800,14 @@ class StagedSpec:
     # (H [n_cols][64], W [K][64][d]): relation k's operand is H·W[slab(k)], made in the kernel
     # (dg_spmm_staged_proj_f32); x / x_ld / x_rows are then unused
     proj: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+    # variable output chunks: host int32 [n_chunks + 1], chunk c = relations [cs[c], cs[c+1])
+    # (out is then [n_chunks, n_rows, d]); None: runs of out_chunk relations
+    chunk_start: Optional[np.ndarray] = None
+
+    def n_out(self) -> int:
+        if self.chunk_start is not None:
+            return len(self.chunk_start) - 1
+        return -(-self.layout.n_rels // self.out_chunk)
 
     def validate(self, d: int) -> None:
         L = self.layout
@@ -836,7 +845,13 @@ class StagedSpec:
                 raise ValueError("dense operand smaller than the slabs address")
             if self.x_rows * self.x_ld >= 2**31:
                 raise ValueError("dense operand too large for 32-bit gather offsets")
-        n_out = -(-L.n_rels // self.out_chunk)
+        if self.chunk_start is not None:
+            cs = np.asarray(self.chunk_start)
+            if (cs.ndim != 1 or not 2 <= len(cs) <= STAGED_MAX_CHUNKS + 1 or cs[0] != 0 or cs[-1] != L.n_rels
+                    or L.n_rels > 65535 or np.diff(cs).min() < 1 or np.diff(cs).max() > 64):
+                raise ValueError("staged chunk_start: 0 = c_0 < ... < c_n = n_rels, 1..64 relations a chunk, "
+                                 f"at most {STAGED_MAX_CHUNKS} chunks")
+        n_out = self.n_out()
         if self.out.numel() < n_out * L.n_rows * d:
             raise ValueError("staged out too small")
 
@@ -852,6 +867,7 @@ class PreparedStaged:
         if any((s.proj is not None) != proj for s in specs):
             raise ValueError("a staged launch's groups are all projected or none")
         parr = (DgStagedProj * len(specs))() if proj else None
+        cstarts = []
         for i, s in enumerate(specs):
             s.validate(d)
             L, g = s.layout, arr[i]
@@ -865,7 +881,11 @@ class PreparedStaged:
             g.x_ld = s.x_ld
             g.n_rows, g.n_cols, g.n_rels = L.n_rows, L.n_cols, L.n_rels
             g.out_chunk, g.x_rows, g.jm_len = s.out_chunk, s.x_rows, L.jm_len
-        self._keep = list(specs)
+            if s.chunk_start is not None:
+                cs = np.ascontiguousarray(s.chunk_start, np.int32)
+                cstarts.append(cs)  # (read at each launch: kept alive with the launch)
+                g.chunk_start, g.n_chunks = cs.ctypes.data, len(cs) - 1
+        self._keep = list(specs) + cstarts
         self._arr, self._parr, self._n, self.d = arr, parr, len(specs), d
         lib = _lib.load()
         self._fn = lib.dg_spmm_staged_proj_f32 if proj else lib.dg_spmm_staged_f32

@@ -58,6 +58,13 @@ def lpt_assign(costs: Sequence[float], world_size: int, start: Optional[Sequence
     return owner
 
 
+# config P's relation dealing: a relation of a group that is not staged (the drug-target group,
+# one relation) costs the rank holding it a launch tail beyond its nonzeros — measured 2.7-3.2 us a
+# step on that rank at N = 8 (round 6) — charged in nonzeros of staged work, so LPT gives that
+# rank fewer drug x drug relations
+GROUP_TAIL = knob("DG_SHARD_GROUP_TAIL", 0)
+
+
 def row_block(n_rows: int, rank: int, world_size: int) -> Tuple[int, int, int]:
     """(first row, end row, padded block size) of `rank`'s block of a row-split node type:
     equal blocks of ceil(n / world) rows (the last one short), so the all-gather moves
@@ -156,7 +163,16 @@ class RelationShard:
         comm=False: no collectives (a one-GPU timing rehearsal of one rank's share);
         collectives = (allreduce, allgather) to use instead of torch.distributed's (the RCCL
         communicator of rccl.py for captured steps)."""
-        nnz = {et: [len(c[1]) for c in rels] for et, rels in graph.adj.items()}
+        from .engine import STAGED_REL_OVERHEAD, stageable
+
+        # LPT cost of a relation: its nonzeros, + the staged kernel's per-relation overhead for a
+        # staged group's, + GROUP_TAIL for any other group's (the latency tail its launch adds on
+        # the rank that holds it)
+        nnz = {}
+        for et, rels in graph.adj.items():
+            n_r, n_c = graph.n_nodes[et[0]], graph.n_nodes[et[1]]
+            extra = STAGED_REL_OVERHEAD if stageable(len(rels), n_r, n_c) else GROUP_TAIL
+            nnz[et] = [len(c[1]) + extra for c in rels]
         if not comm:
             ar, ag = _no_op_reduce, _no_op
         elif collectives is not None:

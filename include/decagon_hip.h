@@ -330,7 +330,15 @@ typedef struct dg_staged_group {
     int32_t out_chunk;          /* relations summed into one output chunk (<= 64)        */
     int32_t x_rows;             /* rows of x addressable                                 */
     int32_t jm_len;             /* ints in jm, including the 1024 spare                  */
+    /* Variable output chunks (or NULL: chunk c = relations [c·out_chunk, (c+1)·out_chunk)):
+     * HOST [n_chunks + 1], chunk c = relations [chunk_start[c], chunk_start[c+1]); starts at 0,
+     * ends at n_rels (<= 65535), 1..64 relations a chunk, n_chunks <= DG_STAGED_MAX_CHUNKS.
+     * out is then [n_chunks][n_rows][d].  Copied into the launch's arguments. */
+    const int32_t* chunk_start;
+    int32_t n_chunks;
+    int32_t pad;
 } dg_staged_group;
+#define DG_STAGED_MAX_CHUNKS 128
 
 int dg_spmm_staged_f32(const dg_staged_group* groups /* HOST */, int32_t n_groups, int32_t d,
                        void* stream);

@@ -123,6 +123,19 @@ def test_abi_rejects_bad_arguments_without_a_device():
     assert lib.dg_rownorm_l2_f32(16, 16, 10, 64, _lib.DG_EPI_L2NORM, None) == _lib.DG_EINVAL
     assert lib.dg_rownorm_l2_f32(16, 16, 10, 62, 0, None) == _lib.DG_EINVAL
     assert lib.dg_rownorm_l2_f32(None, None, 0, 64, 0, None) == _lib.DG_OK
+    # ABI 38: a staged group's variable chunk table is checked before any launch
+    for cs in ([0, 2, 2, 5], [1, 5], [0, 4], [0] + list(range(5, 70, 65)) + [70]):
+        cs_arr = np.asarray(cs, np.int32)
+        grp = (_lib.DgStagedGroup * 1)()
+        g = grp[0]
+        g.pairs = g.jm = g.jmoff = g.x = g.out = 4096
+        g.x_ld, g.n_rows, g.n_cols, g.n_rels, g.out_chunk = 64, 10, 10, 5 if cs[-1] != 70 else 70, 4
+        g.x_rows, g.jm_len = 640, 36 + 1024
+        g.chunk_start, g.n_chunks = cs_arr.ctypes.data, len(cs) - 1
+        if cs[-1] == 70:  # chunk of 65 relations
+            cs_arr = np.asarray([0, 65, 70], np.int32)
+            g.chunk_start, g.n_chunks = cs_arr.ctypes.data, 2
+        assert lib.dg_spmm_staged_f32(grp, 1, 64, None) == _lib.DG_EINVAL, cs
 
 
 def test_merge_chunks_layout():
@@ -501,3 +514,36 @@ def test_balanced_wave_dealing_covers_every_pair_once(proj):
         longest = max(sum(e - a for _, a, e in w) for wg in waves for w in wg)
         assert longest <= max(lens.values()) if proj else longest <= max(
             sum(lens[g, k] for k in range(nr[g])) for g in range(n_groups))
+
+
+def test_staged_var_chunks():
+    """Variable staged output chunks (engine.staged_var_chunks): a permutation of the relations,
+    sub-chunks nested in the top-level chunks, 1..64 relations a chunk, LPT balance."""
+    from decagon_amd import engine
+
+    rng = np.random.default_rng(3)
+    for n, n_top in ((241, 64), (1928, 64), (60, 64), (5, 64), (128, 2)):
+        costs = 1500 + (7500 * rng.zipf(1.6, n).clip(1, 8)).astype(float)
+        order, tops, subs = engine.staged_var_chunks(costs, n_top)
+        assert sorted(order.tolist()) == list(range(n))
+        assert tops[0] == 0 and tops[-1] == n and subs[0] == 0 and subs[-1] == n
+        assert set(tops.tolist()) <= set(subs.tolist())
+        assert len(tops) - 1 == min(n_top, n)
+        for st in (tops, subs):
+            assert np.diff(st).min() >= 1 and np.diff(st).max() <= 64
+        c = costs[order]
+        loads = np.array([c[a:b].sum() for a, b in zip(tops[:-1], tops[1:])])
+        assert loads.max() <= max(costs.max(), costs.sum() / len(loads) + costs.max()) + 1e-6
+
+    class G:  # the fields staged_chunk_starts reads
+        pass
+    g = G()
+    order, tops, subs = engine.staged_var_chunks(np.ones(241), 64)
+    g.var_chunks = (tops, subs)
+    assert engine.staged_chunk_starts(g, 64) is tops           # 4 slices: 64 chunks
+    assert engine.staged_chunk_starts(g, 32) is subs           # 2 slices: 128 chunks
+    st = engine.staged_chunk_starts(g, 128)                    # 8 slices: runs of two chunks
+    assert list(st) == list(tops[::2]) and engine.staged_out_chunk(g, 128) == int(np.diff(st).max())
+    g.var_chunks = None
+    g.n_rels, g.out_chunk = 241, 2
+    assert engine.staged_chunk_starts(g, 64) is None

@@ -721,3 +721,53 @@ def test_spmm_staged_projected(K, d, n_rows, n_cols, density, out_chunk):
     spec.out = out2
     K.PreparedStaged([spec], d)()
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("proj", [False, True])
+@pytest.mark.parametrize("d", [32, 64])
+@pytest.mark.parametrize("n_rows,n_cols,density", [(150, 137, 0.03), (645, 645, 0.05)])
+def test_spmm_staged_var_chunks(K, proj, d, n_rows, n_cols, density):
+    """Variable output chunks (dg_staged_group.chunk_start, ABI 38): chunk c sums relations
+    [cs[c], cs[c+1]) — single-relation chunks, a long chunk, the empty relation alone — and a
+    table of fixed runs is bitwise the fixed out_chunk launch."""
+    from decagon_amd.sparse import coo_to_csr, sparse_to_tuple, staged_layout
+
+    rng = np.random.default_rng(11 * d + n_rows + proj)
+    nrel, total = 23, 30
+    mats = [_rand_csr(rng, n_rows, n_cols, density, empty_rows=0.1) for _ in range(nrel)]
+    mats[4] = sp.csr_matrix((n_rows, n_cols), dtype=np.float32)
+    slabs = rng.choice(total, size=nrel, replace=False).astype(np.int32)
+    lay = staged_layout([coo_to_csr(*sparse_to_tuple(x)) for x in mats], K.staged_block)
+    dev = K.StagedDevice.upload(lay, "cuda")
+    X = rng.standard_normal((total, n_cols, d)).astype(np.float32)
+    Hp = rng.standard_normal((n_cols, 64)).astype(np.float32)
+    W = rng.standard_normal((total, 64, d)).astype(np.float32)
+    if proj:
+        ops = [Hp.astype(np.float64) @ W[s].astype(np.float64) for s in range(total)]
+    else:
+        ops = [X[s].astype(np.float64) for s in range(total)]
+
+    def run(out_chunk, cs):
+        n_out = len(cs) - 1 if cs is not None else -(-nrel // out_chunk)
+        out = torch.zeros((n_out, n_rows, d), device="cuda")
+        kw = dict(slab_max=int(slabs.max()), chunk_start=None if cs is None else np.asarray(cs, np.int32))
+        if proj:
+            kw["proj"] = (torch.from_numpy(Hp).cuda(), torch.from_numpy(W).cuda())
+            spec = K.StagedSpec(dev, torch.from_numpy(slabs).cuda(), None, out, out_chunk, d, 0, **kw)
+        else:
+            spec = K.StagedSpec(dev, torch.from_numpy(slabs).cuda(), torch.from_numpy(X).cuda(), out, out_chunk, d,
+                                total * n_cols, **kw)
+        K.PreparedStaged([spec], d)()
+        torch.cuda.synchronize()
+        return out
+
+    cs = [0, 1, 4, 5, 6, 19, 21, 23]
+    out = run(13, cs)
+    want = np.zeros((len(cs) - 1, n_rows, d))
+    for c in range(len(cs) - 1):
+        for k in range(cs[c], cs[c + 1]):
+            want[c] += mats[k] @ ops[slabs[k]]
+    assert rel_err(out.cpu().numpy(), want) <= 1e-5
+    assert torch.equal(out, run(13, cs))
+    # fixed runs of 5 as a table: bitwise the fixed launch
+    assert torch.equal(run(5, list(range(0, nrel, 5)) + [nrel]), run(5, None))
