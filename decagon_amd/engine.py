@@ -180,6 +180,36 @@ def staged_var_chunks(costs: Sequence[float], n_top: int, split: int = 2, cap: i
     return np.asarray(order, np.int64), np.asarray(tops, np.int32), np.asarray(subs, np.int32)
 
 
+# ... and a relation costing more than STAGED_PIECE x a chunk's mean (a 32-wide layer's chunks are
+# halves) is cut by rows into pieces of at most that (each piece its own staged "relation" reading
+# the same slab): config P's N = 8 rank share holds 58 k-nonzero relations against chunks of ~45 k
+STAGED_PIECE = knob("DG_STAGED_PIECE", 0.5)
+
+
+def staged_pieces(loc: Sequence[HostCSR], costs: Sequence[float], n_top: int, frac: float):
+    """Row pieces of the relations that cost more than frac x sum(costs) / n_top: a list of
+    (relation index, HostCSR) — whole relations as themselves, heavy ones as pieces of consecutive
+    rows of about equal nonzeros, at most that cost each (every row in exactly one piece, so a
+    row's sum over a relation is the same arithmetic)."""
+    mean = float(sum(costs)) / max(1, n_top)
+    out = []
+    for i, (c, cost) in enumerate(zip(loc, costs)):
+        n_p = int(math.ceil(cost / (frac * mean))) if frac > 0 and cost > frac * mean else 1
+        if n_p <= 1:
+            out.append((i, c))
+            continue
+        rp = c.rowptr.astype(np.int64)
+        cuts = np.searchsorted(rp, np.arange(1, n_p) * (c.nnz / n_p), side="left")
+        bounds = np.unique(np.concatenate([[0], np.clip(cuts, 0, c.shape[0]), [c.shape[0]]]))
+        for ra, rb in zip(bounds[:-1], bounds[1:]):
+            p0, p1 = int(rp[ra]), int(rp[rb])
+            if p1 == p0:
+                continue
+            prow = (np.clip(rp, p0, p1) - p0).astype(np.int32)
+            out.append((i, HostCSR(prow, c.col[p0:p1], c.val[p0:p1], tuple(c.shape))))
+    return out
+
+
 def staged_chunk_starts(grp, d: int) -> Optional[np.ndarray]:
     """The variable output chunks of a staged group for a layer of width d (None: fixed runs of
     staged_out_chunk relations): the sub-chunks when the layer wants at least twice the top-level
@@ -201,6 +231,12 @@ def staged_chunk_starts(grp, d: int) -> Optional[np.ndarray]:
     return st.astype(np.int32)
 
 
+def _staged_n(grp) -> int:
+    """Relations of a staged group's layout (row pieces counted one by one)."""
+    lay = getattr(grp, "layout", None)
+    return lay.n_rels if lay is not None else grp.n_rels
+
+
 def staged_out_chunk(grp, d: int) -> int:
     """Relations per output chunk of a staged group for a layer of width d: a multiple of the
     group's snake-bin size (so chunks stay balanced) giving about STAGED_TARGET_BLOCKS
@@ -211,7 +247,7 @@ def staged_out_chunk(grp, d: int) -> int:
         return int(np.diff(st).max())
     n_slices = -(-d // 16)
     want = max(1, STAGED_TARGET_BLOCKS // n_slices)        # output chunks
-    per = max(1, -(-grp.n_rels // want))
+    per = max(1, -(-_staged_n(grp) // want))
     oc = grp.out_chunk * max(1, -(-per // grp.out_chunk))
     return min(oc, 64)
 
@@ -330,6 +366,9 @@ class DeviceGroup:
     out_chunk: int = 1             # staged: snake-bin size (a layer's output chunk is a multiple)
     # staged, variable chunks (STAGED_VAR): (top-level chunk starts, sub-chunk starts), device order
     var_chunks: Optional[Tuple[np.ndarray, np.ndarray]] = None
+    # staged, heavy relations in row pieces (staged_pieces): the layout's slab per piece (global
+    # relation id; the layout then lists pieces, not rel_ids' relations); None: rel_map
+    staged_slab: Optional[torch.Tensor] = None
     layout: Optional["kernels.StagedDevice"] = None  # staged: the diagonal-major layout
     host: Optional[List[HostCSR]] = None  # the local relations (host CSR), device order
     seg: Optional[torch.Tensor] = None    # dg_spmm_seg_f32's segment starts (sparse.chunk_segments)
@@ -391,15 +430,27 @@ class DeviceGraph:
                 # nonzero counts (relation sizes are Zipf-skewed)
                 out_chunk = max(1, -(-len(loc) // STAGED_BINS))
                 costs = [c.nnz + STAGED_REL_OVERHEAD for c in loc]
-                var = None
+                var, pieces = None, None
                 n_top = max(1, STAGED_TARGET_BLOCKS // -(-d_policy // 16))
-                if STAGED_VAR and len(loc) <= 65535 and len(loc) <= 64 * n_top:
-                    perm, tops, subs = staged_var_chunks(costs, n_top)
+                if STAGED_VAR:
+                    pieces = staged_pieces(loc, costs, n_top, STAGED_PIECE)
+                    if len(pieces) == len(loc):
+                        pieces = None
+                n_v = len(pieces) if pieces is not None else len(loc)
+                if STAGED_VAR and n_v <= 65535 and n_v <= 64 * n_top:
+                    vcosts = costs if pieces is None else [c.nnz + STAGED_REL_OVERHEAD for _, c in pieces]
+                    perm, tops, subs = staged_var_chunks(vcosts, n_top)
                     var = (tops, subs)
                 else:
+                    pieces = None
                     perm = snake_bins(costs, out_chunk)
-                ids = ids[perm]
-                loc = [loc[i] for i in perm]
+                if pieces is None:
+                    ids = ids[perm]
+                    loc = [loc[i] for i in perm]
+                    stage_loc, stage_slab = loc, None
+                else:  # the pieces in device order; the group's relations keep their order
+                    stage_loc = [pieces[i][1] for i in perm]
+                    stage_slab = ids[np.asarray([pieces[i][0] for i in perm], np.int64)].astype(np.int32)
                 ch = 1
             if ch is None:
                 ch = choose_chunk(len(loc), n_r, nnz, d_policy, target_waves)
@@ -422,6 +473,8 @@ class DeviceGraph:
             g.staged, g.out_chunk = staged, out_chunk
             if staged:
                 g.var_chunks = var
+                if stage_slab is not None:
+                    g.staged_slab = torch.from_numpy(stage_slab).to(device)
             g.host = loc  # local relations in device order (the backward builds Âᵀ from them)
             if segments and loc and not staged and not windows and m.chunk <= 16:
                 g.seg = torch.from_numpy(chunk_segments(loc, m)).to(device)
@@ -432,7 +485,7 @@ class DeviceGraph:
                 g.seg2 = (up(m2.rowptr), up(m2.vcol), up(m2.val), up(chunk_segments(loc, m2)), m2.chunk, m2.n_chunks,
                           int(m2.vcol.max()) if m2.nnz else -1)
             if staged:
-                lay = staged_layout(loc, kernels.staged_block,
+                lay = staged_layout(stage_loc, kernels.staged_block,
                                     lanes=knob("DG_STAGED_LANES", 1024),
                                     split=knob("DG_STAGED_SPLIT", True))
                 g.layout = kernels.StagedDevice.upload(lay, device)
@@ -896,7 +949,7 @@ class ForwardPlan:
         for et in rest:
             grp = g.groups[et]
             cst = staged_chunk_starts(grp, d) if grp.staged else None
-            n_out = ((len(cst) - 1 if cst is not None else -(-grp.n_rels // staged_out_chunk(grp, d)))
+            n_out = ((len(cst) - 1 if cst is not None else -(-_staged_n(grp) // staged_out_chunk(grp, d)))
                      if grp.staged else grp.n_chunks)
             if et in reassoc:
                 n_out = self._seg_chunks(et)
@@ -912,7 +965,7 @@ class ForwardPlan:
             if grp.staged:
                 sp = (staged_proj or {}).get(et)
                 staged.append(kernels.StagedSpec(
-                    grp.layout, grp.rel_map, xs.get(et), part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
+                    grp.layout, grp.staged_slab if grp.staged_slab is not None else grp.rel_map, xs.get(et), part, staged_out_chunk(grp, d), d, grp.K * grp.n_cols,
                     slab_max=int(grp.rel_ids.max()), proj=sp, chunk_start=cst))
             elif self.seg_mode or et in reassoc:
                 if et in (seg_w or {}):  # layer 2 reassociated: H1_j and W2's stack
