@@ -428,9 +428,11 @@ struct EpiArgs {
     dg::PeerK P;  // PEER launches: the finished rows also go to every peer's copy (peer.h)
 };
 
+constexpr int kEpiBatch = 8;  // partial loads in flight a lane (epilogue_row)
+
 // One wave per output row: LP lanes cover the row's d floats (a float4 each) and the
-// wave's CG = 64/LP lane groups split the chunks (group cg sums chunks cg, cg+CG, ... with four
-// loads in flight), combined by an xor butterfly — every lane ends with the same bits, so the
+// wave's CG = 64/LP lane groups split the chunks (group cg sums chunks cg, cg+CG, ... with
+// kEpiBatch loads in flight), combined by an xor butterfly — every lane ends with the same bits, so the
 // result is deterministic; then the L2 norm over the row's LP lanes.
 template <int LP, bool PEER>
 __device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK& t, int r, int cg, int q) {
@@ -451,19 +453,18 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& a, const EpiTargetK&
         const int nc = a.g[gi].n_chunks;
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
         if (qok) {
-            int c = cg;
+            // eight loads in flight a lane, the last batch predicated: a staged group's 64-128
+            // output chunks (16 a lane group) in two round trips instead of four
 #pragma unroll 1
-            for (; c + 3 * CG < nc; c += 4 * CG) {
-                float4 v[4];
+            for (int c = cg; c < nc; c += kEpiBatch * CG) {
+                float4 v[kEpiBatch];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (c + u * CG) * plane);
+                for (int u = 0; u < kEpiBatch; ++u)
+                    v[u] = c + u * CG < nc ? *reinterpret_cast<const float4*>(p + (c + u * CG) * plane)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) dg::add4(s, crelu ? relu4(v[u]) : v[u]);
-            }
-#pragma unroll 1
-            for (; c < nc; c += CG) {
-                const float4 v = *reinterpret_cast<const float4*>(p + c * plane);
-                dg::add4(s, crelu ? relu4(v) : v);
+                for (int u = 0; u < kEpiBatch; ++u)
+                    if (c + u * CG < nc) dg::add4(s, crelu ? relu4(v[u]) : v[u]);
             }
         }
         s = dg::xor_sum4_from<LP>(s);

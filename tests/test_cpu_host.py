@@ -547,3 +547,30 @@ def test_staged_var_chunks():
     g.var_chunks = None
     g.n_rels, g.out_chunk = 241, 2
     assert engine.staged_chunk_starts(g, 64) is None
+
+
+def test_staged_pieces_partition_rows():
+    """engine.staged_pieces: a heavy relation becomes row pieces whose sum is the relation, every
+    row in exactly one piece; light relations pass through whole."""
+    import scipy.sparse as sp
+
+    from decagon_amd import engine
+    from decagon_amd.sparse import HostCSR
+
+    rng = np.random.default_rng(5)
+    mats = [sp.random(120, 90, density=dd, random_state=i, format="csr", dtype=np.float32)
+            for i, dd in enumerate([0.3, 0.02, 0.05, 0.01])]
+    loc = [HostCSR(m.indptr.astype(np.int32), m.indices.astype(np.int32), m.data, m.shape) for m in mats]
+    costs = [c.nnz + 100 for c in loc]
+    pcs = engine.staged_pieces(loc, costs, 2, 0.5)
+    mean = sum(costs) / 2
+    for i, c in enumerate(loc):
+        mine = [p for j, p in pcs if j == i]
+        assert (len(mine) > 1) == (costs[i] > 0.5 * mean)
+        tot = sum(sp.csr_matrix((p.val, p.col, p.rowptr), shape=p.shape) for p in mine)
+        assert abs(tot - mats[i]).max() == 0
+        rows = [set(np.nonzero(np.diff(p.rowptr))[0]) for p in mine]
+        assert sum(len(r) for r in rows) == len(set().union(*rows))   # disjoint rows
+        assert all(p.nnz <= c.nnz / len(mine) + max(np.diff(c.rowptr)) for p in mine)  # about equal
+    assert engine.staged_pieces(loc, costs, 2, 0.0) == [(i, c) for i, c in enumerate(loc)]
+    del rng
