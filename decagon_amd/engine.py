@@ -974,10 +974,12 @@ class ForwardPlan:
                     segs.append(self._seg_spec(et, xs[et], part))
             else:
                 specs.append(self._spec(et, xs[et], part, d))
+        spmm_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged
+                    and not (self.seg_mode or et in reassoc)]
+        seg_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged
+                   and (self.seg_mode or et in reassoc)]
         if segs:
             d_in = self.h1 if seg_w else d
-            seg_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged
-                       and (self.seg_mode or et in reassoc)]
             for s in range(0, len(segs), DG_MAX_GROUPS):
                 part = segs[s:s + DG_MAX_GROUPS]
                 if WAVE_TABLE and kernels._tab_shape(d_in, d, part):
@@ -986,7 +988,6 @@ class ForwardPlan:
                     launches.append(kernels.PreparedSeg(part, d_in, d))
                 self.launch_groups[id(launches[-1])] = seg_ets[s:s + DG_MAX_GROUPS]
         staged_ets = [et for et in rest if g.groups[et].n_rels and g.groups[et].staged]
-        spmm_ets = [et for et in rest if g.groups[et].n_rels and not g.groups[et].staged]
         for s in range(0, len(staged), DG_MAX_GROUPS):
             launches.append(kernels.PreparedStaged(staged[s:s + DG_MAX_GROUPS], d))
             self.launch_groups[id(launches[-1])] = staged_ets[s:s + DG_MAX_GROUPS]
