@@ -63,6 +63,11 @@ def lpt_assign(costs: Sequence[float], world_size: int, start: Optional[Sequence
 # step on that rank at N = 8 (round 6) — charged in nonzeros of staged work, so LPT gives that
 # rank fewer drug x drug relations
 GROUP_TAIL = knob("DG_SHARD_GROUP_TAIL", 0)
+# ... or such a group (fewer relations than ranks, not staged) dealt by output rows over every
+# rank (RelationShard.dealt), so no rank carries its whole launch tail.  Off: config P at N = 8
+# measured 98.4 / 96.7 µs max against 97.2 / 97.7 — every rank then pays the relation's row-chain
+# tail (93.8-95.6 → 96.0-97.4), which is latency, not row count (round 6)
+DEAL_ROWS = knob("DG_SHARD_DEAL_ROWS", False)
 
 
 def row_block(n_rows: int, rank: int, world_size: int) -> Tuple[int, int, int]:
@@ -105,6 +110,10 @@ class RelationShard:
     # row-split node types in dg_spmm_seg_f32 + the epilogue, layer 2 reassociated (config S's
     # weak scaling at N GPUs; `chunks` then holds the relations per set)
     seg_rows: bool = False
+    # relation-sharded groups of fewer relations than ranks dealt by ROWS instead (split's
+    # deal_rows): every rank holds each of their relations over its block [a, b) of output rows,
+    # the other rows emptied (same shape; the all-reduce adds the blocks) — edge type -> (a, b)
+    dealt: Dict[EdgeType, Tuple[int, int]] = field(default_factory=dict)
     # the row-split blocks exchanged by peer stores over xGMI instead of `allgather`
     # (peer.PeerConfig: the finishing launch pushes its rows and ends with the exchange, or a
     # stand-alone exchange launch); the all-reduce of relation-sharded sums stays `allreduce`
@@ -128,10 +137,12 @@ class RelationShard:
     @staticmethod
     def split(edge_types: Dict[EdgeType, int], n_nodes: Dict[int, int], rel_cost: Dict[EdgeType, Sequence[float]],
               rank: int, world_size: int, allreduce=None, allgather=None,
-              row_split_min: int = ROW_SPLIT_MIN) -> "RelationShard":
+              row_split_min: int = ROW_SPLIT_MIN, deal_rows=()) -> "RelationShard":
         """Row-split the node types of >= row_split_min rows (every rank keeps all relations
         of the groups into them, on its row block); LPT the relations of the groups into the
-        other node types, starting from the row-split work each rank already holds."""
+        other node types, starting from the row-split work each rank already holds.  Groups in
+        `deal_rows` (relation-sharded ones) are dealt by output rows instead: every rank holds
+        all their relations over its row block (`dealt`)."""
         # (every rank must own at least one row of a row-split node type)
         rows = {t for t, n in n_nodes.items()
                 if n >= row_split_min and (world_size - 1) * -(-n // world_size) < n}
@@ -139,11 +150,14 @@ class RelationShard:
         local: Dict[EdgeType, List[int]] = {}
         items, costs = [], []
         base = [0.0] * world_size
+        dealt = {}
         for et, K in edge_types.items():
-            if et[0] in rows:
+            if et[0] in rows or et in deal_rows:
                 local[et] = list(range(K))
                 share = sum(float(c) for c in rel_cost[et]) / world_size
                 base = [b + share for b in base]
+                if et[0] not in rows:
+                    dealt[et] = row_block(n_nodes[et[0]], rank, world_size)[:2]
             else:
                 local[et] = []
                 for k in range(K):
@@ -155,7 +169,7 @@ class RelationShard:
             loads[r] += c
             if r == rank:
                 local[et].append(k)
-        return RelationShard(rank, world_size, local, allreduce, loads, blocks, allgather)
+        return RelationShard(rank, world_size, local, allreduce, loads, blocks, allgather, dealt=dealt)
 
     @staticmethod
     def polypharmacy(graph, rank: int, world_size: int, comm: bool = True, collectives=None) -> "RelationShard":
@@ -168,18 +182,21 @@ class RelationShard:
         # LPT cost of a relation: its nonzeros, + the staged kernel's per-relation overhead for a
         # staged group's, + GROUP_TAIL for any other group's (the latency tail its launch adds on
         # the rank that holds it)
-        nnz = {}
+        nnz, deal = {}, []
         for et, rels in graph.adj.items():
             n_r, n_c = graph.n_nodes[et[0]], graph.n_nodes[et[1]]
-            extra = STAGED_REL_OVERHEAD if stageable(len(rels), n_r, n_c) else GROUP_TAIL
+            staged = stageable(len(rels), n_r, n_c)
+            extra = STAGED_REL_OVERHEAD if staged else GROUP_TAIL
             nnz[et] = [len(c[1]) + extra for c in rels]
+            if DEAL_ROWS and not staged and len(rels) < world_size and n_r >= world_size:
+                deal.append(et)  # (the drug-target relation: its rows over every rank)
         if not comm:
             ar, ag = _no_op_reduce, _no_op
         elif collectives is not None:
             ar, ag = collectives
         else:
             ar, ag = torch_allreduce(), torch_allgather()
-        return RelationShard.split(graph.edge_types, graph.n_nodes, nnz, rank, world_size, ar, ag)
+        return RelationShard.split(graph.edge_types, graph.n_nodes, nnz, rank, world_size, ar, ag, deal_rows=deal)
 
     @staticmethod
     def weak_sets(edge_types: Dict[EdgeType, int], n_nodes: Dict[int, int], rank: int, world_size: int,
@@ -213,15 +230,26 @@ class RelationShard:
     def local_csr(self, csr: Dict[EdgeType, Sequence]) -> Dict[EdgeType, list]:
         """The graph's per-group relation lists with the relations of other ranks replaced by
         empty stand-ins of the same shape (never uploaded; they only carry the group's shape
-        when this rank owns none of its relations)."""
+        when this rank owns none of its relations), and a row-dealt group's relations cut to
+        this rank's rows."""
         from .sparse import HostCSR
 
         def empty(c):
             return HostCSR(np.zeros(c.shape[0] + 1, np.int32), np.zeros(0, np.int32), np.zeros(0, np.float32),
                            tuple(c.shape))
 
-        return {et: [c if k in set(self.local[et]) else empty(c) for k, c in enumerate(v)]
-                for et, v in csr.items()}
+        def rows(c, ab):  # rows [a, b) of c, the others emptied (same shape)
+            a, b = ab
+            rp = c.rowptr.astype(np.int64)
+            p0, p1 = int(rp[a]), int(rp[b])
+            return HostCSR((np.clip(rp, p0, p1) - p0).astype(np.int32), c.col[p0:p1], c.val[p0:p1], tuple(c.shape))
+
+        out = {}
+        for et, v in csr.items():
+            mine = set(self.local[et])
+            out[et] = [(rows(c, self.dealt[et]) if et in self.dealt else c) if k in mine else empty(c)
+                       for k, c in enumerate(v)]
+        return out
 
     def describe(self, backend: str = "nccl") -> str:
         lib = "RCCL" if backend == "nccl" else backend

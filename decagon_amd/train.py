@@ -138,6 +138,8 @@ class TrainPlan:
         # relation into them, so its Âᵀ·dS products over those rows are PARTIAL weight
         # gradients — all-reduced after the backward (every rank then applies the same Adam step)
         rb = dict(fwd.row_block)
+        dealt = set(getattr(fwd.shard, "dealt", None) or ())
+        self._dealt = dealt
         rows_of = lambda i: (rb[i][1] - rb[i][0]) if i in rb else n[i]  # noqa: E731
         self._rowsplit_grads: List[torch.Tensor] = []
         self.gW1: Dict[EdgeType, torch.Tensor] = {}
@@ -186,7 +188,7 @@ class TrainPlan:
             g1 = self.gW1[et] if fj is None else torch.zeros((K, n[j], h1), **f32)
             specs2.append(kernels.RelGroupSpec(rp, vc, vv, dS2, dP, n[j], K, h2, rows_of(i), vcol_max=vmax))
             specs1.append(kernels.RelGroupSpec(rp, vc, vv, dS1, g1, n[j], K, h1, rows_of(i), vcol_max=vmax))
-            if i in rb:
+            if i in rb or et in dealt:  # (row-dealt groups: partial over this rank's rows too)
                 self._rowsplit_grads += [self.gW1[et], self.gW2[et]]
             if fj is not None:  # X_jᵀ's pattern shared by the K chunks, chunk k reading G_k
                 xt, perm = transpose_csr(fj, with_perm=True)
@@ -297,7 +299,7 @@ class TrainPlan:
         shapes, sizes = [], []
         for name, grads in (("w1", self.gW1), ("w2", self.gW2)):
             for et in self.fwd.edge_types:
-                if et[0] in rb:
+                if et[0] in rb or et in self._dealt:
                     continue
                 K = self.fwd.g.groups[et].K
                 shapes.append((name, et, (K,) + tuple(grads[et].shape[1:])))
@@ -317,7 +319,7 @@ class TrainPlan:
             self.allreduce(flat)
         for name, grads in (("w1", self.gW1), ("w2", self.gW2)):
             for et in self.fwd.edge_types:
-                if et[0] in rb:
+                if et[0] in rb or et in self._dealt:
                     out[name][et] = grads[et].clone()
         return out["w1"], out["w2"]
 

@@ -574,3 +574,41 @@ def test_staged_pieces_partition_rows():
         assert all(p.nnz <= c.nnz / len(mine) + max(np.diff(c.rowptr)) for p in mine)  # about equal
     assert engine.staged_pieces(loc, costs, 2, 0.0) == [(i, c) for i, c in enumerate(loc)]
     del rng
+
+
+def test_row_dealt_group_partitions_rows():
+    """RelationShard.split(deal_rows=...): every rank holds each relation of a dealt group over
+    its own block of output rows (the others emptied, same shape); the blocks add up to the
+    relation; polypharmacy deals config P's drug-target relation this way with DG_SHARD_DEAL_ROWS=1."""
+    import scipy.sparse as sp
+
+    from decagon_amd import synthetic
+    from decagon_amd.sharding import RelationShard, _no_op, _no_op_reduce
+
+    g = synthetic.make_P(seed=3, n_proteins=1500, n_drugs=150, n_side_effects=60, ppi_edges=12000,
+                         target_edges=1200)
+    nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
+    csr = g.csr()
+    for world in (2, 3, 8):
+        tot = None
+        for r in range(world):
+            sh = RelationShard.split(g.edge_types, g.n_nodes, nnz, r, world, _no_op_reduce, _no_op,
+                                     row_split_min=1000, deal_rows=[(1, 0)])
+            assert list(sh.dealt) == [(1, 0)] and sh.local[1, 0] == [0]
+            c = sh.local_csr(csr)[1, 0][0]
+            assert c.shape == csr[1, 0][0].shape
+            a, b = sh.dealt[1, 0]
+            m = sp.csr_matrix((c.val, c.col, c.rowptr), shape=c.shape)
+            assert m[:a].nnz == 0 and m[b:].nnz == 0
+            tot = m if tot is None else tot + m
+        ref = csr[1, 0][0]
+        assert abs(tot - sp.csr_matrix((ref.val, ref.col, ref.rowptr), shape=ref.shape)).max() == 0
+    from decagon_amd import sharding
+    gP = synthetic.make_P(seed=0)
+    assert not RelationShard.polypharmacy(gP, 0, 8, comm=False).dealt    # default: LPT owner
+    sharding.DEAL_ROWS = True
+    try:
+        shP = RelationShard.polypharmacy(gP, 0, 8, comm=False)
+    finally:
+        sharding.DEAL_ROWS = False
+    assert list(shP.dealt) == [(1, 0)] and all(len(shP.local[et]) for et in [(1, 0), (0, 0), (0, 1)])

@@ -60,8 +60,11 @@ def _shard(kind, g, rank, world):
     if kind in ("S-rows", "S-rows-fused"):
         return RelationShard.weak_sets(g.edge_types, g.n_nodes, rank, world, torch_allreduce(), torch_allgather(),
                                        form="fused" if kind == "S-rows-fused" else "seg")
+    if kind == "P":  # the driver's partition (bench.py): proteins row-split, drug×drug LPT
+        return RelationShard.polypharmacy(g, rank, world, collectives=(torch_allreduce(), torch_allgather()))
+    # P-small: at 3 and 8 ranks the drug-target relation dealt by rows as well (RelationShard.dealt)
     return RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
-                               row_split_min=1000)
+                               row_split_min=1000, deal_rows=[(1, 0)] if world in (3, 8) else ())
 
 
 def _rank(rank, world, kind, h2=32):
@@ -79,7 +82,7 @@ def _rank(rank, world, kind, h2=32):
                        shard=shard)
     from decagon_amd import engine, kernels
 
-    info = {"row_split": sorted(shard.row_block), "staged": dg.groups[(1, 1)].staged,
+    info = {"row_split": sorted(shard.row_block), "dealt": sorted(shard.dealt), "staged": dg.groups[(1, 1)].staged,
             "local": {et: len(v) for et, v in shard.local.items()}, "fused": sorted(plan.fused),
             "seg": plan.seg_mode, "gemms": len(plan._gemm2)}
     plan.run()
@@ -164,7 +167,8 @@ def _check(kind, world, h2=32):
     split = got[0][0]["row_split"]
     for et in g.edge_types:
         owned = sum(got[r][0]["local"][et] for r in range(world))
-        assert owned == (g.edge_types[et] * (world if et[0] in split else 1))
+        dealt = et in got[0][0]["dealt"]  # (every rank holds a row-dealt group's relations)
+        assert owned == (g.edge_types[et] * (world if et[0] in split or dealt else 1))
 
 
 def test_sharded_S_forward_matches_oracle():
@@ -222,7 +226,7 @@ def _train_rank(rank, world, kind, split=False, dropout=0.0):
     nnz = {et: [len(c[1]) for c in rels] for et, rels in g.adj.items()}
     if split:
         shard = RelationShard.split(g.edge_types, g.n_nodes, nnz, rank, world, torch_allreduce(), torch_allgather(),
-                                    row_split_min=1000)
+                                    row_split_min=1000, deal_rows=[(1, 0)] if split == "deal" else ())
     else:
         shard = RelationShard.lpt(g.edge_types, nnz, rank, world, torch_allreduce())
     w1, w2 = _weights(g, 5)
@@ -267,7 +271,7 @@ def _train_rank(rank, world, kind, split=False, dropout=0.0):
         for et, ids in tp.local_ids.items():
             for k in ids:
                 after[name, et[0], et[1], int(k)] = st.stacks[et][int(k)].cpu().numpy()
-    info = {"row_split": sorted(shard.row_block)}
+    info = {"row_split": sorted(shard.row_block), "dealt": sorted(shard.dealt)}
     return grads, {"R": dR.cpu().numpy(), "l": dl.cpu().numpy()}, float(hinge.loss[0]), after, info
 
 
@@ -309,7 +313,7 @@ def _train_oracle(kind, g, dropout=0.0):
 
 
 @pytest.mark.parametrize("kind,split,dropout", [("S", False, 0.0), ("S", False, 0.1), ("P-small", True, 0.1),
-                                                ("P-small", True, 0.0)])
+                                                ("P-small", True, 0.0), ("P-small", "deal", 0.1)])
 def test_sharded_training_step_matches_oracle(kind, split, dropout):
     """Sharded training on 2 ranks: config S relations LPT-sharded (with and without the
     reference's default dropout 0.1, main.py:305-308), and the scaled-down config P with its
@@ -342,7 +346,7 @@ def test_sharded_training_step_matches_oracle(kind, split, dropout):
                 assert np.max(np.abs(after[name, i, j, k] - p1)) <= 1e-6 * max(1.0, np.max(np.abs(p1)))
                 key = (name, i, j, k)
                 if key in seen:  # only a row-split group's relations live on several ranks
-                    assert split and i in info["row_split"], key
+                    assert split and (i in info["row_split"] or (i, j) in info["dealt"]), key
                     assert np.array_equal(seen[key], after[key]), key
                 seen[key] = after[name, i, j, k]
     assert len(seen) == 2 * sum(g.edge_types.values())  # every relation
